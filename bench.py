@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Benchmark: MPHF build (BBHash, gamma 2.0) keys/s, device-resident, on N MI355X.
+
+A "step" is one complete MPHF build over the synthetic prefix set already resident
+in HBM: FNV-1a key hashes + FNV-1 fingerprints, every BBHash level, level ranks, and
+the mph_fp / mph_pos placement — the work of StreamingMPHFBuilder.Build minus file
+I/O (/root/reference/pkg/format/mphf_streaming.go:122-213).
+
+  python bench.py [--gpus N --steps K --warmup W --config c2]
+  N > 1: torchrun --nproc-per-node N bench.py --gpus N ...  (one process per GPU;
+         RCCL communicator owned by libs3imph; torch.distributed/gloo only for the
+         rendezvous, barriers and the max-over-ranks time).
+
+Workload (BASELINE.json configs[1]): 10M synthetic prefixes per GPU, avg key 32 B
+(weak scaling: N GPUs build one MPHF over N x 10M keys).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "s3-inv-db_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    "c2": dict(kind=0, avg=32, keys_per_gpu=10_000_000,
+               workload="C2: 10M synthetic S3 prefixes per GPU, key length uniform 16-48 B (avg 32 B)"),
+    "c3": dict(kind=0, avg=64, keys_per_gpu=100_000_000,
+               workload="C3: 100M synthetic S3 prefixes per GPU, key length uniform 32-96 B (avg 64 B)"),
+    "c4": dict(kind=0, avg=32, keys_per_gpu=125_000_000,
+               workload="C4: 125M synthetic prefixes per GPU (1B on 8 GPUs), avg key 32 B"),
+    "c5": dict(kind=1, avg=0, keys_per_gpu=25_000_000,
+               workload="C5: 25M prefixes per GPU (200M on 8 GPUs), key length log-uniform 10-1024 B"),
+}
+
+
+def stage_alg_bytes(stage: str, n: int, key_bytes: int, info: dict) -> int | None:
+    """Algorithmic (minimum) HBM bytes of one launch of a stage, per SURVEY.md §8(d) units."""
+    if stage == "hash_mark0":   # key bytes + offsets read once; kh + fp written once
+        return key_bytes + 8 * (n + 1) + 16 * n
+    if stage == "resolve0":     # kh read once; one u64 settle/redo record per key written
+        return 16 * n
+    if stage == "place":        # settle + fp read; fp_out + pos_out written (identity pos)
+        return 32 * n
+    if stage == "rank_scan":
+        return 16 * info.get("total_words", 0)
+    return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="rocprofv3 PMC summary (HBM bytes per launch) to attach as roofline.traffic")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 needs torchrun --nproc-per-node N (one process per GPU)")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local_rank)
+
+    import s3imph
+
+    cfg = CONFIGS[args.config]
+    plan = s3imph.ShardPlan(rank, world, cfg["keys_per_gpu"] * world)
+    blob, offs = s3imph.gen_keys(cfg["kind"], args.seed, cfg["avg"], plan.lo, plan.n_local)
+    n = plan.n_local
+    key_bytes_local = int(offs[-1])
+    dev = f"cuda:{local_rank}"
+    d_blob = torch.from_numpy(blob).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    out_cap = plan.out_per_rank if world > 1 else n
+    d_fp = torch.empty(max(out_cap, 1), dtype=torch.int64, device=dev)
+    d_po = torch.empty(max(out_cap, 1), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+
+    if world == 1:
+        ctx = s3imph.DeviceBuilder(local_rank)
+        ctx.reserve(n)
+
+        def step():
+            return ctx.build(d_blob, d_offs, n, d_fp, d_po)
+    else:
+        uid = [s3imph.dist_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx = s3imph.DistBuilder(local_rank, uid[0], rank, world)
+        ctx.reserve(n, plan.n_global)
+
+        def step():
+            return ctx.build_shard(d_blob, d_offs, n, plan.lo, d_fp, d_po, out_cap)[2]
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_profiling(True)
+    stage_sum: dict[str, float] = {}
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    info = {}
+    for _ in range(args.steps):
+        info = step()
+        for k, v in ctx.stage_times().items():
+            stage_sum[k] = stage_sum.get(k, 0.0) + v
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    ctx.set_profiling(False)
+    dt = (t1 - t0) / args.steps
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        kb = torch.tensor([key_bytes_local], dtype=torch.int64)
+        dist.all_reduce(kb)
+        key_bytes = int(kb.item())
+    else:
+        key_bytes = key_bytes_local
+    n_global = plan.n_global
+    stages = {k: v / args.steps for k, v in stage_sum.items()}
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    mph_len = info.get("mph_bin_len", 0)
+    b_alg = key_bytes + 8 * (n_global + 1) + 16 * n_global + mph_len
+    result = {
+        "metric": "MPHF build keys/s (device-resident)",
+        "value": n_global / dt,
+        "unit": "keys/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (deterministic splitmix64 prefixes, byte-sorted, distinct)",
+        "config": {"workload": cfg["workload"], "config": args.config, "keys": n_global,
+                   "key_bytes": key_bytes, "parallelism": f"shard{world}" if world > 1 else "single",
+                   "gamma": 2.0, "levels": info.get("num_levels")},
+        "key_bytes_GBps": key_bytes / dt / 1e9,
+        "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+        "pipeline_roofline": {"bound": "hbm", "alg_bytes": b_alg, "achieved": b_alg / dt / 1e9,
+                              "peak": HBM_PEAK_GBPS * world, "unit": "GB/s",
+                              "frac": b_alg / dt / 1e9 / (HBM_PEAK_GBPS * world)},
+    }
+    # Roofline of the dominant kernel (rank 0's stage times, HIP events on the build stream).
+    dom = max((k for k in stages if stage_alg_bytes(k, n, key_bytes_local, info) is not None),
+              key=lambda k: stages[k], default=None)
+    if dom is not None:
+        alg = stage_alg_bytes(dom, n, key_bytes_local, info)
+        ach = alg / (stages[dom] / 1e3) / 1e9
+        traffic = None
+        try:
+            with open(args.traffic) as f:
+                pmc = json.load(f)
+            ent = pmc.get(args.config, {}).get(dom)
+            if ent and ent.get("n_gpus", 1) == world:
+                traffic = ent["hbm_bytes_per_launch"]
+        except (OSError, ValueError):
+            pass
+        result["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS,
+                              "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
+                              "alg_bytes": alg, "avg_ms": stages[dom]}
+        result["dominant_stage"] = max(stages, key=stages.get)
+    if world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(blob, offs, args.cpu_baseline_seconds)
+    print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(blob, offs, seconds: float) -> dict:
+    """The oracle's C restatement of the reference algorithm (single thread, like the
+    reference's sequential bbhash.New), timed on this host over the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    lib = O.lib()
+    n = len(offs) - 1
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        st, _, _, _ = lib.build(blob[: int(offs[-1])], offs)
+        assert st == 0
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": n * reps / el, "unit": "keys/s", "cores": 1, "kind": "port",
+            "sample": f"full workload ({n} keys) x {reps} builds, {el:.1f} s, oracle/bbhash_oracle.c "
+                      f"(FNV + sequential BBHash levels + Find-per-key scatter), host CPU {os.cpu_count()} threads visible"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,191 @@
+/*
+ * s3imph.h — C ABI of libs3imph.so, the MI355X-native MPHF (BBHash, gamma = 2.0)
+ * builder for s3-inv-db indexes.
+ *
+ * This ABI is the drop-in boundary for the reference's MPHF stage,
+ * format.StreamingMPHFBuilder (/root/reference/pkg/format/mphf_streaming.go).
+ * The reference has no FFI layer of its own (pure Go, README.md:12); its caller
+ * holds the concrete type at pkg/extsort/indexbuild.go:39 and constructs it at :81.
+ * Each entry point below names the reference interface it replaces (file:line).
+ * INTEGRATION.md shows the cgo binding a maintainer would add.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no C++ exceptions cross this boundary.
+ *   - Every function returns an s3imph_status (0 = OK) unless stated otherwise;
+ *     when `err`/`errlen` are given, a NUL-terminated message is written there,
+ *     worded like the reference's Go errors ("build MPHF: ...").
+ *   - Every call selects its own HIP device (cgo may call from any OS thread).
+ *   - Keys are byte strings laid out as prefix_blob.bin + prefix_offsets.u64:
+ *     key i = blob[offsets[i] .. offsets[i+1]), offsets has n+1 entries.
+ *   - Outputs are byte-identical to the reference's mph.bin / mph_fp.u64 /
+ *     mph_pos.u64 under the restated relab/bbhash spec ("parity").
+ */
+#ifndef S3IMPH_H
+#define S3IMPH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define S3IMPH_ABI_VERSION 1
+
+typedef enum s3imph_status {
+    S3IMPH_OK = 0,
+    S3IMPH_ERR_INVALID = 1,          /* bad argument / misuse */
+    S3IMPH_ERR_DUP_KEY_HASH = 2,     /* duplicate FNV-1a key hashes: bbhash.New cannot place them (mphf_streaming.go:141-144) */
+    S3IMPH_ERR_TOO_MANY_LEVELS = 3,  /* level budget exhausted (relab/bbhash maxLevel analogue) */
+    S3IMPH_ERR_KEY_HASH_ZERO = 4,    /* a key hashes to 0: "MPHF Key(%d) returned 0" (mphf_streaming.go:248-252) */
+    S3IMPH_ERR_HIP = 5,
+    S3IMPH_ERR_RCCL = 6,
+    S3IMPH_ERR_IO = 7,
+    S3IMPH_ERR_NOMEM = 8,
+    S3IMPH_ERR_FORMAT = 9,
+    S3IMPH_ERR_INTERNAL = 10,
+    S3IMPH_ERR_STATE = 11            /* e.g. Add after Build, use after Close */
+} s3imph_status;
+
+int s3imph_abi_version(void);
+const char *s3imph_status_string(int status);
+
+/* ------------------------------------------------------------------------
+ * 1. StreamingMPHFBuilder mirror (pkg/format/mphf_streaming.go:29-232).
+ *    Same method set: New(tempDir) / Add(prefix, pos) / Count() / Build(outDir) / Close().
+ * ------------------------------------------------------------------------ */
+typedef struct s3imph_builder s3imph_builder;
+
+/* NewStreamingMPHFBuilder(tempDir) — mphf_streaming.go:48-64.
+ * temp_dir must name an existing directory (or be NULL/""), as os.CreateTemp requires.
+ * Keys are staged in host memory instead of a temp file. */
+int s3imph_builder_new(const char *temp_dir, int device, s3imph_builder **out, char *err, size_t errlen);
+
+/* Add(prefix, pos) — mphf_streaming.go:68-97. Copies the bytes. */
+int s3imph_builder_add(s3imph_builder *b, const uint8_t *prefix, uint64_t len, uint64_t pos,
+                       char *err, size_t errlen);
+
+/* Batched Add (n keys in blob/offsets layout; pos may be NULL => pos_i = Count()+i).
+ * Same effect as n calls of Add; exists to amortise the per-call FFI cost. */
+int s3imph_builder_add_batch(s3imph_builder *b, const uint8_t *blob, const uint64_t *offsets,
+                             const uint64_t *pos, uint64_t n, char *err, size_t errlen);
+
+/* Count() — mphf_streaming.go:100-102. */
+uint64_t s3imph_builder_count(const s3imph_builder *b);
+
+/* Build(outDir) — mphf_streaming.go:122-232: builds on the GPU and writes mph.bin,
+ * mph_fp.u64, mph_pos.u64, prefix_blob.bin, prefix_offsets.u64 into out_dir.
+ * Count()==0 writes the empty set (writeEmpty, :506-541). On failure mph.bin is removed (:159-168). */
+int s3imph_builder_build(s3imph_builder *b, const char *out_dir, char *err, size_t errlen);
+
+/* Close() — mphf_streaming.go:105-114. Frees everything; b is invalid afterwards. */
+int s3imph_builder_close(s3imph_builder *b);
+
+/* ------------------------------------------------------------------------
+ * 2. One-shot host-memory build: replaces bbhash.New + MarshalBinary +
+ *    computeHashPositionsReverseMap + the scatter loop (mphf_streaming.go:141-204).
+ * ------------------------------------------------------------------------ */
+
+/* fp_out/pos_out: caller-allocated n entries each. *mph_bin is allocated by the
+ * library (free with s3imph_free); n == 0 gives *mph_bin = NULL, *mph_len = 0.
+ * pos may be NULL => pos_i = i (the production caller, indexbuild.go:160-175). */
+int s3imph_build_host(int device, const uint8_t *blob, const uint64_t *offsets, const uint64_t *pos,
+                      uint64_t n, uint64_t *fp_out, uint64_t *pos_out, uint8_t **mph_bin,
+                      uint64_t *mph_len, char *err, size_t errlen);
+
+void s3imph_free(void *p);
+
+/* Emit the 5 files of the MPHF stage with the reference's framing:
+ * mph.bin raw (mphf_streaming.go:152-169), mph_fp.u64 / mph_pos.u64 as S3ID
+ * u64 arrays (writeArraysParallel :546-596; ArrayWriter writer.go:19-46,79-96,113-140;
+ * header format.go:6-32), prefix_blob.bin + prefix_offsets.u64 with the N+1 sentinel
+ * (BlobWriter writer.go:148-237). n == 0 reproduces writeEmpty (:506-541). */
+int s3imph_write_index_files(const char *out_dir, const uint8_t *mph_bin, uint64_t mph_len,
+                             const uint64_t *fp, const uint64_t *pos, uint64_t n,
+                             const uint8_t *blob, const uint64_t *offsets, char *err, size_t errlen);
+
+/* ------------------------------------------------------------------------
+ * 3. Device-resident build (inputs already in HBM; what bench.py times).
+ * ------------------------------------------------------------------------ */
+typedef struct s3imph_ctx s3imph_ctx;
+
+typedef struct s3imph_build_info {
+    int32_t status;            /* s3imph_status of the build */
+    uint32_t num_levels;       /* BBHash levels */
+    uint64_t total_words;      /* u64 words over all level bit vectors */
+    uint64_t mph_bin_len;      /* bytes of the marshalled mph.bin */
+    uint64_t big_levels;       /* levels run as full-grid kernels (rest: single-workgroup tail) */
+    uint64_t n_keys;           /* keys in the whole build (all ranks) */
+} s3imph_build_info;
+
+int s3imph_ctx_create(int device, s3imph_ctx **out, char *err, size_t errlen);
+int s3imph_ctx_destroy(s3imph_ctx *ctx);
+
+/* Pre-size the workspace for up to max_keys keys on this GPU (optional: builds
+ * grow it on demand, but a reserved workspace keeps allocation out of timed runs). */
+int s3imph_ctx_reserve(s3imph_ctx *ctx, uint64_t max_keys, uint64_t max_global_keys);
+
+/* Enqueue the whole build on `stream` (a hipStream_t; NULL = the ctx's own stream)
+ * and wait for it.  d_blob must be readable up to offsets[n] rounded up to 8 bytes.
+ * d_pos may be NULL (identity).  d_fp_out / d_pos_out: n entries each.
+ * The level bit vectors stay on the device until s3imph_ctx_mph_bin(). */
+int s3imph_build_device(s3imph_ctx *ctx, const uint8_t *d_blob, const uint64_t *d_offsets,
+                        const uint64_t *d_pos, uint64_t n, uint64_t *d_fp_out, uint64_t *d_pos_out,
+                        void *stream, s3imph_build_info *info);
+
+/* Marshal the last build's level bit vectors into mph.bin bytes (D2H + framing). */
+int s3imph_ctx_mph_bin(s3imph_ctx *ctx, uint8_t *out, uint64_t cap, uint64_t *len);
+
+/* Per-stage device times of the last build (ms), recorded with HIP events on the
+ * build stream when profiling is on.  names: comma-separated stage names. */
+int s3imph_ctx_set_profiling(s3imph_ctx *ctx, int on);
+int s3imph_ctx_stage_times(s3imph_ctx *ctx, float *ms, int cap, int *count, char *names, size_t names_len);
+
+/* ------------------------------------------------------------------------
+ * 4. Multi-GPU build: one process per GPU, RCCL over xGMI.
+ *    Keys are sharded in contiguous index ranges; each BBHash level's collision
+ *    counts are summed across ranks (RCCL reduce-scatter + all-gather); the
+ *    output (p, fp, pos) triples are exchanged to the rank owning p's range.
+ * ------------------------------------------------------------------------ */
+
+/* Rank 0 creates the 128-byte RCCL unique id; the host broadcasts it. */
+int s3imph_dist_unique_id(uint8_t id_out[128]);
+
+int s3imph_ctx_create_dist(int device, const uint8_t id[128], int rank, int nranks,
+                           s3imph_ctx **out, char *err, size_t errlen);
+
+/* This rank holds keys [key_base, key_base + n_local) of the global set (the
+ * shard's blob/offsets/pos, offsets relative to d_blob).  On return this rank owns
+ * output positions [*out_lo, *out_lo + *out_n) of mph_fp / mph_pos, written to
+ * d_fp_out / d_pos_out (capacity out_cap entries; ceil(N/nranks) suffices).
+ * mph.bin is identical on every rank. */
+int s3imph_build_device_dist(s3imph_ctx *ctx, const uint8_t *d_blob, const uint64_t *d_offsets,
+                             const uint64_t *d_pos, uint64_t n_local, uint64_t key_base,
+                             uint64_t *d_fp_out, uint64_t *d_pos_out, uint64_t out_cap,
+                             uint64_t *out_lo, uint64_t *out_n, void *stream, s3imph_build_info *info);
+
+/* ------------------------------------------------------------------------
+ * 5. Batched lookup on the device: MPHF.Lookup (pkg/format/mphf.go:275-302)
+ *    over the last build's levels, for n query keys; result[i] = pos or
+ *    UINT64_MAX when not found.  Self-verifies a build (VerifyMPHF, :372-393).
+ * ------------------------------------------------------------------------ */
+int s3imph_lookup_device(s3imph_ctx *ctx, const uint8_t *d_blob, const uint64_t *d_offsets, uint64_t n,
+                         const uint64_t *d_fp, const uint64_t *d_pos, uint64_t count,
+                         uint64_t *d_result, void *stream);
+
+/* ------------------------------------------------------------------------
+ * 6. Deterministic synthetic prefix sets (bench/test support, not on the path).
+ *    kind: 0 = s3-like, lengths uniform in [avg/2, 3avg/2];
+ *          1 = lengths log-uniform in [8, 1024] (C5, min 8 keeps keys distinct).
+ *    Keys are distinct, byte-sorted, key 0 = "" when lo == 0.  Generate keys
+ *    [lo, lo+n) of the global sequence: call once with blob == NULL to get the
+ *    byte count, then again to fill.  offsets are relative to the shard start.
+ * ------------------------------------------------------------------------ */
+int s3imph_gen_keys(int kind, uint64_t seed, uint32_t avg_len, uint64_t lo, uint64_t n,
+                    uint8_t *blob, uint64_t *offsets, uint64_t *total_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* S3IMPH_H */

@@ -1,0 +1,311 @@
+/*
+ * bbhash_oracle.c — CPU restatement of the reference's MPHF-build path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
+ * product path in s3-inv-db_amd/csrc.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  The product never links it
+ * and never falls back to it.
+ *
+ * What it restates (reference = /root/reference, eunmann/s3-inv-db @2025-12-26):
+ *   - FNV-1a 64 key hash   : pkg/format/mphf.go:347-353 (hashBytes), Go hash/fnv New64a;
+ *                            the reference restates it at mphf_fingerprints_bench_test.go:480-491.
+ *   - FNV-1 64 fingerprint : pkg/format/mphf.go:363-369 (computeFingerprintBytes), Go hash/fnv New64;
+ *                            restated at mphf_fingerprints_bench_test.go:407-418.
+ *   - bbhash.New(keys, Gamma(2.0), WithReverseMap()) : pkg/format/mphf_streaming.go:141.
+ *     The algorithm lives in github.com/relab/bbhash v0.0.0-20250331135148-7358f69256fb
+ *     (go.mod:10, go.sum:69-70), which is NOT vendored and not in this container.
+ *     It is restated from its public description (toggles T1-T8
+ *     in bbhash_oracle_spec.h).  PARITY OF mph.bin BYTES IS "vs restated spec"
+ *     (unpinned against upstream bytes); everything the reference's own tests check
+ *     (round-trip Lookup, no false positives, FNV values) is pinned.
+ *   - MarshalBinary framing (mph.bin) : mphf_streaming.go:152-169 (T4).
+ *   - computeHashPositionsReverseMap + scatter : mphf_streaming.go:176-204,237-261.
+ *   - MPHF.Lookup : pkg/format/mphf.go:275-302.
+ *
+ * Build: oracle/Makefile -> oracle/_build/liboracle.so (plain gcc, no GPU).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "bbhash_oracle_spec.h"
+
+/* ---------------------------------------------------------------- FNV ---- */
+
+/* mphf.go:349-353 -> hash/fnv New64a: h ^= b; h *= prime */
+uint64_t orc_fnv1a64(const uint8_t *p, uint64_t n) {
+    uint64_t h = ORC_FNV_OFFSET64;
+    for (uint64_t i = 0; i < n; i++) {
+        h ^= (uint64_t)p[i];
+        h *= ORC_FNV_PRIME64;
+    }
+    return h;
+}
+
+/* mphf.go:365-369 -> hash/fnv New64: h *= prime; h ^= b */
+uint64_t orc_fnv1_64(const uint8_t *p, uint64_t n) {
+    uint64_t h = ORC_FNV_OFFSET64;
+    for (uint64_t i = 0; i < n; i++) {
+        h *= ORC_FNV_PRIME64;
+        h ^= (uint64_t)p[i];
+    }
+    return h;
+}
+
+/* StreamingMPHFBuilder.Add (mphf_streaming.go:68-97): per key, hashes[] and fingerprints[]. */
+void orc_hash_keys(const uint8_t *blob, const uint64_t *offsets, uint64_t n,
+                   uint64_t *kh, uint64_t *fp) {
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t *p = blob + offsets[i];
+        uint64_t len = offsets[i + 1] - offsets[i];
+        if (kh) kh[i] = orc_fnv1a64(p, len);
+        if (fp) fp[i] = orc_fnv1_64(p, len);
+    }
+}
+
+/* ------------------------------------------------------------ bbhash ---- */
+
+/* Appendix A.1 (T1): fasthash-style mix, level hash, key hash. */
+static inline uint64_t orc_mix(uint64_t h) {
+    h ^= h >> 23;
+    h *= ORC_MIX_MUL;
+    h ^= h >> 47;
+    return h;
+}
+uint64_t orc_level_hash(uint64_t level) { return orc_mix(level) * ORC_HASH_M; }
+uint64_t orc_key_hash(uint64_t lvl_hash, uint64_t key) {
+    uint64_t h = lvl_hash;
+    h ^= orc_mix(key);
+    h *= ORC_HASH_M;
+    return orc_mix(h);
+}
+
+/* A.2 (T3): words = ceil(gamma*n/64); with gamma = 2.0 exactly ceil(n/32). */
+uint64_t orc_level_words(uint64_t n) {
+    uint64_t bits = ORC_GAMMA_NUM * n / ORC_GAMMA_DEN; /* 2n: exact */
+    uint64_t w = (bits + 63) / 64;
+    return w < ORC_MIN_WORDS ? ORC_MIN_WORDS : w;
+}
+
+typedef struct orc_mphf {
+    uint32_t nlevels;
+    uint64_t *words;      /* words per level */
+    uint64_t *woff;       /* first word of each level in bits[] */
+    uint64_t *bits;       /* concatenated level bit vectors (A_L after peel) */
+    uint64_t total_words;
+    uint64_t *rank_base;  /* per word: # set bits in all earlier words (levels concatenated) */
+    uint64_t nkeys;
+} orc_mphf;
+
+static void orc_compute_ranks(orc_mphf *m) {
+    m->rank_base = (uint64_t *)malloc((m->total_words + 1) * sizeof(uint64_t));
+    uint64_t acc = 0;
+    for (uint64_t w = 0; w < m->total_words; w++) {
+        m->rank_base[w] = acc;
+        acc += (uint64_t)__builtin_popcountll(m->bits[w]);
+    }
+    m->rank_base[m->total_words] = acc;
+    m->nkeys = acc;
+}
+
+void orc_free(orc_mphf *m) {
+    if (!m) return;
+    free(m->words);
+    free(m->woff);
+    free(m->bits);
+    free(m->rank_base);
+    free(m);
+}
+
+/*
+ * bbhash.New(keys, Gamma(2.0)) restated sequentially (A.2):
+ *   level L over active set S_L: i = keyHash(levelHash(L), k) % (64*words_L)
+ *   pass 1: if C[i] skip; else if A[i] { C[i]=1 } else A[i]=1
+ *   pass 2: if C[i] { A[i]=0; k -> S_{L+1} }
+ * Level bit vectors depend only on the SET S_L, never on key order.
+ * Returns ORC_OK, ORC_ERR_TOO_MANY_LEVELS (what relab returns for unresolvable
+ * keys, i.e. duplicates) or ORC_ERR_KEY_ZERO (mphf_streaming.go:248-252).
+ */
+int orc_bbhash_new(const uint64_t *keys, uint64_t n, orc_mphf **out) {
+    *out = NULL;
+    if (n == 0) return ORC_OK;
+    orc_mphf *m = (orc_mphf *)calloc(1, sizeof(orc_mphf));
+    uint32_t cap_levels = ORC_MAX_LEVELS + 1;
+    m->words = (uint64_t *)calloc(cap_levels, sizeof(uint64_t));
+    m->woff = (uint64_t *)calloc(cap_levels, sizeof(uint64_t));
+    uint64_t cap_words = orc_level_words(n) * 4 + 64;
+    m->bits = (uint64_t *)calloc(cap_words, sizeof(uint64_t));
+
+    uint64_t *cur = (uint64_t *)malloc(n * sizeof(uint64_t));
+    uint64_t *nxt = (uint64_t *)malloc(n * sizeof(uint64_t));
+    memcpy(cur, keys, n * sizeof(uint64_t));
+    uint64_t ncur = n;
+    uint64_t *C = (uint64_t *)calloc(orc_level_words(n), sizeof(uint64_t));
+    uint64_t woff = 0;
+    int status = ORC_OK;
+
+    for (uint32_t lvl = 0; ncur > 0; lvl++) {
+        if (lvl >= ORC_MAX_LEVELS) { status = ORC_ERR_TOO_MANY_LEVELS; break; }
+        uint64_t w = orc_level_words(ncur);
+        uint64_t size = w * 64;
+        if (woff + w > cap_words) {
+            uint64_t nc = (woff + w) * 2;
+            m->bits = (uint64_t *)realloc(m->bits, nc * sizeof(uint64_t));
+            memset(m->bits + cap_words, 0, (nc - cap_words) * sizeof(uint64_t));
+            cap_words = nc;
+        }
+        uint64_t *A = m->bits + woff;
+        memset(C, 0, w * sizeof(uint64_t));
+        uint64_t lh = orc_level_hash(lvl);
+        for (uint64_t j = 0; j < ncur; j++) {
+            uint64_t i = orc_key_hash(lh, cur[j]) % size;
+            uint64_t bit = 1ULL << (i & 63);
+            if (C[i >> 6] & bit) continue;
+            if (A[i >> 6] & bit) { C[i >> 6] |= bit; continue; }
+            A[i >> 6] |= bit;
+        }
+        uint64_t nn = 0;
+        for (uint64_t j = 0; j < ncur; j++) {
+            uint64_t i = orc_key_hash(lh, cur[j]) % size;
+            uint64_t bit = 1ULL << (i & 63);
+            if (C[i >> 6] & bit) {
+                A[i >> 6] &= ~bit;
+                nxt[nn++] = cur[j];
+            }
+        }
+        m->words[lvl] = w;
+        m->woff[lvl] = woff;
+        m->nlevels = lvl + 1;
+        woff += w;
+        uint64_t *t = cur; cur = nxt; nxt = t;
+        ncur = nn;
+    }
+    free(cur);
+    free(nxt);
+    free(C);
+    m->total_words = woff;
+    if (status != ORC_OK) { orc_free(m); return status; }
+    orc_compute_ranks(m);
+    *out = m;
+    return ORC_OK;
+}
+
+/* A.3: Find(k) = 1 + #set bits before (level L, bit i) for the first level whose bit is set; 0 if none. */
+uint64_t orc_find(const orc_mphf *m, uint64_t key) {
+    if (!m) return 0;
+    for (uint32_t lvl = 0; lvl < m->nlevels; lvl++) {
+        uint64_t size = m->words[lvl] * 64;
+        uint64_t i = orc_key_hash(orc_level_hash(lvl), key) % size;
+        uint64_t gw = m->woff[lvl] + (i >> 6);
+        uint64_t word = m->bits[gw];
+        uint64_t bit = 1ULL << (i & 63);
+        if (word & bit)
+            return 1 + m->rank_base[gw] + (uint64_t)__builtin_popcountll(word & (bit - 1));
+    }
+    return 0;
+}
+
+uint32_t orc_num_levels(const orc_mphf *m) { return m ? m->nlevels : 0; }
+uint64_t orc_level_word_count(const orc_mphf *m, uint32_t lvl) { return m->words[lvl]; }
+const uint64_t *orc_level_bits(const orc_mphf *m, uint32_t lvl) { return m->bits + m->woff[lvl]; }
+
+/* A.5 (T4): [u64 numPartitions=1][u64 numLevels]{[u64 numWords][words...]}*, all LE. */
+static void put_u64(uint8_t *p, uint64_t v) {
+    for (int b = 0; b < 8; b++) p[b] = (uint8_t)(v >> (8 * b));
+}
+static uint64_t get_u64(const uint8_t *p) {
+    uint64_t v = 0;
+    for (int b = 0; b < 8; b++) v |= (uint64_t)p[b] << (8 * b);
+    return v;
+}
+uint64_t orc_marshal_size(const orc_mphf *m) {
+    if (!m) return 0;
+    return 8 * ORC_MARSHAL_PARTITION_HDR + 8 + 8ULL * m->nlevels + 8ULL * m->total_words;
+}
+void orc_marshal(const orc_mphf *m, uint8_t *out) {
+    uint8_t *p = out;
+    if (ORC_MARSHAL_PARTITION_HDR) { put_u64(p, 1); p += 8; }
+    put_u64(p, m->nlevels); p += 8;
+    for (uint32_t l = 0; l < m->nlevels; l++) {
+        put_u64(p, m->words[l]); p += 8;
+        for (uint64_t w = 0; w < m->words[l]; w++) { put_u64(p, m->bits[m->woff[l] + w]); p += 8; }
+    }
+}
+int orc_unmarshal(const uint8_t *data, uint64_t len, orc_mphf **out) {
+    *out = NULL;
+    const uint8_t *p = data, *end = data + len;
+    if (ORC_MARSHAL_PARTITION_HDR) {
+        if (end - p < 8) return ORC_ERR_FORMAT;
+        if (get_u64(p) != 1) return ORC_ERR_FORMAT;
+        p += 8;
+    }
+    if (end - p < 8) return ORC_ERR_FORMAT;
+    uint64_t nl = get_u64(p); p += 8;
+    if (nl > ORC_MAX_LEVELS) return ORC_ERR_FORMAT;
+    orc_mphf *m = (orc_mphf *)calloc(1, sizeof(orc_mphf));
+    m->nlevels = (uint32_t)nl;
+    m->words = (uint64_t *)calloc(nl + 1, sizeof(uint64_t));
+    m->woff = (uint64_t *)calloc(nl + 1, sizeof(uint64_t));
+    uint64_t total = 0;
+    const uint8_t *q = p;
+    for (uint64_t l = 0; l < nl; l++) {
+        if (end - q < 8) { orc_free(m); return ORC_ERR_FORMAT; }
+        uint64_t w = get_u64(q); q += 8;
+        if ((uint64_t)(end - q) / 8 < w) { orc_free(m); return ORC_ERR_FORMAT; }
+        m->words[l] = w; m->woff[l] = total; total += w; q += 8 * w;
+    }
+    if (q != end) { orc_free(m); return ORC_ERR_FORMAT; }
+    m->bits = (uint64_t *)malloc((total + 1) * sizeof(uint64_t));
+    for (uint64_t l = 0; l < nl; l++) {
+        p += 8;
+        for (uint64_t w = 0; w < m->words[l]; w++) { m->bits[m->woff[l] + w] = get_u64(p); p += 8; }
+    }
+    m->total_words = total;
+    orc_compute_ranks(m);
+    *out = m;
+    return ORC_OK;
+}
+
+/*
+ * StreamingMPHFBuilder.Build minus the file I/O (mphf_streaming.go:122-213):
+ *   bbhash.New -> positions p(i) = Find(k_i) - 1 (what the reverse map inverts to,
+ *   :237-261) -> fp_out[p] = FNV1(key_i), pos_out[p] = pos_i (:197-204).
+ * pos == NULL means pos_i = i (the production caller, indexbuild.go:160-175).
+ */
+int orc_build(const uint8_t *blob, const uint64_t *offsets, const uint64_t *pos, uint64_t n,
+              uint64_t *fp_out, uint64_t *pos_out, orc_mphf **mph_out) {
+    *mph_out = NULL;
+    if (n == 0) return ORC_OK;
+    uint64_t *kh = (uint64_t *)malloc(n * sizeof(uint64_t));
+    uint64_t *fp = (uint64_t *)malloc(n * sizeof(uint64_t));
+    orc_hash_keys(blob, offsets, n, kh, fp);
+    for (uint64_t i = 0; i < n; i++) {
+        if (kh[i] == 0) { free(kh); free(fp); return ORC_ERR_KEY_ZERO; }
+    }
+    orc_mphf *m = NULL;
+    int st = orc_bbhash_new(kh, n, &m);
+    if (st != ORC_OK) { free(kh); free(fp); return st; }
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t v = orc_find(m, kh[i]);
+        if (v == 0 || v > n) { free(kh); free(fp); orc_free(m); return ORC_ERR_INTERNAL; }
+        fp_out[v - 1] = fp[i];
+        pos_out[v - 1] = pos ? pos[i] : i;
+    }
+    free(kh);
+    free(fp);
+    *mph_out = m;
+    return ORC_OK;
+}
+
+/* MPHF.Lookup (mphf.go:275-302). Returns 1 and *pos_out on a hit, 0 otherwise. */
+int orc_lookup(const orc_mphf *m, const uint64_t *fp_arr, const uint64_t *pos_arr, uint64_t count,
+               const uint8_t *key, uint64_t len, uint64_t *pos_out) {
+    if (count == 0 || !m) return 0;
+    uint64_t v = orc_find(m, orc_fnv1a64(key, len));
+    if (v == 0) return 0;
+    uint64_t hp = v - 1;
+    if (hp >= count) return 0;
+    if (fp_arr[hp] != orc_fnv1_64(key, len)) return 0;
+    *pos_out = pos_arr[hp];
+    return 1;
+}

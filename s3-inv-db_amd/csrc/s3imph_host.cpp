@@ -1,0 +1,388 @@
+// s3imph_host.cpp — host side of the boundary: the StreamingMPHFBuilder mirror,
+// the index-file writers (S3ID framing) and the synthetic prefix generator.
+//
+// Reference: pkg/format/mphf_streaming.go (builder, :29-232), pkg/format/writer.go
+// (ArrayWriter :11-145, BlobWriter :148-246), pkg/format/format.go (header :6-45).
+#include <errno.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "s3imph.h"
+#include "s3imph_internal.h"
+
+namespace s3imph {
+
+int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
+                    uint64_t n, uint64_t* fp_out, uint64_t* pos_out, std::vector<uint8_t>* mph,
+                    std::string* msg);
+
+void set_err(char* err, size_t errlen, const std::string& msg) {
+  if (!err || errlen == 0) return;
+  size_t k = std::min(errlen - 1, msg.size());
+  std::memcpy(err, msg.data(), k);
+  err[k] = '\0';
+}
+
+namespace {
+
+void put_le64(uint8_t* p, uint64_t v) {
+  for (int b = 0; b < 8; ++b) p[b] = (uint8_t)(v >> (8 * b));
+}
+void put_le32(uint8_t* p, uint32_t v) {
+  for (int b = 0; b < 4; ++b) p[b] = (uint8_t)(v >> (8 * b));
+}
+
+// EncodeHeader (format.go:25-32): magic, version, count, width — little endian, 20 bytes.
+void s3id_header(uint8_t out[kS3idHeaderSize], uint64_t count, uint32_t width) {
+  put_le32(out, kS3idMagic);
+  put_le32(out + 4, kS3idVersion);
+  put_le64(out + 8, count);
+  put_le32(out + 16, width);
+}
+
+struct File {
+  FILE* f = nullptr;
+  ~File() {
+    if (f) std::fclose(f);
+  }
+};
+
+bool write_all(FILE* f, const void* p, size_t n) { return n == 0 || std::fwrite(p, 1, n, f) == n; }
+
+// ArrayWriter of width 8 holding `n` values (+ an optional trailing sentinel), each
+// value = src[i] - bias.  Writes in 1 MiB chunks.
+bool write_u64_array(const std::string& path, const uint64_t* src, uint64_t n, uint64_t bias,
+                     std::string* msg) {
+  File fh;
+  fh.f = std::fopen(path.c_str(), "wb");
+  if (!fh.f) {
+    *msg = "create array file: open " + path + ": " + std::strerror(errno);
+    return false;
+  }
+  uint8_t hdr[kS3idHeaderSize];
+  s3id_header(hdr, n, 8);
+  if (!write_all(fh.f, hdr, sizeof hdr)) {
+    *msg = "write header: " + path;
+    return false;
+  }
+  std::vector<uint8_t> buf(1 << 20);
+  uint64_t i = 0;
+  while (i < n) {
+    const uint64_t k = std::min<uint64_t>(n - i, buf.size() / 8);
+    for (uint64_t t = 0; t < k; ++t) put_le64(buf.data() + 8 * t, src[i + t] - bias);
+    if (!write_all(fh.f, buf.data(), 8 * k)) {
+      *msg = "write u64 batch: " + path;
+      return false;
+    }
+    i += k;
+  }
+  if (std::fclose(fh.f) != 0) {
+    fh.f = nullptr;
+    *msg = "close file: " + path;
+    return false;
+  }
+  fh.f = nullptr;
+  return true;
+}
+
+bool write_raw(const std::string& path, const uint8_t* p, uint64_t n, std::string* msg) {
+  File fh;
+  fh.f = std::fopen(path.c_str(), "wb");
+  if (!fh.f) {
+    *msg = "create " + path + ": " + std::strerror(errno);
+    return false;
+  }
+  if (!write_all(fh.f, p, n)) {
+    *msg = "write " + path;
+    return false;
+  }
+  if (std::fclose(fh.f) != 0) {
+    fh.f = nullptr;
+    *msg = "close " + path;
+    return false;
+  }
+  fh.f = nullptr;
+  return true;
+}
+
+bool is_dir(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+}  // namespace
+
+int write_index_files(const std::string& dir, const uint8_t* mph_bin, uint64_t mph_len, const uint64_t* fp,
+                      const uint64_t* pos, uint64_t n, const uint8_t* blob, const uint64_t* offsets,
+                      std::string* msg) {
+  const std::string mph_path = dir + "/mph.bin";
+  // mph.bin (mphf_streaming.go:152-169; 0 bytes for the empty set, :509).  On a
+  // marshal/write failure the reference removes the partial file (:159-168).
+  if (!write_raw(mph_path, mph_bin, mph_len, msg)) {
+    ::unlink(mph_path.c_str());
+    *msg = "write MPHF: " + *msg;
+    return S3IMPH_ERR_IO;
+  }
+  // mph_fp.u64 / mph_pos.u64 (writeArraysParallel :546-596).
+  if (!write_u64_array(dir + "/mph_fp.u64", fp, n, 0, msg)) {
+    *msg = "write fingerprints: " + *msg;
+    return S3IMPH_ERR_IO;
+  }
+  if (!write_u64_array(dir + "/mph_pos.u64", pos, n, 0, msg)) {
+    *msg = "write positions: " + *msg;
+    return S3IMPH_ERR_IO;
+  }
+  // prefix_blob.bin + prefix_offsets.u64 (writePrefixBlobPreorder :453-504, BlobWriter
+  // writer.go:148-237): N offsets plus the sentinel, counted N+1 in the header.
+  static const uint64_t kZero = 0;
+  const uint64_t base = (n && offsets) ? offsets[0] : 0;
+  const uint64_t nbytes = (n && offsets) ? offsets[n] - base : 0;
+  if (!write_raw(dir + "/prefix_blob.bin", n ? blob + base : nullptr, nbytes, msg)) {
+    *msg = "write prefix blob: " + *msg;
+    return S3IMPH_ERR_IO;
+  }
+  if (!write_u64_array(dir + "/prefix_offsets.u64", n ? offsets : &kZero, n + 1, base, msg)) {
+    *msg = "write prefix blob: " + *msg;
+    return S3IMPH_ERR_IO;
+  }
+  return S3IMPH_OK;
+}
+
+}  // namespace s3imph
+
+using namespace s3imph;
+
+// --------------------------------------------------------------- builder mirror ----
+struct s3imph_builder {
+  int device = 0;
+  std::string temp_dir;
+  std::vector<uint8_t> blob;
+  std::vector<uint64_t> offsets{0};
+  std::vector<uint64_t> pos;
+  uint64_t count = 0;
+  bool built = false;
+};
+
+extern "C" {
+
+int s3imph_builder_new(const char* temp_dir, int device, s3imph_builder** out, char* err, size_t errlen) {
+  if (!out) return S3IMPH_ERR_INVALID;
+  *out = nullptr;
+  std::string td = temp_dir ? temp_dir : "";
+  if (!td.empty() && !is_dir(td)) {
+    set_err(err, errlen, "create temp file: open " + td + ": no such directory");
+    return S3IMPH_ERR_IO;
+  }
+  try {
+    s3imph_builder* b = new s3imph_builder();
+    b->device = device;
+    b->temp_dir = td;
+    *out = b;
+    return S3IMPH_OK;
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "out of host memory");
+    return S3IMPH_ERR_NOMEM;
+  }
+}
+
+int s3imph_builder_add(s3imph_builder* b, const uint8_t* prefix, uint64_t len, uint64_t pos, char* err,
+                       size_t errlen) {
+  if (!b || (len && !prefix)) return S3IMPH_ERR_INVALID;
+  if (b->built) {
+    set_err(err, errlen, "add to MPHF builder: builder already built");
+    return S3IMPH_ERR_STATE;
+  }
+  try {
+    b->blob.insert(b->blob.end(), prefix, prefix + len);
+    b->offsets.push_back(b->blob.size());
+    b->pos.push_back(pos);
+    ++b->count;
+    return S3IMPH_OK;
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "write prefix: out of host memory");
+    return S3IMPH_ERR_NOMEM;
+  }
+}
+
+int s3imph_builder_add_batch(s3imph_builder* b, const uint8_t* blob, const uint64_t* offsets,
+                             const uint64_t* pos, uint64_t n, char* err, size_t errlen) {
+  if (!b || (n && (!blob || !offsets))) return S3IMPH_ERR_INVALID;
+  if (b->built) {
+    set_err(err, errlen, "add to MPHF builder: builder already built");
+    return S3IMPH_ERR_STATE;
+  }
+  try {
+    const uint64_t base = offsets[0], nbytes = offsets[n] - base, shift = b->blob.size();
+    b->blob.insert(b->blob.end(), blob + base, blob + base + nbytes);
+    b->offsets.reserve(b->offsets.size() + n);
+    b->pos.reserve(b->pos.size() + n);
+    for (uint64_t i = 0; i < n; ++i) {
+      b->offsets.push_back(offsets[i + 1] - base + shift);
+      b->pos.push_back(pos ? pos[i] : b->count + i);
+    }
+    b->count += n;
+    return S3IMPH_OK;
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "write prefix: out of host memory");
+    return S3IMPH_ERR_NOMEM;
+  }
+}
+
+uint64_t s3imph_builder_count(const s3imph_builder* b) { return b ? b->count : 0; }
+
+int s3imph_builder_build(s3imph_builder* b, const char* out_dir, char* err, size_t errlen) {
+  if (!b || !out_dir) return S3IMPH_ERR_INVALID;
+  if (b->built) {
+    set_err(err, errlen, "build MPHF: builder already built");
+    return S3IMPH_ERR_STATE;
+  }
+  const std::string dir = out_dir;
+  if (!is_dir(dir)) {
+    set_err(err, errlen, "create mph file: open " + dir + "/mph.bin: no such directory");
+    return S3IMPH_ERR_IO;
+  }
+  std::string msg;
+  try {
+    const uint64_t n = b->count;
+    std::vector<uint64_t> fp(n), pos_out(n);
+    std::vector<uint8_t> mph;
+    if (n) {
+      int rc = build_from_host(b->device, b->blob.data(), b->offsets.data(), b->pos.data(), n, fp.data(),
+                               pos_out.data(), &mph, &msg);
+      if (rc != S3IMPH_OK) {
+        set_err(err, errlen, msg);
+        return rc;
+      }
+    }
+    int rc = write_index_files(dir, mph.data(), mph.size(), fp.data(), pos_out.data(), n, b->blob.data(),
+                               b->offsets.data(), &msg);
+    if (rc != S3IMPH_OK) {
+      set_err(err, errlen, msg);
+      return rc;
+    }
+    b->built = true;
+    return S3IMPH_OK;
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "build MPHF: out of host memory");
+    return S3IMPH_ERR_NOMEM;
+  }
+}
+
+int s3imph_builder_close(s3imph_builder* b) {
+  delete b;
+  return S3IMPH_OK;
+}
+
+int s3imph_write_index_files(const char* out_dir, const uint8_t* mph_bin, uint64_t mph_len, const uint64_t* fp,
+                             const uint64_t* pos, uint64_t n, const uint8_t* blob, const uint64_t* offsets,
+                             char* err, size_t errlen) {
+  if (!out_dir || (n && (!fp || !pos || !offsets || !blob)) || (mph_len && !mph_bin)) return S3IMPH_ERR_INVALID;
+  std::string msg;
+  try {
+    int rc = write_index_files(out_dir, mph_bin, mph_len, fp, pos, n, blob, offsets, &msg);
+    if (rc != S3IMPH_OK) set_err(err, errlen, msg);
+    return rc;
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "out of host memory");
+    return S3IMPH_ERR_NOMEM;
+  }
+}
+
+// ------------------------------------------------------------ synthetic prefixes ----
+// Key g of the global sequence: g == 0 -> "" (the root prefix, aggregator.go:48);
+// g >= 1 -> 9 lowercase hex digits of g-1, '/', then pseudo-random [a-z0-5] segments
+// separated by '/' every 12 bytes, ending in '/'.  The fixed-width hex head makes the
+// sequence byte-sorted and distinct by construction.
+static inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+
+static uint32_t gen_len(int kind, uint64_t seed, uint32_t avg, uint64_t g) {
+  if (g == 0) return 0;
+  const uint64_t r = splitmix64(seed * 0x9e3779b97f4a7c15ull ^ (g * 0xd1b54a32d192ed03ull));
+  if (kind == 1) {
+    const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);
+    uint32_t L = (uint32_t)std::floor(10.0 * std::pow(1024.0 / 10.0, u));
+    return std::min<uint32_t>(std::max<uint32_t>(L, 10), 1024);
+  }
+  uint32_t lo = std::max<uint32_t>(10, avg / 2), hi = std::max<uint32_t>(lo, avg + avg / 2);
+  return lo + (uint32_t)(r % (uint64_t)(hi - lo + 1));
+}
+
+static void gen_fill(uint64_t seed, uint64_t g, uint32_t L, uint8_t* out) {
+  static const char kHex[] = "0123456789abcdef";
+  static const char kAlpha[] = "abcdefghijklmnopqrstuvwxyz012345";
+  if (L == 0) return;
+  const uint64_t j = g - 1;
+  for (int d = 0; d < 9; ++d) out[d] = (uint8_t)kHex[(j >> (4 * (8 - d))) & 0xf];
+  out[9] = '/';
+  uint64_t state = splitmix64(splitmix64(seed) ^ (g * 0xd6e8feb86659fd93ull));
+  uint64_t r = 0;
+  int avail = 0;
+  for (uint32_t i = 10; i < L; ++i) {
+    if (i + 1 == L || i % 12 == 11) {
+      out[i] = '/';
+      continue;
+    }
+    if (avail == 0) {
+      state += 0x9e3779b97f4a7c15ull;
+      r = splitmix64(state);
+      avail = 12;
+    }
+    out[i] = (uint8_t)kAlpha[r & 31];
+    r >>= 5;
+    --avail;
+  }
+}
+
+int s3imph_gen_keys(int kind, uint64_t seed, uint32_t avg_len, uint64_t lo, uint64_t n, uint8_t* blob,
+                    uint64_t* offsets, uint64_t* total_bytes) {
+  if ((kind != 0 && kind != 1) || (kind == 0 && avg_len == 0)) return S3IMPH_ERR_INVALID;
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (n < 100000) nt = 1;
+  // pass 1: lengths (threaded) and the exclusive prefix sum.
+  std::vector<uint64_t> part(nt + 1, 0);
+  auto len_range = [&](unsigned t, uint64_t a, uint64_t b) {
+    uint64_t s = 0;
+    for (uint64_t i = a; i < b; ++i) {
+      const uint32_t L = gen_len(kind, seed, avg_len, lo + i);
+      if (offsets) offsets[i + 1] = L;
+      s += L;
+    }
+    part[t + 1] = s;
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back(len_range, t, n * t / nt, n * (t + 1) / nt);
+  for (auto& x : th) x.join();
+  th.clear();
+  for (unsigned t = 0; t < nt; ++t) part[t + 1] += part[t];
+  if (total_bytes) *total_bytes = part[nt];
+  if (!offsets) return S3IMPH_OK;
+  offsets[0] = 0;
+  auto scan_fill = [&](unsigned t, uint64_t a, uint64_t b) {
+    uint64_t acc = part[t];
+    for (uint64_t i = a; i < b; ++i) {
+      const uint64_t L = offsets[i + 1];
+      if (blob) gen_fill(seed, lo + i, (uint32_t)L, blob + acc);
+      acc += L;
+      offsets[i + 1] = acc;
+    }
+  };
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back(scan_fill, t, n * t / nt, n * (t + 1) / nt);
+  for (auto& x : th) x.join();
+  return S3IMPH_OK;
+}
+
+}  // extern "C"

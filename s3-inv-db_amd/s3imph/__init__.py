@@ -1,0 +1,383 @@
+"""s3imph — Python binding of libs3imph.so, the MI355X-native MPHF builder.
+
+Mirrors the reference's MPHF stage interface, ``format.StreamingMPHFBuilder``
+(/root/reference/pkg/format/mphf_streaming.go:29-232):
+
+    b = StreamingMPHFBuilder(temp_dir)       # NewStreamingMPHFBuilder (:48)
+    b.add(prefix, pos)                       # Add (:68)
+    b.count()                                # Count (:100)
+    b.build(out_dir)                         # Build (:122) -> mph.bin, mph_fp.u64, mph_pos.u64,
+                                             #                  prefix_blob.bin, prefix_offsets.u64
+    b.close()                                # Close (:105)
+
+plus the device-resident API that bench.py times (``DeviceBuilder``), the
+multi-GPU rank API (``DistBuilder``) and the batched lookup.
+
+Every compute call goes through the HIP library; there is no CPU fallback.
+If libs3imph.so is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+try:  # One HIP runtime per process: let torch load its libamdhip64 first.
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libs3imph.so")
+
+OK = 0
+ERR_INVALID = 1
+ERR_DUP_KEY_HASH = 2
+ERR_TOO_MANY_LEVELS = 3
+ERR_KEY_HASH_ZERO = 4
+ERR_HIP = 5
+ERR_RCCL = 6
+ERR_IO = 7
+ERR_NOMEM = 8
+ERR_FORMAT = 9
+ERR_INTERNAL = 10
+ERR_STATE = 11
+
+# Every entry point include/s3imph.h declares (checked by tests/test_capi.py).
+EXPORTS = (
+    "s3imph_abi_version", "s3imph_status_string",
+    "s3imph_builder_new", "s3imph_builder_add", "s3imph_builder_add_batch", "s3imph_builder_count",
+    "s3imph_builder_build", "s3imph_builder_close",
+    "s3imph_build_host", "s3imph_free", "s3imph_write_index_files",
+    "s3imph_ctx_create", "s3imph_ctx_destroy", "s3imph_ctx_reserve", "s3imph_build_device",
+    "s3imph_ctx_mph_bin", "s3imph_ctx_set_profiling", "s3imph_ctx_stage_times",
+    "s3imph_dist_unique_id", "s3imph_ctx_create_dist", "s3imph_build_device_dist",
+    "s3imph_lookup_device", "s3imph_gen_keys",
+)
+
+
+class MPHFError(RuntimeError):
+    """A non-OK s3imph_status; ``.status`` holds the code."""
+
+    def __init__(self, status: int, msg: str):
+        super().__init__(msg)
+        self.status = status
+
+
+class BuildInfo(ctypes.Structure):
+    _fields_ = [
+        ("status", ctypes.c_int32),
+        ("num_levels", ctypes.c_uint32),
+        ("total_words", ctypes.c_uint64),
+        ("mph_bin_len", ctypes.c_uint64),
+        ("big_levels", ctypes.c_uint64),
+        ("n_keys", ctypes.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libs3imph.so not built at {LIB_PATH}: run `make -C s3-inv-db_amd` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    u64, i32, vp, cp, sz = ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t
+    P = ctypes.POINTER
+    sig = {
+        "s3imph_abi_version": (i32, []),
+        "s3imph_status_string": (cp, [i32]),
+        "s3imph_builder_new": (i32, [cp, i32, P(vp), cp, sz]),
+        "s3imph_builder_add": (i32, [vp, cp, u64, u64, cp, sz]),
+        "s3imph_builder_add_batch": (i32, [vp, vp, vp, vp, u64, cp, sz]),
+        "s3imph_builder_count": (u64, [vp]),
+        "s3imph_builder_build": (i32, [vp, cp, cp, sz]),
+        "s3imph_builder_close": (i32, [vp]),
+        "s3imph_build_host": (i32, [i32, vp, vp, vp, u64, vp, vp, P(vp), P(u64), cp, sz]),
+        "s3imph_free": (None, [vp]),
+        "s3imph_write_index_files": (i32, [cp, vp, u64, vp, vp, u64, vp, vp, cp, sz]),
+        "s3imph_ctx_create": (i32, [i32, P(vp), cp, sz]),
+        "s3imph_ctx_destroy": (i32, [vp]),
+        "s3imph_ctx_reserve": (i32, [vp, u64, u64]),
+        "s3imph_build_device": (i32, [vp, vp, vp, vp, u64, vp, vp, vp, P(BuildInfo)]),
+        "s3imph_ctx_mph_bin": (i32, [vp, vp, u64, P(u64)]),
+        "s3imph_ctx_set_profiling": (i32, [vp, i32]),
+        "s3imph_ctx_stage_times": (i32, [vp, P(ctypes.c_float), i32, P(i32), cp, sz]),
+        "s3imph_dist_unique_id": (i32, [vp]),
+        "s3imph_ctx_create_dist": (i32, [i32, vp, i32, i32, P(vp), cp, sz]),
+        "s3imph_build_device_dist": (i32, [vp, vp, vp, vp, u64, u64, vp, vp, u64, P(u64), P(u64), vp,
+                                           P(BuildInfo)]),
+        "s3imph_lookup_device": (i32, [vp, vp, vp, u64, vp, vp, u64, vp, vp]),
+        "s3imph_gen_keys": (i32, [i32, u64, ctypes.c_uint32, u64, u64, vp, vp, P(u64)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+LIB = _load()
+
+
+def status_string(code: int) -> str:
+    return LIB.s3imph_status_string(code).decode()
+
+
+def _check(rc: int, err: ctypes.Array | None = None, what: str = ""):
+    if rc != OK:
+        msg = err.value.decode(errors="replace") if err is not None and err.value else status_string(rc)
+        raise MPHFError(rc, f"{what}{': ' if what else ''}{msg}")
+
+
+def _np_ptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    return ctypes.c_void_p(a.ctypes.data) if a.size else ctypes.c_void_p(0)
+
+
+def _dev_ptr(t) -> ctypes.c_void_p | None:
+    """Device pointer of a torch tensor, an int address, or None."""
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return ctypes.c_void_p(t)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def keys_to_blob(keys) -> tuple[np.ndarray, np.ndarray]:
+    """Keys (bytes/str) -> (blob u8, offsets u64[N+1]): the prefix_blob.bin / prefix_offsets.u64 layout."""
+    bs = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
+    offs = np.zeros(len(bs) + 1, np.uint64)
+    if bs:
+        offs[1:] = np.cumsum([len(k) for k in bs], dtype=np.uint64)
+    blob = np.frombuffer(b"".join(bs), np.uint8).copy() if bs else np.zeros(0, np.uint8)
+    return blob, offs
+
+
+# ------------------------------------------------------------------- builder mirror --
+class StreamingMPHFBuilder:
+    """format.StreamingMPHFBuilder (mphf_streaming.go:29-232) backed by the GPU build."""
+
+    def __init__(self, temp_dir: str | None = None, device: int = 0):
+        err = ctypes.create_string_buffer(512)
+        h = ctypes.c_void_p()
+        rc = LIB.s3imph_builder_new((temp_dir or "").encode(), device, ctypes.byref(h), err, 512)
+        _check(rc, err, "create temp file" if rc == ERR_IO else "")
+        self._h = h
+
+    def add(self, prefix, pos: int) -> None:
+        b = prefix.encode() if isinstance(prefix, str) else bytes(prefix)
+        err = ctypes.create_string_buffer(256)
+        _check(LIB.s3imph_builder_add(self._h, b, len(b), pos, err, 256), err)
+
+    def add_batch(self, blob: np.ndarray, offsets: np.ndarray, pos: np.ndarray | None = None) -> None:
+        blob = np.ascontiguousarray(blob, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        if pos is not None:
+            pos = np.ascontiguousarray(pos, np.uint64)
+        err = ctypes.create_string_buffer(256)
+        _check(LIB.s3imph_builder_add_batch(self._h, _np_ptr(blob), _np_ptr(offsets), _np_ptr(pos),
+                                            len(offsets) - 1, err, 256), err)
+
+    def count(self) -> int:
+        return LIB.s3imph_builder_count(self._h)
+
+    def build(self, out_dir: str) -> None:
+        err = ctypes.create_string_buffer(1024)
+        _check(LIB.s3imph_builder_build(self._h, out_dir.encode(), err, 1024), err)
+
+    def close(self) -> None:
+        if self._h:
+            LIB.s3imph_builder_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def build_host(blob: np.ndarray, offsets: np.ndarray, pos: np.ndarray | None = None, device: int = 0):
+    """One-shot build from host memory: (fp_out u64[N], pos_out u64[N], mph_bin bytes)."""
+    blob = np.ascontiguousarray(blob, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = len(offsets) - 1
+    if pos is not None:
+        pos = np.ascontiguousarray(pos, np.uint64)
+    fp_out = np.zeros(n, np.uint64)
+    pos_out = np.zeros(n, np.uint64)
+    mp = ctypes.c_void_p()
+    ml = ctypes.c_uint64()
+    err = ctypes.create_string_buffer(1024)
+    rc = LIB.s3imph_build_host(device, _np_ptr(blob), _np_ptr(offsets), _np_ptr(pos), n, _np_ptr(fp_out),
+                               _np_ptr(pos_out), ctypes.byref(mp), ctypes.byref(ml), err, 1024)
+    _check(rc, err)
+    mph = ctypes.string_at(mp.value, ml.value) if ml.value else b""
+    if mp.value:
+        LIB.s3imph_free(mp)
+    return fp_out, pos_out, mph
+
+
+def write_index_files(out_dir: str, mph_bin: bytes, fp: np.ndarray, pos: np.ndarray, blob: np.ndarray,
+                      offsets: np.ndarray) -> None:
+    """Emit mph.bin, mph_fp.u64, mph_pos.u64, prefix_blob.bin, prefix_offsets.u64 (reference framing)."""
+    fp = np.ascontiguousarray(fp, np.uint64)
+    pos = np.ascontiguousarray(pos, np.uint64)
+    blob = np.ascontiguousarray(blob, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    err = ctypes.create_string_buffer(1024)
+    rc = LIB.s3imph_write_index_files(out_dir.encode(), mph_bin, len(mph_bin), _np_ptr(fp), _np_ptr(pos),
+                                      len(fp), _np_ptr(blob), _np_ptr(offsets), err, 1024)
+    _check(rc, err)
+
+
+def gen_keys(kind: int, seed: int, avg_len: int, lo: int, n: int) -> tuple[np.ndarray, np.ndarray]:
+    """Deterministic synthetic prefixes [lo, lo+n) (see include/s3imph.h §6). Blob is padded to 8 bytes."""
+    total = ctypes.c_uint64()
+    _check(LIB.s3imph_gen_keys(kind, seed, avg_len, lo, n, None, None, ctypes.byref(total)))
+    blob = np.zeros(((total.value + 7) // 8) * 8 + 8, np.uint8)
+    offsets = np.zeros(n + 1, np.uint64)
+    _check(LIB.s3imph_gen_keys(kind, seed, avg_len, lo, n, _np_ptr(blob), _np_ptr(offsets), ctypes.byref(total)))
+    return blob, offsets
+
+
+# ----------------------------------------------------------------- device builders --
+class DeviceBuilder:
+    """A device context: device-resident builds, mph.bin marshalling, batched lookup."""
+
+    def __init__(self, device: int = 0):
+        err = ctypes.create_string_buffer(512)
+        h = ctypes.c_void_p()
+        _check(LIB.s3imph_ctx_create(device, ctypes.byref(h), err, 512), err)
+        self._h = h
+        self.device = device
+        self.last_info: dict | None = None
+
+    def reserve(self, max_keys: int, max_global_keys: int = 0) -> None:
+        _check(LIB.s3imph_ctx_reserve(self._h, max_keys, max_global_keys), None, "reserve")
+
+    def set_profiling(self, on: bool) -> None:
+        LIB.s3imph_ctx_set_profiling(self._h, 1 if on else 0)
+
+    def stage_times(self) -> dict:
+        ms = (ctypes.c_float * 64)()
+        cnt = ctypes.c_int()
+        names = ctypes.create_string_buffer(2048)
+        LIB.s3imph_ctx_stage_times(self._h, ms, 64, ctypes.byref(cnt), names, 2048)
+        keys = names.value.decode().split(",") if cnt.value else []
+        return {k: ms[i] for i, k in enumerate(keys)}
+
+    def build(self, d_blob, d_offsets, n: int, d_fp_out, d_pos_out, d_pos=None, stream=None) -> dict:
+        info = BuildInfo()
+        rc = LIB.s3imph_build_device(self._h, _dev_ptr(d_blob), _dev_ptr(d_offsets), _dev_ptr(d_pos), n,
+                                     _dev_ptr(d_fp_out), _dev_ptr(d_pos_out), _stream_ptr(stream),
+                                     ctypes.byref(info))
+        _check(rc, None, "build MPHF")
+        self.last_info = info.as_dict()
+        return self.last_info
+
+    def mph_bin(self) -> bytes:
+        ln = ctypes.c_uint64()
+        LIB.s3imph_ctx_mph_bin(self._h, None, 0, ctypes.byref(ln))
+        buf = ctypes.create_string_buffer(max(ln.value, 1))
+        _check(LIB.s3imph_ctx_mph_bin(self._h, buf, ln.value, ctypes.byref(ln)), None, "marshal MPHF")
+        return buf.raw[: ln.value]
+
+    def lookup(self, d_blob, d_offsets, n: int, d_fp, d_pos, count: int, d_result, stream=None) -> None:
+        _check(LIB.s3imph_lookup_device(self._h, _dev_ptr(d_blob), _dev_ptr(d_offsets), n, _dev_ptr(d_fp),
+                                        _dev_ptr(d_pos), count, _dev_ptr(d_result), _stream_ptr(stream)),
+               None, "lookup")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            LIB.s3imph_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def dist_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _check(LIB.s3imph_dist_unique_id(buf), None, "ncclGetUniqueId")
+    return buf.raw
+
+
+class DistBuilder(DeviceBuilder):
+    """One rank of a multi-GPU build (RCCL communicator owned by the library)."""
+
+    def __init__(self, device: int, unique_id: bytes, rank: int, nranks: int):
+        err = ctypes.create_string_buffer(512)
+        h = ctypes.c_void_p()
+        idbuf = ctypes.create_string_buffer(unique_id, 128)
+        _check(LIB.s3imph_ctx_create_dist(device, idbuf, rank, nranks, ctypes.byref(h), err, 512), err)
+        self._h = h
+        self.device = device
+        self.rank, self.nranks = rank, nranks
+        self.last_info = None
+
+    def build_shard(self, d_blob, d_offsets, n_local: int, key_base: int, d_fp_out, d_pos_out, out_cap: int,
+                    d_pos=None, stream=None) -> tuple[int, int, dict]:
+        info = BuildInfo()
+        lo, cnt = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = LIB.s3imph_build_device_dist(self._h, _dev_ptr(d_blob), _dev_ptr(d_offsets), _dev_ptr(d_pos),
+                                          n_local, key_base, _dev_ptr(d_fp_out), _dev_ptr(d_pos_out), out_cap,
+                                          ctypes.byref(lo), ctypes.byref(cnt), _stream_ptr(stream),
+                                          ctypes.byref(info))
+        _check(rc, None, "build MPHF (dist)")
+        self.last_info = info.as_dict()
+        return lo.value, cnt.value, self.last_info
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+@dataclass
+class ShardPlan:
+    """Contiguous key-index shard of a global prefix set, balanced by key count."""
+    rank: int
+    nranks: int
+    n_global: int
+
+    @property
+    def lo(self) -> int:
+        return self.n_global * self.rank // self.nranks
+
+    @property
+    def hi(self) -> int:
+        return self.n_global * (self.rank + 1) // self.nranks
+
+    @property
+    def n_local(self) -> int:
+        return self.hi - self.lo
+
+    @property
+    def out_per_rank(self) -> int:
+        return (self.n_global + self.nranks - 1) // self.nranks
+
+    @property
+    def out_lo(self) -> int:
+        return min(self.rank * self.out_per_rank, self.n_global)
+
+    @property
+    def out_n(self) -> int:
+        return min(self.out_per_rank, self.n_global - self.out_lo)

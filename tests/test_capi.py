@@ -1,0 +1,129 @@
+"""The C-ABI library loads, exports exactly what include/s3imph.h declares, and its
+host-only entry points (file framing, builder bookkeeping, generator) behave like the
+reference's writers — all without a GPU (no compute calls here)."""
+import ctypes
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle as O
+import s3imph
+from conftest import ROOT
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "s3imph.h")).read()
+    return set(re.findall(r"^(?:int|void|uint64_t|const char)\s*\*?\s*(s3imph_[a-z_]+)\(", src, re.M))
+
+
+def test_header_and_binding_agree():
+    assert _declared() == set(s3imph.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(s3imph.LIB_PATH)
+    for name in _declared():
+        assert hasattr(lib, name), name
+
+
+def test_abi_version_and_status_strings():
+    assert s3imph.LIB.s3imph_abi_version() == 1
+    for code in range(12):
+        assert s3imph.status_string(code)
+
+
+def test_write_index_files_matches_reference_framing(tmp_path, oracle_lib):
+    """Framing of the 5 files == format.go/writer.go restated in the oracle (S3ID header,
+    LE u64 payload, N+1 offsets with the sentinel)."""
+    keys = [b"", b"a/", b"a/b/", b"b/", b"c/"]
+    blob, offs = O.keys_to_blob(keys)
+    st, fp, pos, mph = oracle_lib.build(blob, offs)
+    s3imph.write_index_files(str(tmp_path), mph, fp, pos, blob, offs)
+    want = {"mph.bin": mph, "mph_fp.u64": O.s3id_u64_array(fp), "mph_pos.u64": O.s3id_u64_array(pos),
+            "prefix_blob.bin": blob.tobytes(), "prefix_offsets.u64": O.s3id_u64_array(offs)}
+    for name, data in want.items():
+        assert (tmp_path / name).read_bytes() == data, name
+
+
+def test_write_empty_matches_writeEmpty(tmp_path):
+    """mphf_streaming.go:506-541: 0-byte mph.bin, count-0 arrays, offsets = [0] (count 1), empty blob."""
+    s3imph.write_index_files(str(tmp_path), b"", np.zeros(0, np.uint64), np.zeros(0, np.uint64),
+                             np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+    assert (tmp_path / "mph.bin").read_bytes() == b""
+    assert (tmp_path / "mph_fp.u64").read_bytes() == O.s3id_header(0)
+    assert (tmp_path / "mph_pos.u64").read_bytes() == O.s3id_header(0)
+    assert (tmp_path / "prefix_blob.bin").read_bytes() == b""
+    assert (tmp_path / "prefix_offsets.u64").read_bytes() == O.s3id_header(1) + b"\0" * 8
+
+
+def test_write_files_rebases_offsets(tmp_path):
+    blob = np.frombuffer(b"XXXXab/cd/", np.uint8).copy()
+    offs = np.array([4, 7, 10], np.uint64)
+    s3imph.write_index_files(str(tmp_path), b"\1", np.array([1, 2], np.uint64), np.array([0, 1], np.uint64),
+                             blob, offs)
+    assert (tmp_path / "prefix_blob.bin").read_bytes() == b"ab/cd/"
+    assert (tmp_path / "prefix_offsets.u64").read_bytes() == O.s3id_u64_array([0, 3, 6])
+
+
+def test_write_files_missing_dir_is_io_error(tmp_path):
+    with pytest.raises(s3imph.MPHFError) as e:
+        s3imph.write_index_files(str(tmp_path / "nope"), b"", np.zeros(0, np.uint64), np.zeros(0, np.uint64),
+                                 np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+    assert e.value.status == s3imph.ERR_IO
+
+
+def test_builder_bookkeeping_without_gpu(tmp_path):
+    b = s3imph.StreamingMPHFBuilder(str(tmp_path))
+    assert b.count() == 0
+    b.add("a/", 0)
+    b.add(b"b/", 1)
+    blob, offs = O.keys_to_blob([b"c/", b"d/"])
+    b.add_batch(blob, offs)
+    assert b.count() == 4
+    b.close()
+
+
+def test_builder_bad_temp_dir(tmp_path):
+    with pytest.raises(s3imph.MPHFError) as e:
+        s3imph.StreamingMPHFBuilder(str(tmp_path / "missing"))
+    assert e.value.status == s3imph.ERR_IO
+
+
+def test_builder_empty_build_needs_no_gpu(tmp_path):
+    """Count()==0 -> writeEmpty; no device work at all."""
+    b = s3imph.StreamingMPHFBuilder(str(tmp_path))
+    b.build(str(tmp_path))
+    assert (tmp_path / "mph.bin").read_bytes() == b""
+    assert (tmp_path / "prefix_offsets.u64").read_bytes() == O.s3id_header(1) + b"\0" * 8
+    with pytest.raises(s3imph.MPHFError) as e:
+        b.add("x/", 0)
+    assert e.value.status == s3imph.ERR_STATE
+
+
+def test_generator_sorted_distinct_and_shardable():
+    blob, offs = s3imph.gen_keys(0, 42, 32, 0, 50000)
+    keys = [bytes(blob[offs[i]:offs[i + 1]]) for i in range(50000)]
+    assert keys[0] == b""
+    assert keys == sorted(keys) and len(set(keys)) == len(keys)
+    lens = np.diff(offs.astype(np.int64))[1:]
+    assert lens.min() >= 16 and lens.max() <= 48 and abs(lens.mean() - 32) < 0.5
+    b2, o2 = s3imph.gen_keys(0, 42, 32, 12345, 100)
+    for i in range(100):
+        assert bytes(b2[o2[i]:o2[i + 1]]) == keys[12345 + i]
+    b3, o3 = s3imph.gen_keys(1, 42, 0, 0, 20000)
+    l3 = np.diff(o3.astype(np.int64))[1:]
+    assert l3.min() >= 10 and l3.max() <= 1024
+    assert hashlib.sha256(blob[: offs[-1]].tobytes()).hexdigest() == \
+        hashlib.sha256(s3imph.gen_keys(0, 42, 32, 0, 50000)[0][: offs[-1]].tobytes()).hexdigest()
+
+
+def test_shard_plan_covers_everything():
+    for n in [0, 1, 7, 100, 10**6 + 3]:
+        for p in [1, 2, 3, 8]:
+            plans = [s3imph.ShardPlan(r, p, n) for r in range(p)]
+            assert sum(x.n_local for x in plans) == n
+            assert all(plans[r].hi == plans[r + 1].lo for r in range(p - 1))
+            assert sum(x.out_n for x in plans) == n

@@ -1,0 +1,246 @@
+"""Parity of the HIP build against the CPU oracle (run on an MI355X with -m gpu).
+
+Bit-exact bar: mph.bin bytes, mph_fp.u64 and mph_pos.u64 equal the oracle's for the
+same input (integer path — no tolerance).  Small/medium sets compare everything;
+BASELINE's full sizes are checked through size-independent properties (positions
+form a permutation, every member looks itself up, determinism across runs).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import keysets
+import oracle as O
+from conftest import GOLDEN, from_dev, to_dev
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def s3():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    import s3imph
+    return s3imph
+
+
+@pytest.fixture(scope="module")
+def ctx(s3):
+    c = s3.DeviceBuilder(0)
+    yield c
+    c.close()
+
+
+def _device_build(s3, ctx, blob, offs, pos=None):
+    import torch
+    n = len(offs) - 1
+    d_blob = to_dev(np.ascontiguousarray(blob, np.uint8), pad8=True)
+    d_offs = to_dev(offs)
+    d_pos = to_dev(pos) if pos is not None else None
+    d_fp = torch.zeros(max(n, 1), dtype=torch.int64, device="cuda")
+    d_po = torch.zeros(max(n, 1), dtype=torch.int64, device="cuda")
+    info = ctx.build(d_blob, d_offs, n, d_fp, d_po, d_pos=d_pos)
+    torch.cuda.synchronize()
+    return from_dev(d_fp)[:n], from_dev(d_po)[:n], ctx.mph_bin(), info
+
+
+def _check_vs_oracle(oracle_lib, s3, ctx, keys, pos=None):
+    blob, offs = O.keys_to_blob(keys)
+    st, fp, po, mph = oracle_lib.build(blob, offs, pos)
+    assert st == 0
+    gfp, gpo, gmph, info = _device_build(s3, ctx, blob, offs, pos)
+    assert gmph == mph
+    assert np.array_equal(gfp, fp)
+    assert np.array_equal(gpo, po)
+    return info
+
+
+def _fixture_files():
+    return sorted(p for p in os.listdir(GOLDEN) if p.endswith(".json") and p != "fnv_kat.json")
+
+
+@pytest.mark.parametrize("fname", _fixture_files())
+def test_golden_fixture(s3, ctx, fname):
+    """Device build reproduces each committed fixture (the reference's own test key sets)."""
+    with open(os.path.join(GOLDEN, fname)) as f:
+        fx = json.load(f)
+    name = fx["name"]
+    if "keys" in fx:
+        ks = fx["keys"]
+    else:
+        ks = {"memory_test_10000": keysets.memory_test_prefixes,
+              "wide_single_level_100k": keysets.wide_single_level_prefixes,
+              "realistic_100k": lambda: keysets.realistic_prefixes(100000)}[name]()
+    keys = [k.encode() for k in ks]
+    blob, offs = O.keys_to_blob(keys)
+    gfp, gpo, gmph, _ = _device_build(s3, ctx, blob, offs)
+    got = {"mph.bin": gmph, "mph_fp.u64": O.s3id_u64_array(gfp), "mph_pos.u64": O.s3id_u64_array(gpo)}
+    for k, v in got.items():
+        assert hashlib.sha256(v).hexdigest() == fx["files_sha256"][k], (name, k)
+
+
+def test_builder_writes_identical_files(s3, oracle_lib, tmp_path):
+    """StreamingMPHFBuilder mirror: Add x N -> Build(outDir) -> the 5 files equal the oracle's."""
+    keys = [k.encode() for k in keysets.wide_single_level_prefixes(20000)]
+    b = s3.StreamingMPHFBuilder(str(tmp_path))
+    for i, k in enumerate(keys):
+        b.add(k, i)
+    assert b.count() == len(keys)
+    out = tmp_path / "idx"
+    out.mkdir()
+    b.build(str(out))
+    b.close()
+    blob, offs = O.keys_to_blob(keys)
+    st, fp, po, mph = oracle_lib.build(blob, offs)
+    want = {"mph.bin": mph, "mph_fp.u64": O.s3id_u64_array(fp), "mph_pos.u64": O.s3id_u64_array(po),
+            "prefix_blob.bin": blob.tobytes(), "prefix_offsets.u64": O.s3id_u64_array(offs)}
+    for name, data in want.items():
+        assert (out / name).read_bytes() == data, name
+
+
+def test_build_host_roundtrip_lookup(s3, oracle_lib):
+    """build_host + the oracle's Lookup restatement: every member -> its pos (VerifyMPHF)."""
+    keys = [k.encode() for k in keysets.mphf_test_sets()["mphf_no_false_pos"]]
+    blob, offs = O.keys_to_blob(keys)
+    fp, po, mph = s3.build_host(blob, offs)
+    st, m = oracle_lib.unmarshal(mph)
+    assert st == 0
+    for i, k in enumerate(keys):
+        assert oracle_lib.lookup(m, fp, po, k) == i
+    for k in keysets.NON_MEMBERS:
+        assert oracle_lib.lookup(m, fp, po, k.encode()) is None
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 31, 32, 33, 63, 64, 65, 1000, 4097, 65535, 65536, 65537, 200000])
+def test_sizes_around_boundaries(s3, oracle_lib, ctx, n):
+    blob, offs = s3.gen_keys(0, 7, 24, 0, n)
+    keys = [bytes(blob[offs[i]:offs[i + 1]]) for i in range(n)]
+    _check_vs_oracle(oracle_lib, s3, ctx, keys)
+
+
+def test_ragged_lengths_0_to_1024(s3, oracle_lib, ctx):
+    rng = np.random.default_rng(5)
+    keys = set()
+    while len(keys) < 30000:
+        L = int(rng.integers(0, 1025)) if rng.random() < 0.5 else int(rng.integers(0, 12))
+        keys.add(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+    _check_vs_oracle(oracle_lib, s3, ctx, sorted(keys))
+
+
+def test_unaligned_blob_offsets(s3, oracle_lib, ctx):
+    """Keys starting at every byte phase, including a non-zero offsets[0]."""
+    keys = [bytes([65 + (i % 26)] * (i % 19)) + b"%d/" % i for i in range(5000)]
+    blob, offs = O.keys_to_blob(keys)
+    shifted = np.concatenate([np.frombuffer(b"zzz", np.uint8), blob])
+    st, fp, po, mph = oracle_lib.build(blob, offs)
+    gfp, gpo, gmph, _ = _device_build(s3, ctx, shifted, offs + 3)
+    assert gmph == mph and np.array_equal(gfp, fp) and np.array_equal(gpo, po)
+
+
+def test_custom_positions(s3, oracle_lib, ctx):
+    keys = [("p%06d/" % i).encode() for i in range(50000)]
+    pos = np.random.default_rng(1).permutation(50000).astype(np.uint64) + np.uint64(10**12)
+    _check_vs_oracle(oracle_lib, s3, ctx, keys, pos)
+
+
+def test_empty_and_single(s3, ctx):
+    fp, po, mph, info = _device_build(s3, ctx, np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+    assert mph == b"" and len(fp) == 0 and info["num_levels"] == 0
+    fp, po, mph, info = _device_build(s3, ctx, np.frombuffer(b"a/", np.uint8), np.array([0, 2], np.uint64))
+    assert info["num_levels"] == 1 and po[0] == 0
+
+
+def test_duplicate_keys_error(s3, ctx):
+    keys = [b"a/", b"b/", b"a/", b"c/"]
+    blob, offs = O.keys_to_blob(keys)
+    with pytest.raises(s3.MPHFError) as e:
+        _device_build(s3, ctx, blob, offs)
+    assert e.value.status == s3.ERR_DUP_KEY_HASH
+    # the context stays usable after the error
+    _device_build(s3, ctx, *O.keys_to_blob([b"x/", b"y/"]))
+
+
+def test_duplicate_keys_error_builder(s3, tmp_path):
+    b = s3.StreamingMPHFBuilder(str(tmp_path))
+    for k in ["a/", "b/", "a/"]:
+        b.add(k, 0)
+    with pytest.raises(s3.MPHFError) as e:
+        b.build(str(tmp_path))
+    assert e.value.status == s3.ERR_DUP_KEY_HASH
+    assert "build MPHF" in str(e.value)
+    assert not (tmp_path / "mph.bin").exists()
+
+
+def test_c2_10m_bit_exact(s3, oracle_lib, ctx):
+    """BASELINE config 2: 10M synthetic prefixes, avg 32 B — full bit-exact comparison."""
+    n = 10_000_000
+    blob, offs = s3.gen_keys(0, 42, 32, 0, n)
+    st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)
+    assert st == 0
+    gfp, gpo, gmph, info = _device_build(s3, ctx, blob, offs)
+    assert gmph == mph
+    assert np.array_equal(gfp, fp)
+    assert np.array_equal(gpo, po)
+    assert info["big_levels"] >= 1
+
+
+def test_determinism_and_device_lookup(s3, ctx):
+    """Same input twice -> identical bytes; batched Lookup (mphf.go:275-302) finds every member
+    at its pos and rejects non-members (mphf_test.go:182-217 at scale)."""
+    import torch
+    n = 1_000_000
+    blob, offs = s3.gen_keys(0, 3, 40, 0, n)
+    a = _device_build(s3, ctx, blob, offs)
+    b = _device_build(s3, ctx, blob, offs)
+    assert a[2] == b[2] and np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    d_fp, d_po = to_dev(a[0]), to_dev(a[1])
+    res = torch.zeros(n, dtype=torch.int64, device="cuda")
+    ctx.lookup(to_dev(blob, pad8=True), to_dev(offs), n, d_fp, d_po, n, res)
+    assert np.array_equal(from_dev(res), np.arange(n, dtype=np.uint64))
+    # non-members: keys of a different seed/range
+    qb, qo = s3.gen_keys(0, 4, 40, n + 10, 100000)
+    res2 = torch.zeros(100000, dtype=torch.int64, device="cuda")
+    ctx.lookup(to_dev(qb, pad8=True), to_dev(qo), 100000, d_fp, d_po, n, res2)
+    assert (from_dev(res2) == np.uint64(2**64 - 1)).all()
+
+
+def test_c3_100m_properties(s3, ctx):
+    """BASELINE config 3 (100M keys, avg 64 B) at full size: size-independent properties —
+    positions are a permutation of [0, N), and every key looks itself up."""
+    import torch
+    n = 100_000_000
+    blob, offs = s3.gen_keys(0, 42, 64, 0, n)
+    d_blob = to_dev(blob)
+    d_offs = to_dev(offs)
+    d_fp = torch.zeros(n, dtype=torch.int64, device="cuda")
+    d_po = torch.zeros(n, dtype=torch.int64, device="cuda")
+    info = ctx.build(d_blob, d_offs, n, d_fp, d_po)
+    assert info["n_keys"] == n
+    # pos_out is a permutation of 0..N-1
+    srt = torch.sort(d_po).values
+    assert torch.equal(srt, torch.arange(n, dtype=torch.int64, device="cuda"))
+    del srt
+    res = torch.zeros(n, dtype=torch.int64, device="cuda")
+    ctx.lookup(d_blob, d_offs, n, d_fp, d_po, n, res)
+    assert torch.equal(res, torch.arange(n, dtype=torch.int64, device="cuda"))
+
+
+def test_dist_path_single_rank_matches(s3, oracle_lib):
+    """The RCCL rank path (nranks = 1 on this one-GPU box) is byte-identical to the
+    single-GPU path and the oracle (multi-rank layout is covered by tests/test_dist_model.py)."""
+    import torch
+    uid = s3.dist_unique_id()
+    d = s3.DistBuilder(0, uid, 0, 1)
+    n = 300000
+    blob, offs = s3.gen_keys(0, 11, 32, 0, n)
+    st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)
+    d_fp = torch.zeros(n, dtype=torch.int64, device="cuda")
+    d_po = torch.zeros(n, dtype=torch.int64, device="cuda")
+    lo, cnt, info = d.build_shard(to_dev(blob), to_dev(offs), n, 0, d_fp, d_po, n)
+    assert (lo, cnt) == (0, n)
+    assert d.mph_bin() == mph
+    assert np.array_equal(from_dev(d_fp), fp) and np.array_equal(from_dev(d_po), po)
+    d.close()
