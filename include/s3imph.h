@@ -125,8 +125,9 @@ int s3imph_ctx_destroy(s3imph_ctx *ctx);
  * grow it on demand, but a reserved workspace keeps allocation out of timed runs). */
 int s3imph_ctx_reserve(s3imph_ctx *ctx, uint64_t max_keys, uint64_t max_global_keys);
 
-/* Enqueue the whole build on `stream` (a hipStream_t; NULL = the ctx's own stream)
- * and wait for it.  d_blob must be readable up to offsets[n] rounded up to 8 bytes.
+/* Enqueue the whole build on `stream` (a hipStream_t; NULL = the ctx's own stream,
+ * a blocking stream, i.e. ordered after work queued on the legacy NULL stream) and
+ * wait for it.  d_blob must be readable up to offsets[n] rounded up to 8 bytes.
  * d_pos may be NULL (identity).  d_fp_out / d_pos_out: n entries each.
  * The level bit vectors stay on the device until s3imph_ctx_mph_bin(). */
 int s3imph_build_device(s3imph_ctx *ctx, const uint8_t *d_blob, const uint64_t *d_offsets,

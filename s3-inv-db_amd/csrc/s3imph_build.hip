@@ -59,7 +59,7 @@ struct s3imph_ctx {
   hipStream_t own_stream = nullptr;
   std::mutex mu;
 
-  uint64_t cap_keys = 0, cap_words = 0, cap_blocks = 0;
+  uint64_t cap_keys = 0, cap_words = 0, cap_blocks = 0, seg_cap = 0;
   uint64_t *kh = nullptr, *fp = nullptr, *settle = nullptr, *C = nullptr, *bits = nullptr,
            *rank_base = nullptr;
   uint64_t* rkeys[2] = {nullptr, nullptr};
@@ -156,10 +156,13 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   dalloc(c->kh, cap);
   dalloc(c->fp, cap);
   dalloc(c->settle, cap);
-  dalloc(c->rkeys[0], cap);
-  dalloc(c->rkeys[1], cap);
-  dalloc(c->ridx[0], cap);
-  dalloc(c->ridx[1], cap);
+  // Redo lists: kNSeg segments of seg_cap entries (segment s of level L+1 only ever
+  // receives keys from segment s of level L, which holds <= ceil(n/kNSeg) keys).
+  c->seg_cap = (cap + kNSeg - 1) / kNSeg + 1;
+  dalloc(c->rkeys[0], c->seg_cap * kNSeg);
+  dalloc(c->rkeys[1], c->seg_cap * kNSeg);
+  dalloc(c->ridx[0], c->seg_cap * kNSeg);
+  dalloc(c->ridx[1], c->seg_cap * kNSeg);
   dalloc(c->C, level_words(cap) + 64);
   c->cap_words = cap_words_for(cap);
   dalloc(c->bits, c->cap_words);
@@ -289,20 +292,20 @@ int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   ev_mark(c, s, "init");
   launch_hash_mark0(blob, offsets, n, c->kh, c->fp, c->bits, c->C, words0, c->d_st, grid, s);
   ev_mark(c, s, "hash_mark0");
-  launch_resolve(0, c->kh, nullptr, c->C, c->rkeys[0], c->ridx[0], c->cap_keys, c->settle, c->d_st,
+  launch_resolve(0, c->kh, nullptr, c->C, c->rkeys[0], c->ridx[0], c->seg_cap, c->settle, c->d_st,
                  kTailKeys, grid, s);
   launch_finalize(0, c->bits, c->C, c->cap_words, c->d_st, kTailKeys, default_grid(words0, 256), s);
   ev_mark(c, s, "resolve0");
   for (int L = 1; L <= big; ++L) {
-    const int g = std::max(1, std::min(grid, (int)(grid * std::pow(0.3935, L) * 1.5) + 1));
-    launch_mark(L, c->rkeys[(L - 1) & 1], c->bits, c->C, c->d_st, kTailKeys, g, s);
+    const int g = std::max(kNSeg, std::min(grid, (int)(grid * std::pow(0.3935, L) * 1.5) + 1));
+    launch_mark(L, c->rkeys[(L - 1) & 1], c->seg_cap, c->bits, c->C, c->d_st, kTailKeys, g, s);
     launch_resolve(L, c->rkeys[(L - 1) & 1], c->ridx[(L - 1) & 1], c->C, c->rkeys[L & 1],
-                   c->ridx[L & 1], c->cap_keys, c->settle, c->d_st, kTailKeys, g, s);
+                   c->ridx[L & 1], c->seg_cap, c->settle, c->d_st, kTailKeys, g, s);
     launch_finalize(L, c->bits, c->C, c->cap_words, c->d_st, kTailKeys, g, s);
   }
   ev_mark(c, s, "levels");
   launch_tail(big, c->bits, c->cap_words, c->C, c->rkeys[0], c->ridx[0], c->rkeys[1], c->ridx[1],
-              c->settle, c->d_st, s);
+              c->seg_cap, c->settle, c->d_st, s);
   ev_mark(c, s, "tail");
   launch_rank_scan(c->bits, c->cap_words, c->rank_base, c->block_sums, c->cap_blocks, c->d_st, s);
   ev_mark(c, s, "rank_scan");
@@ -698,7 +701,9 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     HIPCHECK(hipSetDevice(device));
     c = new s3imph_ctx();
     c->device = device;
-    HIPCHECK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    // A blocking stream: implicitly ordered with the legacy NULL stream, so work a
+    // caller queued there (e.g. torch's default stream) completes before ours starts.
+    HIPCHECK(hipStreamCreate(&c->own_stream));
     *out = c;
     return S3IMPH_OK;
   } catch (const Fail& f) {

@@ -12,6 +12,11 @@
 
 namespace s3imph {
 
+// Redo (next-level) key lists are split into kNSeg segments: block b of a big-level
+// kernel reads input segment (b % kNSeg) and appends to the same output segment, so
+// compaction counters are sharded 64 ways and one atomic covers a whole block tile.
+constexpr int kNSeg = 64;
+
 // Device-resident per-build level bookkeeping.  Written only by kernels (and the
 // init kernel); the host copies it back once, after the build.
 struct LevelState {
@@ -24,6 +29,7 @@ struct LevelState {
   unsigned int status;                       // kSt* flags
   unsigned int tail_first;                   // first level run by the single-workgroup tail
   unsigned int pad;
+  unsigned long long seg[kMaxLevels + 2][kNSeg];  // per-segment active keys of level L >= 1
 };
 
 // Device status flags.
@@ -46,15 +52,15 @@ void launch_hash_mark0(const uint8_t* blob, const uint64_t* offsets, uint64_t n,
                        uint64_t* fp, uint64_t* bits, uint64_t* C, uint64_t words0, LevelState* st,
                        int grid, hipStream_t s);
 void launch_resolve(int level, const uint64_t* keys_in, const uint32_t* idx_in, const uint64_t* C,
-                    uint64_t* keys_out, uint32_t* idx_out, uint64_t out_cap, uint64_t* settle,
+                    uint64_t* keys_out, uint32_t* idx_out, uint64_t seg_cap, uint64_t* settle,
                     LevelState* st, unsigned long long gate, int grid, hipStream_t s);
 void launch_finalize(int level, uint64_t* bits, uint64_t* C, uint64_t cap_words, LevelState* st,
                      unsigned long long gate, int grid, hipStream_t s);
-void launch_mark(int level, const uint64_t* keys, uint64_t* bits, uint64_t* C, LevelState* st,
-                 unsigned long long gate, int grid, hipStream_t s);
+void launch_mark(int level, const uint64_t* keys, uint64_t seg_cap, uint64_t* bits, uint64_t* C,
+                 LevelState* st, unsigned long long gate, int grid, hipStream_t s);
 void launch_tail(int big_launched, uint64_t* bits, uint64_t cap_words, uint64_t* C, uint64_t* keys0,
-                 uint32_t* idx0, uint64_t* keys1, uint32_t* idx1, uint64_t* settle, LevelState* st,
-                 hipStream_t s);
+                 uint32_t* idx0, uint64_t* keys1, uint32_t* idx1, uint64_t seg_cap, uint64_t* settle,
+                 LevelState* st, hipStream_t s);
 void launch_rank_scan(const uint64_t* bits, uint64_t cap_words, uint64_t* rank_base,
                       unsigned long long* block_sums, uint64_t max_blocks, LevelState* st,
                       hipStream_t s);

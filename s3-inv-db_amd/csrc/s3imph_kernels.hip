@@ -91,9 +91,10 @@ __device__ __forceinline__ void mark_bit(uint32_t* A, uint32_t* C, uint64_t x) {
 
 // ----------------------------------------------------------------------------------
 __global__ void k_init_state(LevelState* st, uint64_t n) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    unsigned long long* p = reinterpret_cast<unsigned long long*>(st);
-    for (size_t i = 0; i < sizeof(LevelState) / 8; ++i) p[i] = 0;
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(st);
+  for (size_t i = threadIdx.x; i < sizeof(LevelState) / 8; i += blockDim.x) p[i] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
     const uint64_t w = level_words(n);
     st->n[0] = n;
     st->words[0] = w;
@@ -101,6 +102,35 @@ __global__ void k_init_state(LevelState* st, uint64_t n) {
     st->woff[1] = w;
     st->magic[0] = level_magic(w);
   }
+}
+
+// Input segment s of a big level: level 0 splits the contiguous kh array into kNSeg
+// equal ranges (idx = position in kh); level >= 1 reads segment s of the previous
+// level's redo list (capacity seg_cap each, count st->seg[level][s]).
+struct SegView {
+  const uint64_t* keys;
+  const uint32_t* idx;  // nullptr: idx = base + j
+  uint64_t base;
+  uint64_t cnt;
+};
+
+__device__ __forceinline__ SegView seg_view(int level, int s, const uint64_t* keys, const uint32_t* idx,
+                                            uint64_t seg_cap, const LevelState* st) {
+  SegView v;
+  if (level == 0) {
+    const uint64_t n = st->n[0];
+    const uint64_t lo = n * (uint64_t)s / kNSeg, hi = n * (uint64_t)(s + 1) / kNSeg;
+    v.keys = keys + lo;
+    v.idx = nullptr;
+    v.base = lo;
+    v.cnt = hi - lo;
+  } else {
+    v.keys = keys + (uint64_t)s * seg_cap;
+    v.idx = idx + (uint64_t)s * seg_cap;
+    v.base = 0;
+    v.cnt = st->seg[level][s];
+  }
+  return v;
 }
 
 // Level 0, fused with key hashing: one lane per key.
@@ -122,64 +152,101 @@ __global__ __launch_bounds__(kBlock) void k_hash_mark0(
   if (zero) atomicOr(&st->status, kStKeyZero);
 }
 
-// Level >= 1, pass 1 (full grid).  Runs only while the level is big (n > gate).
+// Level >= 1, pass 1 (full grid, gridDim a multiple of kNSeg).  Runs only while the
+// level is big (n > gate).
 __global__ __launch_bounds__(kBlock) void k_mark(int level, const uint64_t* __restrict__ keys,
-                                                 uint64_t* bits, uint32_t* C, LevelState* st,
-                                                 unsigned long long gate) {
+                                                 uint64_t seg_cap, uint64_t* bits, uint32_t* C,
+                                                 LevelState* st, unsigned long long gate) {
   const uint64_t n = st->n[level];
   if (n <= gate || (st->status & kStOverflow)) return;
   const uint64_t words = st->words[level], magic = st->magic[level];
   uint32_t* A = reinterpret_cast<uint32_t*>(bits + st->woff[level]);
   const uint64_t seed = level_seed(level);
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < n; j += stride)
-    mark_bit(A, C, bb_index(seed, keys[j], words, magic));
+  const int sgi = blockIdx.x % kNSeg;
+  const uint64_t sub = blockIdx.x / kNSeg, nsub = gridDim.x / kNSeg;
+  const SegView v = seg_view(level, sgi, keys, nullptr, seg_cap, st);
+  for (uint64_t j = sub * kBlock + threadIdx.x; j < v.cnt; j += nsub * kBlock)
+    mark_bit(A, C, bb_index(seed, v.keys[j], words, magic));
 }
 
-// Pass 2: settled keys record their global bit index; collided keys are compacted
-// (wave ballot + one atomic per wave) into the next level's active list.
+// Pass 2: settled keys record their global bit index; collided keys go to the
+// next level's list.  Block b reads input segment b % kNSeg and appends to output
+// segment b % kNSeg; one atomic per block tile (kResolveKPT*256 keys) reserves space.
+constexpr int kResolveKPT = 4;
+
 template <bool kLevel0>
 __global__ __launch_bounds__(kBlock) void k_resolve(int level, const uint64_t* __restrict__ keys_in,
                                                     const uint32_t* __restrict__ idx_in,
                                                     const uint32_t* __restrict__ C,
                                                     uint64_t* __restrict__ keys_out,
-                                                    uint32_t* __restrict__ idx_out, uint64_t out_cap,
+                                                    uint32_t* __restrict__ idx_out, uint64_t seg_cap,
                                                     uint64_t* __restrict__ settle, LevelState* st,
                                                     unsigned long long gate) {
+  __shared__ unsigned s_wcnt[kBlock / 64];
+  __shared__ unsigned long long s_wbase[kBlock / 64];
   const uint64_t n = st->n[level];
   if ((!kLevel0 && n <= gate) || (st->status & kStOverflow)) return;
   const uint64_t words = st->words[level], magic = st->magic[level];
   const uint64_t gbase = st->woff[level] * 64;
   const uint64_t seed = level_seed(level);
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  const unsigned lane = lane_id();
-  for (uint64_t wbase = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); wbase < n;
-       wbase += stride) {
-    const uint64_t j = wbase + lane;
-    bool redo = false;
-    uint64_t k = 0;
-    uint32_t idx = 0;
-    if (j < n) {
-      k = keys_in[j];
-      idx = kLevel0 ? (uint32_t)j : idx_in[j];
-      const uint64_t x = bb_index(seed, k, words, magic);
-      redo = test_bit32(C, x);
-      if (!redo) settle[idx] = gbase + x;
+  const unsigned lane = lane_id(), wave = threadIdx.x >> 6;
+  const int sgi = blockIdx.x % kNSeg;
+  const uint64_t sub = blockIdx.x / kNSeg, nsub = gridDim.x / kNSeg;
+  const SegView v = seg_view(kLevel0 ? 0 : level, sgi, keys_in, idx_in, seg_cap, st);
+  uint64_t* kout = keys_out + (uint64_t)sgi * seg_cap;
+  uint32_t* iout = idx_out + (uint64_t)sgi * seg_cap;
+  unsigned long long* seg_counter = &st->seg[level + 1][sgi];
+  constexpr uint64_t kTile = (uint64_t)kBlock * kResolveKPT;
+  for (uint64_t t0 = sub * kTile; t0 < v.cnt; t0 += nsub * kTile) {
+    bool r[kResolveKPT];
+    uint64_t k[kResolveKPT];
+    uint32_t id[kResolveKPT];
+#pragma unroll
+    for (int q = 0; q < kResolveKPT; ++q) {
+      const uint64_t j = t0 + (uint64_t)q * kBlock + threadIdx.x;
+      r[q] = false;
+      k[q] = 0;
+      id[q] = 0;
+      if (j < v.cnt) {
+        k[q] = v.keys[j];
+        id[q] = v.idx ? v.idx[j] : (uint32_t)(v.base + j);
+        const uint64_t x = bb_index(seed, k[q], words, magic);
+        r[q] = test_bit32(C, x);
+        if (!r[q]) settle[id[q]] = gbase + x;
+      }
     }
-    const uint64_t m = __ballot(redo);
-    if (m) {
-      unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(&st->n[level + 1], (unsigned long long)__popcll(m));
-      base = __shfl(base, 0);
-      if (redo) {
-        const uint64_t o = base + __popcll(m & lanemask_lt());
-        if (o < out_cap) {
-          keys_out[o] = k;
-          idx_out[o] = idx;
+    uint64_t m[kResolveKPT];
+    unsigned wc = 0;
+#pragma unroll
+    for (int q = 0; q < kResolveKPT; ++q) {
+      m[q] = __ballot(r[q]);
+      wc += __popcll(m[q]);
+    }
+    if (lane == 0) s_wcnt[wave] = wc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned tot = 0;
+      for (int w = 0; w < kBlock / 64; ++w) tot += s_wcnt[w];
+      unsigned long long base = tot ? atomicAdd(seg_counter, (unsigned long long)tot) : 0;
+      for (int w = 0; w < kBlock / 64; ++w) {
+        s_wbase[w] = base;
+        base += s_wcnt[w];
+      }
+    }
+    __syncthreads();
+    uint64_t o = s_wbase[wave];
+#pragma unroll
+    for (int q = 0; q < kResolveKPT; ++q) {
+      if (r[q]) {
+        const uint64_t slot = o + __popcll(m[q] & lanemask_lt());
+        if (slot < seg_cap) {
+          kout[slot] = k[q];
+          iout[slot] = id[q];
         } else {
           atomicOr(&st->status, kStOverflow);
         }
       }
+      o += __popcll(m[q]);
     }
   }
 }
@@ -198,7 +265,9 @@ __global__ __launch_bounds__(kBlock) void k_finalize(int level, uint64_t* bits, 
     C[w] = 0;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const uint64_t n1 = st->n[level + 1];
+    uint64_t n1 = 0;
+    for (int g = 0; g < kNSeg; ++g) n1 += st->seg[level + 1][g];
+    st->n[level + 1] = n1;
     const uint64_t w1 = n1 ? level_words(n1) : 0;
     const uint64_t off1 = st->woff[level] + words;
     st->words[level + 1] = w1;
@@ -212,16 +281,20 @@ __global__ __launch_bounds__(kBlock) void k_finalize(int level, uint64_t* bits, 
 
 // All remaining levels in one workgroup.  A and C live in LDS while the level
 // fits (n <= kTailKeys); larger levels (only if the host under-predicted the big
-// levels) fall back to global bit vectors within the same workgroup.
+// levels) fall back to global bit vectors within the same workgroup.  The first
+// tail level reads the segmented list of the last big level; later tail levels
+// read a contiguous list.
 __global__ __launch_bounds__(kTailThreads) void k_tail(int big_launched, uint64_t* bits,
                                                        uint64_t cap_words, uint32_t* Cg,
                                                        uint64_t* keys0, uint32_t* idx0,
                                                        uint64_t* keys1, uint32_t* idx1,
-                                                       uint64_t* settle, LevelState* st) {
+                                                       uint64_t seg_cap, uint64_t* settle,
+                                                       LevelState* st) {
   __shared__ uint32_t sA[kTailLdsWords32 / 2];
   __shared__ uint32_t sC[kTailLdsWords32 / 2];
-  __shared__ unsigned long long s_n, s_words, s_woff, s_magic, s_next;
-  __shared__ int s_level;
+  __shared__ unsigned long long s_cnt[kNSeg];
+  __shared__ unsigned long long s_n, s_words, s_woff, s_magic, s_next, s_stride;
+  __shared__ int s_level, s_nseg;
   const unsigned tid = threadIdx.x;
   const unsigned lane = lane_id();
 
@@ -234,8 +307,12 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(int big_launched, uint64_
     s_words = st->words[L];
     s_woff = st->woff[L];
     s_magic = st->magic[L];
+    s_nseg = kNSeg;
+    s_stride = seg_cap;
     st->tail_first = L;
   }
+  __syncthreads();
+  if (tid < kNSeg) s_cnt[tid] = st->seg[s_level][tid];
   __syncthreads();
 
   for (;;) {
@@ -247,6 +324,8 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(int big_launched, uint64_
       break;
     }
     const uint64_t words = s_words, woff = s_woff, magic = s_magic;
+    const int nseg = s_nseg;
+    const uint64_t stride = s_stride;
     const uint64_t w32 = 2 * words;
     const bool in_lds = w32 <= (uint64_t)(kTailLdsWords32 / 2);
     uint32_t* A = in_lds ? sA : reinterpret_cast<uint32_t*>(bits + woff);
@@ -265,34 +344,43 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(int big_launched, uint64_
     if (!in_lds) __threadfence();
 
     const uint64_t seed = level_seed(L);
-    for (uint64_t j = tid; j < n; j += kTailThreads) mark_bit(A, C, bb_index(seed, kin[j], words, magic));
+    for (int g = 0; g < nseg; ++g) {
+      const uint64_t* kk = kin + (uint64_t)g * stride;
+      const uint64_t c = s_cnt[g];
+      for (uint64_t j = tid; j < c; j += kTailThreads) mark_bit(A, C, bb_index(seed, kk[j], words, magic));
+    }
     __syncthreads();
     if (!in_lds) __threadfence();
 
-    for (uint64_t wb = tid & ~63u; wb < n; wb += kTailThreads) {
-      const uint64_t j = wb + lane;
-      bool redo = false;
-      uint64_t k = 0;
-      uint32_t idx = 0;
-      if (j < n) {
-        k = kin[j];
-        idx = iin[j];
-        const uint64_t x = bb_index(seed, k, words, magic);
-        // Fallback path: the atomics ran at the memory side, so read back with an
-        // atomic as well (never a possibly stale cached line).
-        const uint32_t cw = in_lds ? C[x >> 5] : atomicAdd(&C[x >> 5], 0u);
-        redo = (cw >> (x & 31)) & 1u;
-        if (!redo) settle[idx] = woff * 64 + x;
-      }
-      const uint64_t m = __ballot(redo);
-      if (m) {
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(&s_next, (unsigned long long)__popcll(m));
-        base = __shfl(base, 0);
-        if (redo) {
-          const uint64_t o = base + __popcll(m & lanemask_lt());
-          kout[o] = k;  // o < n <= buffer capacity
-          iout[o] = idx;
+    for (int g = 0; g < nseg; ++g) {
+      const uint64_t* kk = kin + (uint64_t)g * stride;
+      const uint32_t* ii = iin + (uint64_t)g * stride;
+      const uint64_t c = s_cnt[g];
+      for (uint64_t wb = tid & ~63u; wb < c; wb += kTailThreads) {
+        const uint64_t j = wb + lane;
+        bool redo = false;
+        uint64_t k = 0;
+        uint32_t idx = 0;
+        if (j < c) {
+          k = kk[j];
+          idx = ii[j];
+          const uint64_t x = bb_index(seed, k, words, magic);
+          // Fallback path: the atomics ran at the memory side, so read back with an
+          // atomic as well (never a possibly stale cached line).
+          const uint32_t cw = in_lds ? C[x >> 5] : atomicAdd(&C[x >> 5], 0u);
+          redo = (cw >> (x & 31)) & 1u;
+          if (!redo) settle[idx] = woff * 64 + x;
+        }
+        const uint64_t m = __ballot(redo);
+        if (m) {
+          unsigned long long base = 0;
+          if (lane == 0) base = atomicAdd(&s_next, (unsigned long long)__popcll(m));
+          base = __shfl(base, 0);
+          if (redo) {
+            const uint64_t o = base + __popcll(m & lanemask_lt());
+            kout[o] = k;  // o < n <= buffer capacity
+            iout[o] = idx;
+          }
         }
       }
     }
@@ -329,6 +417,9 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(int big_launched, uint64_
       s_words = w1;
       s_woff = off1;
       s_magic = level_magic(w1);
+      s_nseg = 1;
+      s_stride = 0;
+      s_cnt[0] = n1;
     }
     __syncthreads();
   }
@@ -595,33 +686,58 @@ __global__ __launch_bounds__(kBlock) void k_dist_resolve(int level, const uint64
                                                          uint32_t* __restrict__ idx_out,
                                                          unsigned long long* out_count,
                                                          uint64_t* __restrict__ settle) {
+  __shared__ unsigned s_wcnt[kBlock / 64];
+  __shared__ unsigned long long s_wbase[kBlock / 64];
   const uint64_t seed = level_seed(level);
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  const unsigned lane = lane_id();
+  const unsigned lane = lane_id(), wave = threadIdx.x >> 6;
   const uint64_t* A = bits + woff;
-  for (uint64_t wbase = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); wbase < n;
-       wbase += stride) {
-    const uint64_t j = wbase + lane;
-    bool redo = false;
-    uint64_t k = 0;
-    uint32_t idx = 0;
-    if (j < n) {
-      k = keys_in[j];
-      idx = idx_in ? idx_in[j] : (uint32_t)j;
-      const uint64_t x = bb_index(seed, k, words, magic);
-      redo = !((A[x >> 6] >> (x & 63)) & 1ull);
-      if (!redo) settle[idx] = woff * 64 + x;
-    }
-    const uint64_t m = __ballot(redo);
-    if (m) {
-      unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(out_count, (unsigned long long)__popcll(m));
-      base = __shfl(base, 0);
-      if (redo) {
-        const uint64_t o = base + __popcll(m & lanemask_lt());
-        keys_out[o] = k;
-        idx_out[o] = idx;
+  constexpr uint64_t kTile = (uint64_t)kBlock * kResolveKPT;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * kTile; t0 < n; t0 += (uint64_t)gridDim.x * kTile) {
+    bool r[kResolveKPT];
+    uint64_t k[kResolveKPT];
+    uint32_t id[kResolveKPT];
+#pragma unroll
+    for (int q = 0; q < kResolveKPT; ++q) {
+      const uint64_t j = t0 + (uint64_t)q * kBlock + threadIdx.x;
+      r[q] = false;
+      k[q] = 0;
+      id[q] = 0;
+      if (j < n) {
+        k[q] = keys_in[j];
+        id[q] = idx_in ? idx_in[j] : (uint32_t)j;
+        const uint64_t x = bb_index(seed, k[q], words, magic);
+        r[q] = !((A[x >> 6] >> (x & 63)) & 1ull);
+        if (!r[q]) settle[id[q]] = woff * 64 + x;
       }
+    }
+    uint64_t m[kResolveKPT];
+    unsigned wc = 0;
+#pragma unroll
+    for (int q = 0; q < kResolveKPT; ++q) {
+      m[q] = __ballot(r[q]);
+      wc += __popcll(m[q]);
+    }
+    if (lane == 0) s_wcnt[wave] = wc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned tot = 0;
+      for (int w = 0; w < kBlock / 64; ++w) tot += s_wcnt[w];
+      unsigned long long base = tot ? atomicAdd(out_count, (unsigned long long)tot) : 0;
+      for (int w = 0; w < kBlock / 64; ++w) {
+        s_wbase[w] = base;
+        base += s_wcnt[w];
+      }
+    }
+    __syncthreads();
+    uint64_t o = s_wbase[wave];
+#pragma unroll
+    for (int q = 0; q < kResolveKPT; ++q) {
+      if (r[q]) {
+        const uint64_t slot = o + __popcll(m[q] & lanemask_lt());
+        keys_out[slot] = k[q];
+        idx_out[slot] = id[q];
+      }
+      o += __popcll(m[q]);
     }
   }
 }
@@ -717,7 +833,7 @@ int default_grid(uint64_t work, int block) {
 }
 
 void launch_init_state(LevelState* st, uint64_t n, uint64_t, hipStream_t s) {
-  k_init_state<<<1, 64, 0, s>>>(st, n);
+  k_init_state<<<1, 256, 0, s>>>(st, n);
 }
 
 void launch_hash_mark0(const uint8_t* blob, const uint64_t* offsets, uint64_t n, uint64_t* kh,
@@ -728,14 +844,15 @@ void launch_hash_mark0(const uint8_t* blob, const uint64_t* offsets, uint64_t n,
 }
 
 void launch_resolve(int level, const uint64_t* keys_in, const uint32_t* idx_in, const uint64_t* C,
-                    uint64_t* keys_out, uint32_t* idx_out, uint64_t out_cap, uint64_t* settle,
+                    uint64_t* keys_out, uint32_t* idx_out, uint64_t seg_cap, uint64_t* settle,
                     LevelState* st, unsigned long long gate, int grid, hipStream_t s) {
   const uint32_t* C32 = reinterpret_cast<const uint32_t*>(C);
+  grid = ((grid + kNSeg - 1) / kNSeg) * kNSeg;
   if (level == 0)
-    k_resolve<true><<<grid, kBlock, 0, s>>>(0, keys_in, nullptr, C32, keys_out, idx_out, out_cap, settle,
+    k_resolve<true><<<grid, kBlock, 0, s>>>(0, keys_in, nullptr, C32, keys_out, idx_out, seg_cap, settle,
                                             st, gate);
   else
-    k_resolve<false><<<grid, kBlock, 0, s>>>(level, keys_in, idx_in, C32, keys_out, idx_out, out_cap,
+    k_resolve<false><<<grid, kBlock, 0, s>>>(level, keys_in, idx_in, C32, keys_out, idx_out, seg_cap,
                                              settle, st, gate);
 }
 
@@ -744,16 +861,17 @@ void launch_finalize(int level, uint64_t* bits, uint64_t* C, uint64_t cap_words,
   k_finalize<<<grid, kBlock, 0, s>>>(level, bits, C, cap_words, st, gate);
 }
 
-void launch_mark(int level, const uint64_t* keys, uint64_t* bits, uint64_t* C, LevelState* st,
-                 unsigned long long gate, int grid, hipStream_t s) {
-  k_mark<<<grid, kBlock, 0, s>>>(level, keys, bits, reinterpret_cast<uint32_t*>(C), st, gate);
+void launch_mark(int level, const uint64_t* keys, uint64_t seg_cap, uint64_t* bits, uint64_t* C,
+                 LevelState* st, unsigned long long gate, int grid, hipStream_t s) {
+  grid = ((grid + kNSeg - 1) / kNSeg) * kNSeg;
+  k_mark<<<grid, kBlock, 0, s>>>(level, keys, seg_cap, bits, reinterpret_cast<uint32_t*>(C), st, gate);
 }
 
 void launch_tail(int big_launched, uint64_t* bits, uint64_t cap_words, uint64_t* C, uint64_t* keys0,
-                 uint32_t* idx0, uint64_t* keys1, uint32_t* idx1, uint64_t* settle, LevelState* st,
-                 hipStream_t s) {
+                 uint32_t* idx0, uint64_t* keys1, uint32_t* idx1, uint64_t seg_cap, uint64_t* settle,
+                 LevelState* st, hipStream_t s) {
   k_tail<<<1, kTailThreads, 0, s>>>(big_launched, bits, cap_words, reinterpret_cast<uint32_t*>(C), keys0,
-                                    idx0, keys1, idx1, settle, st);
+                                    idx0, keys1, idx1, seg_cap, settle, st);
 }
 
 void launch_rank_scan(const uint64_t* bits, uint64_t cap_words, uint64_t* rank_base,

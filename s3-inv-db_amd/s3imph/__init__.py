@@ -344,7 +344,13 @@ class DistBuilder(DeviceBuilder):
 
 
 def _stream_ptr(stream):
+    """hipStream_t for a call: an explicit stream, else torch's current stream when it is
+    not the legacy default (the library's own stream is blocking, hence already ordered
+    after work on the default stream)."""
     if stream is None:
+        if torch is not None and torch.cuda.is_initialized():
+            cur = torch.cuda.current_stream().cuda_stream
+            return ctypes.c_void_p(cur) if cur else None
         return None
     if isinstance(stream, int):
         return ctypes.c_void_p(stream)
