@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -40,15 +41,15 @@ CONFIGS = {
 
 
 def stage_alg_bytes(stage: str, n: int, key_bytes: int, info: dict) -> int | None:
-    """Algorithmic (minimum) HBM bytes of one launch of a stage, per SURVEY.md §8(d) units."""
-    if stage == "hash_mark0":   # key bytes + offsets read once; kh + fp written once
+    """Algorithmic (minimum) HBM bytes of one launch of a stage, per SURVEY.md §8(d) units.
+    Level 0 settles a fraction e^{-1/2} of the keys (gamma = 2); the rest move on."""
+    settled = math.exp(-0.5)
+    if stage == "hash_count0":  # key bytes + offsets read once; kh + fp written once
         return key_bytes + 8 * (n + 1) + 16 * n
-    if stage == "resolve0":     # kh read once; one u64 settle/redo record per key written
-        return 16 * n
-    if stage == "place":        # settle + fp read; fp_out + pos_out written (identity pos)
-        return 32 * n
-    if stage == "rank_scan":
-        return 16 * info.get("total_words", 0)
+    if stage == "scatter0":     # kh + fp read, (kh, fp, pos) record written to its tile bucket
+        return 16 * n + 24 * n
+    if stage == "tile0":        # bucket records read once; fp_out/pos_out or the next-level
+        return int(24 * n + 16 * settled * n + 24 * (1 - settled) * n + n // 4)  # record; bits
     return None
 
 

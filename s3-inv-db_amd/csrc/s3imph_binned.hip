@@ -1,0 +1,785 @@
+// s3imph_binned.hip — the single-GPU MPHF build as a position-binned level pipeline.
+//
+// Reference work replaced (/root/reference):
+//   StreamingMPHFBuilder.Add hashing (pkg/format/mphf_streaming.go:73,80; mphf.go:349-369),
+//   bbhash.New level construction (mphf_streaming.go:141; relab/bbhash restated in SURVEY App. A),
+//   computeHashPositionsReverseMap + the fingerprint/position scatter (mphf_streaming.go:176-204).
+//
+// Per big level L (n_L keys, 64*words_L positions, tiles of 2^tb positions):
+//   count    keys -> per-(tile, chunk) histogram (LDS atomics)
+//   hscan    exclusive scan of the histogram, tile-major -> bucket offsets
+//   scatter  records (kh, fp, pos) -> tile buckets.  Each 4096-key round is sorted by
+//            tile in LDS and written run by run, so consecutive lanes store consecutive
+//            slots; chunks are dealt to blocks XCD-contiguously so one L2 sees each
+//            bucket region.  No global atomics.
+//   tile     one workgroup per tile (ticket order): A/C bit vectors in LDS, final
+//            bits A & ~C written once; the tile's global rank prefix comes from a
+//            decoupled look-back over earlier tiles; settled keys write fp_out[p] /
+//            pos_out[p] directly (a tile's keys cover one contiguous p range);
+//            collided records go to the next level's list, one atomic per tile.
+// Small levels run in one workgroup (k_bin_tail) with everything in LDS.
+// Level bit vectors depend only on the SET of keys at each level, so every schedule
+// (bucket order, LDS atomic order, tile order) yields the same bytes.
+#include <hip/hip_runtime.h>
+
+#include "s3imph_device.h"
+#include "s3imph_internal.h"
+
+namespace s3imph {
+
+namespace {
+
+constexpr int kCB = 1024;             // count block
+constexpr int kSB = 1024;             // scatter block
+constexpr int kTB = 1024;             // tile block
+constexpr int kTailT = 1024;          // tail block
+constexpr uint64_t kLdsTiles = kMaxTiles;  // histogram / cursor entries in LDS
+constexpr unsigned long long kGate = kTailKeys;
+constexpr int kTailW32 = (int)(2 * ((kGammaNum * kTailKeys + 63) / 64));  // 4096 u32 words
+constexpr unsigned long long kFlagAgg = 1ull << 62;
+constexpr unsigned long long kFlagInc = 2ull << 62;
+constexpr unsigned long long kFlagVal = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint64_t ntiles_of(uint64_t words, unsigned tb) {
+  return (64 * words + (1ull << tb) - 1) >> tb;
+}
+
+// Sum over the block (NT a multiple of 64, <= 1024).
+template <int NT>
+__device__ __forceinline__ uint64_t block_sum(uint64_t v) {
+  __shared__ uint64_t s_red[NT / 64];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_down(v, d);
+  if (lane_id() == 0) s_red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t t = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) t += s_red[w];
+  __syncthreads();
+  return t;
+}
+
+// Exclusive scan over the block; *total receives the block sum.
+template <int NT>
+__device__ __forceinline__ uint64_t block_exscan(uint64_t v, uint64_t* total) {
+  __shared__ uint64_t s_w[NT / 64];
+  const unsigned lane = lane_id(), wave = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d);
+    if (lane >= (unsigned)d) x += y;
+  }
+  if (lane == 63) s_w[wave] = x;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    if ((unsigned)w < wave) pre += s_w[w];
+    tot += s_w[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+__device__ __forceinline__ bool geom_ok(LevelState* st, uint64_t T, uint64_t B) {
+  if (T > kLdsTiles || T * B > kHistCap) {
+    if (threadIdx.x == 0) atomicOr(&st->status, kStGeometry);
+    return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ bool level_active(int level, const LevelState* st) {
+  return (level == 0 || st->n[level] > kGate) &&
+         !(st->status & (kStGeometry | kStOverflow | kStLookback));
+}
+
+// ---------------------------------------------------------------- level 0 count ----
+// Hash every key (FNV-1a key hash + FNV-1 fingerprint, one pass over the bytes),
+// store both in key order, and histogram the level-0 tiles per chunk.
+__global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__ blob,
+                                                     const uint64_t* __restrict__ offsets, uint64_t n,
+                                                     uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
+                                                     unsigned* __restrict__ hist,
+                                                     unsigned long long* __restrict__ flags, LevelState* st,
+                                                     unsigned tb, uint64_t chunk) {
+  __shared__ unsigned sh[kLdsTiles];
+  const uint64_t words = st->words[0], magic = st->magic[0];
+  const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
+  if (!geom_ok(st, T, B)) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->ntiles[0] = T;
+    st->nchunks[0] = B;
+  }
+  for (uint64_t t = (uint64_t)blockIdx.x * kCB + threadIdx.x; t < T; t += (uint64_t)gridDim.x * kCB) flags[t] = 0;
+  const uint64_t seed = level_seed(0);
+  bool zero = false;
+  for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    for (uint64_t t = threadIdx.x; t < T; t += kCB) sh[t] = 0;
+    __syncthreads();
+    const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kCB) {
+      uint64_t h1, h2;
+      fnv_both(blob, offsets[i], offsets[i + 1], h1, h2);
+      kh[i] = h1;
+      fp[i] = h2;
+      zero |= (h1 == 0);
+      atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
+    }
+    __syncthreads();
+    for (uint64_t t = threadIdx.x; t < T; t += kCB) hist[t * B + b] = sh[t];
+    __syncthreads();
+  }
+  if (zero) atomicOr(&st->status, kStKeyZero);
+}
+
+// ------------------------------------------------------------- level L setup ---------
+// Size level L from the redo count the previous level produced and carry its word
+// offset (the rank base lvl_base[L] was published by the previous level's last tile).
+// Runs only after a big level (the tail sizes its own levels).
+__global__ void k_level_setup(int level, LevelState* st) {
+  const int p = level - 1;
+  if (threadIdx.x != 0) return;
+  if (p > 0 && st->n[p] <= kGate) return;
+  if (st->status & (kStGeometry | kStOverflow | kStLookback)) return;
+  const uint64_t n = st->n[level];
+  const uint64_t w = n ? level_words(n) : 0;
+  st->words[level] = w;
+  st->magic[level] = level_magic(w);
+  st->woff[level] = st->woff[p] + st->words[p];
+  st->woff[level + 1] = st->woff[level] + w;
+  st->nlevels = level;  // levels 0..level-1 are complete; raised again if level runs
+}
+
+// ------------------------------------------------------------ level L count ----------
+__global__ __launch_bounds__(kCB) void k_count(int level, const Rec* __restrict__ list,
+                                               unsigned* __restrict__ hist,
+                                               unsigned long long* __restrict__ flags, LevelState* st,
+                                               unsigned tb, uint64_t chunk, uint64_t cap_words) {
+  __shared__ unsigned sh[kLdsTiles];
+  const uint64_t n = st->n[level];
+  if (n <= kGate || (st->status & (kStGeometry | kStOverflow | kStLookback))) return;
+  const uint64_t words = st->words[level], magic = st->magic[level];
+  const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
+  if (!geom_ok(st, T, B)) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->ntiles[level] = T;
+    st->nchunks[level] = B;
+    if (st->woff[level] + words > cap_words) atomicOr(&st->status, kStOverflow);
+  }
+  for (uint64_t t = (uint64_t)blockIdx.x * kCB + threadIdx.x; t < T; t += (uint64_t)gridDim.x * kCB) flags[t] = 0;
+  const uint64_t seed = level_seed(level);
+  for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    for (uint64_t t = threadIdx.x; t < T; t += kCB) sh[t] = 0;
+    __syncthreads();
+    const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kCB)
+      atomicAdd(&sh[bb_index(seed, list[i].k, words, magic) >> tb], 1u);
+    __syncthreads();
+    for (uint64_t t = threadIdx.x; t < T; t += kCB) hist[t * B + b] = sh[t];
+    __syncthreads();
+  }
+}
+
+// --------------------------------------------------- histogram scan (tile-major) -----
+constexpr int kHS = 8;                 // entries per thread
+constexpr int kHSBlock = kCB * kHS;    // 2048 entries per scan block
+
+__global__ __launch_bounds__(kCB) void k_hscan_reduce(int level, const unsigned* __restrict__ hist,
+                                                      unsigned* __restrict__ sums, LevelState* st) {
+  if (!level_active(level, st)) return;
+  const uint64_t M = st->ntiles[level] * st->nchunks[level];
+  const uint64_t nb = (M + kHSBlock - 1) / kHSBlock;
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint64_t e0 = b * kHSBlock + (uint64_t)threadIdx.x * kHS;
+    uint64_t s = 0;
+#pragma unroll
+    for (int q = 0; q < kHS; ++q)
+      if (e0 + q < M) s += hist[e0 + q];
+    s = block_sum<kCB>(s);
+    if (threadIdx.x == 0) sums[b] = (unsigned)s;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_hscan_top(int level, unsigned* sums, LevelState* st) {
+  if (!level_active(level, st)) return;
+  const uint64_t M = st->ntiles[level] * st->nchunks[level];
+  const uint64_t nb = (M + kHSBlock - 1) / kHSBlock;
+  __shared__ uint64_t s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (uint64_t base = 0; base < nb; base += 1024) {
+    const uint64_t i = base + threadIdx.x;
+    const uint64_t v = i < nb ? sums[i] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_exscan<1024>(v, &tot);
+    const uint64_t carry = s_carry;
+    if (i < nb) sums[i] = (unsigned)(carry + ex);
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry = carry + tot;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kCB) void k_hscan_down(int level, const unsigned* __restrict__ hist,
+                                                    const unsigned* __restrict__ sums,
+                                                    unsigned* __restrict__ off,
+                                                    unsigned* __restrict__ tile_start, LevelState* st) {
+  if (!level_active(level, st)) return;
+  const uint64_t T = st->ntiles[level], B = st->nchunks[level], M = T * B;
+  const uint64_t nb = (M + kHSBlock - 1) / kHSBlock;
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint64_t e0 = b * kHSBlock + (uint64_t)threadIdx.x * kHS;
+    unsigned v[kHS];
+    uint64_t s = 0;
+#pragma unroll
+    for (int q = 0; q < kHS; ++q) {
+      v[q] = (e0 + q < M) ? hist[e0 + q] : 0u;
+      s += v[q];
+    }
+    uint64_t tot;
+    uint64_t run = sums[b] + block_exscan<kCB>(s, &tot);
+#pragma unroll
+    for (int q = 0; q < kHS; ++q) {
+      const uint64_t e = e0 + q;
+      if (e < M) {
+        off[e] = (unsigned)run;
+        if (e % B == 0) tile_start[e / B] = (unsigned)run;
+      }
+      run += v[q];
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) tile_start[T] = (unsigned)st->n[level];
+}
+
+// ------------------------------------------------------------------ scatter --------
+// LDS: 4096 staged records (96 KiB) + tile ids + per-round count/start + chunk cursors.
+constexpr int kScatterKPT = (int)(kSubRound / kSB);  // 4 keys per thread per round
+
+__global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __restrict__ ik,
+                                                 const uint64_t* __restrict__ ifp,
+                                                 const uint64_t* __restrict__ ipos, uint64_t pos_base,
+                                                 const Rec* __restrict__ ilist,
+                                                 const unsigned* __restrict__ off, Rec* __restrict__ bucket,
+                                                 LevelState* st, unsigned tb, uint64_t chunk) {
+  __shared__ Rec stage[kSubRound];
+  __shared__ unsigned short stile[kSubRound];
+  __shared__ unsigned cnt[kLdsTiles];
+  __shared__ unsigned start[kLdsTiles];
+  __shared__ unsigned cur[kLdsTiles];
+  if (!level_active(level, st)) return;
+  const uint64_t n = st->n[level];
+  const uint64_t words = st->words[level], magic = st->magic[level];
+  const uint64_t T = st->ntiles[level], B = st->nchunks[level];
+  const uint64_t seed = level_seed(level);
+  // XCD-contiguous chunk ranges: blocks b, b+8, b+16, ... (one XCD under round-robin
+  // dispatch) take one contiguous eighth of the chunks.  Speed only, never correctness.
+  const unsigned groups = gridDim.x >= 8 ? 8 : 1;
+  const uint64_t xcd = blockIdx.x % groups, r = blockIdx.x / groups, R = gridDim.x / groups;
+  const uint64_t per = (B + groups - 1) / groups;
+  const uint64_t g0 = min(B, xcd * per), g1 = min(B, g0 + per);
+  const uint64_t c0 = g0 + (g1 - g0) * r / R, c1 = g0 + (g1 - g0) * (r + 1) / R;
+  const unsigned tid = threadIdx.x;
+  for (uint64_t b = c0; b < c1; ++b) {
+    for (uint64_t t = tid; t < T; t += kSB) cur[t] = off[t * B + b];
+    const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
+    for (uint64_t r0 = lo; r0 < hi; r0 += kSubRound) {
+      for (uint64_t t = tid; t < T; t += kSB) cnt[t] = 0;
+      __syncthreads();
+      Rec rec[kScatterKPT];
+      unsigned tt[kScatterKPT], rk[kScatterKPT];
+#pragma unroll
+      for (int q = 0; q < kScatterKPT; ++q) {
+        const uint64_t i = r0 + (uint64_t)q * kSB + tid;
+        if (i < hi) {
+          if (ilist) {
+            rec[q] = ilist[i];
+          } else {
+            rec[q].k = ik[i];
+            rec[q].f = ifp[i];
+            rec[q].p = ipos ? ipos[i] : pos_base + i;
+          }
+          tt[q] = (unsigned)(bb_index(seed, rec[q].k, words, magic) >> tb);
+          rk[q] = atomicAdd(&cnt[tt[q]], 1u);
+        }
+      }
+      __syncthreads();
+      // exclusive scan of the round's per-tile counts (kLdsTiles / kSB tiles per thread)
+      constexpr int kTPT = (int)(kLdsTiles / kSB);
+      const uint64_t t0 = (uint64_t)kTPT * tid;
+      unsigned a[kTPT];
+      uint64_t sum = 0;
+#pragma unroll
+      for (int q = 0; q < kTPT; ++q) {
+        a[q] = t0 + q < T ? cnt[t0 + q] : 0u;
+        sum += a[q];
+      }
+      uint64_t tot;
+      uint64_t ex = block_exscan<kSB>(sum, &tot);
+#pragma unroll
+      for (int q = 0; q < kTPT; ++q) {
+        if (t0 + q < T) start[t0 + q] = (unsigned)ex;
+        ex += a[q];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < kScatterKPT; ++q) {
+        const uint64_t i = r0 + (uint64_t)q * kSB + tid;
+        if (i < hi) {
+          const unsigned slot = start[tt[q]] + rk[q];
+          stage[slot] = rec[q];
+          stile[slot] = (unsigned short)tt[q];
+        }
+      }
+      __syncthreads();
+      const unsigned m = (unsigned)min<uint64_t>(kSubRound, hi - r0);
+      for (unsigned j = tid; j < m; j += kSB) {
+        const unsigned t = stile[j];
+        bucket[cur[t] + (j - start[t])] = stage[j];
+      }
+      __syncthreads();
+      for (uint64_t t = tid; t < T; t += kSB) cur[t] += cnt[t];
+      __syncthreads();
+    }
+  }
+}
+
+// --------------------------------------------------------------------- tile --------
+// dyn LDS: A[tpw], C[tpw] u32 (C becomes the per-word rank prefix after finalize);
+// for tiles of <= 2^kCacheBits positions also loc[kCache] u16 (each record's
+// in-tile position), ridx[kCache] u16 (rank -> record) and a redo bitmask.
+constexpr unsigned kCacheBits = 15;
+// Records cached per tile: a tile of 2^tb positions holds 2^tb / 2 keys on average
+// (gamma = 2), so 5/8 of 2^tb covers it with > 30 sigma to spare.
+__host__ __device__ constexpr unsigned cache_keys(unsigned tb) { return (5u << tb) / 8; }
+constexpr int kTU = 4;                         // loads in flight per lane
+
+// Decoupled look-back run by one wave: lane i inspects tile (t-1-i) of the current
+// 64-tile window; the window's aggregates up to the nearest inclusive prefix are summed
+// with one ballot, otherwise the window slides back 64 tiles.  Returns the exclusive
+// prefix of tile t and publishes its inclusive prefix.
+__device__ __forceinline__ unsigned long long look_back_wave(unsigned long long* flags, uint64_t t, uint64_t pop,
+                                                             LevelState* st) {
+  const unsigned lane = lane_id();
+  if (t == 0) {
+    if (lane == 0) __hip_atomic_store(&flags[0], kFlagInc | pop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0) __hip_atomic_store(&flags[t], kFlagAgg | pop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t excl = 0;
+  int64_t top = (int64_t)t - 1;  // newest tile of the window
+  uint64_t spins = 0;
+  while (top >= 0) {
+    const int64_t q = top - (int64_t)lane;
+    unsigned long long v = kFlagInc;  // lanes past tile 0 act as an inclusive zero
+    if (q >= 0) v = __hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t not_ready = __ballot((v & ~kFlagVal) == 0);
+    const uint64_t inc = __ballot((v & ~kFlagVal) == kFlagInc);
+    // lanes up to (and including) the first inclusive one, if every one of them is ready
+    const uint64_t upto = inc ? (inc & (~inc + 1)) * 2 - 1 : ~0ull;
+    if (not_ready & upto) {
+      if (++spins > (1ull << 24)) {  // bounded: a lost predecessor must not hang the GPU
+        if (lane == 0) atomicOr(&st->status, kStLookback);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    uint64_t part = ((upto >> lane) & 1ull) && q >= 0 ? (v & kFlagVal) : 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d);
+    excl += part;
+    if (inc) break;
+    top -= 64;
+  }
+  if (lane == 0) __hip_atomic_store(&flags[t], kFlagInc | (excl + pop), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
+__global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__ bucket,
+                                              const unsigned* __restrict__ tile_start,
+                                              unsigned long long* flags, uint64_t* __restrict__ bits,
+                                              Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
+                                              uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb) {
+  extern __shared__ uint32_t dyn[];
+  __shared__ unsigned long long s_t, s_prefix;
+  __shared__ unsigned s_wc[kTB / 64];
+  __shared__ unsigned long long s_wbase[kTB / 64];
+  if (!level_active(level, st)) return;
+  const uint64_t N = st->n[0];
+  const uint64_t words = st->words[level], magic = st->magic[level];
+  const uint64_t T = st->ntiles[level];
+  const uint64_t w32_level = 2 * words;
+  const unsigned tpw = 1u << (tb - 5);
+  const unsigned per = (tpw + kTB - 1) / kTB;
+  uint32_t* sA = dyn;
+  uint32_t* sC = dyn + tpw;
+  const bool small = tb <= kCacheBits;
+  const unsigned kcap = small ? cache_keys(tb) : 0;
+  unsigned short* sloc = reinterpret_cast<unsigned short*>(dyn + 2 * tpw);
+  unsigned short* sridx = sloc + kcap;
+  uint64_t* srm = reinterpret_cast<uint64_t*>(sridx + kcap);  // kcap / 64 words
+  uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[level]);
+  const uint64_t seed = level_seed(level);
+  const uint64_t lvl_base = st->lvl_base[level];
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  bool bad = false;
+  for (;;) {
+    if (tid == 0) s_t = atomicAdd(&st->ticket[level], 1ull);
+    for (unsigned w = tid; w < tpw; w += kTB) {
+      sA[w] = 0;
+      sC[w] = 0;
+    }
+    __syncthreads();
+    const uint64_t t = s_t;
+    if (t >= T) break;
+    const uint64_t lo = tile_start[t], hi = tile_start[t + 1];
+    const uint64_t nk = hi - lo;
+    const Rec* rb = bucket + lo;
+    const uint64_t tbase = t << tb;
+    const bool cached = small && nk <= kcap;
+    // ---- mark: A/C in LDS (and each record's in-tile position, when cached)
+    for (uint64_t j0 = tid; j0 < nk; j0 += (uint64_t)kTB * kTU) {
+      uint64_t k[kTU];
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        const uint64_t j = j0 + (uint64_t)u * kTB;
+        k[u] = j < nk ? rb[j].k : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        const uint64_t j = j0 + (uint64_t)u * kTB;
+        if (j < nk) {
+          const unsigned loc = (unsigned)(bb_index(seed, k[u], words, magic) - tbase);
+          if (cached) sloc[j] = (unsigned short)loc;
+          const uint32_t bit = 1u << (loc & 31);
+          const uint32_t old = atomicOr(&sA[loc >> 5], bit);
+          if (old & bit) atomicOr(&sC[loc >> 5], bit);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- finalize: A & ~C -> LDS + global bits; per-word rank prefix into C
+    const unsigned w0 = tid * per;
+    uint64_t cntw = 0;
+    for (unsigned q = 0; q < per; ++q) {
+      const unsigned w = w0 + q;
+      if (w < tpw) {
+        const uint32_t v = sA[w] & ~sC[w];
+        sA[w] = v;
+        const uint64_t gw = (uint64_t)t * tpw + w;
+        if (gw < w32_level) g32[gw] = v;
+        cntw += __popc(v);
+      }
+    }
+    uint64_t pop;
+    uint64_t run = block_exscan<kTB>(cntw, &pop);
+    for (unsigned q = 0; q < per; ++q) {
+      const unsigned w = w0 + q;
+      if (w < tpw) {
+        sC[w] = (uint32_t)run;
+        run += __popc(sA[w]);
+      }
+    }
+    if (wave == 0) {
+      const uint64_t excl = look_back_wave(flags, t, pop, st);
+      if (lane == 0) {
+        if (t == T - 1) st->lvl_base[level + 1] = lvl_base + excl + pop;
+        s_prefix = excl;
+      }
+    }
+    __syncthreads();
+    const uint64_t base = lvl_base + s_prefix;
+    unsigned wc = 0;
+    if (cached) {
+      // ---- rank pass (LDS only): rank -> record index; redo bitmask by ballot
+      for (uint64_t jb = wave * 64; jb < nk; jb += kTB) {
+        const uint64_t j = jb + lane;
+        bool redo = false;
+        if (j < nk) {
+          const unsigned loc = sloc[j];
+          const uint32_t wv = sA[loc >> 5];
+          const uint32_t bit = 1u << (loc & 31);
+          if (wv & bit) {
+            sridx[sC[loc >> 5] + __popc(wv & (bit - 1))] = (unsigned short)j;
+          } else {
+            redo = true;
+          }
+        }
+        const uint64_t m = __ballot(redo);
+        if (lane == 0) srm[jb >> 6] = m;
+        wc += __popcll(m);
+      }
+      __syncthreads();
+      // ---- outputs: consecutive ranks -> consecutive fp_out/pos_out slots
+      if (base + pop > N) bad = true;
+      for (uint64_t r0 = tid; r0 < pop && base + pop <= N; r0 += (uint64_t)kTB * kTU) {
+        Rec rc[kTU];
+#pragma unroll
+        for (int u = 0; u < kTU; ++u) {
+          const uint64_t r = r0 + (uint64_t)u * kTB;
+          if (r < pop) rc[u] = rb[sridx[r]];
+        }
+#pragma unroll
+        for (int u = 0; u < kTU; ++u) {
+          const uint64_t r = r0 + (uint64_t)u * kTB;
+          if (r < pop) {
+            fp_out[base + r] = rc[u].f;
+            pos_out[base + r] = rc[u].p;
+          }
+        }
+      }
+    } else {
+      // ---- generic path (tiles too big to cache): rehash, write outputs in place
+      for (uint64_t jb = wave * 64; jb < nk; jb += kTB) {
+        const uint64_t j = jb + lane;
+        bool redo = false;
+        if (j < nk) {
+          const Rec rc = rb[j];
+          const unsigned loc = (unsigned)(bb_index(seed, rc.k, words, magic) - tbase);
+          const uint32_t wv = sA[loc >> 5];
+          const uint32_t bit = 1u << (loc & 31);
+          if (wv & bit) {
+            const uint64_t p = base + sC[loc >> 5] + __popc(wv & (bit - 1));
+            if (p < N) {
+              fp_out[p] = rc.f;
+              pos_out[p] = rc.p;
+            } else {
+              bad = true;
+            }
+          } else {
+            redo = true;
+          }
+        }
+        wc += __popcll(__ballot(redo));
+      }
+    }
+    // ---- collided records -> next level (one reservation per tile, per-wave offsets)
+    if (lane == 0) s_wc[wave] = wc;
+    __syncthreads();
+    if (tid == 0) {
+      unsigned tot = 0;
+      for (int w = 0; w < kTB / 64; ++w) tot += s_wc[w];
+      unsigned long long b0 = tot ? atomicAdd(&st->n[level + 1], (unsigned long long)tot) : 0;
+      for (int w = 0; w < kTB / 64; ++w) {
+        s_wbase[w] = b0;
+        b0 += s_wc[w];
+      }
+    }
+    __syncthreads();
+    if (wc) {
+      uint64_t o = s_wbase[wave];
+      for (uint64_t jb = wave * 64; jb < nk; jb += kTB) {
+        const uint64_t j = jb + lane;
+        uint64_t m;
+        if (cached) {
+          m = srm[jb >> 6];
+        } else {
+          bool redo = false;
+          if (j < nk) {
+            const unsigned loc = (unsigned)(bb_index(seed, rb[j].k, words, magic) - tbase);
+            redo = !((sA[loc >> 5] >> (loc & 31)) & 1u);
+          }
+          m = __ballot(redo);
+        }
+        if ((m >> lane) & 1ull) next[o + __popcll(m & lanemask_lt())] = rb[j];
+        o += __popcll(m);
+      }
+    }
+    __syncthreads();
+  }
+  if (bad) atomicOr(&st->status, kStRank);
+}
+
+// --------------------------------------------------------------------- tail --------
+// Every remaining level in one workgroup: A/C and the rank prefix in LDS, outputs
+// written directly, collided records compacted into the other list.
+__global__ __launch_bounds__(kTailT) void k_bin_tail(int big_launched, Rec* list0, Rec* list1, uint64_t* bits,
+                                                     uint64_t cap_words, uint64_t* __restrict__ fp_out,
+                                                     uint64_t* __restrict__ pos_out, LevelState* st) {
+  __shared__ uint32_t sA[kTailW32];
+  __shared__ uint32_t sC[kTailW32];
+  __shared__ uint32_t spre[kTailW32];
+  __shared__ unsigned long long s_n, s_next;
+  __shared__ int s_level;
+  const unsigned tid = threadIdx.x, lane = lane_id();
+  if (tid == 0) {
+    int L = 1;
+    while (L <= big_launched && st->n[L] > kGate) ++L;
+    s_level = L;
+    s_n = st->n[L];
+    if (st->status & (kStGeometry | kStOverflow | kStLookback)) s_n = 0;
+    if (s_n > kTailKeys) {
+      atomicOr(&st->status, kStTailOverflow);
+      s_n = 0;
+    }
+    st->tail_first = L;
+  }
+  __syncthreads();
+  const uint64_t N = st->n[0];
+  bool bad = false;
+  for (;;) {
+    const int L = s_level;
+    const uint64_t n = s_n;
+    if (n == 0) break;
+    if (L >= kMaxLevels) {
+      if (tid == 0) atomicOr(&st->status, kStTooManyLevels);
+      break;
+    }
+    const uint64_t words = st->words[L], magic = st->magic[L], woff = st->woff[L];
+    const uint64_t base = st->lvl_base[L];
+    const unsigned w32 = (unsigned)(2 * words);
+    const Rec* in = (L & 1) ? list0 : list1;  // level L's records were written by level L-1
+    Rec* out = (L & 1) ? list1 : list0;
+    for (unsigned w = tid; w < w32; w += kTailT) {
+      sA[w] = 0;
+      sC[w] = 0;
+    }
+    if (tid == 0) s_next = 0;
+    __syncthreads();
+    const uint64_t seed = level_seed(L);
+    for (uint64_t j0 = tid; j0 < n; j0 += (uint64_t)kTailT * kTU) {
+      uint64_t k[kTU];
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        const uint64_t j = j0 + (uint64_t)u * kTailT;
+        k[u] = j < n ? in[j].k : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        if (j0 + (uint64_t)u * kTailT < n) {
+          const uint64_t x = bb_index(seed, k[u], words, magic);
+          const uint32_t bit = 1u << (x & 31);
+          const uint32_t old = atomicOr(&sA[x >> 5], bit);
+          if (old & bit) atomicOr(&sC[x >> 5], bit);
+        }
+      }
+    }
+    __syncthreads();
+    constexpr unsigned kPer = kTailW32 / kTailT;
+    uint64_t cnt = 0;
+    uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + woff);
+    for (unsigned q = 0; q < kPer; ++q) {
+      const unsigned w = tid * kPer + q;
+      if (w < w32) {
+        const uint32_t v = sA[w] & ~sC[w];
+        sA[w] = v;
+        g32[w] = v;
+        cnt += __popc(v);
+      }
+    }
+    uint64_t tot;
+    uint64_t run = block_exscan<kTailT>(cnt, &tot);
+    for (unsigned q = 0; q < kPer; ++q) {
+      const unsigned w = tid * kPer + q;
+      if (w < w32) {
+        spre[w] = (uint32_t)run;
+        run += __popc(sA[w]);
+      }
+    }
+    __syncthreads();
+    for (uint64_t jb = tid & ~63u; jb < n; jb += kTailT) {
+      const uint64_t j = jb + lane;
+      bool r = false;
+      Rec rc{0, 0, 0};
+      if (j < n) {
+        rc = in[j];
+        const uint64_t x = bb_index(seed, rc.k, words, magic);
+        const uint32_t wv = sA[x >> 5];
+        const uint32_t bit = 1u << (x & 31);
+        if (wv & bit) {
+          const uint64_t q = base + spre[x >> 5] + __popc(wv & (bit - 1));
+          if (q < N) {
+            fp_out[q] = rc.f;
+            pos_out[q] = rc.p;
+          } else {
+            bad = true;
+          }
+        } else {
+          r = true;
+        }
+      }
+      const uint64_t m = __ballot(r);
+      if (m) {
+        unsigned long long o = 0;
+        if (lane == 0) o = atomicAdd(&s_next, (unsigned long long)__popcll(m));
+        o = __shfl(o, 0);
+        if (r) out[o + __popcll(m & lanemask_lt())] = rc;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const uint64_t n1 = s_next;
+      const uint64_t w1 = n1 ? level_words(n1) : 0;
+      st->n[L + 1] = n1;
+      st->words[L + 1] = w1;
+      st->magic[L + 1] = level_magic(w1);
+      st->woff[L + 1] = woff + words;
+      st->woff[L + 2] = woff + words + w1;
+      st->lvl_base[L + 1] = base + tot;
+      st->nlevels = L + 1;
+      if (woff + words + w1 > cap_words) {
+        atomicOr(&st->status, kStOverflow);
+        s_n = 0;
+      } else {
+        s_n = n1;
+      }
+      s_level = L + 1;
+    }
+    __syncthreads();
+  }
+  if (bad) atomicOr(&st->status, kStRank);
+  if (tid == 0) st->rank_total = st->lvl_base[s_level];
+}
+
+size_t tile_lds_bytes(unsigned tb) {
+  const size_t ac = 2ull * (1ull << (tb - 5)) * sizeof(uint32_t);
+  const size_t kc = cache_keys(tb);
+  return tb <= kCacheBits ? ac + 2 * kc * sizeof(unsigned short) + (kc / 64 + 1) * sizeof(uint64_t) : ac;
+}
+
+}  // namespace
+
+void binned_set_lds_limits() {
+  (void)hipFuncSetAttribute((const void*)k_tile, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)tile_lds_bytes(kTileMaxBits));
+}
+
+void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
+                         LevelGeom g, int grid_chunks, hipStream_t s) {
+  if (level == 0) {
+    k_hash_count0<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.st, g.tb,
+                                              g.chunk);
+  } else {
+    k_level_setup<<<1, 64, 0, s>>>(level, b.st);
+    k_count<<<grid_chunks, kCB, 0, s>>>(level, b.list[(level - 1) & 1], b.hist, b.flags, b.st, g.tb, g.chunk,
+                                        b.cap_words);
+  }
+}
+
+void launch_binned_scan(int level, const BinBuffers& b, hipStream_t s) {
+  const int hs_grid = 256;
+  k_hscan_reduce<<<hs_grid, kCB, 0, s>>>(level, b.hist, b.scan_sums, b.st);
+  k_hscan_top<<<1, 1024, 0, s>>>(level, b.scan_sums, b.st);
+  k_hscan_down<<<hs_grid, kCB, 0, s>>>(level, b.hist, b.scan_sums, b.off, b.tile_start, b.st);
+}
+
+void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s) {
+  const Rec* il = level == 0 ? nullptr : b.list[(level - 1) & 1];
+  k_scatter<<<256, kSB, 0, s>>>(level, b.kh, b.fp, b.pos, b.pos_base, il, b.off, b.bucket, b.st, g.tb, g.chunk);
+}
+
+void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s) {
+  k_tile<<<grid_tiles, kTB, tile_lds_bytes(g.tb), s>>>(level, b.bucket, b.tile_start, b.flags, b.bits,
+                                                       b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb);
+}
+
+void launch_binned_tail(int big_launched, const BinBuffers& b, hipStream_t s) {
+  k_level_setup<<<1, 64, 0, s>>>(big_launched + 1, b.st);
+  k_bin_tail<<<1, kTailT, 0, s>>>(big_launched, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out, b.pos_out,
+                                  b.st);
+}
+
+}  // namespace s3imph

@@ -59,14 +59,21 @@ struct s3imph_ctx {
   hipStream_t own_stream = nullptr;
   std::mutex mu;
 
-  uint64_t cap_keys = 0, cap_words = 0, cap_blocks = 0, seg_cap = 0;
-  uint64_t *kh = nullptr, *fp = nullptr, *settle = nullptr, *C = nullptr, *bits = nullptr,
-           *rank_base = nullptr;
-  uint64_t* rkeys[2] = {nullptr, nullptr};
+  uint64_t cap_keys = 0, cap_words = 0, cap_blocks = 0;
+  uint64_t *kh = nullptr, *fp = nullptr, *settle = nullptr, *bits = nullptr, *rank_base = nullptr;
+  uint64_t* rkeys[2] = {nullptr, nullptr};   // multi-GPU redo lists
   uint32_t* ridx[2] = {nullptr, nullptr};
   unsigned long long* block_sums = nullptr;
   LevelState* d_st = nullptr;
   LevelState* h_st = nullptr;
+  bool rank_valid = false;                   // rank_base matches the last build
+
+  // single-GPU binned pipeline (s3imph_binned.hip)
+  Rec* bucket = nullptr;
+  Rec* list[2] = {nullptr, nullptr};
+  unsigned *hist = nullptr, *hoff = nullptr, *tile_start = nullptr, *scan_sums = nullptr;
+  unsigned long long* flags = nullptr;
+  bool lds_attr_set = false;
 
   // staging for host-memory builds
   uint8_t* s_blob = nullptr;
@@ -150,38 +157,44 @@ uint64_t cap_words_for(uint64_t n) {
   return (n * 5) / 64 + 4 * (uint64_t)kMaxLevels + 64;
 }
 
-void ensure_workspace(s3imph_ctx* c, uint64_t n) {
-  if (n <= c->cap_keys && c->d_st) return;
-  uint64_t cap = std::max<uint64_t>(n, 1024);
-  dalloc(c->kh, cap);
-  dalloc(c->fp, cap);
-  dalloc(c->settle, cap);
-  // Redo lists: kNSeg segments of seg_cap entries (segment s of level L+1 only ever
-  // receives keys from segment s of level L, which holds <= ceil(n/kNSeg) keys).
-  c->seg_cap = (cap + kNSeg - 1) / kNSeg + 1;
-  dalloc(c->rkeys[0], c->seg_cap * kNSeg);
-  dalloc(c->rkeys[1], c->seg_cap * kNSeg);
-  dalloc(c->ridx[0], c->seg_cap * kNSeg);
-  dalloc(c->ridx[1], c->seg_cap * kNSeg);
-  dalloc(c->C, level_words(cap) + 64);
-  c->cap_words = cap_words_for(cap);
-  dalloc(c->bits, c->cap_words);
-  dalloc(c->rank_base, c->cap_words);
-  c->cap_blocks = (c->cap_words + 2047) / 2048 + 1;
-  dalloc(c->block_sums, c->cap_blocks);
+void alloc_common(s3imph_ctx* c, uint64_t n_global) {
+  c->cap_words = cap_words_for(std::max<uint64_t>(n_global, 1024));
   if (!c->d_st) dalloc(c->d_st, 1);
   if (!c->h_st) {
     void* h = nullptr;
     HIPCHECK(hipHostMalloc(&h, sizeof(LevelState), hipHostMallocDefault));
     c->h_st = static_cast<LevelState*>(h);
   }
+}
+
+// Single-GPU workspace: ~88 B per key (level-0 list, tile buckets, two next-level lists).
+void ensure_workspace(s3imph_ctx* c, uint64_t n) {
+  if (n <= c->cap_keys && c->hist) return;
+  const uint64_t cap = std::max<uint64_t>(n, 1024);
+  dalloc(c->kh, cap);
+  dalloc(c->fp, cap);
+  dalloc(c->bucket, cap);
+  dalloc(c->list[0], cap);
+  dalloc(c->list[1], cap);
+  dalloc(c->hist, kHistCap);
+  dalloc(c->hoff, kHistCap);
+  dalloc(c->tile_start, kMaxTiles + 2);
+  dalloc(c->scan_sums, kHistCap / 2048 + 2);
+  dalloc(c->flags, kMaxTiles + 2);
+  alloc_common(c, cap);
+  dalloc(c->bits, c->cap_words);
+  dalloc(c->rank_base, c->cap_words);
+  c->cap_blocks = (c->cap_words + 2047) / 2048 + 1;
+  dalloc(c->block_sums, c->cap_blocks);
   c->cap_keys = cap;
 }
 
 void free_workspace(s3imph_ctx* c) {
-  dfree(c->kh); dfree(c->fp); dfree(c->settle);
+  dfree(c->kh); dfree(c->fp); dfree(c->settle); dfree(c->bits); dfree(c->rank_base);
   dfree(c->rkeys[0]); dfree(c->rkeys[1]); dfree(c->ridx[0]); dfree(c->ridx[1]);
-  dfree(c->C); dfree(c->bits); dfree(c->rank_base); dfree(c->block_sums); dfree(c->d_st);
+  dfree(c->block_sums); dfree(c->d_st);
+  dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
+  dfree(c->hist); dfree(c->hoff); dfree(c->tile_start); dfree(c->scan_sums); dfree(c->flags);
   if (c->h_st) (void)hipHostFree(c->h_st);
   c->h_st = nullptr;
   dfree(c->s_blob); dfree(c->s_offsets); dfree(c->s_pos); dfree(c->s_fp); dfree(c->s_posout);
@@ -257,17 +270,87 @@ int map_status(s3imph_ctx* c, unsigned flags, uint64_t n, std::string* msg) {
     *msg = "MPHF Key(...) returned 0, possible hash collision with sentinel";
     return S3IMPH_ERR_KEY_HASH_ZERO;
   }
-  if (flags & kStRank) {
-    *msg = "build MPHF: internal rank error";
+  if (flags) {
+    *msg = "build MPHF: internal error (device flags " + std::to_string(flags) + ")";
     return S3IMPH_ERR_INTERNAL;
   }
   return S3IMPH_OK;
+}
+
+// Enqueue one attempt of the binned pipeline.  `conservative` sizes every level with
+// the level-0 geometry (always inside the workspace bounds) and runs every level that
+// is still big as a full-grid level; the default predicts each level's size.
+void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
+                    uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
+  BinBuffers b{};
+  b.kh = c->kh;
+  b.fp = c->fp;
+  b.pos = pos;
+  b.pos_base = 0;
+  b.bucket = c->bucket;
+  b.list[0] = c->list[0];
+  b.list[1] = c->list[1];
+  b.hist = c->hist;
+  b.off = c->hoff;
+  b.tile_start = c->tile_start;
+  b.scan_sums = c->scan_sums;
+  b.flags = c->flags;
+  b.bits = c->bits;
+  b.cap_words = c->cap_words;
+  b.fp_out = fp_out;
+  b.pos_out = pos_out;
+  b.st = c->d_st;
+
+  const double q = 1.0 - std::exp(-0.5);  // fraction of keys that collide at load 1/2
+  const LevelGeom g0 = choose_geom(n);
+  auto grids = [](uint64_t nk, LevelGeom g, int* gc, int* gt) {
+    const uint64_t T = (64 * level_words(nk ? nk : 1) + (1ull << g.tb) - 1) >> g.tb;
+    *gc = (int)std::min<uint64_t>(std::max<uint64_t>((nk + g.chunk - 1) / g.chunk, 1), 2048);
+    *gt = (int)std::min<uint64_t>(std::max<uint64_t>(T, 1), 2048);
+  };
+  int gc, gt;
+  launch_init_state(c->d_st, n, 0, s);
+  ev_mark(c, s, "init");
+  grids(n, g0, &gc, &gt);
+  launch_binned_count(0, blob, offsets, n, b, g0, gc, s);
+  ev_mark(c, s, "hash_count0");
+  launch_binned_scan(0, b, s);
+  ev_mark(c, s, "hscan0");
+  launch_binned_scatter(0, b, g0, s);
+  ev_mark(c, s, "scatter0");
+  launch_binned_tile(0, b, g0, gt, s);
+  ev_mark(c, s, "tile0");
+  const int big = conservative ? kMaxLevels - 2 : predict_big_levels(n);
+  int launched = 0;
+  for (int L = 1; L <= big; ++L) {
+    const double pred = (double)n * std::pow(q, L);
+    if (!conservative && pred < 0.25 * (double)kTailKeys) break;
+    launched = L;
+    const uint64_t nb = conservative ? n : (uint64_t)(pred * 1.1) + 4096;
+    const LevelGeom g = conservative ? g0 : choose_geom(nb);
+    grids(nb, g, &gc, &gt);
+    launch_binned_count(L, nullptr, nullptr, 0, b, g, gc, s);
+    launch_binned_scan(L, b, s);
+    launch_binned_scatter(L, b, g, s);
+    launch_binned_tile(L, b, g, gt, s);
+  }
+  ev_mark(c, s, "levels");
+  launch_binned_tail(launched, b, s);
+  ev_mark(c, s, "tail");
+}
+
+void set_lds_attrs(s3imph_ctx* c) {
+  if (c->lds_attr_set) return;
+  // The tile kernels take up to 2 x 64 KiB of dynamic LDS (tiles of 2^19 positions).
+  binned_set_lds_limits();
+  c->lds_attr_set = true;
 }
 
 int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                  uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s,
                  s3imph_build_info* info, std::string* msg) {
   c->have_build = false;
+  c->rank_valid = false;
   *info = s3imph_build_info{};
   info->n_keys = n;
   if (n == 0) {
@@ -281,41 +364,20 @@ int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
     return S3IMPH_ERR_INVALID;
   }
   ensure_workspace(c, n);
-  const uint64_t words0 = level_words(n);
-  const int grid = default_grid(n, 256);
-  const int big = predict_big_levels(n);
-  ev_begin(c);
-  ev_mark(c, s, "start");
-  HIPCHECK(hipMemsetAsync(c->bits, 0, c->cap_words * 8, s));
-  HIPCHECK(hipMemsetAsync(c->C, 0, words0 * 8, s));
-  launch_init_state(c->d_st, n, 0, s);
-  ev_mark(c, s, "init");
-  launch_hash_mark0(blob, offsets, n, c->kh, c->fp, c->bits, c->C, words0, c->d_st, grid, s);
-  ev_mark(c, s, "hash_mark0");
-  launch_resolve(0, c->kh, nullptr, c->C, c->rkeys[0], c->ridx[0], c->seg_cap, c->settle, c->d_st,
-                 kTailKeys, grid, s);
-  launch_finalize(0, c->bits, c->C, c->cap_words, c->d_st, kTailKeys, default_grid(words0, 256), s);
-  ev_mark(c, s, "resolve0");
-  for (int L = 1; L <= big; ++L) {
-    const int g = std::max(kNSeg, std::min(grid, (int)(grid * std::pow(0.3935, L) * 1.5) + 1));
-    launch_mark(L, c->rkeys[(L - 1) & 1], c->seg_cap, c->bits, c->C, c->d_st, kTailKeys, g, s);
-    launch_resolve(L, c->rkeys[(L - 1) & 1], c->ridx[(L - 1) & 1], c->C, c->rkeys[L & 1],
-                   c->ridx[L & 1], c->seg_cap, c->settle, c->d_st, kTailKeys, g, s);
-    launch_finalize(L, c->bits, c->C, c->cap_words, c->d_st, kTailKeys, g, s);
+  set_lds_attrs(c);
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    ev_begin(c);
+    ev_mark(c, s, "start");
+    enqueue_binned(c, blob, offsets, pos, n, fp_out, pos_out, s, attempt > 0);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(c->h_st, c->d_st, sizeof(LevelState), hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    ev_collect(c);
+    // Geometry/tail-capacity misses only mean the level-size prediction was off:
+    // rerun with workspace-safe geometry (same bytes, slower schedule).
+    if (c->h_st->status & (kStGeometry | kStTailOverflow)) continue;
+    break;
   }
-  ev_mark(c, s, "levels");
-  launch_tail(big, c->bits, c->cap_words, c->C, c->rkeys[0], c->ridx[0], c->rkeys[1], c->ridx[1],
-              c->seg_cap, c->settle, c->d_st, s);
-  ev_mark(c, s, "tail");
-  launch_rank_scan(c->bits, c->cap_words, c->rank_base, c->block_sums, c->cap_blocks, c->d_st, s);
-  ev_mark(c, s, "rank_scan");
-  launch_place(n, c->settle, c->fp, pos, 0, c->bits, c->rank_base, fp_out, pos_out, c->d_st, grid, s);
-  ev_mark(c, s, "place");
-  HIPCHECK(hipGetLastError());
-  HIPCHECK(hipMemcpyAsync(c->h_st, c->d_st, sizeof(LevelState), hipMemcpyDeviceToHost, s));
-  HIPCHECK(hipStreamSynchronize(s));
-  ev_collect(c);
-
   const LevelState& st = *c->h_st;
   int rc = map_status(c, st.status, n, msg);
   if (rc != S3IMPH_OK) return rc;
@@ -328,7 +390,7 @@ int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   info->num_levels = st.nlevels;
   info->total_words = st.woff[st.nlevels];
   info->mph_bin_len = 8 * kPartitions + 8 + 8ull * st.nlevels + 8ull * info->total_words;
-  info->big_levels = st.tail_first ? st.tail_first - 1 : 0;
+  info->big_levels = st.tail_first ? st.tail_first : st.nlevels;
   c->have_build = true;
   c->last_n = n;
   c->info = *info;
@@ -408,6 +470,7 @@ int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
   DistState& d = c->d;
   const int P = d.nranks, R = d.rank;
   c->have_build = false;
+  c->rank_valid = false;
   *info = s3imph_build_info{};
   if (n_local > kU32Limit) {
     *msg = "build MPHF: more than 2^32-1 keys on one rank";
@@ -499,6 +562,7 @@ int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
   d.h_pinned[2] = woff;
   HIPCHECK(hipMemcpyAsync(d.counters + 4, d.h_pinned + 2, 8, hipMemcpyHostToDevice, s));
   launch_words_scan(c->bits, woff, c->rank_base, c->block_sums, d.counters + 4, s);
+  c->rank_valid = true;
   ev_mark(c, s, "rank_scan");
 
   // Output exchange: (p, fp, pos) to the owner of p's range.
@@ -870,6 +934,10 @@ int s3imph_lookup_device(s3imph_ctx* c, const uint8_t* d_blob, const uint64_t* d
     if (c->last_n == 0) {
       HIPCHECK(hipMemsetAsync(d_result, 0xff, n * 8, s));
     } else {
+      if (!c->rank_valid) {  // word-level rank prefix, built on first lookup after a build
+        launch_rank_scan(c->bits, c->cap_words, c->rank_base, c->block_sums, c->cap_blocks, c->d_st, s);
+        c->rank_valid = true;
+      }
       launch_lookup(d_blob, d_offsets, n, c->bits, c->rank_base, c->d_st, d_fp, d_pos, count, d_result,
                     default_grid(n, 256), s);
     }

@@ -1,0 +1,85 @@
+// s3imph_device.h — device helpers shared by every kernel file: the FNV hashes of
+// pkg/format/mphf.go:341-369, the restated relab/bbhash position function
+//  and wave-level utilities.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bbhash_spec.h"
+
+namespace s3imph {
+
+static __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
+
+static __device__ __forceinline__ uint64_t lanemask_lt() {
+  return (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
+}
+
+// Position of `key` in a level of 64*words bits: keyHash % (64*words), computed as
+// 64*((h>>6) mod words) + (h & 63) with a Barrett step (q < 2^58, one correction).
+static __device__ __forceinline__ uint64_t bb_index(uint64_t seed, uint64_t key, uint64_t words,
+                                             uint64_t magic) {
+  uint64_t h = key_mix(seed, key);
+  uint64_t q = h >> 6;
+  uint64_t qe = __umul64hi(q, magic);
+  uint64_t r = q - qe * words;
+  if (r >= words) r -= words;
+  return (r << 6) | (h & 63);
+}
+
+static __device__ __forceinline__ void fnv_step(uint64_t& a, uint64_t& b, uint32_t byte) {
+  a = (a ^ byte) * kFnvPrime;  // FNV-1a (hashBytes)
+  b = (b * kFnvPrime) ^ byte;  // FNV-1  (computeFingerprintBytes)
+}
+
+// FNV-1a and FNV-1 of blob[b0, b1) in one pass.  The key's bytes are funnel-shifted
+// out of the aligned 8-byte words that overlap it, so every full 8-byte group runs the
+// same unrolled 8-step body whatever the key's alignment; only the last 0-7 bytes run
+// predicated steps.  Reads stay inside the aligned words overlapping [b0, b1).
+static __device__ __forceinline__ void fnv_8(uint64_t& a, uint64_t& b, uint64_t v) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
+}
+
+static __device__ __forceinline__ void fnv_both(const uint8_t* __restrict__ blob, uint64_t b0, uint64_t b1,
+                                                uint64_t& ha, uint64_t& hb) {
+  uint64_t a = kFnvOffset, b = kFnvOffset;
+  if (b1 > b0) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(blob + (b0 & ~7ull));
+    const uint64_t nw = ((b1 - 1) >> 3) - (b0 >> 3) + 1;  // aligned words overlapping the key
+    const unsigned sh = (unsigned)(b0 & 7) * 8;
+    const uint64_t len = b1 - b0;
+    const uint64_t nfull = len >> 3;
+    uint64_t cur = w[0];
+    for (uint64_t q = 0; q < nfull; ++q) {
+      const uint64_t nxt = (q + 1 < nw) ? w[q + 1] : 0;
+      const uint64_t v = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
+      fnv_8(a, b, v);
+      cur = nxt;
+    }
+    const unsigned rem = (unsigned)(len & 7);
+    if (rem) {
+      const uint64_t nxt = (nfull + 1 < nw) ? w[nfull + 1] : 0;
+      const uint64_t v = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
+#pragma unroll
+      for (unsigned t = 0; t < 7; ++t)
+        if (t < rem) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
+    }
+  }
+  ha = a;
+  hb = b;
+}
+
+static __device__ __forceinline__ bool test_bit32(const uint32_t* v, uint64_t x) {
+  return (v[x >> 5] >> (x & 31)) & 1u;
+}
+
+static __device__ __forceinline__ void mark_bit(uint32_t* A, uint32_t* C, uint64_t x) {
+  const uint32_t bit = 1u << (x & 31);
+  const uint32_t old = atomicOr(&A[x >> 5], bit);
+  if (old & bit) atomicOr(&C[x >> 5], bit);
+}
+
+
+}  // namespace s3imph

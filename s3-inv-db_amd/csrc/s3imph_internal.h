@@ -12,11 +12,6 @@
 
 namespace s3imph {
 
-// Redo (next-level) key lists are split into kNSeg segments: block b of a big-level
-// kernel reads input segment (b % kNSeg) and appends to the same output segment, so
-// compaction counters are sharded 64 ways and one atomic covers a whole block tile.
-constexpr int kNSeg = 64;
-
 // Device-resident per-build level bookkeeping.  Written only by kernels (and the
 // init kernel); the host copies it back once, after the build.
 struct LevelState {
@@ -29,8 +24,44 @@ struct LevelState {
   unsigned int status;                       // kSt* flags
   unsigned int tail_first;                   // first level run by the single-workgroup tail
   unsigned int pad;
-  unsigned long long seg[kMaxLevels + 2][kNSeg];  // per-segment active keys of level L >= 1
+  // Binned pipeline (s3imph_binned.hip).
+  unsigned long long lvl_base[kMaxLevels + 2];  // set bits in all levels < L (= ranks[L] - 1)
+  unsigned long long ntiles[kMaxLevels + 2];    // position tiles of level L
+  unsigned long long nchunks[kMaxLevels + 2];   // key chunks of level L (count/scatter blocks)
+  unsigned long long ticket[kMaxLevels + 2];    // tile tickets (look-back order)
 };
+
+// Binned pipeline geometry.  A level of `size` positions is cut into tiles of 2^tb
+// positions (one workgroup each, A/C in LDS); keys are counted and scattered into
+// per-tile buckets in chunks of `chunk` keys.
+constexpr unsigned kTileMaxBits = 19;                 // 2 x 64 KiB LDS bit vectors
+constexpr unsigned kTileMinBits = 10;
+constexpr uint64_t kMaxTiles = 4096;                  // LDS histogram bound (16 KiB)
+constexpr uint64_t kTargetTiles = 1024;               // aim for (512, 1024] tiles per level
+constexpr uint64_t kHistCap = 8ull << 20;             // tiles x chunks entries
+constexpr unsigned kStTailOverflow = 16u;             // tail reached with a level too big for LDS
+constexpr unsigned kStGeometry = 32u;                 // tiles/chunks outside the workspace
+constexpr unsigned kStLookback = 64u;                 // a look-back wait timed out
+constexpr uint64_t kSubRound = 4096;                  // keys per LDS-sorted scatter round
+
+struct LevelGeom {
+  unsigned tb;        // tile bits
+  uint64_t chunk;     // keys per count/scatter chunk
+};
+
+// Host-side choice for a level of about n keys: (512, 1024] tiles; chunks of a
+// multiple of kSubRound keys, few enough that tiles x chunks stays under kHistCap.
+inline LevelGeom choose_geom(uint64_t n) {
+  const uint64_t size = 64 * level_words(n ? n : 1);
+  unsigned tb = kTileMinBits;
+  while (tb < kTileMaxBits && (size >> tb) > kTargetTiles) ++tb;
+  const uint64_t T = (size + (1ull << tb) - 1) >> tb;
+  // ~1024 chunks (one 1024-thread count block each), a multiple of the scatter round.
+  uint64_t chunk = ((n + 1023) / 1024 + kSubRound - 1) / kSubRound * kSubRound;
+  if (chunk < kSubRound) chunk = kSubRound;
+  while (((n + chunk - 1) / chunk) * T > kHistCap) chunk *= 2;
+  return {tb, chunk};
+}
 
 // Device status flags.
 constexpr unsigned kStKeyZero = 1u;       // some FNV-1a key hash == 0
@@ -48,25 +79,9 @@ struct KernelArgs;  // fwd
 
 // ---- launchers (s3imph_kernels.hip) -------------------------------------------
 void launch_init_state(LevelState* st, uint64_t n, uint64_t key_base, hipStream_t s);
-void launch_hash_mark0(const uint8_t* blob, const uint64_t* offsets, uint64_t n, uint64_t* kh,
-                       uint64_t* fp, uint64_t* bits, uint64_t* C, uint64_t words0, LevelState* st,
-                       int grid, hipStream_t s);
-void launch_resolve(int level, const uint64_t* keys_in, const uint32_t* idx_in, const uint64_t* C,
-                    uint64_t* keys_out, uint32_t* idx_out, uint64_t seg_cap, uint64_t* settle,
-                    LevelState* st, unsigned long long gate, int grid, hipStream_t s);
-void launch_finalize(int level, uint64_t* bits, uint64_t* C, uint64_t cap_words, LevelState* st,
-                     unsigned long long gate, int grid, hipStream_t s);
-void launch_mark(int level, const uint64_t* keys, uint64_t seg_cap, uint64_t* bits, uint64_t* C,
-                 LevelState* st, unsigned long long gate, int grid, hipStream_t s);
-void launch_tail(int big_launched, uint64_t* bits, uint64_t cap_words, uint64_t* C, uint64_t* keys0,
-                 uint32_t* idx0, uint64_t* keys1, uint32_t* idx1, uint64_t seg_cap, uint64_t* settle,
-                 LevelState* st, hipStream_t s);
 void launch_rank_scan(const uint64_t* bits, uint64_t cap_words, uint64_t* rank_base,
                       unsigned long long* block_sums, uint64_t max_blocks, LevelState* st,
                       hipStream_t s);
-void launch_place(uint64_t n, const uint64_t* settle, const uint64_t* fp, const uint64_t* pos,
-                  uint64_t pos_base, const uint64_t* bits, const uint64_t* rank_base,
-                  uint64_t* fp_out, uint64_t* pos_out, LevelState* st, int grid, hipStream_t s);
 void launch_lookup(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const uint64_t* bits,
                    const uint64_t* rank_base, const LevelState* st, const uint64_t* fp,
                    const uint64_t* pos, uint64_t count, uint64_t* result, int grid, hipStream_t s);
@@ -100,6 +115,37 @@ void launch_words_scan(const uint64_t* bits, uint64_t words, uint64_t* rank_base
                        unsigned long long* block_sums, unsigned long long* total, hipStream_t s);
 
 int default_grid(uint64_t work, int block);
+
+// ---- binned pipeline launchers (s3imph_binned.hip) ---------------------------------
+// One key in flight between levels: FNV-1a key hash, FNV-1 fingerprint, position
+// (the preorder pos the reference's Add received, mphf_streaming.go:68).
+struct Rec {
+  uint64_t k, f, p;
+};
+
+struct BinBuffers {
+  uint64_t *kh, *fp;                    // level-0 hashes (key order)
+  const uint64_t* pos;                  // caller positions (nullable: identity)
+  uint64_t pos_base;
+  Rec* bucket;                          // records grouped by position tile
+  Rec* list[2];                         // next-level records (ping-pong)
+  unsigned *hist, *off;                 // tiles x chunks histogram and its exclusive scan
+  unsigned* tile_start;                 // kMaxTiles + 1
+  unsigned* scan_sums;                  // scan block sums
+  unsigned long long* flags;            // decoupled look-back words, one per tile
+  uint64_t* bits;
+  uint64_t cap_words;
+  uint64_t* fp_out;
+  uint64_t* pos_out;
+  LevelState* st;
+};
+void binned_set_lds_limits();
+void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
+                         LevelGeom g, int grid_chunks, hipStream_t s);
+void launch_binned_scan(int level, const BinBuffers& b, hipStream_t s);
+void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s);
+void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s);
+void launch_binned_tail(int big_launched, const BinBuffers& b, hipStream_t s);
 
 // ---- host helpers (s3imph_host.cpp) -------------------------------------------
 void set_err(char* err, size_t errlen, const std::string& msg);
