@@ -194,12 +194,29 @@ def main() -> None:
                               "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
                               "alg_bytes": alg, "avg_ms": stages[dom]}
         result["dominant_stage"] = max(stages, key=stages.get)
+    if world == 1:
+        result["host_e2e"] = host_e2e(s3imph, blob, offs, local_rank)
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(blob, offs, args.cpu_baseline_seconds)
     print(json.dumps(result), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def host_e2e(s3imph, blob, offs, device: int, reps: int = 3) -> dict:
+    """PCIe-inclusive rate of the boundary call the Go caller makes (s3imph_build_host):
+    pageable host blob/offsets in -> H2D -> build -> D2H of mph_fp/mph_pos + mph.bin marshal.
+    Reported beside `value`, never as it (measurement)."""
+    n = len(offs) - 1
+    s3imph.build_host(blob, offs, device=device)  # warm (staging buffers)
+    best = float("inf")
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        s3imph.build_host(blob, offs, device=device)
+        best = min(best, time.perf_counter() - t0)
+    return {"keys_per_s": n / best, "ms": best * 1e3, "key_bytes_GBps": int(offs[-1]) / best / 1e9,
+            "note": "pageable host memory, includes H2D of blob+offsets and D2H of fp/pos/mph.bin"}
 
 
 def cpu_baseline(blob, offs, seconds: float) -> dict:

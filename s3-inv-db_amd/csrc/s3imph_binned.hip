@@ -103,7 +103,8 @@ __global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__
                                                      const uint64_t* __restrict__ offsets, uint64_t n,
                                                      uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
                                                      unsigned* __restrict__ hist,
-                                                     unsigned long long* __restrict__ flags, LevelState* st,
+                                                     unsigned long long* __restrict__ flags,
+                                                     unsigned long long* __restrict__ sflags, LevelState* st,
                                                      unsigned tb, uint64_t chunk) {
   __shared__ unsigned sh[kLdsTiles];
   const uint64_t words = st->words[0], magic = st->magic[0];
@@ -114,6 +115,8 @@ __global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__
     st->nchunks[0] = B;
   }
   for (uint64_t t = (uint64_t)blockIdx.x * kCB + threadIdx.x; t < T; t += (uint64_t)gridDim.x * kCB) flags[t] = 0;
+  const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
+  for (uint64_t q = (uint64_t)blockIdx.x * kCB + threadIdx.x; q < nseg; q += (uint64_t)gridDim.x * kCB) sflags[q] = 0;
   const uint64_t seed = level_seed(0);
   bool zero = false;
   for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
@@ -156,20 +159,35 @@ __global__ void k_level_setup(int level, LevelState* st) {
 // ------------------------------------------------------------ level L count ----------
 __global__ __launch_bounds__(kCB) void k_count(int level, const Rec* __restrict__ list,
                                                unsigned* __restrict__ hist,
-                                               unsigned long long* __restrict__ flags, LevelState* st,
+                                               unsigned long long* __restrict__ flags,
+                                               unsigned long long* __restrict__ sflags, LevelState* st,
                                                unsigned tb, uint64_t chunk, uint64_t cap_words) {
   __shared__ unsigned sh[kLdsTiles];
+  const int p = level - 1;
+  if (p > 0 && st->n[p] <= kGate) return;  // previous level ran in the tail
+  if (st->status & (kStGeometry | kStOverflow | kStLookback)) return;
+  // level setup (every block derives it; block 0 publishes it)
   const uint64_t n = st->n[level];
-  if (n <= kGate || (st->status & (kStGeometry | kStOverflow | kStLookback))) return;
-  const uint64_t words = st->words[level], magic = st->magic[level];
+  const uint64_t words = n ? level_words(n) : 0, magic = level_magic(words);
+  const uint64_t woff = st->woff[p] + st->words[p];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->words[level] = words;
+    st->magic[level] = magic;
+    st->woff[level] = woff;
+    st->woff[level + 1] = woff + words;
+    st->nlevels = level;
+  }
+  if (n <= kGate) return;
   const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
   if (!geom_ok(st, T, B)) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st->ntiles[level] = T;
     st->nchunks[level] = B;
-    if (st->woff[level] + words > cap_words) atomicOr(&st->status, kStOverflow);
+    if (woff + words > cap_words) atomicOr(&st->status, kStOverflow);
   }
   for (uint64_t t = (uint64_t)blockIdx.x * kCB + threadIdx.x; t < T; t += (uint64_t)gridDim.x * kCB) flags[t] = 0;
+  const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
+  for (uint64_t q = (uint64_t)blockIdx.x * kCB + threadIdx.x; q < nseg; q += (uint64_t)gridDim.x * kCB) sflags[q] = 0;
   const uint64_t seed = level_seed(level);
   for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
     for (uint64_t t = threadIdx.x; t < T; t += kCB) sh[t] = 0;
@@ -181,77 +199,6 @@ __global__ __launch_bounds__(kCB) void k_count(int level, const Rec* __restrict_
     for (uint64_t t = threadIdx.x; t < T; t += kCB) hist[t * B + b] = sh[t];
     __syncthreads();
   }
-}
-
-// --------------------------------------------------- histogram scan (tile-major) -----
-constexpr int kHS = 8;                 // entries per thread
-constexpr int kHSBlock = kCB * kHS;    // 2048 entries per scan block
-
-__global__ __launch_bounds__(kCB) void k_hscan_reduce(int level, const unsigned* __restrict__ hist,
-                                                      unsigned* __restrict__ sums, LevelState* st) {
-  if (!level_active(level, st)) return;
-  const uint64_t M = st->ntiles[level] * st->nchunks[level];
-  const uint64_t nb = (M + kHSBlock - 1) / kHSBlock;
-  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
-    const uint64_t e0 = b * kHSBlock + (uint64_t)threadIdx.x * kHS;
-    uint64_t s = 0;
-#pragma unroll
-    for (int q = 0; q < kHS; ++q)
-      if (e0 + q < M) s += hist[e0 + q];
-    s = block_sum<kCB>(s);
-    if (threadIdx.x == 0) sums[b] = (unsigned)s;
-  }
-}
-
-__global__ __launch_bounds__(1024) void k_hscan_top(int level, unsigned* sums, LevelState* st) {
-  if (!level_active(level, st)) return;
-  const uint64_t M = st->ntiles[level] * st->nchunks[level];
-  const uint64_t nb = (M + kHSBlock - 1) / kHSBlock;
-  __shared__ uint64_t s_carry;
-  if (threadIdx.x == 0) s_carry = 0;
-  __syncthreads();
-  for (uint64_t base = 0; base < nb; base += 1024) {
-    const uint64_t i = base + threadIdx.x;
-    const uint64_t v = i < nb ? sums[i] : 0;
-    uint64_t tot;
-    const uint64_t ex = block_exscan<1024>(v, &tot);
-    const uint64_t carry = s_carry;
-    if (i < nb) sums[i] = (unsigned)(carry + ex);
-    __syncthreads();
-    if (threadIdx.x == 0) s_carry = carry + tot;
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(kCB) void k_hscan_down(int level, const unsigned* __restrict__ hist,
-                                                    const unsigned* __restrict__ sums,
-                                                    unsigned* __restrict__ off,
-                                                    unsigned* __restrict__ tile_start, LevelState* st) {
-  if (!level_active(level, st)) return;
-  const uint64_t T = st->ntiles[level], B = st->nchunks[level], M = T * B;
-  const uint64_t nb = (M + kHSBlock - 1) / kHSBlock;
-  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
-    const uint64_t e0 = b * kHSBlock + (uint64_t)threadIdx.x * kHS;
-    unsigned v[kHS];
-    uint64_t s = 0;
-#pragma unroll
-    for (int q = 0; q < kHS; ++q) {
-      v[q] = (e0 + q < M) ? hist[e0 + q] : 0u;
-      s += v[q];
-    }
-    uint64_t tot;
-    uint64_t run = sums[b] + block_exscan<kCB>(s, &tot);
-#pragma unroll
-    for (int q = 0; q < kHS; ++q) {
-      const uint64_t e = e0 + q;
-      if (e < M) {
-        off[e] = (unsigned)run;
-        if (e % B == 0) tile_start[e / B] = (unsigned)run;
-      }
-      run += v[q];
-    }
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) tile_start[T] = (unsigned)st->n[level];
 }
 
 // ------------------------------------------------------------------ scatter --------
@@ -398,11 +345,60 @@ __device__ __forceinline__ unsigned long long look_back_wave(unsigned long long*
   return excl;
 }
 
+// --------------------------------------------------- histogram scan (tile-major) -----
+// One pass: segments of kScanSeg entries in ticket order, prefix by wave look-back.
+constexpr int kHST = 1024;
+constexpr int kHSPer = (int)(kScanSeg / kHST);  // 8 entries per thread
+
+__global__ __launch_bounds__(kHST) void k_hscan(int level, const unsigned* __restrict__ hist,
+                                                unsigned* __restrict__ off, unsigned* __restrict__ tile_start,
+                                                unsigned long long* sflags, LevelState* st) {
+  __shared__ unsigned long long s_seg, s_prefix;
+  if (!level_active(level, st)) return;
+  const uint64_t T = st->ntiles[level], B = st->nchunks[level], M = T * B;
+  const uint64_t nseg = (M + kScanSeg - 1) / kScanSeg;
+  const unsigned tid = threadIdx.x;
+  for (;;) {
+    if (tid == 0) s_seg = atomicAdd(&st->sticket[level], 1ull);
+    __syncthreads();
+    const uint64_t g = s_seg;
+    if (g >= nseg) break;
+    const uint64_t e0 = g * kScanSeg + (uint64_t)tid * kHSPer;
+    unsigned v[kHSPer];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < kHSPer; ++q) {
+      v[q] = (e0 + q < M) ? hist[e0 + q] : 0u;
+      sum += v[q];
+    }
+    uint64_t tot;
+    const uint64_t ex = block_exscan<kHST>(sum, &tot);
+    if (tid < 64) {
+      const uint64_t pre = look_back_wave(sflags, g, tot, st);
+      if (tid == 0) s_prefix = pre;
+    }
+    __syncthreads();
+    uint64_t run = s_prefix + ex;
+#pragma unroll
+    for (int q = 0; q < kHSPer; ++q) {
+      const uint64_t e = e0 + q;
+      if (e < M) {
+        off[e] = (unsigned)run;
+        if (e % B == 0) tile_start[e / B] = (unsigned)run;
+      }
+      run += v[q];
+    }
+    if (g == 0 && tid == 0) tile_start[T] = (unsigned)st->n[level];
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__ bucket,
                                               const unsigned* __restrict__ tile_start,
                                               unsigned long long* flags, uint64_t* __restrict__ bits,
                                               Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
-                                              uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb) {
+                                              uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
+                                              int mode) {
   extern __shared__ uint32_t dyn[];
   __shared__ unsigned long long s_t, s_prefix;
   __shared__ unsigned s_wc[kTB / 64];
@@ -416,7 +412,7 @@ __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__
   const unsigned per = (tpw + kTB - 1) / kTB;
   uint32_t* sA = dyn;
   uint32_t* sC = dyn + tpw;
-  const bool small = tb <= kCacheBits;
+  const bool small = tb <= kCacheBits && mode == 0;
   const unsigned kcap = small ? cache_keys(tb) : 0;
   unsigned short* sloc = reinterpret_cast<unsigned short*>(dyn + 2 * tpw);
   unsigned short* sridx = sloc + kcap;
@@ -750,20 +746,16 @@ void binned_set_lds_limits() {
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s) {
   if (level == 0) {
-    k_hash_count0<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.st, g.tb,
-                                              g.chunk);
+    k_hash_count0<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st,
+                                              g.tb, g.chunk);
   } else {
-    k_level_setup<<<1, 64, 0, s>>>(level, b.st);
-    k_count<<<grid_chunks, kCB, 0, s>>>(level, b.list[(level - 1) & 1], b.hist, b.flags, b.st, g.tb, g.chunk,
-                                        b.cap_words);
+    k_count<<<grid_chunks, kCB, 0, s>>>(level, b.list[(level - 1) & 1], b.hist, b.flags, b.sflags, b.st, g.tb,
+                                        g.chunk, b.cap_words);
   }
 }
 
-void launch_binned_scan(int level, const BinBuffers& b, hipStream_t s) {
-  const int hs_grid = 256;
-  k_hscan_reduce<<<hs_grid, kCB, 0, s>>>(level, b.hist, b.scan_sums, b.st);
-  k_hscan_top<<<1, 1024, 0, s>>>(level, b.scan_sums, b.st);
-  k_hscan_down<<<hs_grid, kCB, 0, s>>>(level, b.hist, b.scan_sums, b.off, b.tile_start, b.st);
+void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s) {
+  k_hscan<<<grid, kHST, 0, s>>>(level, b.hist, b.off, b.tile_start, b.sflags, b.st);
 }
 
 void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s) {
@@ -772,8 +764,10 @@ void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStrea
 }
 
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s) {
-  k_tile<<<grid_tiles, kTB, tile_lds_bytes(g.tb), s>>>(level, b.bucket, b.tile_start, b.flags, b.bits,
-                                                       b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb);
+  const size_t lds = b.tile_mode == 0 ? tile_lds_bytes(g.tb) : 2ull * (1ull << (g.tb - 5)) * sizeof(uint32_t);
+  k_tile<<<grid_tiles, kTB, lds, s>>>(
+      level, b.bucket, b.tile_start, b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb,
+      b.tile_mode);
 }
 
 void launch_binned_tail(int big_launched, const BinBuffers& b, hipStream_t s) {

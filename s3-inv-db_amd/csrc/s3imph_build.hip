@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -73,6 +74,8 @@ struct s3imph_ctx {
   Rec* list[2] = {nullptr, nullptr};
   unsigned *hist = nullptr, *hoff = nullptr, *tile_start = nullptr, *scan_sums = nullptr;
   unsigned long long* flags = nullptr;
+  unsigned long long* sflags = nullptr;
+  int tile_mode = 0;
   bool lds_attr_set = false;
 
   // staging for host-memory builds
@@ -181,6 +184,7 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   dalloc(c->tile_start, kMaxTiles + 2);
   dalloc(c->scan_sums, kHistCap / 2048 + 2);
   dalloc(c->flags, kMaxTiles + 2);
+  dalloc(c->sflags, kHistCap / kScanSeg + 2);
   alloc_common(c, cap);
   dalloc(c->bits, c->cap_words);
   dalloc(c->rank_base, c->cap_words);
@@ -194,7 +198,7 @@ void free_workspace(s3imph_ctx* c) {
   dfree(c->rkeys[0]); dfree(c->rkeys[1]); dfree(c->ridx[0]); dfree(c->ridx[1]);
   dfree(c->block_sums); dfree(c->d_st);
   dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
-  dfree(c->hist); dfree(c->hoff); dfree(c->tile_start); dfree(c->scan_sums); dfree(c->flags);
+  dfree(c->hist); dfree(c->hoff); dfree(c->tile_start); dfree(c->scan_sums); dfree(c->flags); dfree(c->sflags);
   if (c->h_st) (void)hipHostFree(c->h_st);
   c->h_st = nullptr;
   dfree(c->s_blob); dfree(c->s_offsets); dfree(c->s_pos); dfree(c->s_fp); dfree(c->s_posout);
@@ -295,6 +299,8 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   b.tile_start = c->tile_start;
   b.scan_sums = c->scan_sums;
   b.flags = c->flags;
+  b.sflags = c->sflags;
+  b.tile_mode = c->tile_mode;
   b.bits = c->bits;
   b.cap_words = c->cap_words;
   b.fp_out = fp_out;
@@ -303,18 +309,21 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
 
   const double q = 1.0 - std::exp(-0.5);  // fraction of keys that collide at load 1/2
   const LevelGeom g0 = choose_geom(n);
-  auto grids = [](uint64_t nk, LevelGeom g, int* gc, int* gt) {
+  int gc, gt, gs;
+  // Grids from a (predicted) key count; kernels loop over whatever the device finds.
+  auto grids = [&](uint64_t nk, LevelGeom g) {
     const uint64_t T = (64 * level_words(nk ? nk : 1) + (1ull << g.tb) - 1) >> g.tb;
-    *gc = (int)std::min<uint64_t>(std::max<uint64_t>((nk + g.chunk - 1) / g.chunk, 1), 2048);
-    *gt = (int)std::min<uint64_t>(std::max<uint64_t>(T, 1), 2048);
+    const uint64_t B = std::max<uint64_t>((nk + g.chunk - 1) / g.chunk, 1);
+    gc = (int)std::min<uint64_t>(B, 2048);
+    gt = (int)std::min<uint64_t>(std::max<uint64_t>(T, 1), 2048);
+    gs = (int)std::min<uint64_t>((T * B + kScanSeg - 1) / kScanSeg + 2, 256);
   };
-  int gc, gt;
   launch_init_state(c->d_st, n, 0, s);
   ev_mark(c, s, "init");
-  grids(n, g0, &gc, &gt);
+  grids(n, g0);
   launch_binned_count(0, blob, offsets, n, b, g0, gc, s);
   ev_mark(c, s, "hash_count0");
-  launch_binned_scan(0, b, s);
+  launch_binned_scan(0, b, gs, s);
   ev_mark(c, s, "hscan0");
   launch_binned_scatter(0, b, g0, s);
   ev_mark(c, s, "scatter0");
@@ -328,9 +337,9 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
     launched = L;
     const uint64_t nb = conservative ? n : (uint64_t)(pred * 1.1) + 4096;
     const LevelGeom g = conservative ? g0 : choose_geom(nb);
-    grids(nb, g, &gc, &gt);
+    grids(nb, g);
     launch_binned_count(L, nullptr, nullptr, 0, b, g, gc, s);
-    launch_binned_scan(L, b, s);
+    launch_binned_scan(L, b, gs, s);
     launch_binned_scatter(L, b, g, s);
     launch_binned_tile(L, b, g, gt, s);
   }
@@ -765,6 +774,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     HIPCHECK(hipSetDevice(device));
     c = new s3imph_ctx();
     c->device = device;
+    if (const char* m = std::getenv("S3IMPH_TILE_MODE")) c->tile_mode = std::atoi(m);  // A/B knob
     // A blocking stream: implicitly ordered with the legacy NULL stream, so work a
     // caller queued there (e.g. torch's default stream) completes before ours starts.
     HIPCHECK(hipStreamCreate(&c->own_stream));

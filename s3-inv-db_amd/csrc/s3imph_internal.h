@@ -29,6 +29,7 @@ struct LevelState {
   unsigned long long ntiles[kMaxLevels + 2];    // position tiles of level L
   unsigned long long nchunks[kMaxLevels + 2];   // key chunks of level L (count/scatter blocks)
   unsigned long long ticket[kMaxLevels + 2];    // tile tickets (look-back order)
+  unsigned long long sticket[kMaxLevels + 2];   // histogram-scan segment tickets
 };
 
 // Binned pipeline geometry.  A level of `size` positions is cut into tiles of 2^tb
@@ -43,6 +44,7 @@ constexpr unsigned kStTailOverflow = 16u;             // tail reached with a lev
 constexpr unsigned kStGeometry = 32u;                 // tiles/chunks outside the workspace
 constexpr unsigned kStLookback = 64u;                 // a look-back wait timed out
 constexpr uint64_t kSubRound = 4096;                  // keys per LDS-sorted scatter round
+constexpr uint64_t kScanSeg = 8192;                   // histogram entries per scan segment
 
 struct LevelGeom {
   unsigned tb;        // tile bits
@@ -133,6 +135,8 @@ struct BinBuffers {
   unsigned* tile_start;                 // kMaxTiles + 1
   unsigned* scan_sums;                  // scan block sums
   unsigned long long* flags;            // decoupled look-back words, one per tile
+  unsigned long long* sflags;           // look-back words of the histogram scan
+  int tile_mode;                        // 0: rank-order gather, 1: in-order with window writes
   uint64_t* bits;
   uint64_t cap_words;
   uint64_t* fp_out;
@@ -142,7 +146,7 @@ struct BinBuffers {
 void binned_set_lds_limits();
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s);
-void launch_binned_scan(int level, const BinBuffers& b, hipStream_t s);
+void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s);
 void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s);
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s);
 void launch_binned_tail(int big_launched, const BinBuffers& b, hipStream_t s);
