@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 
 #include "s3imph_device.h"
+#include <cstdlib>
+
 #include "s3imph_internal.h"
 
 namespace s3imph {
@@ -33,6 +35,8 @@ constexpr int kCB = 1024;             // count block
 constexpr int kSB = 1024;             // scatter block
 constexpr int kTB = 1024;             // tile block
 constexpr int kTailT = 1024;          // tail block
+constexpr unsigned kLenBuckets = 256;  // key-length classes of the level-0 hash sort
+constexpr uint64_t kTcntWords = (uint64_t)kMaxLevels * kMaxTiles;
 constexpr uint64_t kLdsTiles = kMaxTiles;  // histogram / cursor entries in LDS
 constexpr unsigned long long kGate = kTailKeys;
 constexpr int kTailW32 = (int)(2 * ((kGammaNum * kTailKeys + 63) / 64));  // 4096 u32 words
@@ -40,7 +44,7 @@ constexpr unsigned long long kFlagAgg = 1ull << 62;
 constexpr unsigned long long kFlagInc = 2ull << 62;
 constexpr unsigned long long kFlagVal = (1ull << 62) - 1;
 
-__device__ __forceinline__ uint64_t ntiles_of(uint64_t words, unsigned tb) {
+__host__ __device__ __forceinline__ uint64_t ntiles_of(uint64_t words, unsigned tb) {
   return (64 * words + (1ull << tb) - 1) >> tb;
 }
 
@@ -99,40 +103,157 @@ __device__ __forceinline__ bool level_active(int level, const LevelState* st) {
 // ---------------------------------------------------------------- level 0 count ----
 // Hash every key (FNV-1a key hash + FNV-1 fingerprint, one pass over the bytes),
 // store both in key order, and histogram the level-0 tiles per chunk.
+template <bool kSort, bool kBatched>
 __global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__ blob,
                                                      const uint64_t* __restrict__ offsets, uint64_t n,
                                                      uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
                                                      unsigned* __restrict__ hist,
                                                      unsigned long long* __restrict__ flags,
                                                      unsigned long long* __restrict__ sflags, LevelState* st,
-                                                     unsigned tb, uint64_t chunk) {
+                                                     unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
   __shared__ unsigned sh[kLdsTiles];
+  __shared__ unsigned lcnt[kLenBuckets];
+  __shared__ unsigned short sidx[kCB];
+  __shared__ uint64_t sb0[kCB], sb1[kCB], sh1[kCB], sh2[kCB];
   const uint64_t words = st->words[0], magic = st->magic[0];
   const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
   if (!geom_ok(st, T, B)) return;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  const unsigned tid = threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) {
     st->ntiles[0] = T;
     st->nchunks[0] = B;
   }
-  for (uint64_t t = (uint64_t)blockIdx.x * kCB + threadIdx.x; t < T; t += (uint64_t)gridDim.x * kCB) flags[t] = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * kCB + tid; t < T; t += (uint64_t)gridDim.x * kCB) flags[t] = 0;
   const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
-  for (uint64_t q = (uint64_t)blockIdx.x * kCB + threadIdx.x; q < nseg; q += (uint64_t)gridDim.x * kCB) sflags[q] = 0;
+  for (uint64_t q = (uint64_t)blockIdx.x * kCB + tid; q < nseg; q += (uint64_t)gridDim.x * kCB) sflags[q] = 0;
+  for (uint64_t q = (uint64_t)blockIdx.x * kCB + tid; q < kTcntWords; q += (uint64_t)gridDim.x * kCB) tcnt[q] = 0;
   const uint64_t seed = level_seed(0);
   bool zero = false;
   for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
-    for (uint64_t t = threadIdx.x; t < T; t += kCB) sh[t] = 0;
-    __syncthreads();
+    for (uint64_t t = tid; t < T; t += kCB) sh[t] = 0;
     const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += kCB) {
-      uint64_t h1, h2;
-      fnv_both(blob, offsets[i], offsets[i + 1], h1, h2);
-      kh[i] = h1;
-      fp[i] = h2;
-      zero |= (h1 == 0);
-      atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
+    if (!kSort) {
+      __syncthreads();
+      for (uint64_t i = lo + tid; i < hi; i += kCB) {
+        uint64_t h1, h2;
+        if (kBatched) fnv_both(blob, offsets[i], offsets[i + 1], h1, h2);
+        else fnv_both_loop(blob, offsets[i], offsets[i + 1], h1, h2);
+        kh[i] = h1;
+        fp[i] = h2;
+        zero |= (h1 == 0);
+        atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
+      }
+    } else {
+    for (uint64_t g = lo; g < hi; g += kCB) {
+      // Counting-sort the group's keys by length so that each wave hashes keys of one
+      // length: FNV is one dependent multiply chain per byte, and a wave runs as long as
+      // its longest lane.  Results return to key order through LDS.
+      const uint64_t i = g + tid;
+      uint64_t b0 = 0, b1 = 0;
+      if (i < hi) {
+        b0 = offsets[i];
+        b1 = offsets[i + 1];
+      }
+      if (tid < kLenBuckets) lcnt[tid] = 0;
+      __syncthreads();
+      const unsigned lb = (unsigned)min<uint64_t>(b1 - b0, kLenBuckets - 1);
+      const unsigned rk = atomicAdd(&lcnt[lb], 1u);
+      __syncthreads();
+      uint64_t tot;
+      const uint64_t ex = block_exscan<kCB>(tid < kLenBuckets ? lcnt[tid] : 0u, &tot);
+      if (tid < kLenBuckets) lcnt[tid] = (unsigned)ex;
+      __syncthreads();
+      const unsigned slot = lcnt[lb] + rk;
+      sidx[slot] = (unsigned short)tid;
+      sb0[slot] = b0;
+      sb1[slot] = b1;
+      __syncthreads();
+      const unsigned j = sidx[tid];
+      if (g + j < hi) {
+        uint64_t h1, h2;
+        if (kBatched) fnv_both(blob, sb0[tid], sb1[tid], h1, h2);
+        else fnv_both_loop(blob, sb0[tid], sb1[tid], h1, h2);
+        sh1[j] = h1;
+        sh2[j] = h2;
+        zero |= (h1 == 0);
+        atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
+      }
+      __syncthreads();
+      if (i < hi) {
+        kh[i] = sh1[tid];
+        fp[i] = sh2[tid];
+      }
+    }
     }
     __syncthreads();
-    for (uint64_t t = threadIdx.x; t < T; t += kCB) hist[t * B + b] = sh[t];
+    for (uint64_t t = tid; t < T; t += kCB) hist[t * B + b] = sh[t];
+    __syncthreads();
+  }
+  if (zero) atomicOr(&st->status, kStKeyZero);
+}
+
+// Level-0 hash + count, LDS-staged: per group of kHB keys the block copies the group's
+// aligned blob words into LDS with coalesced, independent loads, then each thread hashes
+// its key out of LDS.  A group whose bytes exceed the window (very long keys) is hashed
+// straight from global memory.  dyn LDS: hist[T] u32, then the window.
+constexpr int kHB = 512;
+constexpr unsigned kHashWinWords = 6144;  // 48 KB window
+__global__ __launch_bounds__(kHB) void k_hash_count0_lds(const uint8_t* __restrict__ blob,
+                                                         const uint64_t* __restrict__ offsets, uint64_t n,
+                                                         uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
+                                                         unsigned* __restrict__ hist,
+                                                         unsigned long long* __restrict__ flags,
+                                                         unsigned long long* __restrict__ sflags, LevelState* st,
+                                                         unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
+  extern __shared__ uint32_t dyn[];
+  const uint64_t words = st->words[0], magic = st->magic[0];
+  const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
+  if (!geom_ok(st, T, B)) return;
+  unsigned* sh = dyn;
+  uint64_t* win = reinterpret_cast<uint64_t*>(dyn) + (T + 1) / 2;
+  const uint64_t* bw = reinterpret_cast<const uint64_t*>(blob);
+  const unsigned tid = threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) {
+    st->ntiles[0] = T;
+    st->nchunks[0] = B;
+  }
+  for (uint64_t t = (uint64_t)blockIdx.x * kHB + tid; t < T; t += (uint64_t)gridDim.x * kHB) flags[t] = 0;
+  const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
+  for (uint64_t q = (uint64_t)blockIdx.x * kHB + tid; q < nseg; q += (uint64_t)gridDim.x * kHB) sflags[q] = 0;
+  for (uint64_t q = (uint64_t)blockIdx.x * kHB + tid; q < kTcntWords; q += (uint64_t)gridDim.x * kHB) tcnt[q] = 0;
+  const uint64_t seed = level_seed(0);
+  bool zero = false;
+  for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    for (uint64_t t = tid; t < T; t += kHB) sh[t] = 0;
+    const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
+    for (uint64_t g = lo; g < hi; g += kHB) {
+      const uint64_t i = g + tid, gend = min(hi, g + kHB);
+      uint64_t b0 = 0, b1 = 0;
+      if (i < hi) {
+        b0 = offsets[i];
+        b1 = offsets[i + 1];
+      }
+      const uint64_t w0 = offsets[g] >> 3, w1 = (offsets[gend] + 7) >> 3;  // group's aligned words
+      const bool fits = w1 - w0 <= kHashWinWords;
+      __syncthreads();  // previous group's window reads (and the hist zeroing) are done
+      if (fits) {
+        const unsigned nwin = (unsigned)(w1 - w0);
+        for (unsigned q = tid; q < nwin; q += kHB) win[q] = bw[w0 + q];
+      }
+      __syncthreads();
+      if (i < hi) {
+        uint64_t h1, h2;
+        const uint64_t nw = b1 > b0 ? ((b1 - 1) >> 3) - (b0 >> 3) + 1 : 0;
+        if (fits) fnv_words(win + ((b0 >> 3) - w0), nw, (unsigned)(b0 & 7) * 8, b1 - b0, h1, h2);
+        else fnv_words(bw + (b0 >> 3), nw, (unsigned)(b0 & 7) * 8, b1 - b0, h1, h2);
+        kh[i] = h1;
+        fp[i] = h2;
+        zero |= (h1 == 0);
+        atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
+      }
+    }
+    __syncthreads();
+    for (uint64_t t = tid; t < T; t += kHB) hist[t * B + b] = sh[t];
     __syncthreads();
   }
   if (zero) atomicOr(&st->status, kStKeyZero);
@@ -221,76 +342,237 @@ __global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __re
   const uint64_t words = st->words[level], magic = st->magic[level];
   const uint64_t T = st->ntiles[level], B = st->nchunks[level];
   const uint64_t seed = level_seed(level);
-  // XCD-contiguous chunk ranges: blocks b, b+8, b+16, ... (one XCD under round-robin
-  // dispatch) take one contiguous eighth of the chunks.  Speed only, never correctness.
+  // Blocks b, b+8, b+16, ... (one XCD under round-robin dispatch) share one contiguous
+  // eighth of the chunks and take them interleaved, so at any moment an XCD's blocks
+  // append adjacent runs of every bucket and its L2 completes whole lines.  Speed only.
   const unsigned groups = gridDim.x >= 8 ? 8 : 1;
   const uint64_t xcd = blockIdx.x % groups, r = blockIdx.x / groups, R = gridDim.x / groups;
   const uint64_t per = (B + groups - 1) / groups;
   const uint64_t g0 = min(B, xcd * per), g1 = min(B, g0 + per);
-  const uint64_t c0 = g0 + (g1 - g0) * r / R, c1 = g0 + (g1 - g0) * (r + 1) / R;
   const unsigned tid = threadIdx.x;
-  for (uint64_t b = c0; b < c1; ++b) {
-    for (uint64_t t = tid; t < T; t += kSB) cur[t] = off[t * B + b];
-    const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
-    for (uint64_t r0 = lo; r0 < hi; r0 += kSubRound) {
-      for (uint64_t t = tid; t < T; t += kSB) cnt[t] = 0;
-      __syncthreads();
-      Rec rec[kScatterKPT];
-      unsigned tt[kScatterKPT], rk[kScatterKPT];
+  // The block's work is the sequence of rounds (chunk b, keys [r0, r0 + kSubRound)).
+  // Software pipeline: round i+1's records are loaded into registers right after
+  // round i has been staged in LDS, so their latency hides behind round i's writes.
+  uint64_t b = g0 + r;
+  if (b >= g1) return;
+  uint64_t r0 = b * chunk, hi = min(n, r0 + chunk);
+  Rec rec[kScatterKPT];
+  auto load_round = [&](uint64_t base, uint64_t end) {
 #pragma unroll
-      for (int q = 0; q < kScatterKPT; ++q) {
-        const uint64_t i = r0 + (uint64_t)q * kSB + tid;
-        if (i < hi) {
-          if (ilist) {
-            rec[q] = ilist[i];
-          } else {
-            rec[q].k = ik[i];
-            rec[q].f = ifp[i];
-            rec[q].p = ipos ? ipos[i] : pos_base + i;
-          }
-          tt[q] = (unsigned)(bb_index(seed, rec[q].k, words, magic) >> tb);
-          rk[q] = atomicAdd(&cnt[tt[q]], 1u);
+    for (int q = 0; q < kScatterKPT; ++q) {
+      const uint64_t i = base + (uint64_t)q * kSB + tid;
+      if (i < end) {
+        if (ilist) {
+          rec[q] = ilist[i];
+        } else {
+          rec[q].k = ik[i];
+          rec[q].f = ifp[i];
+          rec[q].p = ipos ? ipos[i] : pos_base + i;
         }
       }
-      __syncthreads();
-      // exclusive scan of the round's per-tile counts (kLdsTiles / kSB tiles per thread)
-      constexpr int kTPT = (int)(kLdsTiles / kSB);
-      const uint64_t t0 = (uint64_t)kTPT * tid;
-      unsigned a[kTPT];
-      uint64_t sum = 0;
-#pragma unroll
-      for (int q = 0; q < kTPT; ++q) {
-        a[q] = t0 + q < T ? cnt[t0 + q] : 0u;
-        sum += a[q];
-      }
-      uint64_t tot;
-      uint64_t ex = block_exscan<kSB>(sum, &tot);
-#pragma unroll
-      for (int q = 0; q < kTPT; ++q) {
-        if (t0 + q < T) start[t0 + q] = (unsigned)ex;
-        ex += a[q];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int q = 0; q < kScatterKPT; ++q) {
-        const uint64_t i = r0 + (uint64_t)q * kSB + tid;
-        if (i < hi) {
-          const unsigned slot = start[tt[q]] + rk[q];
-          stage[slot] = rec[q];
-          stile[slot] = (unsigned short)tt[q];
-        }
-      }
-      __syncthreads();
-      const unsigned m = (unsigned)min<uint64_t>(kSubRound, hi - r0);
-      for (unsigned j = tid; j < m; j += kSB) {
-        const unsigned t = stile[j];
-        bucket[cur[t] + (j - start[t])] = stage[j];
-      }
-      __syncthreads();
-      for (uint64_t t = tid; t < T; t += kSB) cur[t] += cnt[t];
-      __syncthreads();
     }
+  };
+  load_round(r0, hi);
+  for (uint64_t t = tid; t < T; t += kSB) {
+    cnt[t] = 0;
+    cur[t] = off[t * B + b];
   }
+  __syncthreads();
+  for (;;) {
+    unsigned tt[kScatterKPT], rk[kScatterKPT];
+#pragma unroll
+    for (int q = 0; q < kScatterKPT; ++q) {
+      const uint64_t i = r0 + (uint64_t)q * kSB + tid;
+      if (i < hi) {
+        tt[q] = (unsigned)(bb_index(seed, rec[q].k, words, magic) >> tb);
+        rk[q] = atomicAdd(&cnt[tt[q]], 1u);
+      }
+    }
+    __syncthreads();
+    // exclusive scan of the round's per-tile counts (kLdsTiles / kSB tiles per thread)
+    constexpr int kTPT = (int)(kLdsTiles / kSB);
+    const uint64_t t0 = (uint64_t)kTPT * tid;
+    unsigned a[kTPT];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      a[q] = t0 + q < T ? cnt[t0 + q] : 0u;
+      sum += a[q];
+    }
+    uint64_t tot;
+    uint64_t ex = block_exscan<kSB>(sum, &tot);
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      if (t0 + q < T) start[t0 + q] = (unsigned)ex;
+      ex += a[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kScatterKPT; ++q) {
+      const uint64_t i = r0 + (uint64_t)q * kSB + tid;
+      if (i < hi) {
+        const unsigned slot = start[tt[q]] + rk[q];
+        stage[slot] = rec[q];
+        stile[slot] = (unsigned short)tt[q];
+      }
+    }
+    // advance to the next round and prefetch it
+    const unsigned m = (unsigned)min<uint64_t>(kSubRound, hi - r0);
+    const uint64_t pb = b;
+    r0 += kSubRound;
+    if (r0 >= hi) {
+      b += R;
+      if (b < g1) {
+        r0 = b * chunk;
+        hi = min(n, r0 + chunk);
+      }
+    }
+    const bool more = b < g1;
+    if (more) load_round(r0, hi);
+    __syncthreads();
+    for (unsigned j = tid; j < m; j += kSB) {
+      const unsigned t = stile[j];
+      bucket[cur[t] + (j - start[t])] = stage[j];
+    }
+    __syncthreads();
+    if (!more) break;
+    if (b != pb) {
+      for (uint64_t t = tid; t < T; t += kSB) {
+        cnt[t] = 0;
+        cur[t] = off[t * B + b];
+      }
+    } else {
+      for (uint64_t t = tid; t < T; t += kSB) {
+        cur[t] += cnt[t];
+        cnt[t] = 0;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------- reservation scatter ------
+// Small levels (a few 10^5 .. 10^6 keys) skip the count and histogram-scan kernels:
+// tile t owns the fixed bucket slot [t * cap, (t + 1) * cap), cap = bucket_cap / T
+// (several times the ~n/T keys a tile receives), and each block reserves its run in a
+// tile with one atomic per (round, tile).  Record order inside a tile is then
+// arbitrary, which nothing downstream depends on (ranks come from positions).  A slot
+// overflow sets kStOverflow and the build reruns on the counted path.
+__global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __restrict__ ilist,
+                                                     unsigned* __restrict__ tcnt, Rec* __restrict__ bucket,
+                                                     uint64_t bucket_cap, unsigned long long* __restrict__ flags,
+                                                     LevelState* st, unsigned tb, uint64_t cap_words) {
+  __shared__ Rec stage[kSubRound];
+  __shared__ unsigned short stile[kSubRound];
+  __shared__ unsigned cnt[kLdsTiles];
+  __shared__ unsigned start[kLdsTiles];
+  __shared__ unsigned cur[kLdsTiles];  // bucket indices fit u32 (n < 2^32 per GPU)
+  __shared__ unsigned s_over;
+  const int p = level - 1;
+  if (p > 0 && st->n[p] <= kGate) return;  // previous level ran in the tail
+  if (st->status & (kStGeometry | kStOverflow | kStLookback)) return;
+  // level setup (every block derives it; block 0 publishes it)
+  const uint64_t n = st->n[level];
+  const uint64_t words = n ? level_words(n) : 0, magic = level_magic(words);
+  const uint64_t woff = st->woff[p] + st->words[p];
+  const unsigned tid = threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) {
+    st->words[level] = words;
+    st->magic[level] = magic;
+    st->woff[level] = woff;
+    st->woff[level + 1] = woff + words;
+    st->nlevels = level;
+  }
+  if (n <= kGate) return;
+  const uint64_t T = ntiles_of(words, tb);
+  if (T > kLdsTiles) {
+    if (tid == 0) atomicOr(&st->status, kStGeometry);
+    return;
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    st->ntiles[level] = T;
+    st->nchunks[level] = 0;
+    if (woff + words > cap_words) atomicOr(&st->status, kStOverflow);
+  }
+  for (uint64_t t = (uint64_t)blockIdx.x * kSB + tid; t < T; t += (uint64_t)gridDim.x * kSB) flags[t] = 0;
+  const uint64_t cap = bucket_cap / T;
+  const uint64_t seed = level_seed(level);
+  const uint64_t stride = (uint64_t)gridDim.x * kSubRound;
+  uint64_t r0 = (uint64_t)blockIdx.x * kSubRound;
+  if (r0 >= n) return;
+  Rec rec[kScatterKPT];
+  auto load_round = [&](uint64_t base) {
+#pragma unroll
+    for (int q = 0; q < kScatterKPT; ++q) {
+      const uint64_t i = base + (uint64_t)q * kSB + tid;
+      if (i < n) rec[q] = ilist[i];
+    }
+  };
+  load_round(r0);
+  for (uint64_t t = tid; t < T; t += kSB) cnt[t] = 0;
+  if (tid == 0) s_over = 0;
+  __syncthreads();
+  for (;;) {
+    unsigned tt[kScatterKPT], rk[kScatterKPT];
+#pragma unroll
+    for (int q = 0; q < kScatterKPT; ++q) {
+      const uint64_t i = r0 + (uint64_t)q * kSB + tid;
+      if (i < n) {
+        tt[q] = (unsigned)(bb_index(seed, rec[q].k, words, magic) >> tb);
+        rk[q] = atomicAdd(&cnt[tt[q]], 1u);
+      }
+    }
+    __syncthreads();
+    constexpr int kTPT = (int)(kLdsTiles / kSB);
+    const uint64_t t0 = (uint64_t)kTPT * tid;
+    unsigned a[kTPT];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      a[q] = t0 + q < T ? cnt[t0 + q] : 0u;
+      sum += a[q];
+    }
+    uint64_t tot;
+    uint64_t ex = block_exscan<kSB>(sum, &tot);
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      const uint64_t t = t0 + q;
+      if (t < T) {
+        start[t] = (unsigned)ex;
+        if (a[q]) {
+          const uint64_t at = atomicAdd(&tcnt[t], a[q]);
+          if (at + a[q] > cap) s_over = 1;
+          cur[t] = (unsigned)(t * cap + at);
+        }
+      }
+      ex += a[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kScatterKPT; ++q) {
+      const uint64_t i = r0 + (uint64_t)q * kSB + tid;
+      if (i < n) {
+        const unsigned slot = start[tt[q]] + rk[q];
+        stage[slot] = rec[q];
+        stile[slot] = (unsigned short)tt[q];
+      }
+    }
+    const unsigned m = (unsigned)min<uint64_t>(kSubRound, n - r0);
+    r0 += stride;
+    const bool more = r0 < n;
+    if (more) load_round(r0);
+    __syncthreads();
+    if (s_over) break;
+    for (unsigned j = tid; j < m; j += kSB) {
+      const unsigned t = stile[j];
+      bucket[cur[t] + (j - start[t])] = stage[j];
+    }
+    __syncthreads();
+    if (!more) break;
+    for (uint64_t t = tid; t < T; t += kSB) cnt[t] = 0;
+    __syncthreads();
+  }
+  if (s_over && tid == 0) atomicOr(&st->status, kStOverflow | kStResOverflow);
 }
 
 // --------------------------------------------------------------------- tile --------
@@ -395,6 +677,7 @@ __global__ __launch_bounds__(kHST) void k_hscan(int level, const unsigned* __res
 
 __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__ bucket,
                                               const unsigned* __restrict__ tile_start,
+                                              const unsigned* __restrict__ tcnt, uint64_t bucket_cap,
                                               unsigned long long* flags, uint64_t* __restrict__ bits,
                                               Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
                                               uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
@@ -431,8 +714,15 @@ __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__
     __syncthreads();
     const uint64_t t = s_t;
     if (t >= T) break;
-    const uint64_t lo = tile_start[t], hi = tile_start[t + 1];
-    const uint64_t nk = hi - lo;
+    // bucket range: from the histogram scan, or (reservation path) a fixed slot per tile
+    uint64_t lo, nk;
+    if (tcnt) {
+      lo = t * (bucket_cap / T);
+      nk = tcnt[t];
+    } else {
+      lo = tile_start[t];
+      nk = tile_start[t + 1] - lo;
+    }
     const Rec* rb = bucket + lo;
     const uint64_t tbase = t << tb;
     const bool cached = small && nk <= kcap;
@@ -676,33 +966,40 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int big_launched, Rec* list
       }
     }
     __syncthreads();
-    for (uint64_t jb = tid & ~63u; jb < n; jb += kTailT) {
-      const uint64_t j = jb + lane;
-      bool r = false;
-      Rec rc{0, 0, 0};
-      if (j < n) {
-        rc = in[j];
-        const uint64_t x = bb_index(seed, rc.k, words, magic);
-        const uint32_t wv = sA[x >> 5];
-        const uint32_t bit = 1u << (x & 31);
-        if (wv & bit) {
-          const uint64_t q = base + spre[x >> 5] + __popc(wv & (bit - 1));
-          if (q < N) {
-            fp_out[q] = rc.f;
-            pos_out[q] = rc.p;
-          } else {
-            bad = true;
-          }
-        } else {
-          r = true;
-        }
+    for (uint64_t jb0 = tid & ~63u; jb0 < n; jb0 += (uint64_t)kTailT * kTU) {
+      Rec rc[kTU];
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        const uint64_t j = jb0 + (uint64_t)u * kTailT + lane;
+        if (j < n) rc[u] = in[j];
       }
-      const uint64_t m = __ballot(r);
-      if (m) {
-        unsigned long long o = 0;
-        if (lane == 0) o = atomicAdd(&s_next, (unsigned long long)__popcll(m));
-        o = __shfl(o, 0);
-        if (r) out[o + __popcll(m & lanemask_lt())] = rc;
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        const uint64_t j = jb0 + (uint64_t)u * kTailT + lane;
+        bool r = false;
+        if (j < n) {
+          const uint64_t x = bb_index(seed, rc[u].k, words, magic);
+          const uint32_t wv = sA[x >> 5];
+          const uint32_t bit = 1u << (x & 31);
+          if (wv & bit) {
+            const uint64_t q = base + spre[x >> 5] + __popc(wv & (bit - 1));
+            if (q < N) {
+              fp_out[q] = rc[u].f;
+              pos_out[q] = rc[u].p;
+            } else {
+              bad = true;
+            }
+          } else {
+            r = true;
+          }
+        }
+        const uint64_t m = __ballot(r);
+        if (m) {
+          unsigned long long o = 0;
+          if (lane == 0) o = atomicAdd(&s_next, (unsigned long long)__popcll(m));
+          o = __shfl(o, 0);
+          if (r) out[o + __popcll(m & lanemask_lt())] = rc[u];
+        }
       }
     }
     __syncthreads();
@@ -739,6 +1036,8 @@ size_t tile_lds_bytes(unsigned tb) {
 }  // namespace
 
 void binned_set_lds_limits() {
+  (void)hipFuncSetAttribute((const void*)k_hash_count0_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(((kLdsTiles + 1) / 2 + kHashWinWords) * sizeof(uint64_t)));
   (void)hipFuncSetAttribute((const void*)k_tile, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)tile_lds_bytes(kTileMaxBits));
 }
@@ -746,8 +1045,25 @@ void binned_set_lds_limits() {
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s) {
   if (level == 0) {
-    k_hash_count0<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st,
-                                              g.tb, g.chunk);
+    static const int mode = [] {
+      // A/B knob: 3 direct, loop (default); 0 LDS-staged; 1 direct, batched loads;
+      // 2 length-sorted, loop; 4 length-sorted, batched
+      const char* e = std::getenv("S3IMPH_HASH_MODE");
+      return e ? std::atoi(e) : 3;
+    }();
+    if (mode == 0) {
+      const uint64_t T = ntiles_of(level_words(n ? n : 1), g.tb);
+      const size_t lds = ((T + 1) / 2 + kHashWinWords) * sizeof(uint64_t);
+      k_hash_count0_lds<<<grid_chunks, kHB, lds, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags,
+                                                      b.st, g.tb, g.chunk, b.tcnt);
+      return;
+    }
+    auto kern = mode == 1   ? k_hash_count0<false, true>
+                : mode == 2 ? k_hash_count0<true, false>
+                : mode == 3 ? k_hash_count0<false, false>
+                            : k_hash_count0<true, true>;
+    kern<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st, g.tb, g.chunk,
+                                     b.tcnt);
   } else {
     k_count<<<grid_chunks, kCB, 0, s>>>(level, b.list[(level - 1) & 1], b.hist, b.flags, b.sflags, b.st, g.tb,
                                         g.chunk, b.cap_words);
@@ -763,11 +1079,16 @@ void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStrea
   k_scatter<<<256, kSB, 0, s>>>(level, b.kh, b.fp, b.pos, b.pos_base, il, b.off, b.bucket, b.st, g.tb, g.chunk);
 }
 
-void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s) {
+void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s, bool reserved) {
   const size_t lds = b.tile_mode == 0 ? tile_lds_bytes(g.tb) : 2ull * (1ull << (g.tb - 5)) * sizeof(uint32_t);
   k_tile<<<grid_tiles, kTB, lds, s>>>(
-      level, b.bucket, b.tile_start, b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb,
-      b.tile_mode);
+      level, b.bucket, b.tile_start, reserved ? b.tcnt + (uint64_t)level * kMaxTiles : nullptr, b.bucket_cap,
+      b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.tile_mode);
+}
+
+void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s) {
+  k_scatter_res<<<grid, kSB, 0, s>>>(level, b.list[(level - 1) & 1], b.tcnt + (uint64_t)level * kMaxTiles,
+                                     b.bucket, b.bucket_cap, b.flags, b.st, g.tb, b.cap_words);
 }
 
 void launch_binned_tail(int big_launched, const BinBuffers& b, hipStream_t s) {

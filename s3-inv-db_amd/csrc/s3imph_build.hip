@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -75,7 +76,11 @@ struct s3imph_ctx {
   unsigned *hist = nullptr, *hoff = nullptr, *tile_start = nullptr, *scan_sums = nullptr;
   unsigned long long* flags = nullptr;
   unsigned long long* sflags = nullptr;
+  unsigned* tcnt = nullptr;  // reservation-path tile counters, kMaxLevels x kMaxTiles
   int tile_mode = 0;
+  uint64_t target_tiles = kTargetTiles, target_tiles0 = kTargetTiles, target_chunks = kTargetChunks;
+  uint64_t res_max_keys = kResMaxKeys;
+  bool debug = false;
   bool lds_attr_set = false;
 
   // staging for host-memory builds
@@ -185,6 +190,7 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   dalloc(c->scan_sums, kHistCap / 2048 + 2);
   dalloc(c->flags, kMaxTiles + 2);
   dalloc(c->sflags, kHistCap / kScanSeg + 2);
+  dalloc(c->tcnt, (uint64_t)kMaxLevels * kMaxTiles);
   alloc_common(c, cap);
   dalloc(c->bits, c->cap_words);
   dalloc(c->rank_base, c->cap_words);
@@ -198,6 +204,7 @@ void free_workspace(s3imph_ctx* c) {
   dfree(c->rkeys[0]); dfree(c->rkeys[1]); dfree(c->ridx[0]); dfree(c->ridx[1]);
   dfree(c->block_sums); dfree(c->d_st);
   dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
+  dfree(c->tcnt);
   dfree(c->hist); dfree(c->hoff); dfree(c->tile_start); dfree(c->scan_sums); dfree(c->flags); dfree(c->sflags);
   if (c->h_st) (void)hipHostFree(c->h_st);
   c->h_st = nullptr;
@@ -300,6 +307,8 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   b.scan_sums = c->scan_sums;
   b.flags = c->flags;
   b.sflags = c->sflags;
+  b.tcnt = c->tcnt;
+  b.bucket_cap = c->cap_keys;
   b.tile_mode = c->tile_mode;
   b.bits = c->bits;
   b.cap_words = c->cap_words;
@@ -308,7 +317,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   b.st = c->d_st;
 
   const double q = 1.0 - std::exp(-0.5);  // fraction of keys that collide at load 1/2
-  const LevelGeom g0 = choose_geom(n);
+  const LevelGeom g0 = choose_geom(n, c->target_tiles0, c->target_chunks);
   int gc, gt, gs;
   // Grids from a (predicted) key count; kernels loop over whatever the device finds.
   auto grids = [&](uint64_t nk, LevelGeom g) {
@@ -332,16 +341,25 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   const int big = conservative ? kMaxLevels - 2 : predict_big_levels(n);
   int launched = 0;
   for (int L = 1; L <= big; ++L) {
+    // Level sizes concentrate tightly around n q^L; a level predicted within 1/kTailMargin
+    // of the tail's capacity is left to the tail (an unexpectedly large one is caught by
+    // kStTailOverflow and rerun conservatively).
     const double pred = (double)n * std::pow(q, L);
-    if (!conservative && pred < 0.25 * (double)kTailKeys) break;
+    if (!conservative && pred * kTailMargin < (double)kTailKeys) break;
     launched = L;
     const uint64_t nb = conservative ? n : (uint64_t)(pred * 1.1) + 4096;
-    const LevelGeom g = conservative ? g0 : choose_geom(nb);
+    const LevelGeom g = conservative ? g0 : choose_geom(nb, c->target_tiles, c->target_chunks);
     grids(nb, g);
-    launch_binned_count(L, nullptr, nullptr, 0, b, g, gc, s);
-    launch_binned_scan(L, b, gs, s);
-    launch_binned_scatter(L, b, g, s);
-    launch_binned_tile(L, b, g, gt, s);
+    if (!conservative && nb <= c->res_max_keys) {
+      const int gr = (int)std::min<uint64_t>((nb + kSubRound - 1) / kSubRound, 256);
+      launch_binned_scatter_res(L, b, g, gr, s);
+      launch_binned_tile(L, b, g, gt, s, true);
+    } else {
+      launch_binned_count(L, nullptr, nullptr, 0, b, g, gc, s);
+      launch_binned_scan(L, b, gs, s);
+      launch_binned_scatter(L, b, g, s);
+      launch_binned_tile(L, b, g, gt, s);
+    }
   }
   ev_mark(c, s, "levels");
   launch_binned_tail(launched, b, s);
@@ -382,9 +400,20 @@ int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
     HIPCHECK(hipMemcpyAsync(c->h_st, c->d_st, sizeof(LevelState), hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
     ev_collect(c);
+    if (c->debug) {
+      const LevelState& d = *c->h_st;
+      std::fprintf(stderr, "[s3imph] attempt %d: status 0x%x nlevels %u tail_first %u rank_total %llu\n  n:", attempt,
+                   d.status, d.nlevels, d.tail_first, (unsigned long long)d.rank_total);
+      for (int L = 0; L <= (int)d.nlevels + 1 && L < kMaxLevels; ++L)
+        std::fprintf(stderr, " %llu", (unsigned long long)d.n[L]);
+      std::fprintf(stderr, "\n  T:");
+      for (int L = 0; L <= (int)d.nlevels + 1 && L < kMaxLevels; ++L)
+        std::fprintf(stderr, " %llu", (unsigned long long)d.ntiles[L]);
+      std::fprintf(stderr, "\n");
+    }
     // Geometry/tail-capacity misses only mean the level-size prediction was off:
     // rerun with workspace-safe geometry (same bytes, slower schedule).
-    if (c->h_st->status & (kStGeometry | kStTailOverflow)) continue;
+    if (c->h_st->status & (kStGeometry | kStTailOverflow | kStResOverflow)) continue;
     break;
   }
   const LevelState& st = *c->h_st;
@@ -774,7 +803,12 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     HIPCHECK(hipSetDevice(device));
     c = new s3imph_ctx();
     c->device = device;
-    if (const char* m = std::getenv("S3IMPH_TILE_MODE")) c->tile_mode = std::atoi(m);  // A/B knob
+    if (const char* m = std::getenv("S3IMPH_TILE_MODE")) c->tile_mode = std::atoi(m);  // A/B knobs
+    if (const char* m = std::getenv("S3IMPH_TARGET_TILES")) c->target_tiles = std::strtoull(m, nullptr, 10);
+    if (const char* m = std::getenv("S3IMPH_TARGET_TILES0")) c->target_tiles0 = std::strtoull(m, nullptr, 10);
+    if (const char* m = std::getenv("S3IMPH_CHUNKS")) c->target_chunks = std::strtoull(m, nullptr, 10);
+    if (const char* m = std::getenv("S3IMPH_RES_MAX")) c->res_max_keys = std::strtoull(m, nullptr, 10);
+    c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     // A blocking stream: implicitly ordered with the legacy NULL stream, so work a
     // caller queued there (e.g. torch's default stream) completes before ours starts.
     HIPCHECK(hipStreamCreate(&c->own_stream));

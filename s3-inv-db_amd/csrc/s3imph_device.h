@@ -42,14 +42,13 @@ static __device__ __forceinline__ void fnv_8(uint64_t& a, uint64_t& b, uint64_t 
   for (int t = 0; t < 8; ++t) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
 }
 
-static __device__ __forceinline__ void fnv_both(const uint8_t* __restrict__ blob, uint64_t b0, uint64_t b1,
-                                                uint64_t& ha, uint64_t& hb) {
+// FNV-1a + FNV-1 over a key whose bytes start `sh` bits into aligned word w[0] and
+// span nw aligned words: stream word q = funnel(w[q], w[q+1]).  w may point into
+// global memory or LDS (the caller's pointer decides the address space once inlined).
+static __device__ __forceinline__ void fnv_words(const uint64_t* w, uint64_t nw, unsigned sh, uint64_t len,
+                                                 uint64_t& ha, uint64_t& hb) {
   uint64_t a = kFnvOffset, b = kFnvOffset;
-  if (b1 > b0) {
-    const uint64_t* w = reinterpret_cast<const uint64_t*>(blob + (b0 & ~7ull));
-    const uint64_t nw = ((b1 - 1) >> 3) - (b0 >> 3) + 1;  // aligned words overlapping the key
-    const unsigned sh = (unsigned)(b0 & 7) * 8;
-    const uint64_t len = b1 - b0;
+  if (len) {
     const uint64_t nfull = len >> 3;
     uint64_t cur = w[0];
     for (uint64_t q = 0; q < nfull; ++q) {
@@ -66,6 +65,47 @@ static __device__ __forceinline__ void fnv_both(const uint8_t* __restrict__ blob
       for (unsigned t = 0; t < 7; ++t)
         if (t < rem) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
     }
+  }
+  ha = a;
+  hb = b;
+}
+
+// FNV-1a + FNV-1 of blob[b0, b1), one dependent load per aligned word (funnel shifts).
+static __device__ __forceinline__ void fnv_both_loop(const uint8_t* __restrict__ blob, uint64_t b0, uint64_t b1,
+                                                     uint64_t& ha, uint64_t& hb) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(blob + (b0 & ~7ull));
+  const uint64_t nw = b1 > b0 ? ((b1 - 1) >> 3) - (b0 >> 3) + 1 : 0;  // aligned words overlapping the key
+  fnv_words(w, nw, (unsigned)(b0 & 7) * 8, b1 - b0, ha, hb);
+}
+
+// FNV-1a (key hash) and FNV-1 (fingerprint) of blob[b0, b1) in one pass.  The key's
+// aligned words are loaded 8 at a time (all 8 loads in flight before the first use);
+// stream word q = bytes [8q, 8q+8) of the key = funnel(w[q], w[q+1]) by the key's
+// misalignment.  Never reads past the key's last aligned word.
+static __device__ __forceinline__ void fnv_both(const uint8_t* __restrict__ blob, uint64_t b0, uint64_t b1,
+                                                uint64_t& ha, uint64_t& hb) {
+  uint64_t a = kFnvOffset, b = kFnvOffset;
+  if (b1 > b0) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(blob + (b0 & ~7ull));
+    const uint64_t nw = ((b1 - 1) >> 3) - (b0 >> 3) + 1;  // aligned words overlapping the key
+    const unsigned sh = (unsigned)(b0 & 7) * 8;
+    const uint64_t len = b1 - b0;
+    const uint64_t nfull = len >> 3;
+    const unsigned rem = (unsigned)(len & 7);
+    uint64_t cur = w[0], vrem = 0;
+    for (uint64_t base = 0; base <= nfull; base += 8) {
+      uint64_t W[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) W[q] = (base + q + 1 < nw) ? w[base + q + 1] : 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t v = sh ? (cur >> sh) | (W[q] << (64 - sh)) : cur;
+        if (base + q < nfull) fnv_8(a, b, v);
+        if (base + q == nfull) vrem = v;
+        cur = W[q];
+      }
+    }
+    for (unsigned t = 0; t < rem; ++t) fnv_step(a, b, (uint32_t)(vrem >> (8 * t)) & 0xffu);
   }
   ha = a;
   hb = b;

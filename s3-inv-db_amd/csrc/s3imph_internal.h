@@ -43,6 +43,7 @@ constexpr uint64_t kHistCap = 8ull << 20;             // tiles x chunks entries
 constexpr unsigned kStTailOverflow = 16u;             // tail reached with a level too big for LDS
 constexpr unsigned kStGeometry = 32u;                 // tiles/chunks outside the workspace
 constexpr unsigned kStLookback = 64u;                 // a look-back wait timed out
+constexpr unsigned kStResOverflow = 128u;  // a reservation-path tile slot overflowed (rerun counted)
 constexpr uint64_t kSubRound = 4096;                  // keys per LDS-sorted scatter round
 constexpr uint64_t kScanSeg = 8192;                   // histogram entries per scan segment
 
@@ -51,15 +52,22 @@ struct LevelGeom {
   uint64_t chunk;     // keys per count/scatter chunk
 };
 
-// Host-side choice for a level of about n keys: (512, 1024] tiles; chunks of a
-// multiple of kSubRound keys, few enough that tiles x chunks stays under kHistCap.
-inline LevelGeom choose_geom(uint64_t n) {
+// Host-side choice for a level of about n keys: the smallest tile (>= 2^kTileMinBits
+// positions) that leaves at most target_tiles tiles, and about target_chunks chunks of
+// a multiple of kChunkGran keys (a chunk is one count block's unit of work, so the
+// chunk count is sized to fill the resident blocks in one round), few enough that
+// tiles x chunks stays under kHistCap.
+constexpr uint64_t kChunkGran = 1024;
+constexpr uint64_t kResMaxKeys = 2ull << 20;  // levels up to this size use the reservation scatter
+constexpr double kTailMargin = 1.25;
+constexpr uint64_t kTargetChunks = 768;  // 3 resident 1024-thread count blocks x 256 CUs
+inline LevelGeom choose_geom(uint64_t n, uint64_t target_tiles = kTargetTiles,
+                             uint64_t target_chunks = kTargetChunks) {
   const uint64_t size = 64 * level_words(n ? n : 1);
   unsigned tb = kTileMinBits;
-  while (tb < kTileMaxBits && (size >> tb) > kTargetTiles) ++tb;
+  while (tb < kTileMaxBits && (size >> tb) > target_tiles) ++tb;
   const uint64_t T = (size + (1ull << tb) - 1) >> tb;
-  // ~1024 chunks (one 1024-thread count block each), a multiple of the scatter round.
-  uint64_t chunk = ((n + 1023) / 1024 + kSubRound - 1) / kSubRound * kSubRound;
+  uint64_t chunk = ((n + target_chunks - 1) / target_chunks + kChunkGran - 1) / kChunkGran * kChunkGran;
   if (chunk < kSubRound) chunk = kSubRound;
   while (((n + chunk - 1) / chunk) * T > kHistCap) chunk *= 2;
   return {tb, chunk};
@@ -136,6 +144,8 @@ struct BinBuffers {
   unsigned* scan_sums;                  // scan block sums
   unsigned long long* flags;            // decoupled look-back words, one per tile
   unsigned long long* sflags;           // look-back words of the histogram scan
+  unsigned* tcnt;                       // per-level tile fill counters (reservation path), kMaxLevels x kMaxTiles
+  uint64_t bucket_cap;                  // bucket capacity in records
   int tile_mode;                        // 0: rank-order gather, 1: in-order with window writes
   uint64_t* bits;
   uint64_t cap_words;
@@ -148,7 +158,9 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
                          LevelGeom g, int grid_chunks, hipStream_t s);
 void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s);
 void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s);
-void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s);
+void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s,
+                        bool reserved = false);
+void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s);
 void launch_binned_tail(int big_launched, const BinBuffers& b, hipStream_t s);
 
 // ---- host helpers (s3imph_host.cpp) -------------------------------------------

@@ -174,6 +174,50 @@ def test_duplicate_keys_error_builder(s3, tmp_path):
     assert not (tmp_path / "mph.bin").exists()
 
 
+def test_duplicate_group_overflowing_a_reservation_slot(s3, ctx):
+    """150k copies of one key all land in one tile of every level: the small-level
+    reservation slot overflows, the build reruns on the counted path, and the result is
+    still the reference's duplicate error (mphf_streaming.go:143)."""
+    keys = [b"p/%07d/" % i for i in range(50_000)] + [b"dup/"] * 150_000
+    blob, offs = O.keys_to_blob(keys)
+    with pytest.raises(s3.MPHFError) as e:
+        _device_build(s3, ctx, blob, offs)
+    assert e.value.status == s3.ERR_DUP_KEY_HASH
+    _device_build(s3, ctx, *O.keys_to_blob([b"x/", b"y/"]))
+
+
+def test_repeated_builds_same_context_bit_exact(s3, oracle_lib, ctx):
+    """Builds of different inputs back to back in one context: every one bit-exact, so
+    no level depends on workspace contents left by an earlier build."""
+    for seed, n in [(3, 1_500_000), (4, 1_500_000), (5, 900_000), (3, 1_500_000)]:
+        blob, offs = s3.gen_keys(0, seed, 32, 0, n)
+        st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)
+        assert st == 0
+        gfp, gpo, gmph, _ = _device_build(s3, ctx, blob, offs)
+        assert gmph == mph
+        assert np.array_equal(gfp, fp)
+        assert np.array_equal(gpo, po)
+
+
+@pytest.mark.parametrize("res_max", ["0", "100000000"])
+def test_small_level_paths_bit_exact(s3, oracle_lib, res_max, monkeypatch):
+    """Levels >= 1 on the counted path only (res_max 0) and on the reservation path for
+    every level (res_max large): both bit-exact with the oracle."""
+    monkeypatch.setenv("S3IMPH_RES_MAX", res_max)
+    c = s3.DeviceBuilder(0)
+    try:
+        n = 2_000_000
+        blob, offs = s3.gen_keys(0, 7, 32, 0, n)
+        st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)
+        assert st == 0
+        gfp, gpo, gmph, info = _device_build(s3, c, blob, offs)
+        assert gmph == mph
+        assert np.array_equal(gfp, fp)
+        assert np.array_equal(gpo, po)
+    finally:
+        c.close()
+
+
 def test_c2_10m_bit_exact(s3, oracle_lib, ctx):
     """BASELINE config 2: 10M synthetic prefixes, avg 32 B — full bit-exact comparison."""
     n = 10_000_000

@@ -11,7 +11,7 @@ seg = r[idx[-1]:]
 t0 = int(seg[0]["Start_Timestamp"])
 for x in seg:
     s, e = int(x["Start_Timestamp"]), int(x["End_Timestamp"])
-    nm = x["Kernel_Name"].split("(")[0].split("::")[-1]
+    nm = x["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].split("::")[-1]
     if (e - s) / 1e3 > thresh:
         print(f"{nm:16s} start={(s - t0) / 1e3:8.1f} dur={(e - s) / 1e3:7.1f} "
               f"grid={int(x['Grid_Size_X']) // int(x['Workgroup_Size_X']):>6d} lds={x['LDS_Block_Size']}")
