@@ -33,13 +33,12 @@ namespace {
 
 constexpr int kCB = 1024;             // count block
 constexpr int kSB = 1024;             // scatter block
-constexpr int kTB = 1024;             // tile block
 constexpr int kTailT = 1024;          // tail block
 constexpr unsigned kLenBuckets = 256;  // key-length classes of the level-0 hash sort
 constexpr uint64_t kTcntWords = (uint64_t)kMaxLevels * kMaxTiles;
 constexpr uint64_t kLdsTiles = kMaxTiles;  // histogram / cursor entries in LDS
 constexpr unsigned long long kGate = kTailKeys;
-constexpr int kTailW32 = (int)(2 * ((kGammaNum * kTailKeys + 63) / 64));  // 4096 u32 words
+constexpr int kTailW32 = (int)(2 * ((kGammaNum * kTailKeys + 63) / 64));  // A/C words of the largest tail level
 constexpr unsigned long long kFlagAgg = 1ull << 62;
 constexpr unsigned long long kFlagInc = 2ull << 62;
 constexpr unsigned long long kFlagVal = (1ull << 62) - 1;
@@ -500,15 +499,18 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   const uint64_t stride = (uint64_t)gridDim.x * kSubRound;
   uint64_t r0 = (uint64_t)blockIdx.x * kSubRound;
   if (r0 >= n) return;
-  Rec rec[kScatterKPT];
-  auto load_round = [&](uint64_t base) {
+  // records as three scalar arrays: a conditionally loaded Rec[] would live in scratch
+  uint64_t rk_[kScatterKPT], rf_[kScatterKPT], rp_[kScatterKPT];
 #pragma unroll
-    for (int q = 0; q < kScatterKPT; ++q) {
-      const uint64_t i = base + (uint64_t)q * kSB + tid;
-      if (i < n) rec[q] = ilist[i];
+  for (int q = 0; q < kScatterKPT; ++q) {
+    const uint64_t i = r0 + (uint64_t)q * kSB + tid;
+    rk_[q] = rf_[q] = rp_[q] = 0;
+    if (i < n) {
+      rk_[q] = ilist[i].k;
+      rf_[q] = ilist[i].f;
+      rp_[q] = ilist[i].p;
     }
-  };
-  load_round(r0);
+  }
   for (uint64_t t = tid; t < T; t += kSB) cnt[t] = 0;
   if (tid == 0) s_over = 0;
   __syncthreads();
@@ -518,7 +520,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     for (int q = 0; q < kScatterKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < n) {
-        tt[q] = (unsigned)(bb_index(seed, rec[q].k, words, magic) >> tb);
+        tt[q] = (unsigned)(bb_index(seed, rk_[q], words, magic) >> tb);
         rk[q] = atomicAdd(&cnt[tt[q]], 1u);
       }
     }
@@ -553,14 +555,22 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < n) {
         const unsigned slot = start[tt[q]] + rk[q];
-        stage[slot] = rec[q];
+        stage[slot] = Rec{rk_[q], rf_[q], rp_[q]};
         stile[slot] = (unsigned short)tt[q];
       }
     }
     const unsigned m = (unsigned)min<uint64_t>(kSubRound, n - r0);
     r0 += stride;
     const bool more = r0 < n;
-    if (more) load_round(r0);
+#pragma unroll
+    for (int q = 0; q < kScatterKPT; ++q) {
+      const uint64_t i = r0 + (uint64_t)q * kSB + tid;
+      if (i < n) {
+        rk_[q] = ilist[i].k;
+        rf_[q] = ilist[i].f;
+        rp_[q] = ilist[i].p;
+      }
+    }
     __syncthreads();
     if (s_over) break;
     for (unsigned j = tid; j < m; j += kSB) {
@@ -675,24 +685,25 @@ __global__ __launch_bounds__(kHST) void k_hscan(int level, const unsigned* __res
   }
 }
 
-__global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__ bucket,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ bucket,
                                               const unsigned* __restrict__ tile_start,
                                               const unsigned* __restrict__ tcnt, uint64_t bucket_cap,
                                               unsigned long long* flags, uint64_t* __restrict__ bits,
                                               Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
                                               uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
-                                              int mode) {
+                                              int mode, unsigned long long* __restrict__ prof) {
   extern __shared__ uint32_t dyn[];
   __shared__ unsigned long long s_t, s_prefix;
-  __shared__ unsigned s_wc[kTB / 64];
-  __shared__ unsigned long long s_wbase[kTB / 64];
+  __shared__ unsigned s_wc[NT / 64];
+  __shared__ unsigned long long s_wbase[NT / 64];
   if (!level_active(level, st)) return;
   const uint64_t N = st->n[0];
   const uint64_t words = st->words[level], magic = st->magic[level];
   const uint64_t T = st->ntiles[level];
   const uint64_t w32_level = 2 * words;
   const unsigned tpw = 1u << (tb - 5);
-  const unsigned per = (tpw + kTB - 1) / kTB;
+  const unsigned per = (tpw + NT - 1) / NT;
   uint32_t* sA = dyn;
   uint32_t* sC = dyn + tpw;
   const bool small = tb <= kCacheBits && mode == 0;
@@ -707,13 +718,20 @@ __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__
   bool bad = false;
   for (;;) {
     if (tid == 0) s_t = atomicAdd(&st->ticket[level], 1ull);
-    for (unsigned w = tid; w < tpw; w += kTB) {
+    for (unsigned w = tid; w < tpw; w += NT) {
       sA[w] = 0;
       sC[w] = 0;
     }
     __syncthreads();
     const uint64_t t = s_t;
     if (t >= T) break;
+    // phase timestamps of this tile (debug builds of the schedule only: prof != null)
+    unsigned long long* tp = prof ? prof + ((uint64_t)level * kMaxTiles + (t < kMaxTiles ? t : 0)) * 8 : nullptr;
+#define TPROF(i)                                 \
+  do {                                           \
+    if (tp && tid == 0) tp[i] = wall_clock64(); \
+  } while (0)
+    TPROF(0);
     // bucket range: from the histogram scan, or (reservation path) a fixed slot per tile
     uint64_t lo, nk;
     if (tcnt) {
@@ -727,16 +745,16 @@ __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__
     const uint64_t tbase = t << tb;
     const bool cached = small && nk <= kcap;
     // ---- mark: A/C in LDS (and each record's in-tile position, when cached)
-    for (uint64_t j0 = tid; j0 < nk; j0 += (uint64_t)kTB * kTU) {
+    for (uint64_t j0 = tid; j0 < nk; j0 += (uint64_t)NT * kTU) {
       uint64_t k[kTU];
 #pragma unroll
       for (int u = 0; u < kTU; ++u) {
-        const uint64_t j = j0 + (uint64_t)u * kTB;
+        const uint64_t j = j0 + (uint64_t)u * NT;
         k[u] = j < nk ? rb[j].k : 0;
       }
 #pragma unroll
       for (int u = 0; u < kTU; ++u) {
-        const uint64_t j = j0 + (uint64_t)u * kTB;
+        const uint64_t j = j0 + (uint64_t)u * NT;
         if (j < nk) {
           const unsigned loc = (unsigned)(bb_index(seed, k[u], words, magic) - tbase);
           if (cached) sloc[j] = (unsigned short)loc;
@@ -747,6 +765,7 @@ __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__
       }
     }
     __syncthreads();
+    TPROF(1);
     // ---- finalize: A & ~C -> LDS + global bits; per-word rank prefix into C
     const unsigned w0 = tid * per;
     uint64_t cntw = 0;
@@ -761,7 +780,7 @@ __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__
       }
     }
     uint64_t pop;
-    uint64_t run = block_exscan<kTB>(cntw, &pop);
+    uint64_t run = block_exscan<NT>(cntw, &pop);
     for (unsigned q = 0; q < per; ++q) {
       const unsigned w = w0 + q;
       if (w < tpw) {
@@ -769,6 +788,7 @@ __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__
         run += __popc(sA[w]);
       }
     }
+    TPROF(2);
     if (wave == 0) {
       const uint64_t excl = look_back_wave(flags, t, pop, st);
       if (lane == 0) {
@@ -777,11 +797,12 @@ __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__
       }
     }
     __syncthreads();
+    TPROF(3);
     const uint64_t base = lvl_base + s_prefix;
     unsigned wc = 0;
     if (cached) {
       // ---- rank pass (LDS only): rank -> record index; redo bitmask by ballot
-      for (uint64_t jb = wave * 64; jb < nk; jb += kTB) {
+      for (uint64_t jb = wave * 64; jb < nk; jb += NT) {
         const uint64_t j = jb + lane;
         bool redo = false;
         if (j < nk) {
@@ -799,27 +820,33 @@ __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__
         wc += __popcll(m);
       }
       __syncthreads();
+      TPROF(4);
       // ---- outputs: consecutive ranks -> consecutive fp_out/pos_out slots
       if (base + pop > N) bad = true;
-      for (uint64_t r0 = tid; r0 < pop && base + pop <= N; r0 += (uint64_t)kTB * kTU) {
-        Rec rc[kTU];
+      for (uint64_t r0 = tid; r0 < pop && base + pop <= N; r0 += (uint64_t)NT * kTU) {
+        uint64_t cf[kTU], cp[kTU];  // only f and p are needed for a settled key
 #pragma unroll
         for (int u = 0; u < kTU; ++u) {
-          const uint64_t r = r0 + (uint64_t)u * kTB;
-          if (r < pop) rc[u] = rb[sridx[r]];
+          const uint64_t r = r0 + (uint64_t)u * NT;
+          cf[u] = cp[u] = 0;
+          if (r < pop) {
+            const Rec* src = rb + sridx[r];
+            cf[u] = src->f;
+            cp[u] = src->p;
+          }
         }
 #pragma unroll
         for (int u = 0; u < kTU; ++u) {
-          const uint64_t r = r0 + (uint64_t)u * kTB;
+          const uint64_t r = r0 + (uint64_t)u * NT;
           if (r < pop) {
-            fp_out[base + r] = rc[u].f;
-            pos_out[base + r] = rc[u].p;
+            fp_out[base + r] = cf[u];
+            pos_out[base + r] = cp[u];
           }
         }
       }
     } else {
       // ---- generic path (tiles too big to cache): rehash, write outputs in place
-      for (uint64_t jb = wave * 64; jb < nk; jb += kTB) {
+      for (uint64_t jb = wave * 64; jb < nk; jb += NT) {
         const uint64_t j = jb + lane;
         bool redo = false;
         if (j < nk) {
@@ -843,38 +870,65 @@ __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__
       }
     }
     // ---- collided records -> next level (one reservation per tile, per-wave offsets)
+    if (tp) __syncthreads();
+    TPROF(5);
     if (lane == 0) s_wc[wave] = wc;
     __syncthreads();
     if (tid == 0) {
       unsigned tot = 0;
-      for (int w = 0; w < kTB / 64; ++w) tot += s_wc[w];
+      for (int w = 0; w < NT / 64; ++w) tot += s_wc[w];
       unsigned long long b0 = tot ? atomicAdd(&st->n[level + 1], (unsigned long long)tot) : 0;
-      for (int w = 0; w < kTB / 64; ++w) {
+      for (int w = 0; w < NT / 64; ++w) {
         s_wbase[w] = b0;
         b0 += s_wc[w];
       }
     }
     __syncthreads();
+    TPROF(6);
     if (wc) {
       uint64_t o = s_wbase[wave];
-      for (uint64_t jb = wave * 64; jb < nk; jb += kTB) {
-        const uint64_t j = jb + lane;
-        uint64_t m;
-        if (cached) {
-          m = srm[jb >> 6];
-        } else {
+      const uint64_t lt = lanemask_lt();
+      if (cached) {
+        // kRU 64-record steps per iteration: all their loads in flight before the stores
+        constexpr int kRU = 2;
+        for (uint64_t jb0 = wave * 64; jb0 < nk; jb0 += (uint64_t)NT * kRU) {
+          uint64_t m[kRU], ck[kRU], cf[kRU], cp[kRU];
+#pragma unroll
+          for (int u = 0; u < kRU; ++u) {
+            const uint64_t jb = jb0 + (uint64_t)u * NT;
+            m[u] = jb < nk ? srm[jb >> 6] : 0ull;
+            ck[u] = cf[u] = cp[u] = 0;
+            if ((m[u] >> lane) & 1ull) {
+              ck[u] = rb[jb + lane].k;
+              cf[u] = rb[jb + lane].f;
+              cp[u] = rb[jb + lane].p;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < kRU; ++u) {
+            if ((m[u] >> lane) & 1ull) next[o + __popcll(m[u] & lt)] = Rec{ck[u], cf[u], cp[u]};
+            o += __popcll(m[u]);
+          }
+        }
+      } else {
+        for (uint64_t jb = wave * 64; jb < nk; jb += NT) {
+          const uint64_t j = jb + lane;
           bool redo = false;
+          uint64_t ck = 0;
           if (j < nk) {
-            const unsigned loc = (unsigned)(bb_index(seed, rb[j].k, words, magic) - tbase);
+            ck = rb[j].k;
+            const unsigned loc = (unsigned)(bb_index(seed, ck, words, magic) - tbase);
             redo = !((sA[loc >> 5] >> (loc & 31)) & 1u);
           }
-          m = __ballot(redo);
+          const uint64_t m = __ballot(redo);
+          if (redo) next[o + __popcll(m & lt)] = Rec{ck, rb[j].f, rb[j].p};
+          o += __popcll(m);
         }
-        if ((m >> lane) & 1ull) next[o + __popcll(m & lanemask_lt())] = rb[j];
-        o += __popcll(m);
       }
     }
     __syncthreads();
+    TPROF(7);
+#undef TPROF
   }
   if (bad) atomicOr(&st->status, kStRank);
 }
@@ -884,7 +938,8 @@ __global__ __launch_bounds__(kTB) void k_tile(int level, const Rec* __restrict__
 // written directly, collided records compacted into the other list.
 __global__ __launch_bounds__(kTailT) void k_bin_tail(int big_launched, Rec* list0, Rec* list1, uint64_t* bits,
                                                      uint64_t cap_words, uint64_t* __restrict__ fp_out,
-                                                     uint64_t* __restrict__ pos_out, LevelState* st) {
+                                                     uint64_t* __restrict__ pos_out, LevelState* st,
+                                                     unsigned long long* __restrict__ prof) {
   __shared__ uint32_t sA[kTailW32];
   __shared__ uint32_t sC[kTailW32];
   __shared__ uint32_t spre[kTailW32];
@@ -909,6 +964,8 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int big_launched, Rec* list
   for (;;) {
     const int L = s_level;
     const uint64_t n = s_n;
+    // debug: level start times in the last prof row
+    if (prof && tid == 0 && L < kMaxLevels) prof[(uint64_t)(kMaxLevels - 1) * kMaxTiles * 8 + L] = wall_clock64();
     if (n == 0) break;
     if (L >= kMaxLevels) {
       if (tid == 0) atomicOr(&st->status, kStTooManyLevels);
@@ -967,25 +1024,30 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int big_launched, Rec* list
     }
     __syncthreads();
     for (uint64_t jb0 = tid & ~63u; jb0 < n; jb0 += (uint64_t)kTailT * kTU) {
-      Rec rc[kTU];
+      uint64_t ck[kTU], cf[kTU], cp[kTU];
 #pragma unroll
       for (int u = 0; u < kTU; ++u) {
         const uint64_t j = jb0 + (uint64_t)u * kTailT + lane;
-        if (j < n) rc[u] = in[j];
+        ck[u] = cf[u] = cp[u] = 0;
+        if (j < n) {
+          ck[u] = in[j].k;
+          cf[u] = in[j].f;
+          cp[u] = in[j].p;
+        }
       }
 #pragma unroll
       for (int u = 0; u < kTU; ++u) {
         const uint64_t j = jb0 + (uint64_t)u * kTailT + lane;
         bool r = false;
         if (j < n) {
-          const uint64_t x = bb_index(seed, rc[u].k, words, magic);
+          const uint64_t x = bb_index(seed, ck[u], words, magic);
           const uint32_t wv = sA[x >> 5];
           const uint32_t bit = 1u << (x & 31);
           if (wv & bit) {
             const uint64_t q = base + spre[x >> 5] + __popc(wv & (bit - 1));
             if (q < N) {
-              fp_out[q] = rc[u].f;
-              pos_out[q] = rc[u].p;
+              fp_out[q] = cf[u];
+              pos_out[q] = cp[u];
             } else {
               bad = true;
             }
@@ -998,7 +1060,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int big_launched, Rec* list
           unsigned long long o = 0;
           if (lane == 0) o = atomicAdd(&s_next, (unsigned long long)__popcll(m));
           o = __shfl(o, 0);
-          if (r) out[o + __popcll(m & lanemask_lt())] = rc[u];
+          if (r) out[o + __popcll(m & lanemask_lt())] = Rec{ck[u], cf[u], cp[u]};
         }
       }
     }
@@ -1038,7 +1100,9 @@ size_t tile_lds_bytes(unsigned tb) {
 void binned_set_lds_limits() {
   (void)hipFuncSetAttribute((const void*)k_hash_count0_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(((kLdsTiles + 1) / 2 + kHashWinWords) * sizeof(uint64_t)));
-  (void)hipFuncSetAttribute((const void*)k_tile, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_tile<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)tile_lds_bytes(kTileMaxBits));
+  (void)hipFuncSetAttribute((const void*)k_tile<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)tile_lds_bytes(kTileMaxBits));
 }
 
@@ -1081,9 +1145,10 @@ void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStrea
 
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s, bool reserved) {
   const size_t lds = b.tile_mode == 0 ? tile_lds_bytes(g.tb) : 2ull * (1ull << (g.tb - 5)) * sizeof(uint32_t);
-  k_tile<<<grid_tiles, kTB, lds, s>>>(
+  auto kern = b.tile_block == 512 ? k_tile<512> : k_tile<1024>;
+  kern<<<grid_tiles, b.tile_block == 512 ? 512 : 1024, lds, s>>>(
       level, b.bucket, b.tile_start, reserved ? b.tcnt + (uint64_t)level * kMaxTiles : nullptr, b.bucket_cap,
-      b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.tile_mode);
+      b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.tile_mode, b.tile_prof);
 }
 
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s) {
@@ -1094,7 +1159,7 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
 void launch_binned_tail(int big_launched, const BinBuffers& b, hipStream_t s) {
   k_level_setup<<<1, 64, 0, s>>>(big_launched + 1, b.st);
   k_bin_tail<<<1, kTailT, 0, s>>>(big_launched, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out, b.pos_out,
-                                  b.st);
+                                  b.st, b.tile_prof);
 }
 
 }  // namespace s3imph

@@ -78,9 +78,11 @@ struct s3imph_ctx {
   unsigned long long* sflags = nullptr;
   unsigned* tcnt = nullptr;  // reservation-path tile counters, kMaxLevels x kMaxTiles
   int tile_mode = 0;
+  int tile_block = 1024;
   uint64_t target_tiles = kTargetTiles, target_tiles0 = kTargetTiles, target_chunks = kTargetChunks;
   uint64_t res_max_keys = kResMaxKeys;
   bool debug = false;
+  unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps
   bool lds_attr_set = false;
 
   // staging for host-memory builds
@@ -205,6 +207,7 @@ void free_workspace(s3imph_ctx* c) {
   dfree(c->block_sums); dfree(c->d_st);
   dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
   dfree(c->tcnt);
+  dfree(c->tile_prof);
   dfree(c->hist); dfree(c->hoff); dfree(c->tile_start); dfree(c->scan_sums); dfree(c->flags); dfree(c->sflags);
   if (c->h_st) (void)hipHostFree(c->h_st);
   c->h_st = nullptr;
@@ -310,6 +313,14 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   b.tcnt = c->tcnt;
   b.bucket_cap = c->cap_keys;
   b.tile_mode = c->tile_mode;
+  b.tile_block = c->tile_block;
+  b.tile_prof = nullptr;
+  if (c->debug) {
+    const size_t nprof = (size_t)kMaxLevels * kMaxTiles * 8;
+    if (!c->tile_prof) HIPCHECK(hipMalloc(&c->tile_prof, nprof * sizeof(unsigned long long)));
+    HIPCHECK(hipMemsetAsync(c->tile_prof, 0, nprof * sizeof(unsigned long long), s));
+    b.tile_prof = c->tile_prof;
+  }
   b.bits = c->bits;
   b.cap_words = c->cap_words;
   b.fp_out = fp_out;
@@ -373,6 +384,47 @@ void set_lds_attrs(s3imph_ctx* c) {
   c->lds_attr_set = true;
 }
 
+// Debug: per-level averages of the tile kernel's phase durations (wall clock, 100 MHz).
+void print_tile_profile(s3imph_ctx* c) {
+  if (!c->tile_prof) return;
+  std::vector<unsigned long long> h((size_t)kMaxLevels * kMaxTiles * 8);
+  HIPCHECK(hipMemcpy(h.data(), c->tile_prof, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  static const char* names[7] = {"mark", "final", "lookbk", "rank", "output", "redoN", "redoW"};
+  {
+    const unsigned long long* tl = &h[(size_t)(kMaxLevels - 1) * kMaxTiles * 8];
+    std::fprintf(stderr, "  tail level starts (us from first):");
+    unsigned long long t0 = 0;
+    for (int L = 0; L < kMaxLevels; ++L) {
+      if (!tl[L]) continue;
+      if (!t0) t0 = tl[L];
+      std::fprintf(stderr, " L%d@%.1f", L, (tl[L] - t0) / 100.0);
+    }
+    std::fprintf(stderr, "\n");
+  }
+  for (int L = 0; L < kMaxLevels - 1; ++L) {
+    double sum[7] = {0};
+    unsigned long long lo = ~0ull, hi = 0;
+    int cnt = 0;
+    for (int t = 0; t < kMaxTiles; ++t) {
+      const unsigned long long* p = &h[((size_t)L * kMaxTiles + t) * 8];
+      if (!p[0] || !p[7]) continue;
+      ++cnt;
+      lo = std::min(lo, p[0]);
+      hi = std::max(hi, p[7]);
+      unsigned long long prev = p[0];
+      for (int i = 1; i < 8; ++i) {
+        const unsigned long long v = p[i] ? p[i] : prev;
+        sum[i - 1] += (double)(v - prev);
+        prev = v;
+      }
+    }
+    if (!cnt) continue;
+    std::fprintf(stderr, "  tile L%d: %d tiles, span %.1f us, avg us:", L, cnt, (hi - lo) / 100.0);
+    for (int i = 0; i < 7; ++i) std::fprintf(stderr, " %s %.2f", names[i], sum[i] / cnt / 100.0);
+    std::fprintf(stderr, "\n");
+  }
+}
+
 int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                  uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s,
                  s3imph_build_info* info, std::string* msg) {
@@ -410,6 +462,7 @@ int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
       for (int L = 0; L <= (int)d.nlevels + 1 && L < kMaxLevels; ++L)
         std::fprintf(stderr, " %llu", (unsigned long long)d.ntiles[L]);
       std::fprintf(stderr, "\n");
+      print_tile_profile(c);
     }
     // Geometry/tail-capacity misses only mean the level-size prediction was off:
     // rerun with workspace-safe geometry (same bytes, slower schedule).
@@ -809,6 +862,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     if (const char* m = std::getenv("S3IMPH_CHUNKS")) c->target_chunks = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_RES_MAX")) c->res_max_keys = std::strtoull(m, nullptr, 10);
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
+    if (const char* m = std::getenv("S3IMPH_TILE_BLOCK")) c->tile_block = std::atoi(m);
     // A blocking stream: implicitly ordered with the legacy NULL stream, so work a
     // caller queued there (e.g. torch's default stream) completes before ours starts.
     HIPCHECK(hipStreamCreate(&c->own_stream));

@@ -59,7 +59,7 @@ struct LevelGeom {
 // tiles x chunks stays under kHistCap.
 constexpr uint64_t kChunkGran = 1024;
 constexpr uint64_t kResMaxKeys = 2ull << 20;  // levels up to this size use the reservation scatter
-constexpr double kTailMargin = 1.25;
+constexpr double kTailMargin = 1.1;
 constexpr uint64_t kTargetChunks = 768;  // 3 resident 1024-thread count blocks x 256 CUs
 inline LevelGeom choose_geom(uint64_t n, uint64_t target_tiles = kTargetTiles,
                              uint64_t target_chunks = kTargetChunks) {
@@ -81,7 +81,7 @@ constexpr unsigned kStRank = 8u;           // a position landed outside [0, N)
 
 // Levels whose active-key count is at most this run inside one workgroup with
 // LDS-resident bit vectors (k_tail); larger levels run as full-grid kernels.
-constexpr unsigned long long kTailKeys = 65536;
+constexpr unsigned long long kTailKeys = 16384;
 constexpr int kTailThreads = 1024;
 constexpr int kTailLdsWords32 = 2 * 2 * ((kGammaNum * kTailKeys + 63) / 64);  // A and C, u32 words
 
@@ -146,7 +146,9 @@ struct BinBuffers {
   unsigned long long* sflags;           // look-back words of the histogram scan
   unsigned* tcnt;                       // per-level tile fill counters (reservation path), kMaxLevels x kMaxTiles
   uint64_t bucket_cap;                  // bucket capacity in records
-  int tile_mode;                        // 0: rank-order gather, 1: in-order with window writes
+  int tile_mode;
+  int tile_block;                       // tile workgroup size (512 or 1024)
+  unsigned long long* tile_prof;        // debug: per (level, tile) phase timestamps, or null                        // 0: rank-order gather, 1: in-order with window writes
   uint64_t* bits;
   uint64_t cap_words;
   uint64_t* fp_out;
