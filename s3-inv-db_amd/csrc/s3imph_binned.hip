@@ -933,6 +933,260 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
   if (bad) atomicOr(&st->status, kStRank);
 }
 
+// ------------------------------------------------------- register-resident tile -----
+// Tiles of at most 2^kRegMaxBits positions hold ~2^(tb-1) records, at most kRegR per
+// thread (record r NT + i belongs to thread i, so every load instruction is coalesced):
+// each thread loads its records once (all loads in flight together) and keeps
+// (k, f, p, in-tile position) in registers through mark -> finalize -> look-back.
+// Settled records go to an LDS stage indexed by rank (copied out coalesced), collided
+// ones straight from registers to the next list: the bucket is read exactly once.
+// A tile with more records than fit takes a streaming fallback (never at load 1/2).
+constexpr int kRegR = 20;
+constexpr unsigned kRegMaxBits = 14;
+constexpr int kRT = 512;
+// Settled-record stage: a tile settles ~0.30 x 2^tb keys (gamma 2); 3/8 x 2^tb covers
+// it with a wide margin, ranks past it are written directly.
+__host__ __device__ constexpr unsigned reg_stage(unsigned tb) { return (3u << tb) / 8; }
+size_t tile_reg_lds_bytes(unsigned tb) {
+  return (size_t)reg_stage(tb) * 16 + 2ull * (1ull << (tb - 5)) * sizeof(uint32_t);
+}
+
+__global__ __launch_bounds__(kRT) void k_tile_reg(int level, const Rec* __restrict__ bucket,
+                                                  const unsigned* __restrict__ tile_start,
+                                                  const unsigned* __restrict__ tcnt, uint64_t bucket_cap,
+                                                  unsigned long long* flags, uint64_t* __restrict__ bits,
+                                                  Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
+                                                  uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
+                                                  unsigned long long* __restrict__ prof) {
+  constexpr int NT = kRT;
+  extern __shared__ uint64_t dyn64[];
+  __shared__ unsigned long long s_t, s_prefix;
+  __shared__ unsigned s_wc[NT / 64];
+  __shared__ unsigned long long s_wbase[NT / 64];
+  if (!level_active(level, st)) return;
+  const uint64_t N = st->n[0];
+  const uint64_t words = st->words[level], magic = st->magic[level];
+  const uint64_t T = st->ntiles[level];
+  const uint64_t w32_level = 2 * words;
+  const unsigned tpw = 1u << (tb - 5);
+  const unsigned per = (tpw + NT - 1) / NT;
+  const unsigned scap = reg_stage(tb);
+  uint64_t* sf = dyn64;
+  uint64_t* sp = dyn64 + scap;
+  uint32_t* sA = reinterpret_cast<uint32_t*>(dyn64 + 2 * scap);
+  uint32_t* sC = sA + tpw;
+  uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[level]);
+  const uint64_t seed = level_seed(level);
+  const uint64_t lvl_base = st->lvl_base[level];
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint64_t lt = lanemask_lt();
+  bool bad = false;
+  for (;;) {
+    if (tid == 0) s_t = atomicAdd(&st->ticket[level], 1ull);
+    for (unsigned w = tid; w < tpw; w += NT) {
+      sA[w] = 0;
+      sC[w] = 0;
+    }
+    __syncthreads();
+    const uint64_t t = s_t;
+    if (t >= T) break;
+    unsigned long long* tp = prof ? prof + ((uint64_t)level * kMaxTiles + (t < kMaxTiles ? t : 0)) * 8 : nullptr;
+#define TPROF(i)                                 \
+  do {                                           \
+    if (tp && tid == 0) tp[i] = wall_clock64(); \
+  } while (0)
+    TPROF(0);
+    uint64_t lo, nk;
+    if (tcnt) {
+      lo = t * (bucket_cap / T);
+      nk = tcnt[t];
+    } else {
+      lo = tile_start[t];
+      nk = tile_start[t + 1] - lo;
+    }
+    const Rec* rb = bucket + lo;
+    const uint64_t tbase = t << tb;
+    const bool fits = nk <= (uint64_t)kRegR * NT;
+    uint64_t k[kRegR], f[kRegR], p[kRegR];
+    unsigned loc2[(kRegR + 1) / 2];  // in-tile positions (< 2^14), two per register
+#define LOC(r) ((loc2[(r) >> 1] >> (((r) & 1) * 16)) & 0xffffu)
+    // ---- load + mark
+    if (fits) {
+#pragma unroll
+      for (int r = 0; r < kRegR; ++r) {
+        const unsigned j = r * NT + tid;
+        k[r] = f[r] = p[r] = 0;
+        if (j < nk) {
+          const Rec* q = rb + j;
+          k[r] = q->k;
+          f[r] = q->f;
+          p[r] = q->p;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < (kRegR + 1) / 2; ++r) loc2[r] = 0;
+#pragma unroll
+      for (int r = 0; r < kRegR; ++r) {
+        const unsigned j = r * NT + tid;
+        if (j < nk) {
+          const unsigned x = (unsigned)(bb_index(seed, k[r], words, magic) - tbase);
+          loc2[r >> 1] |= x << ((r & 1) * 16);
+          const uint32_t bit = 1u << (x & 31);
+          const uint32_t old = atomicOr(&sA[x >> 5], bit);
+          if (old & bit) atomicOr(&sC[x >> 5], bit);
+        }
+      }
+    } else {
+      for (uint64_t j = tid; j < nk; j += NT) {
+        const unsigned x = (unsigned)(bb_index(seed, rb[j].k, words, magic) - tbase);
+        const uint32_t bit = 1u << (x & 31);
+        const uint32_t old = atomicOr(&sA[x >> 5], bit);
+        if (old & bit) atomicOr(&sC[x >> 5], bit);
+      }
+    }
+    __syncthreads();
+    TPROF(1);
+    // ---- finalize: A & ~C -> LDS + global bits; per-word rank prefix into C
+    const unsigned w0 = tid * per;
+    uint64_t cntw = 0;
+    for (unsigned q = 0; q < per; ++q) {
+      const unsigned w = w0 + q;
+      if (w < tpw) {
+        const uint32_t v = sA[w] & ~sC[w];
+        sA[w] = v;
+        const uint64_t gw = (uint64_t)t * tpw + w;
+        if (gw < w32_level) g32[gw] = v;
+        cntw += __popc(v);
+      }
+    }
+    uint64_t pop;
+    uint64_t run = block_exscan<NT>(cntw, &pop);
+    for (unsigned q = 0; q < per; ++q) {
+      const unsigned w = w0 + q;
+      if (w < tpw) {
+        sC[w] = (uint32_t)run;
+        run += __popc(sA[w]);
+      }
+    }
+    TPROF(2);
+    if (wave == 0) {
+      const uint64_t excl = look_back_wave(flags, t, pop, st);
+      if (lane == 0) {
+        if (t == T - 1) st->lvl_base[level + 1] = lvl_base + excl + pop;
+        s_prefix = excl;
+      }
+    }
+    __syncthreads();
+    TPROF(3);
+    const uint64_t base = lvl_base + s_prefix;
+    const bool ok = base + pop <= N;
+    if (!ok) bad = true;
+    // ---- classify: settled -> stage[rank] (or direct past the stage); collided -> count
+    unsigned wc = 0;
+    if (fits) {
+#pragma unroll
+      for (int r = 0; r < kRegR; ++r) {
+        const unsigned j = r * NT + tid;
+        bool redo = false;
+        if (j < nk) {
+          const unsigned x = LOC(r);
+          const uint32_t wv = sA[x >> 5];
+          const uint32_t bit = 1u << (x & 31);
+          if (wv & bit) {
+            const unsigned rank = sC[x >> 5] + __popc(wv & (bit - 1));
+            if (rank < scap) {
+              sf[rank] = f[r];
+              sp[rank] = p[r];
+            } else if (ok) {
+              fp_out[base + rank] = f[r];
+              pos_out[base + rank] = p[r];
+            }
+          } else {
+            redo = true;
+          }
+        }
+        wc += __popcll(__ballot(redo));
+      }
+    } else {
+      for (uint64_t jb = wave * 64; jb < nk; jb += NT) {
+        const uint64_t j = jb + lane;
+        bool redo = false;
+        if (j < nk) {
+          const unsigned x = (unsigned)(bb_index(seed, rb[j].k, words, magic) - tbase);
+          const uint32_t wv = sA[x >> 5];
+          const uint32_t bit = 1u << (x & 31);
+          if (wv & bit) {
+            const unsigned rank = sC[x >> 5] + __popc(wv & (bit - 1));
+            if (ok) {
+              fp_out[base + rank] = rb[j].f;
+              pos_out[base + rank] = rb[j].p;
+            }
+          } else {
+            redo = true;
+          }
+        }
+        wc += __popcll(__ballot(redo));
+      }
+    }
+    TPROF(4);
+    if (lane == 0) s_wc[wave] = wc;
+    __syncthreads();
+    TPROF(5);
+    if (tid == 0) {
+      unsigned tot = 0;
+      for (int w = 0; w < NT / 64; ++w) tot += s_wc[w];
+      unsigned long long b0 = tot ? atomicAdd(&st->n[level + 1], (unsigned long long)tot) : 0;
+      for (int w = 0; w < NT / 64; ++w) {
+        s_wbase[w] = b0;
+        b0 += s_wc[w];
+      }
+    }
+    __syncthreads();
+    TPROF(6);
+    // ---- collided records -> next level; staged settled records -> outputs
+    if (wc) {
+      uint64_t o = s_wbase[wave];
+      if (fits) {
+#pragma unroll
+        for (int r = 0; r < kRegR; ++r) {
+          const unsigned j = r * NT + tid;
+          const unsigned x = LOC(r);
+          const bool redo = j < nk && !((sA[x >> 5] >> (x & 31)) & 1u);
+          const uint64_t m = __ballot(redo);
+          if (redo) next[o + __popcll(m & lt)] = Rec{k[r], f[r], p[r]};
+          o += __popcll(m);
+        }
+      } else {
+        for (uint64_t jb = wave * 64; jb < nk; jb += NT) {
+          const uint64_t j = jb + lane;
+          bool redo = false;
+          uint64_t ck = 0;
+          if (j < nk) {
+            ck = rb[j].k;
+            const unsigned x = (unsigned)(bb_index(seed, ck, words, magic) - tbase);
+            redo = !((sA[x >> 5] >> (x & 31)) & 1u);
+          }
+          const uint64_t m = __ballot(redo);
+          if (redo) next[o + __popcll(m & lt)] = Rec{ck, rb[j].f, rb[j].p};
+          o += __popcll(m);
+        }
+      }
+    }
+    if (ok && fits) {
+      const uint64_t ns = min<uint64_t>(pop, scap);
+      for (uint64_t i = tid; i < ns; i += NT) {
+        fp_out[base + i] = sf[i];
+        pos_out[base + i] = sp[i];
+      }
+    }
+    __syncthreads();
+    TPROF(7);
+#undef TPROF
+#undef LOC
+  }
+  if (bad) atomicOr(&st->status, kStRank);
+}
+
 // --------------------------------------------------------------------- tail --------
 // Every remaining level in one workgroup: A/C and the rank prefix in LDS, outputs
 // written directly, collided records compacted into the other list.
@@ -1104,6 +1358,8 @@ void binned_set_lds_limits() {
                             (int)tile_lds_bytes(kTileMaxBits));
   (void)hipFuncSetAttribute((const void*)k_tile<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)tile_lds_bytes(kTileMaxBits));
+  (void)hipFuncSetAttribute((const void*)k_tile_reg, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)tile_reg_lds_bytes(kRegMaxBits));
 }
 
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
@@ -1144,6 +1400,12 @@ void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStrea
 }
 
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s, bool reserved) {
+  if (b.tile_mode == 0 && g.tb <= kRegMaxBits) {
+    k_tile_reg<<<grid_tiles, kRT, tile_reg_lds_bytes(g.tb), s>>>(
+        level, b.bucket, b.tile_start, reserved ? b.tcnt + (uint64_t)level * kMaxTiles : nullptr, b.bucket_cap,
+        b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.tile_prof);
+    return;
+  }
   const size_t lds = b.tile_mode == 0 ? tile_lds_bytes(g.tb) : 2ull * (1ull << (g.tb - 5)) * sizeof(uint32_t);
   auto kern = b.tile_block == 512 ? k_tile<512> : k_tile<1024>;
   kern<<<grid_tiles, b.tile_block == 512 ? 512 : 1024, lds, s>>>(

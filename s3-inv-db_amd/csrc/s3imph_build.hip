@@ -79,7 +79,7 @@ struct s3imph_ctx {
   unsigned* tcnt = nullptr;  // reservation-path tile counters, kMaxLevels x kMaxTiles
   int tile_mode = 0;
   int tile_block = 1024;
-  uint64_t target_tiles = kTargetTiles, target_tiles0 = kTargetTiles, target_chunks = kTargetChunks;
+  uint64_t target_tiles = kTargetTiles, target_tiles0 = kTargetTiles0, target_chunks = kTargetChunks;
   uint64_t res_max_keys = kResMaxKeys;
   bool debug = false;
   unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps

@@ -38,6 +38,7 @@ struct LevelState {
 constexpr unsigned kTileMaxBits = 19;                 // 2 x 64 KiB LDS bit vectors
 constexpr unsigned kTileMinBits = 10;
 constexpr uint64_t kMaxTiles = 4096;                  // LDS histogram bound (16 KiB)
+constexpr uint64_t kTargetTiles0 = 2048;              // level 0: 2^14-position tiles at 10M keys
 constexpr uint64_t kTargetTiles = 1024;               // aim for (512, 1024] tiles per level
 constexpr uint64_t kHistCap = 8ull << 20;             // tiles x chunks entries
 constexpr unsigned kStTailOverflow = 16u;             // tail reached with a level too big for LDS
