@@ -35,7 +35,7 @@ constexpr int kCB = 1024;             // count block
 constexpr int kSB = 1024;             // scatter block
 constexpr int kTailT = 1024;          // tail block
 constexpr unsigned kLenBuckets = 256;  // key-length classes of the level-0 hash sort
-constexpr uint64_t kTcntWords = (uint64_t)kMaxLevels * kMaxTiles;
+constexpr uint64_t kTcntWords = (uint64_t)kResLevels * kMaxTiles * kResShards;
 constexpr uint64_t kLdsTiles = kMaxTiles;  // histogram / cursor entries in LDS
 constexpr unsigned long long kGate = kTailKeys;
 constexpr int kTailW32 = (int)(2 * ((kGammaNum * kTailKeys + 63) / 64));  // A/C words of the largest tail level
@@ -183,6 +183,88 @@ __global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__
         fp[i] = sh2[tid];
       }
     }
+    }
+    __syncthreads();
+    for (uint64_t t = tid; t < T; t += kCB) hist[t * B + b] = sh[t];
+    __syncthreads();
+  }
+  if (zero) atomicOr(&st->status, kStKeyZero);
+}
+
+// Level-0 hash + count, length-classed: FNV costs one dependent multiply chain per
+// byte and a wave runs as long as its longest lane, so each 1024-key group is ranked
+// into 16 classes by whole 8-byte words (wave ballots + a 256-entry scan, no LDS
+// atomics) and every wave hashes keys of one class.  Results return to key order
+// through LDS so the kh/fp stores stay coalesced.
+constexpr int kClasses = 16;
+__global__ __launch_bounds__(kCB) void k_hash_count0_cls(const uint8_t* __restrict__ blob,
+                                                         const uint64_t* __restrict__ offsets, uint64_t n,
+                                                         uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
+                                                         unsigned* __restrict__ hist,
+                                                         unsigned long long* __restrict__ flags,
+                                                         unsigned long long* __restrict__ sflags, LevelState* st,
+                                                         unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
+  __shared__ unsigned sh[kLdsTiles];
+  __shared__ unsigned scls[kClasses * (kCB / 64)];  // class-major (class, wave) counts -> bases
+  __shared__ unsigned short sidx[kCB];
+  __shared__ uint64_t sb0[kCB], sb1[kCB], sh1[kCB], sh2[kCB];
+  const uint64_t words = st->words[0], magic = st->magic[0];
+  const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
+  if (!geom_ok(st, T, B)) return;
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint64_t lt = lanemask_lt();
+  if (blockIdx.x == 0 && tid == 0) {
+    st->ntiles[0] = T;
+    st->nchunks[0] = B;
+  }
+  for (uint64_t t = (uint64_t)blockIdx.x * kCB + tid; t < T; t += (uint64_t)gridDim.x * kCB) flags[t] = 0;
+  const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
+  for (uint64_t q = (uint64_t)blockIdx.x * kCB + tid; q < nseg; q += (uint64_t)gridDim.x * kCB) sflags[q] = 0;
+  for (uint64_t q = (uint64_t)blockIdx.x * kCB + tid; q < kTcntWords; q += (uint64_t)gridDim.x * kCB) tcnt[q] = 0;
+  const uint64_t seed = level_seed(0);
+  bool zero = false;
+  for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    for (uint64_t t = tid; t < T; t += kCB) sh[t] = 0;
+    const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
+    for (uint64_t g = lo; g < hi; g += kCB) {
+      const uint64_t i = g + tid;
+      uint64_t b0 = 0, b1 = 0;
+      if (i < hi) {
+        b0 = offsets[i];
+        b1 = offsets[i + 1];
+      }
+      const unsigned cls = i < hi ? (unsigned)min<uint64_t>((b1 - b0) >> 3, kClasses - 1) : kClasses - 1;
+      unsigned myrank = 0;
+#pragma unroll
+      for (int c = 0; c < kClasses; ++c) {
+        const uint64_t m = __ballot(cls == (unsigned)c);
+        if (lane == 0) scls[c * (kCB / 64) + wave] = (unsigned)__popcll(m);
+        if (cls == (unsigned)c) myrank = (unsigned)__popcll(m & lt);
+      }
+      __syncthreads();
+      uint64_t tot;
+      const uint64_t ex = block_exscan<kCB>(tid < kClasses * (kCB / 64) ? scls[tid] : 0u, &tot);
+      if (tid < kClasses * (kCB / 64)) scls[tid] = (unsigned)ex;
+      __syncthreads();
+      const unsigned slot = scls[cls * (kCB / 64) + wave] + myrank;
+      sidx[slot] = (unsigned short)tid;
+      sb0[slot] = b0;
+      sb1[slot] = b1;
+      __syncthreads();
+      const unsigned j = sidx[tid];
+      if (g + j < hi) {
+        uint64_t h1, h2;
+        fnv_both_loop(blob, sb0[tid], sb1[tid], h1, h2);
+        sh1[j] = h1;
+        sh2[j] = h2;
+        zero |= (h1 == 0);
+        atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
+      }
+      __syncthreads();
+      if (i < hi) {
+        kh[i] = sh1[tid];
+        fp[i] = sh2[tid];
+      }
     }
     __syncthreads();
     for (uint64_t t = tid; t < T; t += kCB) hist[t * B + b] = sh[t];
@@ -453,14 +535,15 @@ __global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __re
 // ---------------------------------------------------------- reservation scatter ------
 // Small levels (a few 10^5 .. 10^6 keys) skip the count and histogram-scan kernels:
 // tile t owns the fixed bucket slot [t * cap, (t + 1) * cap), cap = bucket_cap / T
-// (several times the ~n/T keys a tile receives), and each block reserves its run in a
-// tile with one atomic per (round, tile).  Record order inside a tile is then
+// (several times the ~n/T keys a tile receives), cut into kResShards shards, and each
+// block reserves its run in its shard of a tile with one atomic per (round, tile).  Record order inside a tile is then
 // arbitrary, which nothing downstream depends on (ranks come from positions).  A slot
 // overflow sets kStOverflow and the build reruns on the counted path.
 __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __restrict__ ilist,
                                                      unsigned* __restrict__ tcnt, Rec* __restrict__ bucket,
                                                      uint64_t bucket_cap, unsigned long long* __restrict__ flags,
-                                                     LevelState* st, unsigned tb, uint64_t cap_words) {
+                                                     LevelState* st, unsigned tb, uint64_t cap_words,
+                                                     unsigned long long* __restrict__ prof) {
   __shared__ Rec stage[kSubRound];
   __shared__ unsigned short stile[kSubRound];
   __shared__ unsigned cnt[kLdsTiles];
@@ -494,11 +577,23 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     if (woff + words > cap_words) atomicOr(&st->status, kStOverflow);
   }
   for (uint64_t t = (uint64_t)blockIdx.x * kSB + tid; t < T; t += (uint64_t)gridDim.x * kSB) flags[t] = 0;
-  const uint64_t cap = bucket_cap / T;
+  // tile t's slot is cut into kResShards shards, one per XCD under round-robin dispatch,
+  // so a counter sees ~1/8 of the blocks: returning atomics on one address serialize
+  const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
+  const unsigned shard = blockIdx.x % kResShards;
   const uint64_t seed = level_seed(level);
   const uint64_t stride = (uint64_t)gridDim.x * kSubRound;
   uint64_t r0 = (uint64_t)blockIdx.x * kSubRound;
   if (r0 >= n) return;
+  // debug: round-0 phase timestamps of this block in prof row 32 + level
+  unsigned long long* tp =
+      prof && blockIdx.x < kMaxTiles ? prof + ((uint64_t)(32 + level) * kMaxTiles + blockIdx.x) * 8 : nullptr;
+  int round = 0;
+#define SPROF(i)                                                \
+  do {                                                          \
+    if (tp && tid == 0 && round == 0) tp[i] = wall_clock64(); \
+  } while (0)
+  SPROF(0);
   // records as three scalar arrays: a conditionally loaded Rec[] would live in scratch
   uint64_t rk_[kScatterKPT], rf_[kScatterKPT], rp_[kScatterKPT];
 #pragma unroll
@@ -525,6 +620,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
       }
     }
     __syncthreads();
+    SPROF(1);
     constexpr int kTPT = (int)(kLdsTiles / kSB);
     const uint64_t t0 = (uint64_t)kTPT * tid;
     unsigned a[kTPT];
@@ -538,18 +634,20 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     uint64_t ex = block_exscan<kSB>(sum, &tot);
 #pragma unroll
     for (int q = 0; q < kTPT; ++q) {
-      const uint64_t t = t0 + q;
-      if (t < T) {
-        start[t] = (unsigned)ex;
-        if (a[q]) {
-          const uint64_t at = atomicAdd(&tcnt[t], a[q]);
-          if (at + a[q] > cap) s_over = 1;
-          cur[t] = (unsigned)(t * cap + at);
-        }
-      }
+      if (t0 + q < T) start[t0 + q] = (unsigned)ex;
       ex += a[q];
     }
+    // one tile per thread, so the returning atomics of a round are all in flight at once
+    for (uint64_t t = tid; t < T; t += kSB) {
+      const unsigned c = cnt[t];
+      if (c) {
+        const uint64_t at = atomicAdd(&tcnt[t * kResShards + shard], c);
+        if (at + c > scap) s_over = 1;
+        cur[t] = (unsigned)(t * cap + shard * scap + at);
+      }
+    }
     __syncthreads();
+    SPROF(2);
 #pragma unroll
     for (int q = 0; q < kScatterKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
@@ -572,17 +670,22 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
       }
     }
     __syncthreads();
+    SPROF(3);
     if (s_over) break;
     for (unsigned j = tid; j < m; j += kSB) {
       const unsigned t = stile[j];
       bucket[cur[t] + (j - start[t])] = stage[j];
     }
     __syncthreads();
+    SPROF(4);
+    SPROF(7);
+    ++round;
     if (!more) break;
     for (uint64_t t = tid; t < T; t += kSB) cnt[t] = 0;
     __syncthreads();
   }
   if (s_over && tid == 0) atomicOr(&st->status, kStOverflow | kStResOverflow);
+#undef SPROF
 }
 
 // --------------------------------------------------------------------- tile --------
@@ -941,9 +1044,7 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
 // Settled records go to an LDS stage indexed by rank (copied out coalesced), collided
 // ones straight from registers to the next list: the bucket is read exactly once.
 // A tile with more records than fit takes a streaming fallback (never at load 1/2).
-constexpr int kRegR = 20;
 constexpr unsigned kRegMaxBits = 14;
-constexpr int kRT = 512;
 // Settled-record stage: a tile settles ~0.30 x 2^tb keys (gamma 2); 3/8 x 2^tb covers
 // it with a wide margin, ranks past it are written directly.
 __host__ __device__ constexpr unsigned reg_stage(unsigned tb) { return (3u << tb) / 8; }
@@ -951,14 +1052,14 @@ size_t tile_reg_lds_bytes(unsigned tb) {
   return (size_t)reg_stage(tb) * 16 + 2ull * (1ull << (tb - 5)) * sizeof(uint32_t);
 }
 
-__global__ __launch_bounds__(kRT) void k_tile_reg(int level, const Rec* __restrict__ bucket,
+template <int NT, int kRegR, int kWaves, bool kShard>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) void k_tile_reg(int level, const Rec* __restrict__ bucket,
                                                   const unsigned* __restrict__ tile_start,
                                                   const unsigned* __restrict__ tcnt, uint64_t bucket_cap,
                                                   unsigned long long* flags, uint64_t* __restrict__ bits,
                                                   Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
                                                   uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
                                                   unsigned long long* __restrict__ prof) {
-  constexpr int NT = kRT;
   extern __shared__ uint64_t dyn64[];
   __shared__ unsigned long long s_t, s_prefix;
   __shared__ unsigned s_wc[NT / 64];
@@ -996,15 +1097,37 @@ __global__ __launch_bounds__(kRT) void k_tile_reg(int level, const Rec* __restri
     if (tp && tid == 0) tp[i] = wall_clock64(); \
   } while (0)
     TPROF(0);
-    uint64_t lo, nk;
-    if (tcnt) {
-      lo = t * (bucket_cap / T);
-      nk = tcnt[t];
+    // bucket range: contiguous from the histogram scan, or kResShards shard ranges
+    // (reservation path); record j lives at rb[shard_off(j)]
+    uint64_t lo, nk, shcap = 0;  // shcap: records per reservation shard
+    unsigned pre[kResShards];  // exclusive prefix of the shard fills (uniform)
+    if (kShard) {
+      const uint64_t cap = bucket_cap / T;
+      shcap = cap / kResShards;
+      lo = t * cap;
+      unsigned acc = 0;
+#pragma unroll
+      for (int x = 0; x < kResShards; ++x) {
+        pre[x] = acc;
+        acc += tcnt[t * kResShards + x];
+      }
+      nk = acc;
     } else {
       lo = tile_start[t];
       nk = tile_start[t + 1] - lo;
+#pragma unroll
+      for (int x = 0; x < kResShards; ++x) pre[x] = x ? 0xffffffffu : 0u;
     }
     const Rec* rb = bucket + lo;
+    auto shard_off = [&](unsigned j) -> uint64_t {
+      uint64_t o = j;
+      if (kShard) {
+#pragma unroll
+        for (int x = 1; x < kResShards; ++x)
+          if (j >= pre[x]) o = (uint64_t)x * shcap + (j - pre[x]);
+      }
+      return o;
+    };
     const uint64_t tbase = t << tb;
     const bool fits = nk <= (uint64_t)kRegR * NT;
     uint64_t k[kRegR], f[kRegR], p[kRegR];
@@ -1017,12 +1140,13 @@ __global__ __launch_bounds__(kRT) void k_tile_reg(int level, const Rec* __restri
         const unsigned j = r * NT + tid;
         k[r] = f[r] = p[r] = 0;
         if (j < nk) {
-          const Rec* q = rb + j;
+          const Rec* q = rb + shard_off(j);
           k[r] = q->k;
           f[r] = q->f;
           p[r] = q->p;
         }
       }
+
 #pragma unroll
       for (int r = 0; r < (kRegR + 1) / 2; ++r) loc2[r] = 0;
 #pragma unroll
@@ -1038,7 +1162,7 @@ __global__ __launch_bounds__(kRT) void k_tile_reg(int level, const Rec* __restri
       }
     } else {
       for (uint64_t j = tid; j < nk; j += NT) {
-        const unsigned x = (unsigned)(bb_index(seed, rb[j].k, words, magic) - tbase);
+        const unsigned x = (unsigned)(bb_index(seed, rb[shard_off((unsigned)j)].k, words, magic) - tbase);
         const uint32_t bit = 1u << (x & 31);
         const uint32_t old = atomicOr(&sA[x >> 5], bit);
         if (old & bit) atomicOr(&sC[x >> 5], bit);
@@ -1112,14 +1236,15 @@ __global__ __launch_bounds__(kRT) void k_tile_reg(int level, const Rec* __restri
         const uint64_t j = jb + lane;
         bool redo = false;
         if (j < nk) {
-          const unsigned x = (unsigned)(bb_index(seed, rb[j].k, words, magic) - tbase);
+          const Rec* q = rb + shard_off((unsigned)j);
+          const unsigned x = (unsigned)(bb_index(seed, q->k, words, magic) - tbase);
           const uint32_t wv = sA[x >> 5];
           const uint32_t bit = 1u << (x & 31);
           if (wv & bit) {
             const unsigned rank = sC[x >> 5] + __popc(wv & (bit - 1));
             if (ok) {
-              fp_out[base + rank] = rb[j].f;
-              pos_out[base + rank] = rb[j].p;
+              fp_out[base + rank] = q->f;
+              pos_out[base + rank] = q->p;
             }
           } else {
             redo = true;
@@ -1161,13 +1286,14 @@ __global__ __launch_bounds__(kRT) void k_tile_reg(int level, const Rec* __restri
           const uint64_t j = jb + lane;
           bool redo = false;
           uint64_t ck = 0;
+          const Rec* q = rb + shard_off((unsigned)j);
           if (j < nk) {
-            ck = rb[j].k;
+            ck = q->k;
             const unsigned x = (unsigned)(bb_index(seed, ck, words, magic) - tbase);
             redo = !((sA[x >> 5] >> (x & 31)) & 1u);
           }
           const uint64_t m = __ballot(redo);
-          if (redo) next[o + __popcll(m & lt)] = Rec{ck, rb[j].f, rb[j].p};
+          if (redo) next[o + __popcll(m & lt)] = Rec{ck, q->f, q->p};
           o += __popcll(m);
         }
       }
@@ -1358,7 +1484,9 @@ void binned_set_lds_limits() {
                             (int)tile_lds_bytes(kTileMaxBits));
   (void)hipFuncSetAttribute((const void*)k_tile<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)tile_lds_bytes(kTileMaxBits));
-  (void)hipFuncSetAttribute((const void*)k_tile_reg, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_tile_reg<512, 20, 2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)tile_reg_lds_bytes(kRegMaxBits));
+  (void)hipFuncSetAttribute((const void*)k_tile_reg<512, 20, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)tile_reg_lds_bytes(kRegMaxBits));
 }
 
@@ -1367,10 +1495,15 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
   if (level == 0) {
     static const int mode = [] {
       // A/B knob: 3 direct, loop (default); 0 LDS-staged; 1 direct, batched loads;
-      // 2 length-sorted, loop; 4 length-sorted, batched
+      // 2 length-sorted, loop; 4 length-sorted, batched; 5 word-count classes
       const char* e = std::getenv("S3IMPH_HASH_MODE");
       return e ? std::atoi(e) : 3;
     }();
+    if (mode == 5) {
+      k_hash_count0_cls<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st,
+                                                     g.tb, g.chunk, b.tcnt);
+      return;
+    }
     if (mode == 0) {
       const uint64_t T = ntiles_of(level_words(n ? n : 1), g.tb);
       const size_t lds = ((T + 1) / 2 + kHashWinWords) * sizeof(uint64_t);
@@ -1401,21 +1534,31 @@ void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStrea
 
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s, bool reserved) {
   if (b.tile_mode == 0 && g.tb <= kRegMaxBits) {
-    k_tile_reg<<<grid_tiles, kRT, tile_reg_lds_bytes(g.tb), s>>>(
-        level, b.bucket, b.tile_start, reserved ? b.tcnt + (uint64_t)level * kMaxTiles : nullptr, b.bucket_cap,
-        b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.tile_prof);
+    // records per tile ~2^(tb-1): pick the variant whose NT x R covers it with margin
+    // (lighter variants keep several tiles resident per CU)
+    const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kMaxTiles * kResShards : nullptr;
+    const size_t lds = tile_reg_lds_bytes(g.tb);
+#define S3_TILE_REG(NT_, R_, W_)                                                                             \
+  (tc ? k_tile_reg<NT_, R_, W_, true> : k_tile_reg<NT_, R_, W_, false>)<<<grid_tiles, NT_, lds, s>>>(level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags, \
+                                                   b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb,  \
+                                                   b.tile_prof)
+    if (g.tb == 14) S3_TILE_REG(512, 20, 2);       // 1 tile per CU
+    else if (g.tb == 13) S3_TILE_REG(256, 20, 2);  // 2 tiles per CU
+    else if (g.tb == 12) S3_TILE_REG(256, 10, 3);  // 3 tiles per CU
+    else S3_TILE_REG(256, 5, 5);                   // 5 tiles per CU
+#undef S3_TILE_REG
     return;
   }
   const size_t lds = b.tile_mode == 0 ? tile_lds_bytes(g.tb) : 2ull * (1ull << (g.tb - 5)) * sizeof(uint32_t);
   auto kern = b.tile_block == 512 ? k_tile<512> : k_tile<1024>;
   kern<<<grid_tiles, b.tile_block == 512 ? 512 : 1024, lds, s>>>(
-      level, b.bucket, b.tile_start, reserved ? b.tcnt + (uint64_t)level * kMaxTiles : nullptr, b.bucket_cap,
+      level, b.bucket, b.tile_start, nullptr, b.bucket_cap,
       b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.tile_mode, b.tile_prof);
 }
 
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s) {
-  k_scatter_res<<<grid, kSB, 0, s>>>(level, b.list[(level - 1) & 1], b.tcnt + (uint64_t)level * kMaxTiles,
-                                     b.bucket, b.bucket_cap, b.flags, b.st, g.tb, b.cap_words);
+  k_scatter_res<<<grid, kSB, 0, s>>>(level, b.list[(level - 1) & 1], b.tcnt + (uint64_t)level * kMaxTiles * kResShards,
+                                     b.bucket, b.bucket_cap, b.flags, b.st, g.tb, b.cap_words, b.tile_prof);
 }
 
 void launch_binned_tail(int big_launched, const BinBuffers& b, hipStream_t s) {

@@ -76,11 +76,12 @@ struct s3imph_ctx {
   unsigned *hist = nullptr, *hoff = nullptr, *tile_start = nullptr, *scan_sums = nullptr;
   unsigned long long* flags = nullptr;
   unsigned long long* sflags = nullptr;
-  unsigned* tcnt = nullptr;  // reservation-path tile counters, kMaxLevels x kMaxTiles
+  unsigned* tcnt = nullptr;  // reservation-path shard fills, kResLevels x kMaxTiles x kResShards
   int tile_mode = 0;
   int tile_block = 1024;
   uint64_t target_tiles = kTargetTiles, target_tiles0 = kTargetTiles0, target_chunks = kTargetChunks;
   uint64_t res_max_keys = kResMaxKeys;
+  uint64_t target_tiles_res = kTargetTilesRes;
   bool debug = false;
   unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps
   bool lds_attr_set = false;
@@ -192,7 +193,7 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   dalloc(c->scan_sums, kHistCap / 2048 + 2);
   dalloc(c->flags, kMaxTiles + 2);
   dalloc(c->sflags, kHistCap / kScanSeg + 2);
-  dalloc(c->tcnt, (uint64_t)kMaxLevels * kMaxTiles);
+  dalloc(c->tcnt, (uint64_t)kResLevels * kMaxTiles * kResShards);
   alloc_common(c, cap);
   dalloc(c->bits, c->cap_words);
   dalloc(c->rank_base, c->cap_words);
@@ -328,7 +329,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   b.st = c->d_st;
 
   const double q = 1.0 - std::exp(-0.5);  // fraction of keys that collide at load 1/2
-  const LevelGeom g0 = choose_geom(n, c->target_tiles0, c->target_chunks);
+  const LevelGeom g0 = choose_geom(n, c->target_tiles0, c->target_chunks, kRegTileMaxBits);
   int gc, gt, gs;
   // Grids from a (predicted) key count; kernels loop over whatever the device finds.
   auto grids = [&](uint64_t nk, LevelGeom g) {
@@ -359,9 +360,12 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
     if (!conservative && pred * kTailMargin < (double)kTailKeys) break;
     launched = L;
     const uint64_t nb = conservative ? n : (uint64_t)(pred * 1.1) + 4096;
-    const LevelGeom g = conservative ? g0 : choose_geom(nb, c->target_tiles, c->target_chunks);
+    const bool res = !conservative && nb <= c->res_max_keys && L < kResLevels && c->tile_mode == 0;
+    const LevelGeom g = conservative ? g0
+                        : res        ? choose_geom(nb, c->target_tiles_res, c->target_chunks, kRegTileMaxBits)
+                                     : choose_geom(nb, c->target_tiles, c->target_chunks, kRegTileMaxBits);
     grids(nb, g);
-    if (!conservative && nb <= c->res_max_keys) {
+    if (res && g.tb <= kRegTileMaxBits) {
       const int gr = (int)std::min<uint64_t>((nb + kSubRound - 1) / kSubRound, 256);
       launch_binned_scatter_res(L, b, g, gr, s);
       launch_binned_tile(L, b, g, gt, s, true);
@@ -419,8 +423,11 @@ void print_tile_profile(s3imph_ctx* c) {
       }
     }
     if (!cnt) continue;
-    std::fprintf(stderr, "  tile L%d: %d tiles, span %.1f us, avg us:", L, cnt, (hi - lo) / 100.0);
-    for (int i = 0; i < 7; ++i) std::fprintf(stderr, " %s %.2f", names[i], sum[i] / cnt / 100.0);
+    static const char* snames[7] = {"count", "resv", "stage", "write", "-", "-", "-"};
+    const bool sc = L >= 32;
+    std::fprintf(stderr, "  %s L%d: %d %s, span %.1f us, avg us:", sc ? "scatter_res" : "tile", sc ? L - 32 : L, cnt,
+                 sc ? "blocks (round 0)" : "tiles", (hi - lo) / 100.0);
+    for (int i = 0; i < (sc ? 4 : 7); ++i) std::fprintf(stderr, " %s %.2f", (sc ? snames : names)[i], sum[i] / cnt / 100.0);
     std::fprintf(stderr, "\n");
   }
 }
@@ -861,6 +868,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     if (const char* m = std::getenv("S3IMPH_TARGET_TILES0")) c->target_tiles0 = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_CHUNKS")) c->target_chunks = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_RES_MAX")) c->res_max_keys = std::strtoull(m, nullptr, 10);
+    if (const char* m = std::getenv("S3IMPH_TARGET_TILES_RES")) c->target_tiles_res = std::strtoull(m, nullptr, 10);
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     if (const char* m = std::getenv("S3IMPH_TILE_BLOCK")) c->tile_block = std::atoi(m);
     // A blocking stream: implicitly ordered with the legacy NULL stream, so work a

@@ -39,7 +39,9 @@ constexpr unsigned kTileMaxBits = 19;                 // 2 x 64 KiB LDS bit vect
 constexpr unsigned kTileMinBits = 10;
 constexpr uint64_t kMaxTiles = 4096;                  // LDS histogram bound (16 KiB)
 constexpr uint64_t kTargetTiles0 = 2048;              // level 0: 2^14-position tiles at 10M keys
-constexpr uint64_t kTargetTiles = 1024;               // aim for (512, 1024] tiles per level
+constexpr uint64_t kTargetTiles = 1024;               // levels >= 1 on the counted path
+constexpr uint64_t kTargetTilesRes = 256;             // reservation-path levels: ~1 tile per CU
+constexpr unsigned kRegTileMaxBits = 14;              // largest tile of the register-resident kernel
 constexpr uint64_t kHistCap = 8ull << 20;             // tiles x chunks entries
 constexpr unsigned kStTailOverflow = 16u;             // tail reached with a level too big for LDS
 constexpr unsigned kStGeometry = 32u;                 // tiles/chunks outside the workspace
@@ -60,13 +62,16 @@ struct LevelGeom {
 // tiles x chunks stays under kHistCap.
 constexpr uint64_t kChunkGran = 1024;
 constexpr uint64_t kResMaxKeys = 2ull << 20;  // levels up to this size use the reservation scatter
+constexpr int kResShards = 8;                 // per-tile reservation counters (one per XCD)
+constexpr int kResLevels = 32;                // levels that may use the reservation path
 constexpr double kTailMargin = 1.1;
 constexpr uint64_t kTargetChunks = 768;  // 3 resident 1024-thread count blocks x 256 CUs
 inline LevelGeom choose_geom(uint64_t n, uint64_t target_tiles = kTargetTiles,
-                             uint64_t target_chunks = kTargetChunks) {
+                             uint64_t target_chunks = kTargetChunks, unsigned max_tb = kTileMaxBits) {
   const uint64_t size = 64 * level_words(n ? n : 1);
   unsigned tb = kTileMinBits;
-  while (tb < kTileMaxBits && (size >> tb) > target_tiles) ++tb;
+  while (tb < max_tb && (size >> tb) > target_tiles) ++tb;
+  while (tb < kTileMaxBits && ((size + (1ull << tb) - 1) >> tb) > kMaxTiles) ++tb;  // workspace bound
   const uint64_t T = (size + (1ull << tb) - 1) >> tb;
   uint64_t chunk = ((n + target_chunks - 1) / target_chunks + kChunkGran - 1) / kChunkGran * kChunkGran;
   if (chunk < kSubRound) chunk = kSubRound;
@@ -145,7 +150,7 @@ struct BinBuffers {
   unsigned* scan_sums;                  // scan block sums
   unsigned long long* flags;            // decoupled look-back words, one per tile
   unsigned long long* sflags;           // look-back words of the histogram scan
-  unsigned* tcnt;                       // per-level tile fill counters (reservation path), kMaxLevels x kMaxTiles
+  unsigned* tcnt;                       // reservation-path shard fills, kResLevels x kMaxTiles x kResShards
   uint64_t bucket_cap;                  // bucket capacity in records
   int tile_mode;
   int tile_block;                       // tile workgroup size (512 or 1024)
