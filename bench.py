@@ -154,7 +154,7 @@ def main() -> None:
     mph_len = info.get("mph_bin_len", 0)
     b_alg = key_bytes + 8 * (n_global + 1) + 16 * n_global + mph_len
     result = {
-        "metric": "MPHF build keys/s (device-resident)",
+        "metric": "MPHF build keys/s + key-bytes GB/s (device-resident), 1/2/4/8 MI355X",
         "value": n_global / dt,
         "unit": "keys/s",
         "n_gpus": world,

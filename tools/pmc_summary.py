@@ -10,6 +10,13 @@ import json
 import sys
 
 
+def kname(full: str) -> str:
+    """'void ns::(anonymous namespace)::k_tile_reg<512, 20, 2, false>(int, ...)' -> 'k_tile_reg'."""
+    s = full.replace("(anonymous namespace)::", "")
+    s = s.split("(")[0].split("<")[0].split("::")[-1]
+    return s.split(" ")[-1]
+
+
 def load(path, counter):
     rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
@@ -22,7 +29,7 @@ def main():
     write = load(sys.argv[2], "WRITE_SIZE")
     out = []
     for f, w in zip(fetch, write):
-        name = f["Kernel_Name"].split("(")[0].split("::")[-1]
+        name = kname(f["Kernel_Name"])
         dur = (int(f["End_Timestamp"]) - int(f["Start_Timestamp"])) / 1e3
         fk, wk = float(f["Counter_Value"]), float(w["Counter_Value"])
         out.append({"kernel": name, "grid": int(f["Grid_Size"]), "fetch_kib": fk, "write_kib": wk,
@@ -33,6 +40,24 @@ def main():
                   f"write={o['write_bytes']/1e6:8.1f} MB")
     if len(sys.argv) > 3:
         json.dump(out, open(sys.argv[3], "w"), indent=1)
+    if len(sys.argv) > 5:  # merge the level-0 stages into bench.py's traffic file: CONFIG PATH
+        cfg, path = sys.argv[4], sys.argv[5]
+        try:
+            tr = json.load(open(path))
+        except (OSError, ValueError):
+            tr = {}
+        first = {}
+        for o in out:
+            first.setdefault(o["kernel"], o)
+        ent = tr.setdefault(cfg, {})
+        for stage, kern in (("hash_count0", "k_hash_count0"), ("scatter0", "k_scatter"), ("tile0", "k_tile_reg"),
+                            ("hash_scatter0", "k_hash_scatter0")):
+            if kern in first:
+                o = first[kern]
+                ent[stage] = {"kernel": kern, "n_gpus": 1,
+                              "hbm_bytes_per_launch": int(o["read_bytes_corrected"] + o["write_bytes"]),
+                              "read_bytes": int(o["read_bytes_corrected"]), "write_bytes": int(o["write_bytes"])}
+        json.dump(tr, open(path, "w"), indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
