@@ -91,23 +91,24 @@ def main() -> None:
     dev = f"cuda:{local_rank}"
     d_blob = torch.from_numpy(blob).to(dev)
     d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
-    out_cap = plan.out_per_rank if world > 1 else n
-    d_fp = torch.empty(max(out_cap, 1), dtype=torch.int64, device=dev)
-    d_po = torch.empty(max(out_cap, 1), dtype=torch.int64, device=dev)
-    torch.cuda.synchronize()
-
     if world == 1:
         ctx = s3imph.DeviceBuilder(local_rank)
         ctx.reserve(n)
-
-        def step():
-            return ctx.build(d_blob, d_offs, n, d_fp, d_po)
+        out_cap = n
     else:
         uid = [s3imph.dist_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx = s3imph.DistBuilder(local_rank, uid[0], rank, world)
         ctx.reserve(n, plan.n_global)
+        out_cap = ctx.out_cap(plan.n_global)
+    d_fp = torch.empty(max(out_cap, 1), dtype=torch.int64, device=dev)
+    d_po = torch.empty(max(out_cap, 1), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
 
+    if world == 1:
+        def step():
+            return ctx.build(d_blob, d_offs, n, d_fp, d_po)
+    else:
         def step():
             return ctx.build_shard(d_blob, d_offs, n, plan.lo, d_fp, d_po, out_cap)[2]
 

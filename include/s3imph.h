@@ -143,10 +143,18 @@ int s3imph_ctx_set_profiling(s3imph_ctx *ctx, int on);
 int s3imph_ctx_stage_times(s3imph_ctx *ctx, float *ms, int cap, int *count, char *names, size_t names_len);
 
 /* ------------------------------------------------------------------------
- * 4. Multi-GPU build: one process per GPU, RCCL over xGMI.
- *    Keys are sharded in contiguous index ranges; each BBHash level's collision
- *    counts are summed across ranks (RCCL reduce-scatter + all-gather); the
- *    output (p, fp, pos) triples are exchanged to the rank owning p's range.
+ * 4. Multi-GPU build: one process per GPU, RCCL over xGMI.  No reference
+ *    counterpart (the reference builds in one process, mphf_streaming.go:141);
+ *    the outputs are byte-identical to the single-GPU build.
+ *
+ *    Keys are sharded in contiguous index ranges.  At each large BBHash level
+ *    rank r owns a contiguous range of the level's bit positions: every rank
+ *    routes its active records to the owners (one all-to-all), each owner
+ *    resolves collisions and ranks for its range, and its settled keys fill
+ *    consecutive local output slots.  Small levels run replicated on every rank
+ *    (outputs written by rank 0).  A rank's outputs are therefore a few
+ *    contiguous segments of mph_fp / mph_pos (s3imph_dist_segments), which the
+ *    caller writes at their global offsets (e.g. pwrite into the column files).
  * ------------------------------------------------------------------------ */
 
 /* Rank 0 creates the 128-byte RCCL unique id; the host broadcasts it. */
@@ -155,15 +163,40 @@ int s3imph_dist_unique_id(uint8_t id_out[128]);
 int s3imph_ctx_create_dist(int device, const uint8_t id[128], int rank, int nranks,
                            s3imph_ctx **out, char *err, size_t errlen);
 
+/* Host-callback collectives (test transport: several ranks may share one GPU).
+ * allgather: recv (nranks * bytes) = every rank's send, in rank order.
+ * alltoallv: send_bytes[q] bytes at send + send_off[q] go to rank q; the bytes from
+ *            rank q land at recv + recv_off[q] (recv_bytes[q]).  Host pointers.
+ * Each returns 0 on success. */
+typedef struct s3imph_host_comm {
+    void *user;
+    int (*allgather)(void *user, const void *send, void *recv, uint64_t bytes);
+    int (*alltoallv)(void *user, const void *send, const uint64_t *send_off, const uint64_t *send_bytes,
+                     void *recv, const uint64_t *recv_off, const uint64_t *recv_bytes);
+} s3imph_host_comm;
+
+int s3imph_ctx_create_dist_host(int device, const s3imph_host_comm *comm, int rank, int nranks,
+                                s3imph_ctx **out, char *err, size_t errlen);
+
 /* This rank holds keys [key_base, key_base + n_local) of the global set (the
- * shard's blob/offsets/pos, offsets relative to d_blob).  On return this rank owns
- * output positions [*out_lo, *out_lo + *out_n) of mph_fp / mph_pos, written to
- * d_fp_out / d_pos_out (capacity out_cap entries; ceil(N/nranks) suffices).
- * mph.bin is identical on every rank. */
+ * shard's blob/offsets/pos, offsets relative to d_blob; d_pos NULL => pos_i =
+ * key_base + i).  On return *out_n local outputs are in d_fp_out / d_pos_out
+ * (capacity out_cap entries, at least s3imph_dist_out_cap()).  mph.bin is
+ * identical on every rank. */
 int s3imph_build_device_dist(s3imph_ctx *ctx, const uint8_t *d_blob, const uint64_t *d_offsets,
                              const uint64_t *d_pos, uint64_t n_local, uint64_t key_base,
                              uint64_t *d_fp_out, uint64_t *d_pos_out, uint64_t out_cap,
-                             uint64_t *out_lo, uint64_t *out_n, void *stream, s3imph_build_info *info);
+                             uint64_t *out_n, void *stream, s3imph_build_info *info);
+
+/* The last build's output segments of this rank: seg[3i] = first global position p,
+ * seg[3i+1] = count, seg[3i+2] = offset in d_fp_out / d_pos_out.  *count = segments. */
+int s3imph_dist_segments(s3imph_ctx *ctx, uint64_t *seg, uint64_t cap, uint64_t *count);
+
+/* Output capacity (entries) one rank needs for a build of n_global keys. */
+uint64_t s3imph_dist_out_cap(s3imph_ctx *ctx, uint64_t n_global);
+
+/* Message of the last failed device-resident build on ctx ("" if none). */
+const char *s3imph_ctx_last_error(s3imph_ctx *ctx);
 
 /* ------------------------------------------------------------------------
  * 5. Batched lookup on the device: MPHF.Lookup (pkg/format/mphf.go:275-302)

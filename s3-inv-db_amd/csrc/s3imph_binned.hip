@@ -95,7 +95,7 @@ __device__ __forceinline__ bool geom_ok(LevelState* st, uint64_t T, uint64_t B) 
 }
 
 __device__ __forceinline__ bool level_active(int level, const LevelState* st) {
-  return (level == 0 || st->n[level] > kGate) &&
+  return (st->preset[level] || level == 0 || st->n[level] > kGate) &&
          !(st->status & (kStGeometry | kStOverflow | kStLookback));
 }
 
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(kHB) void k_hash_count0_lds(const uint8_t* __restri
 __global__ void k_level_setup(int level, LevelState* st) {
   const int p = level - 1;
   if (threadIdx.x != 0) return;
-  if (p > 0 && st->n[p] <= kGate) return;
+  if (p > 0 && !st->preset[p] && st->n[p] <= kGate) return;
   if (st->status & (kStGeometry | kStOverflow | kStLookback)) return;
   const uint64_t n = st->n[level];
   const uint64_t w = n ? level_words(n) : 0;
@@ -366,21 +366,30 @@ __global__ __launch_bounds__(kCB) void k_count(int level, const Rec* __restrict_
                                                unsigned tb, uint64_t chunk, uint64_t cap_words) {
   __shared__ unsigned sh[kLdsTiles];
   const int p = level - 1;
-  if (p > 0 && st->n[p] <= kGate) return;  // previous level ran in the tail
+  const bool preset = st->preset[level] != 0;
+  if (!preset && p > 0 && !st->preset[p] && st->n[p] <= kGate) return;  // previous level ran in the tail
   if (st->status & (kStGeometry | kStOverflow | kStLookback)) return;
-  // level setup (every block derives it; block 0 publishes it)
   const uint64_t n = st->n[level];
-  const uint64_t words = n ? level_words(n) : 0, magic = level_magic(words);
-  const uint64_t woff = st->woff[p] + st->words[p];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->words[level] = words;
-    st->magic[level] = magic;
-    st->woff[level] = woff;
-    st->woff[level + 1] = woff + words;
-    st->nlevels = level;
+  uint64_t words, magic, woff;
+  if (preset) {  // sized by the multi-GPU build: global words, this rank's records
+    words = st->words[level];
+    magic = st->magic[level];
+    woff = st->woff[level];
+  } else {  // level setup (every block derives it; block 0 publishes it)
+    words = n ? level_words(n) : 0;
+    magic = level_magic(words);
+    woff = st->woff[p] + st->words[p];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->words[level] = words;
+      st->magic[level] = magic;
+      st->woff[level] = woff;
+      st->woff[level + 1] = woff + words;
+      st->nlevels = level;
+    }
+    if (n <= kGate) return;
   }
-  if (n <= kGate) return;
-  const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
+  const LevelRange rg = level_range(st, level, words);
+  const uint64_t T = ntiles_of(rg.rw, tb), B = (n + chunk - 1) / chunk;
   if (!geom_ok(st, T, B)) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st->ntiles[level] = T;
@@ -396,7 +405,7 @@ __global__ __launch_bounds__(kCB) void k_count(int level, const Rec* __restrict_
     __syncthreads();
     const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
     for (uint64_t i = lo + threadIdx.x; i < hi; i += kCB)
-      atomicAdd(&sh[bb_index(seed, list[i].k, words, magic) >> tb], 1u);
+      atomicAdd(&sh[(bb_index(seed, list[i].k, words, magic) - rg.plo) >> tb], 1u);
     __syncthreads();
     for (uint64_t t = threadIdx.x; t < T; t += kCB) hist[t * B + b] = sh[t];
     __syncthreads();
@@ -422,6 +431,7 @@ __global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __re
   const uint64_t n = st->n[level];
   const uint64_t words = st->words[level], magic = st->magic[level];
   const uint64_t T = st->ntiles[level], B = st->nchunks[level];
+  const uint64_t plo = level_range(st, level, words).plo;
   const uint64_t seed = level_seed(level);
   // Blocks b, b+8, b+16, ... (one XCD under round-robin dispatch) share one contiguous
   // eighth of the chunks and take them interleaved, so at any moment an XCD's blocks
@@ -465,7 +475,7 @@ __global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __re
     for (int q = 0; q < kScatterKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < hi) {
-        tt[q] = (unsigned)(bb_index(seed, rec[q].k, words, magic) >> tb);
+        tt[q] = (unsigned)((bb_index(seed, rec[q].k, words, magic) - plo) >> tb);
         rk[q] = atomicAdd(&cnt[tt[q]], 1u);
       }
     }
@@ -551,22 +561,31 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   __shared__ unsigned cur[kLdsTiles];  // bucket indices fit u32 (n < 2^32 per GPU)
   __shared__ unsigned s_over;
   const int p = level - 1;
-  if (p > 0 && st->n[p] <= kGate) return;  // previous level ran in the tail
+  const bool preset = st->preset[level] != 0;
+  if (!preset && p > 0 && !st->preset[p] && st->n[p] <= kGate) return;  // previous level ran in the tail
   if (st->status & (kStGeometry | kStOverflow | kStLookback)) return;
-  // level setup (every block derives it; block 0 publishes it)
   const uint64_t n = st->n[level];
-  const uint64_t words = n ? level_words(n) : 0, magic = level_magic(words);
-  const uint64_t woff = st->woff[p] + st->words[p];
   const unsigned tid = threadIdx.x;
-  if (blockIdx.x == 0 && tid == 0) {
-    st->words[level] = words;
-    st->magic[level] = magic;
-    st->woff[level] = woff;
-    st->woff[level + 1] = woff + words;
-    st->nlevels = level;
+  uint64_t words, magic, woff;
+  if (preset) {  // sized by the multi-GPU build: global words, this rank's records
+    words = st->words[level];
+    magic = st->magic[level];
+    woff = st->woff[level];
+  } else {  // level setup (every block derives it; block 0 publishes it)
+    words = n ? level_words(n) : 0;
+    magic = level_magic(words);
+    woff = st->woff[p] + st->words[p];
+    if (blockIdx.x == 0 && tid == 0) {
+      st->words[level] = words;
+      st->magic[level] = magic;
+      st->woff[level] = woff;
+      st->woff[level + 1] = woff + words;
+      st->nlevels = level;
+    }
+    if (n <= kGate) return;
   }
-  if (n <= kGate) return;
-  const uint64_t T = ntiles_of(words, tb);
+  const LevelRange rg = level_range(st, level, words);
+  const uint64_t T = ntiles_of(rg.rw, tb);
   if (T > kLdsTiles) {
     if (tid == 0) atomicOr(&st->status, kStGeometry);
     return;
@@ -615,7 +634,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     for (int q = 0; q < kScatterKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < n) {
-        tt[q] = (unsigned)(bb_index(seed, rk_[q], words, magic) >> tb);
+        tt[q] = (unsigned)((bb_index(seed, rk_[q], words, magic) - rg.plo) >> tb);
         rk[q] = atomicAdd(&cnt[tt[q]], 1u);
       }
     }
@@ -753,6 +772,10 @@ __global__ __launch_bounds__(kHST) void k_hscan(int level, const unsigned* __res
   const uint64_t T = st->ntiles[level], B = st->nchunks[level], M = T * B;
   const uint64_t nseg = (M + kScanSeg - 1) / kScanSeg;
   const unsigned tid = threadIdx.x;
+  if (B == 0) {  // no records (a multi-GPU rank whose range received none): empty tiles
+    for (uint64_t t = (uint64_t)blockIdx.x * kHST + tid; t <= T; t += (uint64_t)gridDim.x * kHST) tile_start[t] = 0;
+    return;
+  }
   for (;;) {
     if (tid == 0) s_seg = atomicAdd(&st->sticket[level], 1ull);
     __syncthreads();
@@ -801,10 +824,12 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
   __shared__ unsigned s_wc[NT / 64];
   __shared__ unsigned long long s_wbase[NT / 64];
   if (!level_active(level, st)) return;
-  const uint64_t N = st->n[0];
+  const uint64_t N = st->out_cap;
+  const bool out_on = level_out_on(st, level);
   const uint64_t words = st->words[level], magic = st->magic[level];
   const uint64_t T = st->ntiles[level];
-  const uint64_t w32_level = 2 * words;
+  const LevelRange rg = level_range(st, level, words);
+  const uint64_t w32_level = 2 * rg.rw;
   const unsigned tpw = 1u << (tb - 5);
   const unsigned per = (tpw + NT - 1) / NT;
   uint32_t* sA = dyn;
@@ -814,7 +839,7 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
   unsigned short* sloc = reinterpret_cast<unsigned short*>(dyn + 2 * tpw);
   unsigned short* sridx = sloc + kcap;
   uint64_t* srm = reinterpret_cast<uint64_t*>(sridx + kcap);  // kcap / 64 words
-  uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[level]);
+  uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[level] + rg.plo / 64);
   const uint64_t seed = level_seed(level);
   const uint64_t lvl_base = st->lvl_base[level];
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -845,7 +870,7 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
       nk = tile_start[t + 1] - lo;
     }
     const Rec* rb = bucket + lo;
-    const uint64_t tbase = t << tb;
+    const uint64_t tbase = rg.plo + (t << tb);
     const bool cached = small && nk <= kcap;
     // ---- mark: A/C in LDS (and each record's in-tile position, when cached)
     for (uint64_t j0 = tid; j0 < nk; j0 += (uint64_t)NT * kTU) {
@@ -925,8 +950,8 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
       __syncthreads();
       TPROF(4);
       // ---- outputs: consecutive ranks -> consecutive fp_out/pos_out slots
-      if (base + pop > N) bad = true;
-      for (uint64_t r0 = tid; r0 < pop && base + pop <= N; r0 += (uint64_t)NT * kTU) {
+      if (base + pop > N && out_on) bad = true;
+      for (uint64_t r0 = tid; out_on && r0 < pop && base + pop <= N; r0 += (uint64_t)NT * kTU) {
         uint64_t cf[kTU], cp[kTU];  // only f and p are needed for a settled key
 #pragma unroll
         for (int u = 0; u < kTU; ++u) {
@@ -960,9 +985,11 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
           if (wv & bit) {
             const uint64_t p = base + sC[loc >> 5] + __popc(wv & (bit - 1));
             if (p < N) {
-              fp_out[p] = rc.f;
-              pos_out[p] = rc.p;
-            } else {
+              if (out_on) {
+                fp_out[p] = rc.f;
+                pos_out[p] = rc.p;
+              }
+            } else if (out_on) {
               bad = true;
             }
           } else {
@@ -1065,10 +1092,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
   __shared__ unsigned s_wc[NT / 64];
   __shared__ unsigned long long s_wbase[NT / 64];
   if (!level_active(level, st)) return;
-  const uint64_t N = st->n[0];
+  const uint64_t N = st->out_cap;
+  const bool out_on = level_out_on(st, level);
   const uint64_t words = st->words[level], magic = st->magic[level];
   const uint64_t T = st->ntiles[level];
-  const uint64_t w32_level = 2 * words;
+  const LevelRange rg = level_range(st, level, words);
+  const uint64_t w32_level = 2 * rg.rw;
   const unsigned tpw = 1u << (tb - 5);
   const unsigned per = (tpw + NT - 1) / NT;
   const unsigned scap = reg_stage(tb);
@@ -1076,7 +1105,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
   uint64_t* sp = dyn64 + scap;
   uint32_t* sA = reinterpret_cast<uint32_t*>(dyn64 + 2 * scap);
   uint32_t* sC = sA + tpw;
-  uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[level]);
+  uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[level] + rg.plo / 64);
   const uint64_t seed = level_seed(level);
   const uint64_t lvl_base = st->lvl_base[level];
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -1128,7 +1157,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
       }
       return o;
     };
-    const uint64_t tbase = t << tb;
+    const uint64_t tbase = rg.plo + (t << tb);
     const bool fits = nk <= (uint64_t)kRegR * NT;
     uint64_t k[kRegR], f[kRegR], p[kRegR];
     unsigned loc2[(kRegR + 1) / 2];  // in-tile positions (< 2^14), two per register
@@ -1204,7 +1233,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
     TPROF(3);
     const uint64_t base = lvl_base + s_prefix;
     const bool ok = base + pop <= N;
-    if (!ok) bad = true;
+    if (!ok && out_on) bad = true;
     // ---- classify: settled -> stage[rank] (or direct past the stage); collided -> count
     unsigned wc = 0;
     if (fits) {
@@ -1221,7 +1250,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
             if (rank < scap) {
               sf[rank] = f[r];
               sp[rank] = p[r];
-            } else if (ok) {
+            } else if (ok && out_on) {
               fp_out[base + rank] = f[r];
               pos_out[base + rank] = p[r];
             }
@@ -1242,7 +1271,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
           const uint32_t bit = 1u << (x & 31);
           if (wv & bit) {
             const unsigned rank = sC[x >> 5] + __popc(wv & (bit - 1));
-            if (ok) {
+            if (ok && out_on) {
               fp_out[base + rank] = q->f;
               pos_out[base + rank] = q->p;
             }
@@ -1298,7 +1327,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
         }
       }
     }
-    if (ok && fits) {
+    if (ok && fits && out_on) {
       const uint64_t ns = min<uint64_t>(pop, scap);
       for (uint64_t i = tid; i < ns; i += NT) {
         fp_out[base + i] = sf[i];
@@ -1316,7 +1345,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
 // --------------------------------------------------------------------- tail --------
 // Every remaining level in one workgroup: A/C and the rank prefix in LDS, outputs
 // written directly, collided records compacted into the other list.
-__global__ __launch_bounds__(kTailT) void k_bin_tail(int big_launched, Rec* list0, Rec* list1, uint64_t* bits,
+__global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_launched, Rec* list0, Rec* list1, uint64_t* bits,
                                                      uint64_t cap_words, uint64_t* __restrict__ fp_out,
                                                      uint64_t* __restrict__ pos_out, LevelState* st,
                                                      unsigned long long* __restrict__ prof) {
@@ -1327,7 +1356,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int big_launched, Rec* list
   __shared__ int s_level;
   const unsigned tid = threadIdx.x, lane = lane_id();
   if (tid == 0) {
-    int L = 1;
+    int L = first_level > 1 ? first_level : 1;
     while (L <= big_launched && st->n[L] > kGate) ++L;
     s_level = L;
     s_n = st->n[L];
@@ -1339,7 +1368,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int big_launched, Rec* list
     st->tail_first = L;
   }
   __syncthreads();
-  const uint64_t N = st->n[0];
+  const uint64_t N = st->out_cap;
   bool bad = false;
   for (;;) {
     const int L = s_level;
@@ -1426,9 +1455,11 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int big_launched, Rec* list
           if (wv & bit) {
             const uint64_t q = base + spre[x >> 5] + __popc(wv & (bit - 1));
             if (q < N) {
-              fp_out[q] = cf[u];
-              pos_out[q] = cp[u];
-            } else {
+              if (level_out_on(st, L)) {
+                fp_out[q] = cf[u];
+                pos_out[q] = cp[u];
+              }
+            } else if (level_out_on(st, L)) {
               bad = true;
             }
           } else {
@@ -1492,7 +1523,7 @@ void binned_set_lds_limits() {
 
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s) {
-  if (level == 0) {
+  if (level == 0 && !b.dist) {
     static const int mode = [] {
       // A/B knob: 3 direct, loop (default); 0 LDS-staged; 1 direct, batched loads;
       // 2 length-sorted, loop; 4 length-sorted, batched; 5 word-count classes
@@ -1528,7 +1559,7 @@ void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s)
 }
 
 void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s) {
-  const Rec* il = level == 0 ? nullptr : b.list[(level - 1) & 1];
+  const Rec* il = level == 0 && !b.dist ? nullptr : b.list[(level - 1) & 1];
   k_scatter<<<256, kSB, 0, s>>>(level, b.kh, b.fp, b.pos, b.pos_base, il, b.off, b.bucket, b.st, g.tb, g.chunk);
 }
 
@@ -1561,9 +1592,9 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
                                      b.bucket, b.bucket_cap, b.flags, b.st, g.tb, b.cap_words, b.tile_prof);
 }
 
-void launch_binned_tail(int big_launched, const BinBuffers& b, hipStream_t s) {
+void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s) {
   k_level_setup<<<1, 64, 0, s>>>(big_launched + 1, b.st);
-  k_bin_tail<<<1, kTailT, 0, s>>>(big_launched, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out, b.pos_out,
+  k_bin_tail<<<1, kTailT, 0, s>>>(first_level, big_launched, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out, b.pos_out,
                                   b.st, b.tile_prof);
 }
 

@@ -5,12 +5,12 @@
 // full-grid kernels gated on the device-resident key count, the geometric tail of
 // small levels runs inside one workgroup with LDS bit vectors.
 //
-// Multi-GPU (s3imph_build_device_dist): one process per GPU, RCCL over xGMI.  Keys
-// shard by contiguous index range.  Per level every rank marks its keys into a
-// full-size local A/C pair, expands it to one saturating count byte per position,
-// RCCL reduce-scatters the bytes (sum), decides "exactly one key here" on its slice,
-// and all-gathers the packed final bit vector.  Keys then settle or move to the next
-// level locally.  At the end (p, fp, pos) triples go to the rank owning p's range.
+// Multi-GPU (s3imph_build_device_dist): one process per GPU.  Position-range
+// ownership (s3imph_dist.hip): per level every rank routes its records to the owner of
+// their position with one all-to-all, each owner runs the single-GPU tile pipeline on
+// its range, and once the active set is small every rank finishes it identically.
+// Collectives go through a Comm: RCCL over xGMI in production, or host callbacks
+// (the test transport that runs several ranks on one GPU).
 //
 // Reference: pkg/format/mphf_streaming.go:122-232 (Build), :141 (bbhash.New),
 // :176-204 + :237-261 (positions and scatter).
@@ -34,24 +34,35 @@ using namespace s3imph;
 
 namespace {
 
-struct DistState {
-  ncclComm_t comm = nullptr;
+// Collectives of the multi-GPU build, on device buffers, ordered on stream s.
+struct Comm {
   int rank = 0, nranks = 1;
-  uint64_t cap_local = 0, cap_global_words = 0, cap_out = 0;
-  uint32_t* A = nullptr;          // local seen bits, full level size (u32 words)
-  uint32_t* C = nullptr;          // local collided bits
-  uint8_t* cnt = nullptr;         // count bytes, full (padded) level size
-  uint8_t* sum = nullptr;         // this rank's reduce-scatter slice
-  uint64_t* packed = nullptr;     // this rank's packed final bits
-  unsigned long long* counters = nullptr;  // [0] local redo count, [1] global, [2..] scratch
-  unsigned long long* owner_counts = nullptr;  // nranks
-  unsigned long long* count_matrix = nullptr;  // nranks * nranks
-  unsigned long long* bucket_fill = nullptr;   // nranks
-  unsigned long long* bucket_off = nullptr;    // nranks
-  uint64_t* send = nullptr;       // 3 * cap_local
-  uint64_t* recv = nullptr;       // 3 * cap_out
-  unsigned* status = nullptr;
-  unsigned long long* h_pinned = nullptr;      // host staging
+  virtual ~Comm() = default;
+  // d_recv[r * bytes ..) <- rank r's d_send[0 .. bytes)
+  virtual void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) = 0;
+  // element-wise u64 sum over ranks
+  virtual void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
+                             hipStream_t s) = 0;
+  // d_send + soff[q] (sbytes[q] bytes) -> rank q; rank q's bytes -> d_recv + roff[q] (rbytes[q]); host arrays
+  virtual void alltoallv(const void* d_send, const uint64_t* soff, const uint64_t* sbytes, void* d_recv,
+                         const uint64_t* roff, const uint64_t* rbytes, hipStream_t s) = 0;
+};
+
+constexpr uint64_t kDistSwitchKeysDefault = 2ull << 20;  // levels below this run replicated
+
+struct DistState {
+  Comm* comm = nullptr;
+  int rank = 0, nranks = 1;
+  uint64_t cap_list = 0, cap_send = 0, cap_stage_words = 0;
+  Rec* send = nullptr;                       // per-owner send regions / replicated gather staging
+  uint64_t* stage_bits = nullptr;            // level bit-vector all-gather staging
+  unsigned long long* scnt = nullptr;        // per-owner send counts (nranks)
+  unsigned long long* mat = nullptr;         // all-gathered send counts (nranks x nranks)
+  unsigned long long* gslot = nullptr;       // per-level global counts (kMaxLevels + 2)
+  unsigned long long* small = nullptr;       // scratch for tiny collectives (2 x 64 x 64)
+  unsigned long long* h_pinned = nullptr;    // host staging (64 x 64 + 256 u64)
+  std::vector<uint64_t> seg;                 // last build: (p_lo, count, local_off) triples
+  uint64_t out_n = 0;
 };
 
 }  // namespace
@@ -62,9 +73,7 @@ struct s3imph_ctx {
   std::mutex mu;
 
   uint64_t cap_keys = 0, cap_words = 0, cap_blocks = 0;
-  uint64_t *kh = nullptr, *fp = nullptr, *settle = nullptr, *bits = nullptr, *rank_base = nullptr;
-  uint64_t* rkeys[2] = {nullptr, nullptr};   // multi-GPU redo lists
-  uint32_t* ridx[2] = {nullptr, nullptr};
+  uint64_t *kh = nullptr, *fp = nullptr, *bits = nullptr, *rank_base = nullptr;
   unsigned long long* block_sums = nullptr;
   LevelState* d_st = nullptr;
   LevelState* h_st = nullptr;
@@ -73,6 +82,7 @@ struct s3imph_ctx {
   // single-GPU binned pipeline (s3imph_binned.hip)
   Rec* bucket = nullptr;
   Rec* list[2] = {nullptr, nullptr};
+  uint64_t bucket_cap = 0;                   // records in bucket / each list
   unsigned *hist = nullptr, *hoff = nullptr, *tile_start = nullptr, *scan_sums = nullptr;
   unsigned long long* flags = nullptr;
   unsigned long long* sflags = nullptr;
@@ -103,7 +113,9 @@ struct s3imph_ctx {
   std::vector<float> stage_ms;
   std::vector<std::string> stage_names;
 
+  std::string last_msg;  // message of the last failed device-resident call
   bool dist = false;
+  uint64_t dist_switch = kDistSwitchKeysDefault;  // global keys below which levels run replicated
   DistState d;
 };
 
@@ -200,11 +212,11 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   c->cap_blocks = (c->cap_words + 2047) / 2048 + 1;
   dalloc(c->block_sums, c->cap_blocks);
   c->cap_keys = cap;
+  c->bucket_cap = cap;
 }
 
 void free_workspace(s3imph_ctx* c) {
-  dfree(c->kh); dfree(c->fp); dfree(c->settle); dfree(c->bits); dfree(c->rank_base);
-  dfree(c->rkeys[0]); dfree(c->rkeys[1]); dfree(c->ridx[0]); dfree(c->ridx[1]);
+  dfree(c->kh); dfree(c->fp); dfree(c->bits); dfree(c->rank_base);
   dfree(c->block_sums); dfree(c->d_st);
   dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
   dfree(c->tcnt);
@@ -214,11 +226,10 @@ void free_workspace(s3imph_ctx* c) {
   c->h_st = nullptr;
   dfree(c->s_blob); dfree(c->s_offsets); dfree(c->s_pos); dfree(c->s_fp); dfree(c->s_posout);
   DistState& d = c->d;
-  dfree(d.A); dfree(d.C); dfree(d.cnt); dfree(d.sum); dfree(d.packed); dfree(d.counters);
-  dfree(d.owner_counts); dfree(d.count_matrix); dfree(d.bucket_fill); dfree(d.bucket_off);
-  dfree(d.send); dfree(d.recv); dfree(d.status);
+  dfree(d.send); dfree(d.stage_bits); dfree(d.scnt); dfree(d.mat); dfree(d.gslot); dfree(d.small);
   if (d.h_pinned) (void)hipHostFree(d.h_pinned);
   d.h_pinned = nullptr;
+  d.cap_list = d.cap_send = d.cap_stage_words = 0;
   for (auto e : c->events) (void)hipEventDestroy(e);
   c->events.clear();
   c->cap_keys = 0;
@@ -292,11 +303,7 @@ int map_status(s3imph_ctx* c, unsigned flags, uint64_t n, std::string* msg) {
   return S3IMPH_OK;
 }
 
-// Enqueue one attempt of the binned pipeline.  `conservative` sizes every level with
-// the level-0 geometry (always inside the workspace bounds) and runs every level that
-// is still big as a full-grid level; the default predicts each level's size.
-void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
-                    uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
+BinBuffers make_bufs(s3imph_ctx* c, const uint64_t* pos, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s) {
   BinBuffers b{};
   b.kh = c->kh;
   b.fp = c->fp;
@@ -312,7 +319,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   b.flags = c->flags;
   b.sflags = c->sflags;
   b.tcnt = c->tcnt;
-  b.bucket_cap = c->cap_keys;
+  b.bucket_cap = c->bucket_cap;
   b.tile_mode = c->tile_mode;
   b.tile_block = c->tile_block;
   b.tile_prof = nullptr;
@@ -327,58 +334,92 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   b.fp_out = fp_out;
   b.pos_out = pos_out;
   b.st = c->d_st;
+  b.dist = c->dist;
+  return b;
+}
 
-  const double q = 1.0 - std::exp(-0.5);  // fraction of keys that collide at load 1/2
-  const LevelGeom g0 = choose_geom(n, c->target_tiles0, c->target_chunks, kRegTileMaxBits);
+// Launch grids for a level of about nk records over `size` positions; the kernels loop
+// over whatever the device finds.
+struct Grids {
   int gc, gt, gs;
-  // Grids from a (predicted) key count; kernels loop over whatever the device finds.
-  auto grids = [&](uint64_t nk, LevelGeom g) {
-    const uint64_t T = (64 * level_words(nk ? nk : 1) + (1ull << g.tb) - 1) >> g.tb;
-    const uint64_t B = std::max<uint64_t>((nk + g.chunk - 1) / g.chunk, 1);
-    gc = (int)std::min<uint64_t>(B, 2048);
-    gt = (int)std::min<uint64_t>(std::max<uint64_t>(T, 1), 2048);
-    gs = (int)std::min<uint64_t>((T * B + kScanSeg - 1) / kScanSeg + 2, 256);
-  };
-  launch_init_state(c->d_st, n, 0, s);
-  ev_mark(c, s, "init");
-  grids(n, g0);
-  launch_binned_count(0, blob, offsets, n, b, g0, gc, s);
-  ev_mark(c, s, "hash_count0");
-  launch_binned_scan(0, b, gs, s);
-  ev_mark(c, s, "hscan0");
-  launch_binned_scatter(0, b, g0, s);
-  ev_mark(c, s, "scatter0");
-  launch_binned_tile(0, b, g0, gt, s);
-  ev_mark(c, s, "tile0");
-  const int big = conservative ? kMaxLevels - 2 : predict_big_levels(n);
-  int launched = 0;
-  for (int L = 1; L <= big; ++L) {
+};
+Grids level_grids(uint64_t nk, uint64_t size, LevelGeom g) {
+  const uint64_t T = (size + (1ull << g.tb) - 1) >> g.tb;
+  const uint64_t B = std::max<uint64_t>((nk + g.chunk - 1) / g.chunk, 1);
+  Grids r;
+  r.gc = (int)std::min<uint64_t>(B, 2048);
+  r.gt = (int)std::min<uint64_t>(std::max<uint64_t>(T, 1), 2048);
+  r.gs = (int)std::min<uint64_t>((T * B + kScanSeg - 1) / kScanSeg + 2, 256);
+  return r;
+}
+
+// One list-input level L (records in list[(L-1)&1]): about nb records over `size`
+// positions.  Small levels take the reservation scatter (no count / histogram scan).
+void enqueue_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, uint64_t size, bool conservative,
+                        const LevelGeom* force, hipStream_t s) {
+  // reservation slots are bucket_cap / T records per tile: keep them >= 4x the mean fill
+  const bool res = !conservative && nb <= c->res_max_keys && nb * 4 <= c->bucket_cap && L < kResLevels &&
+                   c->tile_mode == 0;
+  const LevelGeom g = force ? *force
+                      : res ? choose_geom_sz(nb, size, c->target_tiles_res, c->target_chunks, kRegTileMaxBits)
+                            : choose_geom_sz(nb, size, c->target_tiles, c->target_chunks, kRegTileMaxBits);
+  const Grids gr = level_grids(nb, size, g);
+  if (res && g.tb <= kRegTileMaxBits) {
+    const int gsr = (int)std::min<uint64_t>((nb + kSubRound - 1) / kSubRound, 256);
+    launch_binned_scatter_res(L, b, g, std::max(gsr, 1), s);
+    launch_binned_tile(L, b, g, gr.gt, s, true);
+  } else {
+    launch_binned_count(L, nullptr, nullptr, 0, b, g, gr.gc, s);
+    launch_binned_scan(L, b, gr.gs, s);
+    launch_binned_scatter(L, b, g, s);
+    launch_binned_tile(L, b, g, gr.gt, s);
+  }
+}
+
+// Levels L0, L0+1, ... of a whole-level build (every position on this GPU), starting
+// from n0 records in list[(L0-1)&1]: predicted-big levels as full-grid kernels, then
+// the single-workgroup tail.  Returns the last big level launched (L0-1 if none).
+int enqueue_levels_from(s3imph_ctx* c, const BinBuffers& b, int L0, uint64_t n0, const LevelGeom& gcons,
+                        bool conservative, hipStream_t s) {
+  const double q = 1.0 - std::exp(-0.5);  // fraction of keys that collide at load 1/2
+  const int big = conservative ? kMaxLevels - 2 : L0 - 1 + predict_big_levels(n0 / q);
+  int launched = L0 - 1;
+  for (int L = L0; L <= big && L < kMaxLevels - 1; ++L) {
     // Level sizes concentrate tightly around n q^L; a level predicted within 1/kTailMargin
     // of the tail's capacity is left to the tail (an unexpectedly large one is caught by
     // kStTailOverflow and rerun conservatively).
-    const double pred = (double)n * std::pow(q, L);
+    const double pred = (double)n0 * std::pow(q, L - L0);
     if (!conservative && pred * kTailMargin < (double)kTailKeys) break;
     launched = L;
-    const uint64_t nb = conservative ? n : (uint64_t)(pred * 1.1) + 4096;
-    const bool res = !conservative && nb <= c->res_max_keys && L < kResLevels && c->tile_mode == 0;
-    const LevelGeom g = conservative ? g0
-                        : res        ? choose_geom(nb, c->target_tiles_res, c->target_chunks, kRegTileMaxBits)
-                                     : choose_geom(nb, c->target_tiles, c->target_chunks, kRegTileMaxBits);
-    grids(nb, g);
-    if (res && g.tb <= kRegTileMaxBits) {
-      const int gr = (int)std::min<uint64_t>((nb + kSubRound - 1) / kSubRound, 256);
-      launch_binned_scatter_res(L, b, g, gr, s);
-      launch_binned_tile(L, b, g, gt, s, true);
-    } else {
-      launch_binned_count(L, nullptr, nullptr, 0, b, g, gc, s);
-      launch_binned_scan(L, b, gs, s);
-      launch_binned_scatter(L, b, g, s);
-      launch_binned_tile(L, b, g, gt, s);
-    }
+    const uint64_t nb = conservative ? n0 : (uint64_t)(pred * 1.1) + 4096;
+    enqueue_list_level(c, b, L, nb, 64 * level_words(nb), conservative, conservative ? &gcons : nullptr, s);
   }
   ev_mark(c, s, "levels");
-  launch_binned_tail(launched, b, s);
+  launch_binned_tail(L0, launched, b, s);
   ev_mark(c, s, "tail");
+  return launched;
+}
+
+// Enqueue one attempt of the binned pipeline.  `conservative` sizes every level with
+// the level-0 geometry (always inside the workspace bounds) and runs every level that
+// is still big as a full-grid level; the default predicts each level's size.
+void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
+                    uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
+  const BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
+  const double q = 1.0 - std::exp(-0.5);
+  const LevelGeom g0 = choose_geom(n, c->target_tiles0, c->target_chunks, kRegTileMaxBits);
+  launch_init_state(c->d_st, n, n, s);
+  ev_mark(c, s, "init");
+  const Grids gr = level_grids(n, 64 * level_words(n), g0);
+  launch_binned_count(0, blob, offsets, n, b, g0, gr.gc, s);
+  ev_mark(c, s, "hash_count0");
+  launch_binned_scan(0, b, gr.gs, s);
+  ev_mark(c, s, "hscan0");
+  launch_binned_scatter(0, b, g0, s);
+  ev_mark(c, s, "scatter0");
+  launch_binned_tile(0, b, g0, gr.gt, s);
+  ev_mark(c, s, "tile0");
+  enqueue_levels_from(c, b, 1, conservative ? n : (uint64_t)((double)n * q), g0, conservative, s);
 }
 
 void set_lds_attrs(s3imph_ctx* c) {
@@ -496,235 +537,415 @@ int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
 }
 
 // -------------------------------------------------------------------- distributed ----
+// RCCL over xGMI: all-to-all as grouped point-to-point send/recv (xGMI is a full mesh
+// of point-to-point links, so every pair streams on its own link), all-gathers and
+// all-reduces as RCCL collectives; the rank's own share is a device-to-device copy.
+struct RcclComm final : Comm {
+  ncclComm_t comm = nullptr;
+  ~RcclComm() override {
+    if (comm) (void)ncclCommDestroy(comm);
+  }
+  void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
+    NCCLCHECK(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, s));
+  }
+  void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
+                     hipStream_t s) override {
+    NCCLCHECK(ncclAllReduce(d_in, d_out, count, ncclUint64, ncclSum, comm, s));
+  }
+  void alltoallv(const void* d_send, const uint64_t* soff, const uint64_t* sbytes, void* d_recv,
+                 const uint64_t* roff, const uint64_t* rbytes, hipStream_t s) override {
+    const char* sb = static_cast<const char*>(d_send);
+    char* rb = static_cast<char*>(d_recv);
+    NCCLCHECK(ncclGroupStart());
+    for (int q = 0; q < nranks; ++q) {
+      if (q == rank) continue;
+      if (sbytes[q]) NCCLCHECK(ncclSend(sb + soff[q], sbytes[q], ncclUint8, q, comm, s));
+      if (rbytes[q]) NCCLCHECK(ncclRecv(rb + roff[q], rbytes[q], ncclUint8, q, comm, s));
+    }
+    NCCLCHECK(ncclGroupEnd());
+    if (sbytes[rank])
+      HIPCHECK(hipMemcpyAsync(rb + roff[rank], sb + soff[rank], sbytes[rank], hipMemcpyDeviceToDevice, s));
+  }
+};
+
+// Host-callback transport (s3imph_host_comm): the test harness's collectives (e.g.
+// torch.distributed/gloo) on host copies.  Lets several ranks share one GPU.
+struct HostComm final : Comm {
+  s3imph_host_comm cb{};
+  std::vector<uint8_t> hs, hr;
+  void d2h(void* h, const void* d, uint64_t bytes, hipStream_t s) {
+    if (bytes) HIPCHECK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s));
+  }
+  void h2d(void* d, const void* h, uint64_t bytes, hipStream_t s) {
+    if (bytes) HIPCHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
+  }
+  void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
+    hs.resize(bytes + 1);
+    hr.resize(bytes * nranks + 1);
+    d2h(hs.data(), d_send, bytes, s);
+    HIPCHECK(hipStreamSynchronize(s));
+    if (cb.allgather(cb.user, hs.data(), hr.data(), bytes) != 0) throw Fail{S3IMPH_ERR_RCCL, "host allgather failed"};
+    h2d(d_recv, hr.data(), bytes * nranks, s);
+    HIPCHECK(hipStreamSynchronize(s));
+  }
+  void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
+                     hipStream_t s) override {
+    const uint64_t bytes = 8 * count;
+    hs.resize(bytes + 1);
+    hr.resize(bytes * nranks + 1);
+    d2h(hs.data(), d_in, bytes, s);
+    HIPCHECK(hipStreamSynchronize(s));
+    if (cb.allgather(cb.user, hs.data(), hr.data(), bytes) != 0) throw Fail{S3IMPH_ERR_RCCL, "host allgather failed"};
+    std::vector<unsigned long long> sum(count, 0);
+    for (int r = 0; r < nranks; ++r)
+      for (uint64_t i = 0; i < count; ++i) {
+        unsigned long long v;
+        std::memcpy(&v, hr.data() + r * bytes + 8 * i, 8);
+        sum[i] += v;
+      }
+    h2d(d_out, sum.data(), bytes, s);
+    HIPCHECK(hipStreamSynchronize(s));
+  }
+  void alltoallv(const void* d_send, const uint64_t* soff, const uint64_t* sbytes, void* d_recv,
+                 const uint64_t* roff, const uint64_t* rbytes, hipStream_t s) override {
+    std::vector<uint64_t> ps(nranks), pr(nranks);
+    uint64_t st = 0, rt = 0;
+    for (int q = 0; q < nranks; ++q) {
+      ps[q] = st;
+      st += sbytes[q];
+      pr[q] = rt;
+      rt += rbytes[q];
+    }
+    hs.resize(st + 1);
+    hr.resize(rt + 1);
+    for (int q = 0; q < nranks; ++q) d2h(hs.data() + ps[q], static_cast<const char*>(d_send) + soff[q], sbytes[q], s);
+    HIPCHECK(hipStreamSynchronize(s));
+    if (cb.alltoallv(cb.user, hs.data(), ps.data(), sbytes, hr.data(), pr.data(), rbytes) != 0)
+      throw Fail{S3IMPH_ERR_RCCL, "host alltoallv failed"};
+    for (int q = 0; q < nranks; ++q) h2d(static_cast<char*>(d_recv) + roff[q], hr.data() + pr[q], rbytes[q], s);
+    HIPCHECK(hipStreamSynchronize(s));
+  }
+};
+
+constexpr int kMaxDistLevels = 16;
+constexpr uint64_t kSmallWords = 2 * 64 * 64;
+
+void ensure_dist_small(s3imph_ctx* c) {
+  DistState& d = c->d;
+  if (d.small) return;
+  dalloc(d.scnt, kMaxRanks + 1);
+  dalloc(d.mat, (uint64_t)(kMaxRanks + 1) * kMaxRanks);
+  dalloc(d.gslot, kMaxLevels + 2);
+  dalloc(d.small, kSmallWords);
+  void* h = nullptr;
+  HIPCHECK(hipHostMalloc(&h, sizeof(unsigned long long) * (kSmallWords + 256), hipHostMallocDefault));
+  d.h_pinned = static_cast<unsigned long long*>(h);
+  if (!c->d_st) dalloc(c->d_st, 1);
+  if (!c->h_st) {
+    void* hs = nullptr;
+    HIPCHECK(hipHostMalloc(&hs, sizeof(LevelState), hipHostMallocDefault));
+    c->h_st = static_cast<LevelState*>(hs);
+  }
+}
+
+// Output entries one rank may need: its share of the positions settles about N/P keys
+// (binomial spread), and rank 0 also writes the replicated tail levels.
+uint64_t dist_out_cap(const s3imph_ctx* c, uint64_t n_global) {
+  const uint64_t P = (uint64_t)c->d.nranks;
+  const uint64_t share = (n_global + P - 1) / P;
+  return share + share / 16 + 65536 + std::min<uint64_t>(n_global, c->dist_switch + c->dist_switch / 4);
+}
+
+// Multi-GPU workspace: records this rank may hold at a distributed level (its received
+// share, about N/P, or its own keys), or all records of the first replicated level.
 void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
   DistState& d = c->d;
   const int P = d.nranks;
-  const uint64_t per_rank = (n_global + P - 1) / P;
-  if (n_local <= d.cap_local && level_words(n_global) <= d.cap_global_words && per_rank <= d.cap_out &&
-      c->d_st)
+  ensure_dist_small(c);
+  const uint64_t share = std::max<uint64_t>(n_local, (n_global + P - 1) / P);
+  const uint64_t capl = std::max<uint64_t>(share + share / 10 + 65536, c->dist_switch + c->dist_switch / 4 + 65536);
+  const uint64_t caps = capl + 4096ull * P;
+  const uint64_t stagew = level_words(std::max<uint64_t>(n_global, 1)) + 2ull * P + 64;
+  const uint64_t capw = cap_words_for(std::max<uint64_t>(n_global, 1024)) + stagew;
+  if (capl <= d.cap_list && caps <= d.cap_send && stagew <= d.cap_stage_words && capw <= c->cap_words && c->hist)
     return;
-  const uint64_t capl = std::max<uint64_t>(n_local, 1024);
-  const uint64_t w0 = level_words(std::max<uint64_t>(n_global, 1024));
-  const uint64_t pos_pad = ((64 * w0 + 64ull * P - 1) / (64ull * P)) * (64ull * P);
-  dalloc(c->kh, capl);
-  dalloc(c->fp, capl);
-  dalloc(c->settle, capl);
-  dalloc(c->rkeys[0], capl);
-  dalloc(c->rkeys[1], capl);
-  dalloc(c->ridx[0], capl);
-  dalloc(c->ridx[1], capl);
+  dalloc(c->bucket, capl);
+  dalloc(c->list[0], capl);
+  dalloc(c->list[1], capl);
+  c->bucket_cap = capl;
   c->cap_keys = capl;
-  c->cap_words = cap_words_for(std::max<uint64_t>(n_global, 1024)) + (pos_pad / 64);
-  dalloc(c->bits, c->cap_words);
-  dalloc(c->rank_base, c->cap_words);
-  c->cap_blocks = (c->cap_words + 2047) / 2048 + 1;
+  dalloc(c->hist, kHistCap);
+  dalloc(c->hoff, kHistCap);
+  dalloc(c->tile_start, kMaxTiles + 2);
+  dalloc(c->scan_sums, kHistCap / 2048 + 2);
+  dalloc(c->flags, kMaxTiles + 2);
+  dalloc(c->sflags, kHistCap / kScanSeg + 2);
+  dalloc(c->tcnt, (uint64_t)kResLevels * kMaxTiles * kResShards);
+  c->cap_words = capw;
+  dalloc(c->bits, capw);
+  dalloc(c->rank_base, capw);
+  c->cap_blocks = (capw + 2047) / 2048 + 1;
   dalloc(c->block_sums, c->cap_blocks);
-  if (!c->d_st) dalloc(c->d_st, 1);
-  if (!c->h_st) {
-    void* h = nullptr;
-    HIPCHECK(hipHostMalloc(&h, sizeof(LevelState), hipHostMallocDefault));
-    c->h_st = static_cast<LevelState*>(h);
-  }
-  dalloc(d.A, pos_pad / 32);
-  dalloc(d.C, pos_pad / 32);
-  dalloc(d.cnt, pos_pad);
-  dalloc(d.sum, pos_pad / P);
-  dalloc(d.packed, pos_pad / P / 64 + 1);
-  dalloc(d.counters, 8);
-  dalloc(d.owner_counts, P);
-  dalloc(d.count_matrix, (uint64_t)P * P);
-  dalloc(d.bucket_fill, P);
-  dalloc(d.bucket_off, P);
-  const uint64_t per = std::max<uint64_t>(per_rank, 1024);
-  dalloc(d.send, 3 * capl);
-  dalloc(d.recv, 3 * per);
-  dalloc(d.status, 1);
-  if (!d.h_pinned) {
-    void* h = nullptr;
-    HIPCHECK(hipHostMalloc(&h, sizeof(unsigned long long) * (4 + 2 * 64 * 64), hipHostMallocDefault));
-    d.h_pinned = static_cast<unsigned long long*>(h);
-  }
-  HIPCHECK(hipMemset(d.A, 0, pos_pad / 32 * 4));
-  HIPCHECK(hipMemset(d.C, 0, pos_pad / 32 * 4));
-  d.cap_local = capl;
-  d.cap_global_words = w0;
-  d.cap_out = per;
+  dalloc(d.send, caps);
+  dalloc(d.stage_bits, stagew);
+  d.cap_list = capl;
+  d.cap_send = caps;
+  d.cap_stage_words = stagew;
 }
 
-uint64_t allreduce_sum_u64(s3imph_ctx* c, unsigned long long* dbuf, uint64_t v, hipStream_t s) {
-  DistState& d = c->d;
-  d.h_pinned[0] = v;
-  HIPCHECK(hipMemcpyAsync(dbuf, d.h_pinned, 8, hipMemcpyHostToDevice, s));
-  NCCLCHECK(ncclAllReduce(dbuf, dbuf, 1, ncclUint64, ncclSum, d.comm, s));
-  HIPCHECK(hipMemcpyAsync(d.h_pinned, dbuf, 8, hipMemcpyDeviceToHost, s));
-  HIPCHECK(hipStreamSynchronize(s));
-  return d.h_pinned[0];
+bool records_have_duplicates(const Rec* d_list, uint64_t n) {
+  std::vector<Rec> h(n);
+  if (n) HIPCHECK(hipMemcpy(h.data(), d_list, n * sizeof(Rec), hipMemcpyDeviceToHost));
+  std::vector<uint64_t> k(n);
+  for (uint64_t i = 0; i < n; ++i) k[i] = h[i].k;
+  std::sort(k.begin(), k.end());
+  return std::adjacent_find(k.begin(), k.end()) != k.end();
 }
 
-int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
-               uint64_t n_local, uint64_t key_base, uint64_t* fp_out, uint64_t* pos_out,
-               uint64_t out_cap, uint64_t* out_lo, uint64_t* out_n, hipStream_t s,
-               s3imph_build_info* info, std::string* msg) {
+constexpr int kDistRetry = -1;
+
+// One attempt of the multi-GPU build (see s3imph_dist.hip for the decomposition).
+// `conservative` runs every level on the counted path and the replicated levels with
+// one geometry; every rank takes the same branches (all decisions use global counts).
+int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
+                 uint64_t n_local, uint64_t key_base, uint64_t N, uint64_t* fp_out, uint64_t* pos_out,
+                 uint64_t out_cap, hipStream_t s, bool conservative, s3imph_build_info* info, std::string* msg) {
   DistState& d = c->d;
+  Comm& cm = *d.comm;
   const int P = d.nranks, R = d.rank;
-  c->have_build = false;
-  c->rank_valid = false;
-  *info = s3imph_build_info{};
-  if (n_local > kU32Limit) {
-    *msg = "build MPHF: more than 2^32-1 keys on one rank";
-    return S3IMPH_ERR_INVALID;
-  }
-  ev_begin(c);
-  ev_mark(c, s, "start");
-  // Global key count (also a rendezvous: every rank must reach the same build).
-  if (!d.counters) dalloc(d.counters, 8);
-  if (!d.h_pinned) {
-    void* h = nullptr;
-    HIPCHECK(hipHostMalloc(&h, sizeof(unsigned long long) * (4 + 2 * 64 * 64), hipHostMallocDefault));
-    d.h_pinned = static_cast<unsigned long long*>(h);
-  }
-  const uint64_t N = allreduce_sum_u64(c, d.counters + 2, n_local, s);
-  info->n_keys = N;
-  const uint64_t per_rank = (N + P - 1) / P;
-  *out_lo = std::min<uint64_t>((uint64_t)R * per_rank, N);
-  *out_n = std::min<uint64_t>(per_rank, N - *out_lo);
-  if (N == 0) {
-    c->have_build = true;
-    c->last_n = 0;
-    c->info = *info;
-    return S3IMPH_OK;
-  }
-  if (*out_n > out_cap) {
-    *msg = "build MPHF: output slice capacity too small";
-    return S3IMPH_ERR_INVALID;
-  }
-  ensure_dist_workspace(c, n_local, N);
-  HIPCHECK(hipMemsetAsync(d.status, 0, 4, s));
-  HIPCHECK(hipMemsetAsync(c->bits, 0, c->cap_words * 8, s));
-  LevelState& hs = *c->h_st;
-  std::memset(&hs, 0, sizeof(LevelState));
-  const int grid = default_grid(std::max<uint64_t>(n_local, 1), 256);
-
-  uint64_t nL = N, nloc = n_local, woff = 0;
-  int L = 0;
+  LevelState* st = c->d_st;
+  const BinBuffers b = make_bufs(c, nullptr, fp_out, pos_out, s);
+  const double q = 1.0 - std::exp(-0.5);
+  launch_init_state(st, 0, out_cap, s);
+  HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kMaxTiles * kResShards * sizeof(unsigned), s));
+  launch_dist_setup(st, 0, nullptr, N, R, P, s);
   ev_mark(c, s, "init");
+  std::vector<uint64_t> hw, hS;  // words and per-rank range of each distributed level
+  std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
+  double src_pred = (double)n_local;  // records this rank routes at the current level
+  unsigned long long* M = d.h_pinned;  // (P + 1) x P gathered counts, row r = rank r's [scnt, overflow]
+  int L = 0;
   for (;;) {
-    if (L >= kMaxLevels) {
-      *msg = "build MPHF: can't find minimal perfect hash after " + std::to_string(kMaxLevels) + " levels";
-      return S3IMPH_ERR_TOO_MANY_LEVELS;
+    // ---- route level L's records to their owners
+    uint64_t C = (uint64_t)(src_pred / P * 1.15) + 4096;
+    for (int tries = 0;; ++tries) {
+      if ((uint64_t)P * C > d.cap_send) {
+        HIPCHECK(hipStreamSynchronize(s));
+        dalloc(d.send, (uint64_t)P * C);
+        d.cap_send = (uint64_t)P * C;
+      }
+      HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
+      if (L == 0)
+        launch_route0(blob, offsets, pos, key_base, n_local, d.send, C, d.scnt, st, P, s);
+      else
+        launch_route(L, c->list[(L - 1) & 1], (uint64_t)src_pred, d.send, C, d.scnt, st, P, s);
+      launch_route_flag(st, d.scnt, P, s);
+      cm.allgather(d.scnt, d.mat, 8ull * (P + 1), s);
+      HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipStreamSynchronize(s));
+      bool over = false;
+      uint64_t need = 0;
+      for (int r = 0; r < P; ++r) over |= M[(uint64_t)r * (P + 1) + P] != 0;
+      for (int t = 0; t < P; ++t) need = std::max<uint64_t>(need, M[(uint64_t)R * (P + 1) + t]);
+      if (!over) break;
+      if (tries >= 3) {
+        *msg = "build MPHF: route regions keep overflowing";
+        return S3IMPH_ERR_INTERNAL;
+      }
+      C = need + need / 8 + 4096;
     }
-    const uint64_t words = level_words(nL);
-    const uint64_t positions = 64 * words;
-    const uint64_t pos_pad = ((positions + 64ull * P - 1) / (64ull * P)) * (64ull * P);
-    const uint64_t S = pos_pad / P;
-    if (woff + pos_pad / 64 > c->cap_words) {
-      *msg = "build MPHF: workspace overflow";
-      return S3IMPH_ERR_INTERNAL;
+    uint64_t nL = 0, m = 0;
+    for (int r = 0; r < P; ++r)
+      for (int t = 0; t < P; ++t) nL += M[(uint64_t)r * (P + 1) + t];
+    for (int r = 0; r < P; ++r) m += M[(uint64_t)r * (P + 1) + R];
+    const uint64_t w = level_words(nL), S = (w + P - 1) / P;
+    const uint64_t lo = std::min<uint64_t>((uint64_t)R * S, w), rw = std::min<uint64_t>(S, w - lo);
+    hw.push_back(w);
+    hS.push_back(S);
+    if (m > c->bucket_cap) {
+      *msg = "build MPHF: rank " + std::to_string(R) + " received " + std::to_string(m) + " records (capacity " +
+             std::to_string(c->bucket_cap) + ")";
+      return S3IMPH_ERR_NOMEM;
     }
-    hs.n[L] = nL;
-    hs.words[L] = words;
-    hs.woff[L] = woff;
-    hs.magic[L] = level_magic(words);
-    const uint64_t* kin = (L == 0) ? c->kh : c->rkeys[(L - 1) & 1];
-    const uint32_t* iin = (L == 0) ? nullptr : c->ridx[(L - 1) & 1];
-    if (L == 0)
-      launch_dist_hash_mark0(blob, offsets, nloc, c->kh, c->fp, words, d.A, d.C, d.status, grid, s);
-    else if (nloc)
-      launch_dist_mark(L, kin, nloc, words, d.A, d.C, default_grid(nloc, 256), s);
-    launch_dist_counts(d.A, d.C, pos_pad, d.cnt, default_grid(pos_pad / 32, 256), s);
-    NCCLCHECK(ncclReduceScatter(d.cnt, d.sum, S, ncclUint8, ncclSum, d.comm, s));
-    launch_dist_pack(d.sum, S, d.packed, default_grid(S / 64, 256), s);
-    NCCLCHECK(ncclAllGather(d.packed, c->bits + woff, S / 64, ncclUint64, d.comm, s));
-    HIPCHECK(hipMemsetAsync(d.counters, 0, 8, s));
-    if (nloc)
-      launch_dist_resolve(L, kin, iin, nloc, words, woff, c->bits, c->rkeys[L & 1], c->ridx[L & 1],
-                          d.counters, c->settle, default_grid(nloc, 256), s);
-    NCCLCHECK(ncclAllReduce(d.counters, d.counters + 1, 1, ncclUint64, ncclSum, d.comm, s));
-    HIPCHECK(hipMemcpyAsync(d.h_pinned, d.counters, 16, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    nloc = d.h_pinned[0];
-    const uint64_t next = d.h_pinned[1];
-    woff += words;
+    // ---- exchange: the received records become this level's list, list[(L-1)&1]
+    uint64_t acc = 0;
+    for (int t = 0; t < P; ++t) {
+      soff[t] = (uint64_t)t * C * sizeof(Rec);
+      sbytes[t] = M[(uint64_t)R * (P + 1) + t] * sizeof(Rec);
+      roff[t] = acc;
+      rbytes[t] = M[(uint64_t)t * (P + 1) + R] * sizeof(Rec);
+      acc += rbytes[t];
+    }
+    cm.alltoallv(d.send, soff.data(), sbytes.data(), c->list[(L - 1) & 1], roff.data(), rbytes.data(), s);
+    launch_set_u64(&st->n[L], m, s);
+    ev_mark(c, s, L == 0 ? "route0" : "route");
+    // ---- the owner's tile pipeline over positions [64 lo, 64 (lo + rw))
+    enqueue_list_level(c, b, L, m, 64 * rw, conservative, nullptr, s);
+    ev_mark(c, s, L == 0 ? "level0" : "levels");
+    // ---- size the next level from the global redo count (device side, no host sync)
+    cm.allreduce_u64(&st->n[L + 1], d.gslot + L + 1, 1, s);
+    src_pred = (double)m * q * 1.05 + 1024;
+    if (L + 1 >= kMaxDistLevels || (double)nL * q <= (double)c->dist_switch) break;
     ++L;
-    if (L == 1) ev_mark(c, s, "level0");
-    if (next == 0) break;
-    if (next >= nL && nL <= 64) {
-      // no progress on a tiny remainder: keep going until the level budget says stop
-    }
-    nL = next;
+    launch_dist_setup(st, L, d.gslot + L, 0, R, P, s);
   }
-  ev_mark(c, s, "levels");
-  hs.nlevels = L;
-  hs.woff[L] = woff;
-  // Ranks over all level words (identical on every rank).
-  d.h_pinned[2] = woff;
-  HIPCHECK(hipMemcpyAsync(d.counters + 4, d.h_pinned + 2, 8, hipMemcpyHostToDevice, s));
-  launch_words_scan(c->bits, woff, c->rank_base, c->block_sums, d.counters + 4, s);
-  c->rank_valid = true;
-  ev_mark(c, s, "rank_scan");
-
-  // Output exchange: (p, fp, pos) to the owner of p's range.
-  HIPCHECK(hipMemsetAsync(d.owner_counts, 0, 8 * P, s));
-  HIPCHECK(hipMemsetAsync(d.bucket_fill, 0, 8 * P, s));
-  if (n_local)
-    launch_dist_count_owners(n_local, c->settle, c->bits, c->rank_base, per_rank, P, d.owner_counts,
-                             grid, s);
-  NCCLCHECK(ncclAllGather(d.owner_counts, d.count_matrix, P, ncclUint64, d.comm, s));
-  HIPCHECK(hipMemcpyAsync(d.h_pinned + 8, d.count_matrix, 8ull * P * P, hipMemcpyDeviceToHost, s));
-  HIPCHECK(hipMemcpyAsync(d.h_pinned + 3, d.counters + 5, 8, hipMemcpyDeviceToHost, s));
+  const int Ls = L + 1;  // first replicated level
+  // ---- gather every rank's remaining records; all ranks finish the build identically
+  HIPCHECK(hipMemcpyAsync(d.small, &st->n[Ls], 8, hipMemcpyDeviceToDevice, s));
+  cm.allgather(d.small, d.small + 64, 8, s);
+  HIPCHECK(hipMemcpyAsync(M, d.small + 64, 8ull * P, hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
-  const unsigned long long* M = d.h_pinned + 8;  // M[src * P + dst]
-  if (d.h_pinned[3] != N) {
-    *msg = "build MPHF: internal error: ranked " + std::to_string(d.h_pinned[3]) + " of " + std::to_string(N);
-    return S3IMPH_ERR_INTERNAL;
+  uint64_t total = 0, maxc = 0;
+  std::vector<uint64_t> cnt(M, M + P);
+  for (int r = 0; r < P; ++r) {
+    total += cnt[r];
+    maxc = std::max(maxc, cnt[r]);
   }
-  std::vector<unsigned long long> soff(P), roff(P);
-  uint64_t acc = 0, racc = 0;
-  for (int q = 0; q < P; ++q) {
-    soff[q] = acc;
-    acc += M[(uint64_t)R * P + q];
-    roff[q] = racc;
-    racc += M[(uint64_t)q * P + R];
+  if (total > c->bucket_cap) {
+    *msg = "build MPHF: replicated level of " + std::to_string(total) + " records exceeds the workspace";
+    return S3IMPH_ERR_NOMEM;
   }
-  if (racc != *out_n) {
-    *msg = "build MPHF: internal error: received " + std::to_string(racc) + " of " + std::to_string(*out_n);
-    return S3IMPH_ERR_INTERNAL;
+  Rec* rl = c->list[(Ls - 1) & 1];
+  if (total) {
+    if ((uint64_t)P * maxc > d.cap_send) {
+      dalloc(d.send, (uint64_t)P * maxc);
+      d.cap_send = (uint64_t)P * maxc;
+    }
+    cm.allgather(rl, d.send, maxc * sizeof(Rec), s);
+    uint64_t o = 0;
+    for (int r = 0; r < P; ++r) {
+      if (cnt[r])
+        HIPCHECK(hipMemcpyAsync(rl + o, d.send + (uint64_t)r * maxc, cnt[r] * sizeof(Rec), hipMemcpyDeviceToDevice, s));
+      o += cnt[r];
+    }
   }
-  std::memcpy(d.h_pinned + 8 + (uint64_t)P * P, soff.data(), 8 * P);
-  HIPCHECK(hipMemcpyAsync(d.bucket_off, d.h_pinned + 8 + (uint64_t)P * P, 8 * P, hipMemcpyHostToDevice, s));
-  if (n_local)
-    launch_dist_place(n_local, c->settle, c->fp, pos, key_base, c->bits, c->rank_base, per_rank, P,
-                      d.bucket_fill, d.bucket_off, d.send, d.status, grid, s);
-  NCCLCHECK(ncclGroupStart());
-  for (int q = 0; q < P; ++q) {
-    const uint64_t sc = M[(uint64_t)R * P + q], rc = M[(uint64_t)q * P + R];
-    if (sc) NCCLCHECK(ncclSend(d.send + 3 * soff[q], 3 * sc, ncclUint64, q, d.comm, s));
-    if (rc) NCCLCHECK(ncclRecv(d.recv + 3 * roff[q], 3 * rc, ncclUint64, q, d.comm, s));
+  launch_dist_replicate(st, Ls, total, R == 0 ? 0 : (uint64_t)Ls, s);
+  ev_mark(c, s, "gather");
+  const LevelGeom gcons = choose_geom(std::max<uint64_t>(total, 1), c->target_tiles, c->target_chunks, kRegTileMaxBits);
+  enqueue_levels_from(c, b, Ls, total, gcons, conservative, s);
+  // ---- level bit vectors of the distributed levels: all-gather each rank's word range
+  uint64_t woff = 0;
+  for (int l = 0; l < Ls; ++l) {
+    cm.allgather(c->bits + woff + (uint64_t)R * hS[l], d.stage_bits, hS[l] * 8, s);
+    HIPCHECK(hipMemcpyAsync(c->bits + woff, d.stage_bits, hw[l] * 8, hipMemcpyDeviceToDevice, s));
+    woff += hw[l];
   }
-  NCCLCHECK(ncclGroupEnd());
-  if (racc)
-    launch_dist_unpack(d.recv, racc, *out_lo, *out_n, fp_out, pos_out, d.status,
-                       default_grid(racc, 256), s);
-  ev_mark(c, s, "exchange");
+  ev_mark(c, s, "bits");
   HIPCHECK(hipGetLastError());
-  HIPCHECK(hipMemcpyAsync(d.h_pinned + 4, d.status, 4, hipMemcpyDeviceToHost, s));
-  HIPCHECK(hipMemcpyAsync(c->d_st, c->h_st, sizeof(LevelState), hipMemcpyHostToDevice, s));
+  HIPCHECK(hipMemcpyAsync(c->h_st, st, sizeof(LevelState), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  // ---- per-rank level bases, totals and flags -> this rank's output segments
+  const LevelState& hs = *c->h_st;
+  const int K = Ls + 3;
+  for (int l = 0; l <= Ls; ++l) M[l] = hs.lvl_base[l];
+  M[Ls + 1] = hs.rank_total;
+  M[Ls + 2] = hs.status;
+  HIPCHECK(hipMemcpyAsync(d.small, M, 8ull * K, hipMemcpyHostToDevice, s));
+  cm.allgather(d.small, d.small + 64, 8ull * K, s);
+  HIPCHECK(hipMemcpyAsync(M, d.small + 64, 8ull * K * P, hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   ev_collect(c);
-  const unsigned flags = (unsigned)(d.h_pinned[4] & 0xffffffffu);
+  auto lb = [&](int r, int l) { return M[(uint64_t)r * K + l]; };
+  unsigned flags = 0;
+  for (int r = 0; r < P; ++r) flags |= (unsigned)lb(r, Ls + 2);
+  if (flags & (kStGeometry | kStTailOverflow | kStResOverflow)) return conservative ? S3IMPH_ERR_INTERNAL : kDistRetry;
+  if (flags & kStTooManyLevels) {
+    const unsigned nl = hs.nlevels;
+    const uint64_t rem = nl < (unsigned)kMaxLevels + 2 ? hs.n[nl] : 0;
+    if (records_have_duplicates(c->list[(nl - 1) & 1], rem)) {
+      *msg = "build MPHF: duplicate FNV-1a key hashes: bbhash cannot place them";
+      return S3IMPH_ERR_DUP_KEY_HASH;
+    }
+    *msg = "build MPHF: can't find minimal perfect hash after " + std::to_string(kMaxLevels) + " levels";
+    return S3IMPH_ERR_TOO_MANY_LEVELS;
+  }
   if (flags & kStKeyZero) {
     *msg = "MPHF Key(...) returned 0, possible hash collision with sentinel";
     return S3IMPH_ERR_KEY_HASH_ZERO;
   }
   if (flags) {
-    *msg = "build MPHF: internal error flags " + std::to_string(flags);
+    *msg = "build MPHF: internal error (device flags " + std::to_string(flags) + ")";
     return S3IMPH_ERR_INTERNAL;
   }
+  d.seg.clear();
+  uint64_t G = 0;
+  for (int l = 0; l < Ls; ++l) {
+    uint64_t before = 0, tot = 0;
+    for (int r = 0; r < P; ++r) {
+      const uint64_t cl = lb(r, l + 1) - lb(r, l);
+      if (r < R) before += cl;
+      tot += cl;
+    }
+    const uint64_t mine = lb(R, l + 1) - lb(R, l);
+    if (mine) d.seg.insert(d.seg.end(), {G + before, mine, lb(R, l)});
+    G += tot;
+  }
+  const uint64_t rep = lb(0, Ls + 1) - lb(0, Ls);  // replicated levels, written by rank 0
+  if (R == 0 && rep) d.seg.insert(d.seg.end(), {G, rep, lb(0, Ls)});
+  G += rep;
+  if (G != N) {
+    *msg = "build MPHF: internal error: ranked " + std::to_string(G) + " of " + std::to_string(N) + " keys";
+    return S3IMPH_ERR_INTERNAL;
+  }
+  d.out_n = R == 0 ? lb(0, Ls + 1) : lb(R, Ls);
   info->status = S3IMPH_OK;
-  info->num_levels = L;
-  info->total_words = woff;
-  info->mph_bin_len = 8 * kPartitions + 8 + 8ull * L + 8ull * woff;
-  info->big_levels = L;
+  info->num_levels = hs.nlevels;
+  info->total_words = hs.woff[hs.nlevels];
+  info->mph_bin_len = 8 * kPartitions + 8 + 8ull * hs.nlevels + 8ull * info->total_words;
+  info->big_levels = (uint64_t)Ls;
+  return S3IMPH_OK;
+}
+
+int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
+               uint64_t n_local, uint64_t key_base, uint64_t* fp_out, uint64_t* pos_out, uint64_t out_cap,
+               uint64_t* out_n, hipStream_t s, s3imph_build_info* info, std::string* msg) {
+  DistState& d = c->d;
+  c->have_build = false;
+  c->rank_valid = false;
+  *info = s3imph_build_info{};
+  *out_n = 0;
+  d.seg.clear();
+  d.out_n = 0;
+  if (n_local > kU32Limit) {
+    *msg = "build MPHF: more than 2^32-1 keys on one rank";
+    return S3IMPH_ERR_INVALID;
+  }
+  ensure_dist_small(c);
+  ev_begin(c);
+  ev_mark(c, s, "start");
+  // global key count (also a rendezvous: every rank must reach the same build)
+  d.h_pinned[0] = n_local;
+  HIPCHECK(hipMemcpyAsync(d.small, d.h_pinned, 8, hipMemcpyHostToDevice, s));
+  d.comm->allreduce_u64(d.small, d.small + 1, 1, s);
+  HIPCHECK(hipMemcpyAsync(d.h_pinned + 1, d.small + 1, 8, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  const uint64_t N = d.h_pinned[1];
+  info->n_keys = N;
+  if (N == 0) {
+    c->have_build = true;
+    c->last_n = 0;
+    c->info = *info;
+    ev_collect(c);
+    return S3IMPH_OK;
+  }
+  ensure_dist_workspace(c, n_local, N);
+  set_lds_attrs(c);
+  int rc = S3IMPH_OK;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    ev_begin(c);
+    ev_mark(c, s, "start");
+    rc = dist_attempt(c, blob, offsets, pos, n_local, key_base, N, fp_out, pos_out, out_cap, s, attempt > 0, info,
+                      msg);
+    if (rc != kDistRetry) break;
+  }
+  if (rc != S3IMPH_OK) return rc;
+  if (d.out_n > out_cap) {
+    *msg = "build MPHF: output capacity " + std::to_string(out_cap) + " < " + std::to_string(d.out_n) +
+           " (see s3imph_dist_out_cap)";
+    return S3IMPH_ERR_INVALID;
+  }
+  *out_n = d.out_n;
+  info->n_keys = N;
   c->have_build = true;
   c->last_n = N;
   c->info = *info;
@@ -871,6 +1092,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     if (const char* m = std::getenv("S3IMPH_TARGET_TILES_RES")) c->target_tiles_res = std::strtoull(m, nullptr, 10);
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     if (const char* m = std::getenv("S3IMPH_TILE_BLOCK")) c->tile_block = std::atoi(m);
+    if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);
     // A blocking stream: implicitly ordered with the legacy NULL stream, so work a
     // caller queued there (e.g. torch's default stream) completes before ours starts.
     HIPCHECK(hipStreamCreate(&c->own_stream));
@@ -897,7 +1119,8 @@ int s3imph_ctx_destroy(s3imph_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   free_workspace(c);
-  if (c->d.comm) (void)ncclCommDestroy(c->d.comm);
+  delete c->d.comm;
+  c->d.comm = nullptr;
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return S3IMPH_OK;
@@ -930,6 +1153,7 @@ int s3imph_build_device(s3imph_ctx* c, const uint8_t* d_blob, const uint64_t* d_
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
     int rc = c->dist ? S3IMPH_ERR_STATE
                      : build_single(c, d_blob, d_offsets, d_pos, n, d_fp_out, d_pos_out, s, info, &msg);
+    c->last_msg = msg;
     info->status = rc;
     return rc;
   } catch (const Fail& f) {
@@ -985,20 +1209,44 @@ int s3imph_dist_unique_id(uint8_t id_out[128]) {
 
 int s3imph_ctx_create_dist(int device, const uint8_t id[128], int rank, int nranks, s3imph_ctx** out,
                            char* err, size_t errlen) {
-  if (!id || !out || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks) return S3IMPH_ERR_INVALID;
+  if (!id || !out || nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks) return S3IMPH_ERR_INVALID;
   int rc = s3imph_ctx_create(device, out, err, errlen);
   if (rc != S3IMPH_OK) return rc;
   s3imph_ctx* c = *out;
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
-  ncclResult_t r = ncclCommInitRank(&c->d.comm, nranks, uid, rank);
+  RcclComm* rc_comm = new RcclComm();
+  ncclResult_t r = ncclCommInitRank(&rc_comm->comm, nranks, uid, rank);
   if (r != ncclSuccess) {
     set_err(err, errlen, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    delete rc_comm;
     s3imph_ctx_destroy(c);
     *out = nullptr;
     return S3IMPH_ERR_RCCL;
   }
+  rc_comm->rank = rank;
+  rc_comm->nranks = nranks;
   c->dist = true;
+  c->d.comm = rc_comm;
+  c->d.rank = rank;
+  c->d.nranks = nranks;
+  return S3IMPH_OK;
+}
+
+int s3imph_ctx_create_dist_host(int device, const s3imph_host_comm* comm, int rank, int nranks, s3imph_ctx** out,
+                                char* err, size_t errlen) {
+  if (!comm || !comm->allgather || !comm->alltoallv || !out || nranks < 1 || nranks > kMaxRanks || rank < 0 ||
+      rank >= nranks)
+    return S3IMPH_ERR_INVALID;
+  int rc = s3imph_ctx_create(device, out, err, errlen);
+  if (rc != S3IMPH_OK) return rc;
+  s3imph_ctx* c = *out;
+  HostComm* hc = new HostComm();
+  hc->cb = *comm;
+  hc->rank = rank;
+  hc->nranks = nranks;
+  c->dist = true;
+  c->d.comm = hc;
   c->d.rank = rank;
   c->d.nranks = nranks;
   return S3IMPH_OK;
@@ -1006,19 +1254,21 @@ int s3imph_ctx_create_dist(int device, const uint8_t id[128], int rank, int nran
 
 int s3imph_build_device_dist(s3imph_ctx* c, const uint8_t* d_blob, const uint64_t* d_offsets,
                              const uint64_t* d_pos, uint64_t n_local, uint64_t key_base,
-                             uint64_t* d_fp_out, uint64_t* d_pos_out, uint64_t out_cap, uint64_t* out_lo,
-                             uint64_t* out_n, void* stream, s3imph_build_info* info) {
-  if (!c || !c->dist || !info || !out_lo || !out_n) return S3IMPH_ERR_INVALID;
+                             uint64_t* d_fp_out, uint64_t* d_pos_out, uint64_t out_cap, uint64_t* out_n,
+                             void* stream, s3imph_build_info* info) {
+  if (!c || !c->dist || !info || !out_n || (n_local && (!d_blob || !d_offsets))) return S3IMPH_ERR_INVALID;
   std::lock_guard<std::mutex> lk(c->mu);
   std::string msg;
   try {
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
-    int rc = build_dist(c, d_blob, d_offsets, d_pos, n_local, key_base, d_fp_out, d_pos_out, out_cap, out_lo,
-                        out_n, s, info, &msg);
+    int rc = build_dist(c, d_blob, d_offsets, d_pos, n_local, key_base, d_fp_out, d_pos_out, out_cap, out_n, s,
+                        info, &msg);
+    c->last_msg = msg;
     info->status = rc;
     return rc;
   } catch (const Fail& f) {
+    c->last_msg = f.msg;
     info->status = f.code;
     return f.code;
   } catch (const std::bad_alloc&) {
@@ -1026,6 +1276,23 @@ int s3imph_build_device_dist(s3imph_ctx* c, const uint8_t* d_blob, const uint64_
     return S3IMPH_ERR_NOMEM;
   }
 }
+
+int s3imph_dist_segments(s3imph_ctx* c, uint64_t* seg, uint64_t cap, uint64_t* count) {
+  if (!c || !c->dist || !count) return S3IMPH_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const uint64_t n = c->d.seg.size() / 3;
+  *count = n;
+  if (!c->have_build) return S3IMPH_ERR_STATE;
+  if (seg && cap) std::memcpy(seg, c->d.seg.data(), 8 * 3 * std::min(n, cap));
+  return cap >= n || !seg ? S3IMPH_OK : S3IMPH_ERR_INVALID;
+}
+
+uint64_t s3imph_dist_out_cap(s3imph_ctx* c, uint64_t n_global) {
+  if (!c || !c->dist) return n_global;
+  return dist_out_cap(c, n_global);
+}
+
+const char* s3imph_ctx_last_error(s3imph_ctx* c) { return c ? c->last_msg.c_str() : ""; }
 
 int s3imph_lookup_device(s3imph_ctx* c, const uint8_t* d_blob, const uint64_t* d_offsets, uint64_t n,
                          const uint64_t* d_fp, const uint64_t* d_pos, uint64_t count, uint64_t* d_result,

@@ -111,15 +111,5 @@ static __device__ __forceinline__ void fnv_both(const uint8_t* __restrict__ blob
   hb = b;
 }
 
-static __device__ __forceinline__ bool test_bit32(const uint32_t* v, uint64_t x) {
-  return (v[x >> 5] >> (x & 31)) & 1u;
-}
-
-static __device__ __forceinline__ void mark_bit(uint32_t* A, uint32_t* C, uint64_t x) {
-  const uint32_t bit = 1u << (x & 31);
-  const uint32_t old = atomicOr(&A[x >> 5], bit);
-  if (old & bit) atomicOr(&C[x >> 5], bit);
-}
-
 
 }  // namespace s3imph

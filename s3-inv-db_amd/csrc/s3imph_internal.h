@@ -30,7 +30,36 @@ struct LevelState {
   unsigned long long nchunks[kMaxLevels + 2];   // key chunks of level L (count/scatter blocks)
   unsigned long long ticket[kMaxLevels + 2];    // tile tickets (look-back order)
   unsigned long long sticket[kMaxLevels + 2];   // histogram-scan segment tickets
+  // Output bound and gating.  out_cap: fp_out/pos_out entries (= n on one GPU);
+  // out_skip_from != 0 disables output writes of levels >= out_skip_from (the
+  // replicated tail levels of a multi-GPU build run on every rank, written by rank 0).
+  unsigned long long out_cap;
+  unsigned long long out_skip_from;
+  // Multi-GPU position-range ownership (s3imph_dist.hip).  A level with preset[L] != 0
+  // was sized by the host/collectives: words[L] is the GLOBAL level size, n[L] the
+  // records this rank received, and this rank owns words [wlo[L], wlo[L] + rw[L]).
+  // Levels with preset[L] == 0 cover the whole level (plo = 0, rw = words).
+  unsigned long long preset[kMaxLevels + 2];
+  unsigned long long wlo[kMaxLevels + 2];
+  unsigned long long rw[kMaxLevels + 2];
+  unsigned long long dS[kMaxLevels + 2];       // words per rank range (owner = word / dS)
+  unsigned long long dmagic[kMaxLevels + 2];   // Barrett reciprocal of dS
+  unsigned long long gn[kMaxLevels + 2];       // global key count of level L
 };
+
+#if defined(__HIPCC__)
+// Position range [plo, plo + 64 rw) of level L handled by this GPU.
+struct LevelRange {
+  uint64_t plo, rw;
+};
+__device__ __forceinline__ LevelRange level_range(const LevelState* st, int L, uint64_t words) {
+  if (st->preset[L]) return {64 * st->wlo[L], st->rw[L]};
+  return {0, words};
+}
+__device__ __forceinline__ bool level_out_on(const LevelState* st, int L) {
+  return !(st->out_skip_from && (unsigned long long)L >= st->out_skip_from);
+}
+#endif
 
 // Binned pipeline geometry.  A level of `size` positions is cut into tiles of 2^tb
 // positions (one workgroup each, A/C in LDS); keys are counted and scattered into
@@ -66,9 +95,10 @@ constexpr int kResShards = 8;                 // per-tile reservation counters (
 constexpr int kResLevels = 32;                // levels that may use the reservation path
 constexpr double kTailMargin = 1.1;
 constexpr uint64_t kTargetChunks = 768;  // 3 resident 1024-thread count blocks x 256 CUs
-inline LevelGeom choose_geom(uint64_t n, uint64_t target_tiles = kTargetTiles,
-                             uint64_t target_chunks = kTargetChunks, unsigned max_tb = kTileMaxBits) {
-  const uint64_t size = 64 * level_words(n ? n : 1);
+// n records over `size` positions (64 * level_words(n) for a whole level).
+inline LevelGeom choose_geom_sz(uint64_t n, uint64_t size, uint64_t target_tiles = kTargetTiles,
+                                uint64_t target_chunks = kTargetChunks, unsigned max_tb = kTileMaxBits) {
+  if (size == 0) size = 64;
   unsigned tb = kTileMinBits;
   while (tb < max_tb && (size >> tb) > target_tiles) ++tb;
   while (tb < kTileMaxBits && ((size + (1ull << tb) - 1) >> tb) > kMaxTiles) ++tb;  // workspace bound
@@ -78,12 +108,17 @@ inline LevelGeom choose_geom(uint64_t n, uint64_t target_tiles = kTargetTiles,
   while (((n + chunk - 1) / chunk) * T > kHistCap) chunk *= 2;
   return {tb, chunk};
 }
+inline LevelGeom choose_geom(uint64_t n, uint64_t target_tiles = kTargetTiles,
+                             uint64_t target_chunks = kTargetChunks, unsigned max_tb = kTileMaxBits) {
+  return choose_geom_sz(n, 64 * level_words(n ? n : 1), target_tiles, target_chunks, max_tb);
+}
 
 // Device status flags.
 constexpr unsigned kStKeyZero = 1u;       // some FNV-1a key hash == 0
 constexpr unsigned kStTooManyLevels = 2u;  // level budget exhausted (duplicates)
 constexpr unsigned kStOverflow = 4u;       // workspace capacity exceeded
 constexpr unsigned kStRank = 8u;           // a position landed outside [0, N)
+constexpr unsigned kStRouteOverflow = 256u;  // a multi-GPU send region overflowed (rerun bigger)
 
 // Levels whose active-key count is at most this run inside one workgroup with
 // LDS-resident bit vectors (k_tail); larger levels run as full-grid kernels.
@@ -94,41 +129,13 @@ constexpr int kTailLdsWords32 = 2 * 2 * ((kGammaNum * kTailKeys + 63) / 64);  //
 struct KernelArgs;  // fwd
 
 // ---- launchers (s3imph_kernels.hip) -------------------------------------------
-void launch_init_state(LevelState* st, uint64_t n, uint64_t key_base, hipStream_t s);
+void launch_init_state(LevelState* st, uint64_t n, uint64_t out_cap, hipStream_t s);
 void launch_rank_scan(const uint64_t* bits, uint64_t cap_words, uint64_t* rank_base,
                       unsigned long long* block_sums, uint64_t max_blocks, LevelState* st,
                       hipStream_t s);
 void launch_lookup(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const uint64_t* bits,
                    const uint64_t* rank_base, const LevelState* st, const uint64_t* fp,
                    const uint64_t* pos, uint64_t count, uint64_t* result, int grid, hipStream_t s);
-
-// Distributed (per-level count exchange) kernels.
-void launch_dist_mark(int level, const uint64_t* keys, uint64_t n_local, uint64_t words,
-                      uint32_t* A, uint32_t* C, int grid, hipStream_t s);
-void launch_dist_hash_mark0(const uint8_t* blob, const uint64_t* offsets, uint64_t n,
-                            uint64_t* kh, uint64_t* fp, uint64_t words0, uint32_t* A, uint32_t* C,
-                            unsigned* status, int grid, hipStream_t s);
-void launch_dist_counts(const uint32_t* A, const uint32_t* C, uint64_t positions, uint8_t* cnt,
-                        int grid, hipStream_t s);
-void launch_dist_pack(const uint8_t* sum, uint64_t positions, uint64_t* words_out, int grid,
-                      hipStream_t s);
-void launch_dist_resolve(int level, const uint64_t* keys_in, const uint32_t* idx_in, uint64_t n_local,
-                         uint64_t words, uint64_t woff, const uint64_t* bits, uint64_t* keys_out,
-                         uint32_t* idx_out, unsigned long long* out_count, uint64_t* settle,
-                         int grid, hipStream_t s);
-void launch_dist_place(uint64_t n, const uint64_t* settle, const uint64_t* fp, const uint64_t* pos,
-                       uint64_t pos_base, const uint64_t* bits, const uint64_t* rank_base,
-                       uint64_t per_rank, int nranks, unsigned long long* bucket_fill,
-                       const unsigned long long* bucket_off, uint64_t* triples, unsigned* status,
-                       int grid, hipStream_t s);
-void launch_dist_count_owners(uint64_t n, const uint64_t* settle, const uint64_t* bits,
-                              const uint64_t* rank_base, uint64_t per_rank, int nranks,
-                              unsigned long long* counts, int grid, hipStream_t s);
-void launch_dist_unpack(const uint64_t* triples, uint64_t count, uint64_t lo, uint64_t out_n,
-                        uint64_t* fp_out, uint64_t* pos_out, unsigned* status, int grid,
-                        hipStream_t s);
-void launch_words_scan(const uint64_t* bits, uint64_t words, uint64_t* rank_base,
-                       unsigned long long* block_sums, unsigned long long* total, hipStream_t s);
 
 int default_grid(uint64_t work, int block);
 
@@ -160,6 +167,7 @@ struct BinBuffers {
   uint64_t* fp_out;
   uint64_t* pos_out;
   LevelState* st;
+  bool dist;                            // multi-GPU owner levels: level 0 reads list[1] too
 };
 void binned_set_lds_limits();
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
@@ -169,7 +177,19 @@ void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStrea
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s,
                         bool reserved = false);
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s);
-void launch_binned_tail(int big_launched, const BinBuffers& b, hipStream_t s);
+void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s);
+
+// ---- multi-GPU launchers (s3imph_dist.hip) ------------------------------------------
+constexpr int kMaxRanks = 64;
+void launch_route0(const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t pos_base, uint64_t n,
+                   Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, hipStream_t s);
+void launch_route(int level, const Rec* list, uint64_t n_pred, Rec* send, uint64_t cap, unsigned long long* scnt,
+                  LevelState* st, int P, hipStream_t s);
+void launch_dist_setup(LevelState* st, int L, const unsigned long long* gcount, uint64_t n_value, int rank, int P,
+                       hipStream_t s);
+void launch_set_u64(unsigned long long* p, uint64_t v, hipStream_t s);
+void launch_route_flag(LevelState* st, unsigned long long* scnt, int P, hipStream_t s);
+void launch_dist_replicate(LevelState* st, int L, uint64_t n_all, uint64_t skip_from, hipStream_t s);
 
 // ---- host helpers (s3imph_host.cpp) -------------------------------------------
 void set_err(char* err, size_t errlen, const std::string& msg);

@@ -53,7 +53,8 @@ EXPORTS = (
     "s3imph_build_host", "s3imph_free", "s3imph_write_index_files",
     "s3imph_ctx_create", "s3imph_ctx_destroy", "s3imph_ctx_reserve", "s3imph_build_device",
     "s3imph_ctx_mph_bin", "s3imph_ctx_set_profiling", "s3imph_ctx_stage_times",
-    "s3imph_dist_unique_id", "s3imph_ctx_create_dist", "s3imph_build_device_dist",
+    "s3imph_dist_unique_id", "s3imph_ctx_create_dist", "s3imph_ctx_create_dist_host", "s3imph_build_device_dist",
+    "s3imph_dist_segments", "s3imph_dist_out_cap", "s3imph_ctx_last_error",
     "s3imph_lookup_device", "s3imph_gen_keys",
 )
 
@@ -64,6 +65,17 @@ class MPHFError(RuntimeError):
     def __init__(self, status: int, msg: str):
         super().__init__(msg)
         self.status = status
+
+
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                ctypes.POINTER(ctypes.c_uint64))
+
+
+class HostComm(ctypes.Structure):
+    """s3imph_host_comm: host-callback collectives (include/s3imph.h, section 4)."""
+    _fields_ = [("user", ctypes.c_void_p), ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN)]
 
 
 class BuildInfo(ctypes.Structure):
@@ -108,8 +120,11 @@ def _load():
         "s3imph_ctx_stage_times": (i32, [vp, P(ctypes.c_float), i32, P(i32), cp, sz]),
         "s3imph_dist_unique_id": (i32, [vp]),
         "s3imph_ctx_create_dist": (i32, [i32, vp, i32, i32, P(vp), cp, sz]),
-        "s3imph_build_device_dist": (i32, [vp, vp, vp, vp, u64, u64, vp, vp, u64, P(u64), P(u64), vp,
-                                           P(BuildInfo)]),
+        "s3imph_ctx_create_dist_host": (i32, [i32, P(HostComm), i32, i32, P(vp), cp, sz]),
+        "s3imph_build_device_dist": (i32, [vp, vp, vp, vp, u64, u64, vp, vp, u64, P(u64), vp, P(BuildInfo)]),
+        "s3imph_dist_segments": (i32, [vp, P(u64), u64, P(u64)]),
+        "s3imph_dist_out_cap": (u64, [vp, u64]),
+        "s3imph_ctx_last_error": (cp, [vp]),
         "s3imph_lookup_device": (i32, [vp, vp, vp, u64, vp, vp, u64, vp, vp]),
         "s3imph_gen_keys": (i32, [i32, u64, ctypes.c_uint32, u64, u64, vp, vp, P(u64)]),
     }
@@ -278,12 +293,16 @@ class DeviceBuilder:
         keys = names.value.decode().split(",") if cnt.value else []
         return {k: ms[i] for i, k in enumerate(keys)}
 
+    def last_error(self) -> str:
+        return LIB.s3imph_ctx_last_error(self._h).decode(errors="replace")
+
     def build(self, d_blob, d_offsets, n: int, d_fp_out, d_pos_out, d_pos=None, stream=None) -> dict:
         info = BuildInfo()
         rc = LIB.s3imph_build_device(self._h, _dev_ptr(d_blob), _dev_ptr(d_offsets), _dev_ptr(d_pos), n,
                                      _dev_ptr(d_fp_out), _dev_ptr(d_pos_out), _stream_ptr(stream),
                                      ctypes.byref(info))
-        _check(rc, None, "build MPHF")
+        if rc != OK:
+            raise MPHFError(rc, f"build MPHF: {self.last_error() or status_string(rc)}")
         self.last_info = info.as_dict()
         return self.last_info
 
@@ -318,29 +337,109 @@ def dist_unique_id() -> bytes:
 
 
 class DistBuilder(DeviceBuilder):
-    """One rank of a multi-GPU build (RCCL communicator owned by the library)."""
+    """One rank of a multi-GPU build.  Collectives: RCCL (the library owns the
+    communicator; `unique_id` from rank 0's dist_unique_id()), or, with `host_comm`,
+    the given torch.distributed process group on host copies (test transport:
+    several ranks may share one GPU)."""
 
-    def __init__(self, device: int, unique_id: bytes, rank: int, nranks: int):
+    def __init__(self, device: int, unique_id: bytes | None, rank: int, nranks: int, host_comm=None):
         err = ctypes.create_string_buffer(512)
         h = ctypes.c_void_p()
-        idbuf = ctypes.create_string_buffer(unique_id, 128)
-        _check(LIB.s3imph_ctx_create_dist(device, idbuf, rank, nranks, ctypes.byref(h), err, 512), err)
+        if host_comm is None:
+            idbuf = ctypes.create_string_buffer(unique_id, 128)
+            _check(LIB.s3imph_ctx_create_dist(device, idbuf, rank, nranks, ctypes.byref(h), err, 512), err)
+        else:
+            self._comm = _TorchHostComm(None if host_comm is True else host_comm, nranks)
+            _check(LIB.s3imph_ctx_create_dist_host(device, ctypes.byref(self._comm.cstruct), rank, nranks,
+                                                   ctypes.byref(h), err, 512), err)
         self._h = h
         self.device = device
         self.rank, self.nranks = rank, nranks
         self.last_info = None
 
+    def out_cap(self, n_global: int) -> int:
+        return LIB.s3imph_dist_out_cap(self._h, n_global)
+
+    def segments(self) -> list[tuple[int, int, int]]:
+        """(global p, count, local offset) of this rank's outputs in the last build."""
+        cnt = ctypes.c_uint64()
+        LIB.s3imph_dist_segments(self._h, None, 0, ctypes.byref(cnt))
+        buf = (ctypes.c_uint64 * max(3 * cnt.value, 1))()
+        _check(LIB.s3imph_dist_segments(self._h, buf, cnt.value, ctypes.byref(cnt)), None, "segments")
+        return [(buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i in range(cnt.value)]
+
     def build_shard(self, d_blob, d_offsets, n_local: int, key_base: int, d_fp_out, d_pos_out, out_cap: int,
-                    d_pos=None, stream=None) -> tuple[int, int, dict]:
+                    d_pos=None, stream=None) -> tuple[int, list, dict]:
+        """Build this rank's share; returns (local outputs, segments, info)."""
         info = BuildInfo()
-        lo, cnt = ctypes.c_uint64(), ctypes.c_uint64()
+        cnt = ctypes.c_uint64()
         rc = LIB.s3imph_build_device_dist(self._h, _dev_ptr(d_blob), _dev_ptr(d_offsets), _dev_ptr(d_pos),
                                           n_local, key_base, _dev_ptr(d_fp_out), _dev_ptr(d_pos_out), out_cap,
-                                          ctypes.byref(lo), ctypes.byref(cnt), _stream_ptr(stream),
-                                          ctypes.byref(info))
-        _check(rc, None, "build MPHF (dist)")
+                                          ctypes.byref(cnt), _stream_ptr(stream), ctypes.byref(info))
+        if rc != OK:
+            raise MPHFError(rc, f"build MPHF (dist): {self.last_error() or status_string(rc)}")
         self.last_info = info.as_dict()
-        return lo.value, cnt.value, self.last_info
+        return cnt.value, self.segments(), self.last_info
+
+
+class _TorchHostComm:
+    """s3imph_host_comm over a torch.distributed process group (gloo), CPU tensors."""
+
+    def __init__(self, group, nranks: int):
+        import torch.distributed as tdist
+        self.group, self.nranks, self.dist = group, nranks, tdist
+        self.cstruct = HostComm(None, ALLGATHER_FN(self._allgather), ALLTOALLV_FN(self._alltoallv))
+
+    def _allgather(self, _user, send, recv, nbytes):
+        try:
+            src = torch.frombuffer((ctypes.c_uint8 * max(nbytes, 1)).from_address(send), dtype=torch.uint8)[:nbytes]
+            out = torch.empty(nbytes * self.nranks, dtype=torch.uint8)
+            self.dist.all_gather_into_tensor(out, src.clone(), group=self.group)
+            if nbytes:
+                ctypes.memmove(recv, out.data_ptr(), nbytes * self.nranks)
+            return 0
+        except Exception:  # noqa: BLE001 - reported to the library as a failed collective
+            import traceback
+            traceback.print_exc()
+            return 1
+
+    def _alltoallv(self, _user, send, soff, sbytes, recv, roff, rbytes):
+        try:
+            P = self.nranks
+            sb = [sbytes[q] for q in range(P)]
+            rb = [rbytes[q] for q in range(P)]
+            st, rt = sum(sb), sum(rb)
+            src = torch.empty(st, dtype=torch.uint8)
+            for q in range(P):
+                if sb[q]:
+                    ctypes.memmove(src.data_ptr() + sum(sb[:q]), send + soff[q], sb[q])
+            out = torch.empty(rt, dtype=torch.uint8)
+            self.dist.all_to_all_single(out, src, rb, sb, group=self.group)
+            for q in range(P):
+                if rb[q]:
+                    ctypes.memmove(recv + roff[q], out.data_ptr() + sum(rb[:q]), rb[q])
+            return 0
+        except Exception:  # noqa: BLE001
+            import traceback
+            traceback.print_exc()
+            return 1
+
+
+def assemble_dist(parts: list, n_global: int) -> tuple[np.ndarray, np.ndarray]:
+    """Global (mph_fp, mph_pos) from every rank's (local fp, local pos, segments)."""
+    fp = np.zeros(n_global, np.uint64)
+    po = np.zeros(n_global, np.uint64)
+    seen = np.zeros(n_global, bool)
+    for lfp, lpo, segs in parts:
+        for p0, cnt, off in segs:
+            if seen[p0:p0 + cnt].any():
+                raise ValueError("overlapping output segments")
+            seen[p0:p0 + cnt] = True
+            fp[p0:p0 + cnt] = lfp[off:off + cnt]
+            po[p0:p0 + cnt] = lpo[off:off + cnt]
+    if not seen.all():
+        raise ValueError("output segments do not cover [0, N)")
+    return fp, po
 
 
 def _stream_ptr(stream):
@@ -375,15 +474,3 @@ class ShardPlan:
     @property
     def n_local(self) -> int:
         return self.hi - self.lo
-
-    @property
-    def out_per_rank(self) -> int:
-        return (self.n_global + self.nranks - 1) // self.nranks
-
-    @property
-    def out_lo(self) -> int:
-        return min(self.rank * self.out_per_rank, self.n_global)
-
-    @property
-    def out_n(self) -> int:
-        return min(self.out_per_rank, self.n_global - self.out_lo)

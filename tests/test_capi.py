@@ -126,4 +126,3 @@ def test_shard_plan_covers_everything():
             plans = [s3imph.ShardPlan(r, p, n) for r in range(p)]
             assert sum(x.n_local for x in plans) == n
             assert all(plans[r].hi == plans[r + 1].lo for r in range(p - 1))
-            assert sum(x.out_n for x in plans) == n

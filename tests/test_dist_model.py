@@ -1,17 +1,22 @@
-"""World-size-2 gloo test (CPU) of the multi-GPU decomposition used by
-s3imph_build_device_dist (s3-inv-db_amd/csrc/s3imph_build.hip, build_dist):
+"""World-size 2/3 gloo test (CPU) of the multi-GPU decomposition used by
+s3imph_build_device_dist (s3-inv-db_amd/csrc/s3imph_dist.hip, s3imph_build.hip:
+dist_attempt):
 
-  per level: each rank marks its own keys into full-size local A/C bit vectors ->
-  one saturating count byte per position (0, 1, 2+) -> cross-rank SUM (RCCL
-  reduce-scatter on the GPU; gloo all-reduce here) -> final bit = (sum == 1), padded
-  to 64*P positions and sliced per rank -> each rank settles keys whose bit is set,
-  the rest form its next-level set; level sizes from the summed redo counts.
-  After the levels: (p, fp, pos) go to the rank owning p's range (ShardPlan.out_*).
+  level L (global n_L keys, words_L = ceil(2 n_L / 64)): rank r owns words
+  [r*S, min((r+1)*S, words_L)), S = ceil(words_L / P).  Every rank routes its active
+  records (k, f, pos) to the owner of their level-L position (all-to-all); the owner
+  marks A/C over its range, settles keys at positions hit exactly once, numbers them
+  in position order into consecutive LOCAL output slots, and keeps the collided ones
+  for the next level.  While n_L * (1 - e^-1/2) > switch the next level is routed
+  again; then every rank all-gathers the remaining records and finishes the build
+  identically, rank 0 writing those outputs.  Each (level, rank) is one output segment
+  whose global start is a prefix sum over (level, rank) settled counts.
 
 The per-rank arithmetic is a numpy restatement of the kernels; the cross-rank
-exchange is real torch.distributed traffic.  The result must equal the oracle's
-single-process build byte for byte, whatever the number of ranks.
+exchange is real torch.distributed traffic.  The assembled result must equal the
+oracle's single-process build byte for byte, whatever the number of ranks.
 """
+import math
 import os
 import socket
 
@@ -20,7 +25,7 @@ import pytest
 
 import oracle as O
 
-M64 = (1 << 64) - 1
+Q = 1.0 - math.exp(-0.5)
 
 
 def _mix(h):
@@ -33,7 +38,7 @@ def _positions(level, keys, words):
     with np.errstate(over="ignore"):
         seed = _mix(np.uint64(level)) * np.uint64(O.HASH_M)
         h = _mix((seed ^ _mix(keys.astype(np.uint64))) * np.uint64(O.HASH_M))
-    return (h % np.uint64(64 * words)).astype(np.uint64)
+    return (h % np.uint64(64 * words)).astype(np.int64)
 
 
 def _free_port():
@@ -44,13 +49,25 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, blob, offs, result_q):
+def _settle(level, k, f, p, words, plo, prange):
+    """One owner's level over positions [plo, plo + prange): A/C marking, final bits,
+    in-range ranks.  Returns (bits of the range, settled (f, p) in rank order, redo)."""
+    x = _positions(level, k, words) - plo
+    assert ((x >= 0) & (x < prange)).all()
+    cnt = np.bincount(x, minlength=prange)
+    final = cnt == 1
+    ok = final[x]
+    order = np.argsort(x[ok], kind="stable")
+    return final, (f[ok][order], p[ok][order]), (k[~ok], f[~ok], p[~ok])
+
+
+def _rank_main(rank, world, port, blob, offs, switch, result_q):
     import torch
     import torch.distributed as dist
     import sys
-    for p in (os.path.join(os.path.dirname(__file__), "..", "s3-inv-db_amd"),
+    for d in (os.path.join(os.path.dirname(__file__), "..", "s3-inv-db_amd"),
               os.path.join(os.path.dirname(__file__), "..", "oracle")):
-        sys.path.insert(0, p)
+        sys.path.insert(0, d)
     import oracle as Orc
     from s3imph import ShardPlan
 
@@ -58,79 +75,101 @@ def _rank_main(rank, world, port, blob, offs, result_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n_global = len(offs) - 1
     plan = ShardPlan(rank, world, n_global)
-    lo, hi = plan.lo, plan.hi
     kh, fp = Orc.lib().hash_keys(blob, offs)
-    kh, fp = kh[lo:hi], fp[lo:hi]
-    idx = np.arange(hi - lo, dtype=np.int64)
-    settle = np.zeros(hi - lo, np.uint64)
-    nL, woff, levels = n_global, 0, []
-    keys = kh.copy()
-    level = 0
+    k, f = kh[plan.lo:plan.hi], fp[plan.lo:plan.hi]
+    p = np.arange(plan.lo, plan.hi, dtype=np.uint64)
+    out_f, out_p, segs_local, level_bits = [], [], [], []
+    local_base = 0
+    nL, level = n_global, 0
     while True:
         words = (2 * nL + 63) // 64
-        pos_pad = -(-64 * words // (64 * world)) * (64 * world)
-        x = _positions(level, keys, words).astype(np.int64)
-        cnt = np.bincount(x, minlength=pos_pad).astype(np.int64)
-        lanes = torch.from_numpy(np.minimum(cnt, 2).astype(np.uint8))   # k_dist_counts
-        dist.all_reduce(lanes)                                           # RCCL reduce-scatter (+ slice)
-        total = lanes.numpy().astype(np.int64)
-        S = pos_pad // world
-        mine = (total[rank * S:(rank + 1) * S] == 1)                     # k_dist_pack on the slice
-        gathered = [torch.zeros(S, dtype=torch.uint8) for _ in range(world)]
-        dist.all_gather(gathered, torch.from_numpy(mine.astype(np.uint8)))  # ncclAllGather
-        final = np.concatenate([g.numpy() for g in gathered]).astype(bool)[: 64 * words]
-        ok = final[x]                                                    # k_dist_resolve
-        settle[idx[ok]] = np.uint64(woff * 64) + x[ok].astype(np.uint64)
-        keys, idx = keys[~ok], idx[~ok]
-        nxt = torch.tensor([len(keys)], dtype=torch.int64)
+        S = -(-words // world)
+        lo, hi = min(rank * S, words), min((rank + 1) * S, words)
+        # route: records to the owner of their position (k_route + all-to-all)
+        owner = _positions(level, k, words) // 64 // S
+        send = [np.stack([k[owner == q], f[owner == q], p[owner == q]]) for q in range(world)]
+        counts = torch.tensor([s.shape[1] for s in send], dtype=torch.int64)
+        allc = [torch.zeros(world, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(allc, counts)
+        recv = [None] * world
+        reqs = []
+        for q in range(world):
+            if q == rank:
+                recv[q] = torch.from_numpy(send[q].view(np.int64).copy())
+                continue
+            recv[q] = torch.zeros((3, int(allc[q][rank])), dtype=torch.int64)
+            reqs.append(dist.isend(torch.from_numpy(send[q].view(np.int64).copy()), q))
+            reqs.append(dist.irecv(recv[q], q))
+        for r in reqs:
+            r.wait()
+        mine = np.concatenate([r.numpy().view(np.uint64) for r in recv], axis=1)
+        final, (sf, sp), (k, f, p) = _settle(level, mine[0], mine[1], mine[2], words, 64 * lo, 64 * (hi - lo))
+        segs_local.append((level, len(sf), local_base))
+        out_f.append(sf)
+        out_p.append(sp)
+        local_base += len(sf)
+        level_bits.append((words, S, final))
+        nxt = torch.tensor([len(k)], dtype=torch.int64)
         dist.all_reduce(nxt)
-        bits = np.packbits(final, bitorder="little").view(np.uint64)
-        levels.append(bits)
-        woff += words
-        level += 1
-        if int(nxt.item()) == 0:
+        if nL * Q <= switch:
             break
         nL = int(nxt.item())
-    allbits = np.concatenate(levels)
-    pc = np.array([bin(int(w)).count("1") for w in allbits], np.uint64)
-    rank_base = np.concatenate([[0], np.cumsum(pc)[:-1]]).astype(np.uint64)
-    w = (settle >> np.uint64(6)).astype(np.int64)
-    below = (np.uint64(1) << (settle & np.uint64(63))) - np.uint64(1)
-    p = rank_base[w] + np.array([bin(int(v)).count("1") for v in (allbits[w] & below)], np.uint64)
-    # owner exchange (ncclSend/Recv of (p, fp, pos) triples)
-    per = plan.out_per_rank
-    owner = np.minimum(p // np.uint64(per), world - 1).astype(np.int64)
-    send = [torch.from_numpy(np.stack([p[owner == q], fp[owner == q],
-                                       (np.arange(lo, hi, dtype=np.uint64))[owner == q]]).view(np.int64).copy())
-            for q in range(world)]
-    counts = torch.tensor([s.shape[1] for s in send], dtype=torch.int64)
-    allc = [torch.zeros(world, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(allc, counts)
-    recv = [torch.zeros((3, int(allc[q][rank])), dtype=torch.int64) for q in range(world)]
-    reqs = []
-    for q in range(world):
-        if q == rank:
-            recv[q] = send[q]
-            continue
-        reqs.append(dist.isend(send[q], q))
-        reqs.append(dist.irecv(recv[q], q))
-    for r in reqs:
-        r.wait()
-    trip = np.concatenate([r.numpy().view(np.uint64) for r in recv], axis=1)
-    fp_slice = np.zeros(plan.out_n, np.uint64)
-    pos_slice = np.zeros(plan.out_n, np.uint64)
-    rel = (trip[0] - np.uint64(plan.out_lo)).astype(np.int64)
-    fp_slice[rel] = trip[1]
-    pos_slice[rel] = trip[2]
-    mph = np.uint64(1).tobytes() + np.uint64(len(levels)).tobytes() + b"".join(
-        np.uint64(len(b)).tobytes() + b.tobytes() for b in levels)
-    result_q.put((rank, plan.out_lo, fp_slice, pos_slice, mph))
+        level += 1
+    Ls = level + 1
+    # replicated tail: all-gather the remaining records, every rank runs them
+    cnts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(cnts, torch.tensor([len(k)], dtype=torch.int64))
+    maxc = max(int(c.item()) for c in cnts)
+    pad = np.zeros((3, maxc), np.uint64)
+    pad[:, :len(k)] = np.stack([k, f, p])
+    gat = [torch.zeros((3, maxc), dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(gat, torch.from_numpy(pad.view(np.int64).copy()))
+    allr = np.concatenate([g.numpy().view(np.uint64)[:, :int(c.item())] for g, c in zip(gat, cnts)], axis=1)
+    k, f, p = allr
+    rep_f, rep_p, tail_bits = [], [], []
+    L = Ls
+    while len(k):
+        words = (2 * len(k) + 63) // 64
+        final, (sf, sp), (k, f, p) = _settle(L, k, f, p, words, 0, 64 * words)
+        rep_f.append(sf)
+        rep_p.append(sp)
+        tail_bits.append(final)
+        L += 1
+    # output segments: prefix sums over (level, rank) settled counts
+    mycounts = torch.tensor([c for _, c, _ in segs_local], dtype=torch.int64)
+    allcounts = [torch.zeros(Ls, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(allcounts, mycounts)
+    C = np.stack([a.numpy() for a in allcounts])  # [rank, level]
+    segs, G = [], 0
+    for lvl in range(Ls):
+        segs.append((G + int(C[:rank, lvl].sum()), int(C[rank, lvl]), segs_local[lvl][2]))
+        G += int(C[:, lvl].sum())
+    lf = np.concatenate(out_f) if out_f else np.zeros(0, np.uint64)
+    lp = np.concatenate(out_p) if out_p else np.zeros(0, np.uint64)
+    if rank == 0 and rep_f:
+        rf, rp = np.concatenate(rep_f), np.concatenate(rep_p)
+        segs.append((G, len(rf), len(lf)))
+        lf, lp = np.concatenate([lf, rf]), np.concatenate([lp, rp])
+    # level bit vectors: all-gather of each rank's word range, then the tail levels
+    bits_levels = []
+    for words, S, final in level_bits:
+        pad = np.zeros(64 * S, bool)
+        pad[:len(final)] = final
+        g = [torch.zeros(64 * S, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(g, torch.from_numpy(pad.astype(np.uint8)))
+        full = np.concatenate([x.numpy() for x in g]).astype(bool)[:64 * words]
+        bits_levels.append(np.packbits(full, bitorder="little").view(np.uint64))
+    for final in tail_bits:
+        bits_levels.append(np.packbits(final, bitorder="little").view(np.uint64))
+    mph = np.uint64(1).tobytes() + np.uint64(len(bits_levels)).tobytes() + b"".join(
+        np.uint64(len(b)).tobytes() + b.tobytes() for b in bits_levels)
+    result_q.put((rank, lf, lp, [s for s in segs if s[1]], mph, Ls))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_levels_match_single_process(world, oracle_lib):
+@pytest.mark.parametrize("world,switch", [(2, 5000), (3, 5000), (3, 10 ** 9)])
+def test_position_range_ownership_matches_single_process(world, switch, oracle_lib):
     import torch.multiprocessing as mp
     import s3imph
 
@@ -142,16 +181,17 @@ def test_sharded_levels_match_single_process(world, oracle_lib):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, blob, offs, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, blob, offs, switch, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    res.sort()
-    got_fp = np.concatenate([r[2] for r in res])
-    got_pos = np.concatenate([r[3] for r in res])
+    res.sort(key=lambda r: r[0])
     assert all(r[4] == mph for r in res)
+    if switch < n:
+        assert res[0][5] >= 3  # several routed levels before the replicated tail
+    got_fp, got_pos = s3imph.assemble_dist([(r[1], r[2], r[3]) for r in res], n)
     assert np.array_equal(got_fp, fp)
     assert np.array_equal(got_pos, po)

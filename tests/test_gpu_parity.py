@@ -270,21 +270,3 @@ def test_c3_100m_properties(s3, ctx):
     res = torch.zeros(n, dtype=torch.int64, device="cuda")
     ctx.lookup(d_blob, d_offs, n, d_fp, d_po, n, res)
     assert torch.equal(res, torch.arange(n, dtype=torch.int64, device="cuda"))
-
-
-def test_dist_path_single_rank_matches(s3, oracle_lib):
-    """The RCCL rank path (nranks = 1 on this one-GPU box) is byte-identical to the
-    single-GPU path and the oracle (multi-rank layout is covered by tests/test_dist_model.py)."""
-    import torch
-    uid = s3.dist_unique_id()
-    d = s3.DistBuilder(0, uid, 0, 1)
-    n = 300000
-    blob, offs = s3.gen_keys(0, 11, 32, 0, n)
-    st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)
-    d_fp = torch.zeros(n, dtype=torch.int64, device="cuda")
-    d_po = torch.zeros(n, dtype=torch.int64, device="cuda")
-    lo, cnt, info = d.build_shard(to_dev(blob), to_dev(offs), n, 0, d_fp, d_po, n)
-    assert (lo, cnt) == (0, n)
-    assert d.mph_bin() == mph
-    assert np.array_equal(from_dev(d_fp), fp) and np.array_equal(from_dev(d_po), po)
-    d.close()
