@@ -61,6 +61,10 @@ def main() -> None:
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist", action="store_true", help="use the multi-GPU build path even at N=1")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
+                    help="N>1 collectives: RCCL over xGMI (default), or host copies over gloo — a rehearsal "
+                         "mode that lets several ranks share one GPU (not a measurement)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC summary (HBM bytes per launch) to attach as roofline.traffic")
@@ -72,6 +76,8 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.transport == "host":
+        local_rank = local_rank % max(torch.cuda.device_count(), 1)
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 needs torchrun --nproc-per-node N (one process per GPU)")
@@ -91,21 +97,26 @@ def main() -> None:
     dev = f"cuda:{local_rank}"
     d_blob = torch.from_numpy(blob).to(dev)
     d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
-    if world == 1:
+    use_dist = world > 1 or args.dist
+    if not use_dist:
         ctx = s3imph.DeviceBuilder(local_rank)
         ctx.reserve(n)
         out_cap = n
     else:
-        uid = [s3imph.dist_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        ctx = s3imph.DistBuilder(local_rank, uid[0], rank, world)
+        if args.transport == "host":
+            ctx = s3imph.DistBuilder(local_rank, None, rank, world, host_comm=True)
+        else:
+            uid = [s3imph.dist_unique_id() if rank == 0 else None]
+            if dist is not None:
+                dist.broadcast_object_list(uid, src=0)
+            ctx = s3imph.DistBuilder(local_rank, uid[0], rank, world)
         ctx.reserve(n, plan.n_global)
         out_cap = ctx.out_cap(plan.n_global)
     d_fp = torch.empty(max(out_cap, 1), dtype=torch.int64, device=dev)
     d_po = torch.empty(max(out_cap, 1), dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
 
-    if world == 1:
+    if not use_dist:
         def step():
             return ctx.build(d_blob, d_offs, n, d_fp, d_po)
     else:
@@ -168,7 +179,8 @@ def main() -> None:
         "dtype": "u64",
         "data": "synthetic (deterministic splitmix64 prefixes, byte-sorted, distinct)",
         "config": {"workload": cfg["workload"], "config": args.config, "keys": n_global,
-                   "key_bytes": key_bytes, "parallelism": f"shard{world}" if world > 1 else "single",
+                   "transport": args.transport if world > 1 else None,
+                   "key_bytes": key_bytes, "parallelism": f"shard{world}" if use_dist else "single",
                    "gamma": 2.0, "levels": info.get("num_levels")},
         "key_bytes_GBps": key_bytes / dt / 1e9,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},

@@ -707,6 +707,117 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
 #undef SPROF
 }
 
+// ------------------------------------------------------- fused level-0 hash + scatter ----
+// Level 0 in one pass over the key bytes: FNV-1a + FNV-1 of each key (one pass over its
+// bytes, StreamingMPHFBuilder.Add, mphf_streaming.go:73,80), its level-0 tile, and the
+// record (kh, fp, pos) written straight into the tile's reservation slot (the layout of
+// k_scatter_res: tile t owns [t cap, (t+1) cap), cut into kResShards shards, one per
+// XCD).  Each round of NT*KPT keys is counting-sorted by tile in LDS; one atomic per
+// (round, tile) reserves the run.  No kh/fp arrays, no histogram scan.  A slot
+// overflow sets kStResOverflow and the build reruns on the counted path.
+// dyn LDS: stage Rec[R], stile u16[R], cnt/start/cur u32[T].
+template <int NT, int KPT>
+__global__ __launch_bounds__(NT) void k_hash_scatter0(const uint8_t* __restrict__ blob,
+                                                      const uint64_t* __restrict__ offsets, uint64_t n,
+                                                      const uint64_t* __restrict__ ipos, uint64_t pos_base,
+                                                      unsigned* __restrict__ tcnt, Rec* __restrict__ bucket,
+                                                      uint64_t bucket_cap, unsigned long long* __restrict__ flags,
+                                                      LevelState* st, unsigned tb) {
+  constexpr int R = NT * KPT;
+  extern __shared__ uint64_t dyn64[];
+  __shared__ unsigned s_over;
+  Rec* stage = reinterpret_cast<Rec*>(dyn64);
+  unsigned short* stile = reinterpret_cast<unsigned short*>(stage + R);
+  unsigned* cnt = reinterpret_cast<unsigned*>(stile + R);
+  const uint64_t words = st->words[0], magic = st->magic[0];
+  const uint64_t T = ntiles_of(words, tb);
+  unsigned* start = cnt + T;
+  unsigned* cur = start + T;
+  const unsigned tid = threadIdx.x;
+  if (T > kLdsTiles) {
+    if (tid == 0) atomicOr(&st->status, kStGeometry);
+    return;
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    st->ntiles[0] = T;
+    st->nchunks[0] = 0;
+  }
+  for (uint64_t t = (uint64_t)blockIdx.x * NT + tid; t < T; t += (uint64_t)gridDim.x * NT) flags[t] = 0;
+  const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
+  const unsigned shard = blockIdx.x % kResShards;
+  const uint64_t seed = level_seed(0);
+  if (tid == 0) s_over = 0;
+  for (uint64_t t = tid; t < T; t += NT) cnt[t] = 0;
+  __syncthreads();
+  bool zero = false;
+  for (uint64_t r0 = (uint64_t)blockIdx.x * R; r0 < n; r0 += (uint64_t)gridDim.x * R) {
+    uint64_t rk_[KPT], rf_[KPT];
+    unsigned tt[KPT], rk[KPT];
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+      const uint64_t i = r0 + (uint64_t)q * NT + tid;
+      if (i < n) {
+        fnv_both_loop(blob, offsets[i], offsets[i + 1], rk_[q], rf_[q]);
+        zero |= (rk_[q] == 0);
+        tt[q] = (unsigned)(bb_index(seed, rk_[q], words, magic) >> tb);
+        rk[q] = atomicAdd(&cnt[tt[q]], 1u);
+      }
+    }
+    __syncthreads();
+    // exclusive scan of the round's per-tile counts
+    constexpr int kTPT = (int)(kLdsTiles / NT);
+    const uint64_t t0 = (uint64_t)kTPT * tid;
+    unsigned a[kTPT];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      a[q] = t0 + q < T ? cnt[t0 + q] : 0u;
+      sum += a[q];
+    }
+    uint64_t tot;
+    uint64_t ex = block_exscan<NT>(sum, &tot);
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      if (t0 + q < T) start[t0 + q] = (unsigned)ex;
+      ex += a[q];
+    }
+    // reservations: every touched tile's atomic in flight at once
+    for (uint64_t t = tid; t < T; t += NT) {
+      const unsigned c = cnt[t];
+      if (c) {
+        const uint64_t at = atomicAdd(&tcnt[t * kResShards + shard], c);
+        if (at + c > scap) s_over = 1;
+        cur[t] = (unsigned)(t * cap + shard * scap + at);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+      const uint64_t i = r0 + (uint64_t)q * NT + tid;
+      if (i < n) {
+        const unsigned slot = start[tt[q]] + rk[q];
+        stage[slot] = Rec{rk_[q], rf_[q], ipos ? ipos[i] : pos_base + i};
+        stile[slot] = (unsigned short)tt[q];
+      }
+    }
+    __syncthreads();
+    if (s_over) break;
+    const unsigned m = (unsigned)min<uint64_t>(R, n - r0);
+    for (unsigned j = tid; j < m; j += NT) {
+      const unsigned t = stile[j];
+      bucket[cur[t] + (j - start[t])] = stage[j];
+    }
+    for (uint64_t t = tid; t < T; t += NT) cnt[t] = 0;
+    __syncthreads();
+  }
+  if (zero) atomicOr(&st->status, kStKeyZero);
+  if (s_over && tid == 0) atomicOr(&st->status, kStOverflow | kStResOverflow);
+}
+
+size_t hash_scatter0_lds_bytes(int R, uint64_t T) {
+  return (size_t)R * (sizeof(Rec) + sizeof(unsigned short)) + 3 * T * sizeof(unsigned);
+}
+
 // --------------------------------------------------------------------- tile --------
 // dyn LDS: A[tpw], C[tpw] u32 (C becomes the per-word rank prefix after finalize);
 // for tiles of <= 2^kCacheBits positions also loc[kCache] u16 (each record's
@@ -1511,6 +1622,10 @@ size_t tile_lds_bytes(unsigned tb) {
 void binned_set_lds_limits() {
   (void)hipFuncSetAttribute((const void*)k_hash_count0_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(((kLdsTiles + 1) / 2 + kHashWinWords) * sizeof(uint64_t)));
+  (void)hipFuncSetAttribute((const void*)k_hash_scatter0<1024, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)hash_scatter0_lds_bytes(4096, kLdsTiles));
+  (void)hipFuncSetAttribute((const void*)k_hash_scatter0<1024, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)hash_scatter0_lds_bytes(2048, kLdsTiles));
   (void)hipFuncSetAttribute((const void*)k_tile<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)tile_lds_bytes(kTileMaxBits));
   (void)hipFuncSetAttribute((const void*)k_tile<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1585,6 +1700,19 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
   kern<<<grid_tiles, b.tile_block == 512 ? 512 : 1024, lds, s>>>(
       level, b.bucket, b.tile_start, nullptr, b.bucket_cap,
       b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.tile_mode, b.tile_prof);
+}
+
+void launch_hash_scatter0(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
+                          int variant, hipStream_t s) {
+  const uint64_t T = ntiles_of(level_words(n ? n : 1), g.tb);
+  const int cus = 256;
+  if (variant == 1) {  // 2 x 2048-key rounds resident per CU
+    k_hash_scatter0<1024, 2><<<2 * cus, 1024, hash_scatter0_lds_bytes(2048, T), s>>>(
+        blob, offsets, n, b.pos, b.pos_base, b.tcnt, b.bucket, b.bucket_cap, b.flags, b.st, g.tb);
+  } else {  // one 4096-key round per CU
+    k_hash_scatter0<1024, 4><<<cus, 1024, hash_scatter0_lds_bytes(4096, T), s>>>(
+        blob, offsets, n, b.pos, b.pos_base, b.tcnt, b.bucket, b.bucket_cap, b.flags, b.st, g.tb);
+  }
 }
 
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s) {

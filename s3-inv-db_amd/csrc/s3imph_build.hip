@@ -91,6 +91,7 @@ struct s3imph_ctx {
   int tile_block = 1024;
   uint64_t target_tiles = kTargetTiles, target_tiles0 = kTargetTiles0, target_chunks = kTargetChunks;
   uint64_t res_max_keys = kResMaxKeys;
+  int l0_mode = 0;  // level 0: 0 hash+count / scan / scatter; 1, 2 fused hash+scatter (4096 / 2048-key rounds)
   uint64_t target_tiles_res = kTargetTilesRes;
   bool debug = false;
   unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps
@@ -196,7 +197,8 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   const uint64_t cap = std::max<uint64_t>(n, 1024);
   dalloc(c->kh, cap);
   dalloc(c->fp, cap);
-  dalloc(c->bucket, cap);
+  const uint64_t bcap = cap + cap / 4 + 4096;  // level-0 reservation slots: >= 1.25x the mean fill
+  dalloc(c->bucket, bcap);
   dalloc(c->list[0], cap);
   dalloc(c->list[1], cap);
   dalloc(c->hist, kHistCap);
@@ -212,7 +214,7 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   c->cap_blocks = (c->cap_words + 2047) / 2048 + 1;
   dalloc(c->block_sums, c->cap_blocks);
   c->cap_keys = cap;
-  c->bucket_cap = cap;
+  c->bucket_cap = bcap;
 }
 
 void free_workspace(s3imph_ctx* c) {
@@ -411,6 +413,16 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   launch_init_state(c->d_st, n, n, s);
   ev_mark(c, s, "init");
   const Grids gr = level_grids(n, 64 * level_words(n), g0);
+  if (!conservative && c->l0_mode && g0.tb <= kRegTileMaxBits) {
+    // fused level 0: hash straight into reservation slots, then the sharded tile kernel
+    HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kMaxTiles * kResShards * sizeof(unsigned), s));
+    launch_hash_scatter0(blob, offsets, n, b, g0, c->l0_mode - 1, s);
+    ev_mark(c, s, "hash_scatter0");
+    launch_binned_tile(0, b, g0, gr.gt, s, true);
+    ev_mark(c, s, "tile0");
+    enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
+    return;
+  }
   launch_binned_count(0, blob, offsets, n, b, g0, gr.gc, s);
   ev_mark(c, s, "hash_count0");
   launch_binned_scan(0, b, gr.gs, s);
@@ -1093,6 +1105,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     if (const char* m = std::getenv("S3IMPH_TILE_BLOCK")) c->tile_block = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);
+    if (const char* m = std::getenv("S3IMPH_L0")) c->l0_mode = std::atoi(m);
     // A blocking stream: implicitly ordered with the legacy NULL stream, so work a
     // caller queued there (e.g. torch's default stream) completes before ours starts.
     HIPCHECK(hipStreamCreate(&c->own_stream));

@@ -176,6 +176,8 @@ void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s)
 void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s);
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s,
                         bool reserved = false);
+void launch_hash_scatter0(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
+                          int variant, hipStream_t s);
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s);
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s);
 

@@ -270,3 +270,26 @@ def test_c3_100m_properties(s3, ctx):
     res = torch.zeros(n, dtype=torch.int64, device="cuda")
     ctx.lookup(d_blob, d_offs, n, d_fp, d_po, n, res)
     assert torch.equal(res, torch.arange(n, dtype=torch.int64, device="cuda"))
+
+
+@pytest.mark.parametrize("l0", ["0", "1", "2"])
+@pytest.mark.parametrize("n,kind,avg", [(70_000, 0, 32), (1_000_000, 1, 0), (10_000_000, 0, 32)])
+def test_level0_variants_bit_exact(s3, oracle_lib, monkeypatch, l0, n, kind, avg):
+    """Level 0 as hash+count / scan / scatter (S3IMPH_L0=0) and as the fused hash ->
+    reservation-slot scatter (1: 4096-key rounds, 2: 2048-key rounds), ragged and C2-sized
+    inputs with custom positions on one of them: all bit-exact with the oracle."""
+    monkeypatch.setenv("S3IMPH_L0", l0)
+    c = s3.DeviceBuilder(0)
+    try:
+        blob, offs = s3.gen_keys(kind, 19, avg, 0, n)
+        pos = None
+        if n == 1_000_000:
+            pos = np.random.default_rng(5).permutation(n).astype(np.uint64) * np.uint64(3)
+        st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs, pos)
+        assert st == 0
+        gfp, gpo, gmph, info = _device_build(s3, c, blob, offs, pos)
+        assert gmph == mph
+        assert np.array_equal(gfp, fp)
+        assert np.array_equal(gpo, po)
+    finally:
+        c.close()
