@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -25,6 +26,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "s3imph.h"
@@ -67,6 +69,24 @@ struct DistState {
 
 }  // namespace
 
+namespace {
+
+// Pinned staging for host-memory builds (the Go caller's buffers are pageable):
+// kStageWorkers threads, each with its own pinned chunk buffer and stream, move the
+// data through pinned memory, so the CPU copies of one worker overlap the DMA of the
+// others and the PCIe link runs at its pinned rate.
+constexpr int kStageWorkers = 8;
+constexpr uint64_t kStageChunk = 8ull << 20;
+
+struct Stager {
+  void* pin[kStageWorkers][2] = {};  // double-buffered: one chunk in DMA while the other is copied
+  hipStream_t st[kStageWorkers] = {};
+  hipEvent_t ev[kStageWorkers][2] = {};
+  bool ready = false;
+};
+
+}  // namespace
+
 struct s3imph_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -102,6 +122,7 @@ struct s3imph_ctx {
   uint64_t s_blob_cap = 0;
   uint64_t *s_offsets = nullptr, *s_pos = nullptr, *s_fp = nullptr, *s_posout = nullptr;
   uint64_t s_cap = 0;
+  Stager stager;
 
   bool have_build = false;
   uint64_t last_n = 0;
@@ -227,6 +248,17 @@ void free_workspace(s3imph_ctx* c) {
   if (c->h_st) (void)hipHostFree(c->h_st);
   c->h_st = nullptr;
   dfree(c->s_blob); dfree(c->s_offsets); dfree(c->s_pos); dfree(c->s_fp); dfree(c->s_posout);
+  for (int w = 0; w < kStageWorkers; ++w) {
+    for (int b = 0; b < 2; ++b) {
+      if (c->stager.pin[w][b]) (void)hipHostFree(c->stager.pin[w][b]);
+      if (c->stager.ev[w][b]) (void)hipEventDestroy(c->stager.ev[w][b]);
+      c->stager.pin[w][b] = nullptr;
+      c->stager.ev[w][b] = nullptr;
+    }
+    if (c->stager.st[w]) (void)hipStreamDestroy(c->stager.st[w]);
+    c->stager.st[w] = nullptr;
+  }
+  c->stager.ready = false;
   DistState& d = c->d;
   dfree(d.send); dfree(d.stage_bits); dfree(d.scnt); dfree(d.mat); dfree(d.gslot); dfree(d.small);
   if (d.h_pinned) (void)hipHostFree(d.h_pinned);
@@ -990,10 +1022,93 @@ s3imph_ctx* default_ctx(int device, std::string* msg) {
   return g_default[device];
 }
 
+void stager_init(s3imph_ctx* c) {
+  Stager& g = c->stager;
+  if (g.ready) return;
+  for (int w = 0; w < kStageWorkers; ++w) {
+    for (int b = 0; b < 2; ++b) {
+      HIPCHECK(hipHostMalloc(&g.pin[w][b], kStageChunk, hipHostMallocDefault));
+      HIPCHECK(hipEventCreateWithFlags(&g.ev[w][b], hipEventDisableTiming));
+    }
+    HIPCHECK(hipStreamCreateWithFlags(&g.st[w], hipStreamNonBlocking));
+  }
+  g.ready = true;
+}
+
+// Chunked copy between pageable host memory and the device through the pinned
+// buffers.  h2d: device dst <- host src; with `bias`, src holds u64 words and each is
+// stored minus bias (offsets rebased to a blob that starts at offsets[0]).
+void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias = 0) {
+  if (!bytes) return;
+  // Pageable H2D through the runtime already runs at the PCIe rate (C2: 400 MB in
+  // 7.4 ms, 54 GB/s); pageable D2H does not (17 GB/s), and neither does rebasing.
+  // S3IMPH_STAGE=0 / =2 force the runtime / staged path for every copy (A/B).
+  static const int mode = [] {
+    const char* e = std::getenv("S3IMPH_STAGE");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (!bias && (mode == 0 || (mode == 1 && h2d))) {
+    HIPCHECK(hipMemcpy(dst, src, bytes, h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost));
+    return;
+  }
+  stager_init(c);
+  Stager& g = c->stager;
+  const uint64_t nch = (bytes + kStageChunk - 1) / kStageChunk;
+  const int nw = (int)std::min<uint64_t>(kStageWorkers, nch);
+  std::vector<std::string> errs(nw);
+  auto work = [&](int w) {
+    try {
+      HIPCHECK(hipSetDevice(c->device));
+      auto clen = [&](uint64_t ch) { return std::min(kStageChunk, bytes - ch * kStageChunk); };
+      int b = 0;
+      if (h2d) {
+        for (uint64_t ch = w; ch < nch; ch += nw, b ^= 1) {
+          const uint64_t off = ch * kStageChunk, len = clen(ch);
+          HIPCHECK(hipEventSynchronize(g.ev[w][b]));  // this buffer's previous DMA is done
+          if (bias) {
+            const uint64_t* s64 = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(src) + off);
+            uint64_t* d64 = static_cast<uint64_t*>(g.pin[w][b]);
+            for (uint64_t i = 0; i < len / 8; ++i) d64[i] = s64[i] - bias;
+          } else {
+            std::memcpy(g.pin[w][b], static_cast<const uint8_t*>(src) + off, len);
+          }
+          HIPCHECK(hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, g.pin[w][b], len, hipMemcpyHostToDevice,
+                                  g.st[w]));
+          HIPCHECK(hipEventRecord(g.ev[w][b], g.st[w]));
+        }
+      } else {
+        // prefetch the worker's first chunk, then: issue chunk i+1's DMA, copy out chunk i
+        auto issue = [&](uint64_t ch, int buf) {
+          HIPCHECK(hipMemcpyAsync(g.pin[w][buf], static_cast<const uint8_t*>(src) + ch * kStageChunk, clen(ch),
+                                  hipMemcpyDeviceToHost, g.st[w]));
+          HIPCHECK(hipEventRecord(g.ev[w][buf], g.st[w]));
+        };
+        if ((uint64_t)w < nch) issue(w, 0);
+        for (uint64_t ch = w; ch < nch; ch += nw, b ^= 1) {
+          if (ch + nw < nch) issue(ch + nw, b ^ 1);
+          HIPCHECK(hipEventSynchronize(g.ev[w][b]));
+          std::memcpy(static_cast<uint8_t*>(dst) + ch * kStageChunk, g.pin[w][b], clen(ch));
+        }
+      }
+      HIPCHECK(hipStreamSynchronize(g.st[w]));
+    } catch (const Fail& f) {
+      errs[w] = f.msg.empty() ? "staged copy failed" : f.msg;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int w = 1; w < nw; ++w) th.emplace_back(work, w);
+  work(0);
+  for (auto& t : th) t.join();
+  for (const auto& e : errs)
+    if (!e.empty()) throw Fail{S3IMPH_ERR_HIP, e};
+}
+
 // Host-memory build through the device path (used by s3imph_build_host and the builder).
 int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, std::vector<uint8_t>* mph,
                     std::string* msg) {
+  using clk = std::chrono::steady_clock;
+  const auto te = clk::now();
   s3imph_ctx* c = default_ctx(device, msg);
   if (!c) return S3IMPH_ERR_HIP;
   std::lock_guard<std::mutex> lk(c->mu);
@@ -1015,27 +1130,30 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
       c->s_cap = n;
     }
     hipStream_t s = c->own_stream;
-    std::vector<uint64_t> rel;
-    const uint64_t* offs = offsets;
-    if (b0 != 0) {
-      rel.resize(n + 1);
-      for (uint64_t i = 0; i <= n; ++i) rel[i] = offsets[i] - b0;
-      offs = rel.data();
-    }
-    if (nbytes) HIPCHECK(hipMemcpyAsync(c->s_blob, blob + b0, nbytes, hipMemcpyHostToDevice, s));
-    HIPCHECK(hipMemcpyAsync(c->s_offsets, offs, (n + 1) * 8, hipMemcpyHostToDevice, s));
-    if (pos) HIPCHECK(hipMemcpyAsync(c->s_pos, pos, n * 8, hipMemcpyHostToDevice, s));
+    HIPCHECK(hipStreamSynchronize(s));  // staging buffers may be in use by the last build
+    const auto t0 = clk::now();
+    staged_copy(c, true, c->s_blob, blob + b0, nbytes);
+    staged_copy(c, true, c->s_offsets, offsets, (n + 1) * 8, b0);
+    if (pos) staged_copy(c, true, c->s_pos, pos, n * 8);
+    const auto t1 = clk::now();
     s3imph_build_info info;
     int rc = build_single(c, c->s_blob, c->s_offsets, pos ? c->s_pos : nullptr, n, c->s_fp, c->s_posout, s,
                           &info, msg);
     if (rc != S3IMPH_OK) return rc;
-    HIPCHECK(hipMemcpyAsync(fp_out, c->s_fp, n * 8, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipMemcpyAsync(pos_out, c->s_posout, n * 8, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    const auto t2 = clk::now();
+    staged_copy(c, false, fp_out, c->s_fp, n * 8);
+    staged_copy(c, false, pos_out, c->s_posout, n * 8);
+    const auto t3 = clk::now();
     mph->resize(info.mph_bin_len);
     uint64_t len = 0;
     // ctx mutex already held: marshal inline.
-    return marshal_locked(c, mph->data(), mph->size(), &len, msg);
+    rc = marshal_locked(c, mph->data(), mph->size(), &len, msg);
+    if (c->debug) {
+      auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
+      std::fprintf(stderr, "[s3imph] host build: entry %.2f, h2d %.2f ms, build %.2f ms, d2h %.2f ms, marshal %.2f ms\n",
+                   ms(t0 - te), ms(t1 - t0), ms(t2 - t1), ms(t3 - t2), ms(clk::now() - t3));
+    }
+    return rc;
   } catch (const Fail& f) {
     *msg = f.msg;
     return f.code;
@@ -1061,18 +1179,19 @@ int marshal_locked(s3imph_ctx* c, uint8_t* out, uint64_t cap, uint64_t* len, std
     *msg = "buffer too small";
     return S3IMPH_ERR_INVALID;
   }
-  std::vector<uint64_t> words(c->info.total_words);
-  HIPCHECK(hipMemcpy(words.data(), c->bits, words.size() * 8, hipMemcpyDeviceToHost));
+  // Little-endian host: each level's words are copied straight behind its header.
+  static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "mph.bin words are little-endian");
   uint8_t* p = out;
   auto put = [&](uint64_t v) {
-    for (int b = 0; b < 8; ++b) *p++ = (uint8_t)(v >> (8 * b));
+    std::memcpy(p, &v, 8);
+    p += 8;
   };
   put(kPartitions);
   put(st.nlevels);
   for (unsigned L = 0; L < st.nlevels; ++L) {
     put(st.words[L]);
-    const uint64_t* w = words.data() + st.woff[L];
-    for (uint64_t k = 0; k < st.words[L]; ++k) put(w[k]);
+    if (st.words[L]) HIPCHECK(hipMemcpy(p, c->bits + st.woff[L], 8 * st.words[L], hipMemcpyDeviceToHost));
+    p += 8 * st.words[L];
   }
   return S3IMPH_OK;
 }

@@ -223,15 +223,23 @@ class StreamingMPHFBuilder:
             pass
 
 
-def build_host(blob: np.ndarray, offsets: np.ndarray, pos: np.ndarray | None = None, device: int = 0):
-    """One-shot build from host memory: (fp_out u64[N], pos_out u64[N], mph_bin bytes)."""
+def build_host(blob: np.ndarray, offsets: np.ndarray, pos: np.ndarray | None = None, device: int = 0,
+               out: tuple[np.ndarray, np.ndarray] | None = None):
+    """One-shot build from host memory: (fp_out u64[N], pos_out u64[N], mph_bin bytes).
+    `out` may supply the two output arrays (u64, N each) to be filled in place."""
     blob = np.ascontiguousarray(blob, np.uint8)
     offsets = np.ascontiguousarray(offsets, np.uint64)
     n = len(offsets) - 1
     if pos is not None:
         pos = np.ascontiguousarray(pos, np.uint64)
-    fp_out = np.zeros(n, np.uint64)
-    pos_out = np.zeros(n, np.uint64)
+    if out is not None:
+        fp_out, pos_out = out
+        if fp_out.dtype != np.uint64 or pos_out.dtype != np.uint64 or len(fp_out) < n or len(pos_out) < n \
+                or not fp_out.flags.c_contiguous or not pos_out.flags.c_contiguous:
+            raise ValueError("out arrays must be contiguous uint64 with at least N entries")
+    else:
+        fp_out = np.zeros(n, np.uint64)
+        pos_out = np.zeros(n, np.uint64)
     mp = ctypes.c_void_p()
     ml = ctypes.c_uint64()
     err = ctypes.create_string_buffer(1024)

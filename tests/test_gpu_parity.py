@@ -114,6 +114,22 @@ def test_build_host_roundtrip_lookup(s3, oracle_lib):
         assert oracle_lib.lookup(m, fp, po, k.encode()) is None
 
 
+def test_build_host_staged_chunks_offset_blob_custom_pos(s3, oracle_lib):
+    """s3imph_build_host moves pageable host data through the pinned chunk stager
+    (8 MiB chunks over 8 workers): a multi-chunk set whose blob starts at a non-zero
+    offsets[0] (rebased while staged) with custom positions, bit-exact vs the oracle."""
+    n = 3_000_000
+    blob, offs = s3.gen_keys(0, 23, 32, 0, n)
+    blob = blob[: int(offs[-1])]
+    pos = np.random.default_rng(9).permutation(n).astype(np.uint64) * np.uint64(5)
+    st, fp, po, mph = oracle_lib.build(blob, offs, pos)
+    assert st == 0
+    shifted = np.concatenate([np.frombuffer(b"0123456789abc", np.uint8), blob])
+    gfp, gpo, gmph = s3.build_host(shifted, offs + np.uint64(13), pos)
+    assert gmph == mph
+    assert np.array_equal(gfp, fp) and np.array_equal(gpo, po)
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 31, 32, 33, 63, 64, 65, 1000, 4097, 65535, 65536, 65537, 200000])
 def test_sizes_around_boundaries(s3, oracle_lib, ctx, n):
     blob, offs = s3.gen_keys(0, 7, 24, 0, n)
