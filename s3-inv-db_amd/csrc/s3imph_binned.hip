@@ -34,7 +34,7 @@ namespace {
 constexpr int kCB = 1024;             // count block
 constexpr int kSB = 1024;             // scatter block
 constexpr int kTailT = 1024;          // tail block
-constexpr unsigned kLenBuckets = 256;  // key-length classes of the level-0 hash sort
+constexpr unsigned kLenBuckets = 256;  // key-length classes (4 B each) of the level-0 hash sort
 constexpr uint64_t kTcntWords = (uint64_t)kResLevels * kMaxTiles * kResShards;
 constexpr uint64_t kLdsTiles = kMaxTiles;  // histogram / cursor entries in LDS
 constexpr unsigned long long kGate = kTailKeys;
@@ -102,18 +102,32 @@ __device__ __forceinline__ bool level_active(int level, const LevelState* st) {
 // ---------------------------------------------------------------- level 0 count ----
 // Hash every key (FNV-1a key hash + FNV-1 fingerprint, one pass over the bytes),
 // store both in key order, and histogram the level-0 tiles per chunk.
-template <bool kSort, bool kBatched>
+// kVar: 0 one load per word (fnv_both_loop), 1 batched 8-word loads (fnv_both),
+// 2 loads pipelined two words ahead (fnv_both_pf).
+template <int kVar>
+__device__ __forceinline__ void hash_key(const uint8_t* blob, uint64_t b0, uint64_t b1, uint64_t& h1, uint64_t& h2) {
+  if (kVar == 1) fnv_both(blob, b0, b1, h1, h2);
+  else if (kVar == 2) fnv_both_pf(blob, b0, b1, h1, h2);
+  else fnv_both_loop(blob, b0, b1, h1, h2);
+}
+
+// gate >= 0: run only if st->skew == gate (k_init_state sampled the key lengths), so the
+// direct and the length-sorted variant are both enqueued and the device picks one.
+template <bool kSort, int kBatched>
 __global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__ blob,
                                                      const uint64_t* __restrict__ offsets, uint64_t n,
                                                      uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
                                                      unsigned* __restrict__ hist,
                                                      unsigned long long* __restrict__ flags,
                                                      unsigned long long* __restrict__ sflags, LevelState* st,
-                                                     unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
+                                                     unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt,
+                                                     int gate) {
   __shared__ unsigned sh[kLdsTiles];
   __shared__ unsigned lcnt[kLenBuckets];
   __shared__ unsigned short sidx[kCB];
   __shared__ uint64_t sb0[kCB], sb1[kCB], sh1[kCB], sh2[kCB];
+  __shared__ uint64_t s_lmax[kCB / 64], s_lsum[kCB / 64];
+  if (gate >= 0 && (int)st->skew != gate) return;
   const uint64_t words = st->words[0], magic = st->magic[0];
   const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
   if (!geom_ok(st, T, B)) return;
@@ -135,8 +149,7 @@ __global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__
       __syncthreads();
       for (uint64_t i = lo + tid; i < hi; i += kCB) {
         uint64_t h1, h2;
-        if (kBatched) fnv_both(blob, offsets[i], offsets[i + 1], h1, h2);
-        else fnv_both_loop(blob, offsets[i], offsets[i + 1], h1, h2);
+        hash_key<kBatched>(blob, offsets[i], offsets[i + 1], h1, h2);
         kh[i] = h1;
         fp[i] = h2;
         zero |= (h1 == 0);
@@ -154,8 +167,41 @@ __global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__
         b1 = offsets[i + 1];
       }
       if (tid < kLenBuckets) lcnt[tid] = 0;
+      // Sort only a skewed group (longest key > 2x the mean + 16 B): for near-uniform
+      // lengths the shuffle costs more than the idle lanes it saves.
+      {
+        uint64_t mx = b1 - b0, sm = b1 - b0;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+          mx = max(mx, (uint64_t)__shfl_xor(mx, d));
+          sm += __shfl_xor(sm, d);
+        }
+        if (lane_id() == 0) {
+          s_lmax[tid >> 6] = mx;
+          s_lsum[tid >> 6] = sm;
+        }
+      }
       __syncthreads();
-      const unsigned lb = (unsigned)min<uint64_t>(b1 - b0, kLenBuckets - 1);
+      uint64_t gmax = 0, gsum = 0;
+#pragma unroll
+      for (int w = 0; w < kCB / 64; ++w) {
+        gmax = max(gmax, s_lmax[w]);
+        gsum += s_lsum[w];
+      }
+      const uint64_t gcnt = min<uint64_t>(kCB, hi - g);
+      if (gmax * gcnt <= 2 * gsum + 16 * gcnt) {
+        if (i < hi) {
+          uint64_t h1, h2;
+          hash_key<kBatched>(blob, b0, b1, h1, h2);
+          kh[i] = h1;
+          fp[i] = h2;
+          zero |= (h1 == 0);
+          atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
+        }
+        __syncthreads();
+        continue;
+      }
+      const unsigned lb = (unsigned)min<uint64_t>((b1 - b0) >> 2, kLenBuckets - 1);
       const unsigned rk = atomicAdd(&lcnt[lb], 1u);
       __syncthreads();
       uint64_t tot;
@@ -170,8 +216,7 @@ __global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__
       const unsigned j = sidx[tid];
       if (g + j < hi) {
         uint64_t h1, h2;
-        if (kBatched) fnv_both(blob, sb0[tid], sb1[tid], h1, h2);
-        else fnv_both_loop(blob, sb0[tid], sb1[tid], h1, h2);
+        hash_key<kBatched>(blob, sb0[tid], sb1[tid], h1, h2);
         sh1[j] = h1;
         sh2[j] = h2;
         zero |= (h1 == 0);
@@ -186,155 +231,6 @@ __global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__
     }
     __syncthreads();
     for (uint64_t t = tid; t < T; t += kCB) hist[t * B + b] = sh[t];
-    __syncthreads();
-  }
-  if (zero) atomicOr(&st->status, kStKeyZero);
-}
-
-// Level-0 hash + count, length-classed: FNV costs one dependent multiply chain per
-// byte and a wave runs as long as its longest lane, so each 1024-key group is ranked
-// into 16 classes by whole 8-byte words (wave ballots + a 256-entry scan, no LDS
-// atomics) and every wave hashes keys of one class.  Results return to key order
-// through LDS so the kh/fp stores stay coalesced.
-constexpr int kClasses = 16;
-__global__ __launch_bounds__(kCB) void k_hash_count0_cls(const uint8_t* __restrict__ blob,
-                                                         const uint64_t* __restrict__ offsets, uint64_t n,
-                                                         uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
-                                                         unsigned* __restrict__ hist,
-                                                         unsigned long long* __restrict__ flags,
-                                                         unsigned long long* __restrict__ sflags, LevelState* st,
-                                                         unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
-  __shared__ unsigned sh[kLdsTiles];
-  __shared__ unsigned scls[kClasses * (kCB / 64)];  // class-major (class, wave) counts -> bases
-  __shared__ unsigned short sidx[kCB];
-  __shared__ uint64_t sb0[kCB], sb1[kCB], sh1[kCB], sh2[kCB];
-  const uint64_t words = st->words[0], magic = st->magic[0];
-  const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
-  if (!geom_ok(st, T, B)) return;
-  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  const uint64_t lt = lanemask_lt();
-  if (blockIdx.x == 0 && tid == 0) {
-    st->ntiles[0] = T;
-    st->nchunks[0] = B;
-  }
-  for (uint64_t t = (uint64_t)blockIdx.x * kCB + tid; t < T; t += (uint64_t)gridDim.x * kCB) flags[t] = 0;
-  const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
-  for (uint64_t q = (uint64_t)blockIdx.x * kCB + tid; q < nseg; q += (uint64_t)gridDim.x * kCB) sflags[q] = 0;
-  for (uint64_t q = (uint64_t)blockIdx.x * kCB + tid; q < kTcntWords; q += (uint64_t)gridDim.x * kCB) tcnt[q] = 0;
-  const uint64_t seed = level_seed(0);
-  bool zero = false;
-  for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
-    for (uint64_t t = tid; t < T; t += kCB) sh[t] = 0;
-    const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
-    for (uint64_t g = lo; g < hi; g += kCB) {
-      const uint64_t i = g + tid;
-      uint64_t b0 = 0, b1 = 0;
-      if (i < hi) {
-        b0 = offsets[i];
-        b1 = offsets[i + 1];
-      }
-      const unsigned cls = i < hi ? (unsigned)min<uint64_t>((b1 - b0) >> 3, kClasses - 1) : kClasses - 1;
-      unsigned myrank = 0;
-#pragma unroll
-      for (int c = 0; c < kClasses; ++c) {
-        const uint64_t m = __ballot(cls == (unsigned)c);
-        if (lane == 0) scls[c * (kCB / 64) + wave] = (unsigned)__popcll(m);
-        if (cls == (unsigned)c) myrank = (unsigned)__popcll(m & lt);
-      }
-      __syncthreads();
-      uint64_t tot;
-      const uint64_t ex = block_exscan<kCB>(tid < kClasses * (kCB / 64) ? scls[tid] : 0u, &tot);
-      if (tid < kClasses * (kCB / 64)) scls[tid] = (unsigned)ex;
-      __syncthreads();
-      const unsigned slot = scls[cls * (kCB / 64) + wave] + myrank;
-      sidx[slot] = (unsigned short)tid;
-      sb0[slot] = b0;
-      sb1[slot] = b1;
-      __syncthreads();
-      const unsigned j = sidx[tid];
-      if (g + j < hi) {
-        uint64_t h1, h2;
-        fnv_both_loop(blob, sb0[tid], sb1[tid], h1, h2);
-        sh1[j] = h1;
-        sh2[j] = h2;
-        zero |= (h1 == 0);
-        atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
-      }
-      __syncthreads();
-      if (i < hi) {
-        kh[i] = sh1[tid];
-        fp[i] = sh2[tid];
-      }
-    }
-    __syncthreads();
-    for (uint64_t t = tid; t < T; t += kCB) hist[t * B + b] = sh[t];
-    __syncthreads();
-  }
-  if (zero) atomicOr(&st->status, kStKeyZero);
-}
-
-// Level-0 hash + count, LDS-staged: per group of kHB keys the block copies the group's
-// aligned blob words into LDS with coalesced, independent loads, then each thread hashes
-// its key out of LDS.  A group whose bytes exceed the window (very long keys) is hashed
-// straight from global memory.  dyn LDS: hist[T] u32, then the window.
-constexpr int kHB = 512;
-constexpr unsigned kHashWinWords = 6144;  // 48 KB window
-__global__ __launch_bounds__(kHB) void k_hash_count0_lds(const uint8_t* __restrict__ blob,
-                                                         const uint64_t* __restrict__ offsets, uint64_t n,
-                                                         uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
-                                                         unsigned* __restrict__ hist,
-                                                         unsigned long long* __restrict__ flags,
-                                                         unsigned long long* __restrict__ sflags, LevelState* st,
-                                                         unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
-  extern __shared__ uint32_t dyn[];
-  const uint64_t words = st->words[0], magic = st->magic[0];
-  const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
-  if (!geom_ok(st, T, B)) return;
-  unsigned* sh = dyn;
-  uint64_t* win = reinterpret_cast<uint64_t*>(dyn) + (T + 1) / 2;
-  const uint64_t* bw = reinterpret_cast<const uint64_t*>(blob);
-  const unsigned tid = threadIdx.x;
-  if (blockIdx.x == 0 && tid == 0) {
-    st->ntiles[0] = T;
-    st->nchunks[0] = B;
-  }
-  for (uint64_t t = (uint64_t)blockIdx.x * kHB + tid; t < T; t += (uint64_t)gridDim.x * kHB) flags[t] = 0;
-  const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
-  for (uint64_t q = (uint64_t)blockIdx.x * kHB + tid; q < nseg; q += (uint64_t)gridDim.x * kHB) sflags[q] = 0;
-  for (uint64_t q = (uint64_t)blockIdx.x * kHB + tid; q < kTcntWords; q += (uint64_t)gridDim.x * kHB) tcnt[q] = 0;
-  const uint64_t seed = level_seed(0);
-  bool zero = false;
-  for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
-    for (uint64_t t = tid; t < T; t += kHB) sh[t] = 0;
-    const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
-    for (uint64_t g = lo; g < hi; g += kHB) {
-      const uint64_t i = g + tid, gend = min(hi, g + kHB);
-      uint64_t b0 = 0, b1 = 0;
-      if (i < hi) {
-        b0 = offsets[i];
-        b1 = offsets[i + 1];
-      }
-      const uint64_t w0 = offsets[g] >> 3, w1 = (offsets[gend] + 7) >> 3;  // group's aligned words
-      const bool fits = w1 - w0 <= kHashWinWords;
-      __syncthreads();  // previous group's window reads (and the hist zeroing) are done
-      if (fits) {
-        const unsigned nwin = (unsigned)(w1 - w0);
-        for (unsigned q = tid; q < nwin; q += kHB) win[q] = bw[w0 + q];
-      }
-      __syncthreads();
-      if (i < hi) {
-        uint64_t h1, h2;
-        const uint64_t nw = b1 > b0 ? ((b1 - 1) >> 3) - (b0 >> 3) + 1 : 0;
-        if (fits) fnv_words(win + ((b0 >> 3) - w0), nw, (unsigned)(b0 & 7) * 8, b1 - b0, h1, h2);
-        else fnv_words(bw + (b0 >> 3), nw, (unsigned)(b0 & 7) * 8, b1 - b0, h1, h2);
-        kh[i] = h1;
-        fp[i] = h2;
-        zero |= (h1 == 0);
-        atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
-      }
-    }
-    __syncthreads();
-    for (uint64_t t = tid; t < T; t += kHB) hist[t * B + b] = sh[t];
     __syncthreads();
   }
   if (zero) atomicOr(&st->status, kStKeyZero);
@@ -1620,8 +1516,6 @@ size_t tile_lds_bytes(unsigned tb) {
 }  // namespace
 
 void binned_set_lds_limits() {
-  (void)hipFuncSetAttribute((const void*)k_hash_count0_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(((kLdsTiles + 1) / 2 + kHashWinWords) * sizeof(uint64_t)));
   (void)hipFuncSetAttribute((const void*)k_hash_scatter0<1024, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)hash_scatter0_lds_bytes(4096, kLdsTiles));
   (void)hipFuncSetAttribute((const void*)k_hash_scatter0<1024, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1640,29 +1534,28 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
                          LevelGeom g, int grid_chunks, hipStream_t s) {
   if (level == 0 && !b.dist) {
     static const int mode = [] {
-      // A/B knob: 3 direct, loop (default); 0 LDS-staged; 1 direct, batched loads;
-      // 2 length-sorted, loop; 4 length-sorted, batched; 5 word-count classes
+      // A/B knob: 0 auto (default: 7 for near-uniform lengths, 4 for skewed ones, picked
+      // on the device from sampled lengths); 1 direct, batched 8-word loads; 2 length-
+      // sorted, one load per word; 3 direct, one load per word; 4 length-sorted, batched;
+      // 7 direct, loads two words ahead; 8 length-sorted, loads two words ahead.
       const char* e = std::getenv("S3IMPH_HASH_MODE");
-      return e ? std::atoi(e) : 3;
+      return e ? std::atoi(e) : 0;
     }();
-    if (mode == 5) {
-      k_hash_count0_cls<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st,
-                                                     g.tb, g.chunk, b.tcnt);
-      return;
+#define S3_HASH(KS, KV, GATE)                                                                                   \
+  k_hash_count0<KS, KV><<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st, \
+                                                    g.tb, g.chunk, b.tcnt, GATE)
+    switch (mode) {
+      case 1: S3_HASH(false, 1, -1); break;
+      case 2: S3_HASH(true, 0, -1); break;
+      case 3: S3_HASH(false, 0, -1); break;
+      case 4: S3_HASH(true, 1, -1); break;
+      case 7: S3_HASH(false, 2, -1); break;
+      case 8: S3_HASH(true, 2, -1); break;
+      default:
+        S3_HASH(false, 2, 0);
+        S3_HASH(true, 1, 1);
     }
-    if (mode == 0) {
-      const uint64_t T = ntiles_of(level_words(n ? n : 1), g.tb);
-      const size_t lds = ((T + 1) / 2 + kHashWinWords) * sizeof(uint64_t);
-      k_hash_count0_lds<<<grid_chunks, kHB, lds, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags,
-                                                      b.st, g.tb, g.chunk, b.tcnt);
-      return;
-    }
-    auto kern = mode == 1   ? k_hash_count0<false, true>
-                : mode == 2 ? k_hash_count0<true, false>
-                : mode == 3 ? k_hash_count0<false, false>
-                            : k_hash_count0<true, true>;
-    kern<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st, g.tb, g.chunk,
-                                     b.tcnt);
+#undef S3_HASH
   } else {
     k_count<<<grid_chunks, kCB, 0, s>>>(level, b.list[(level - 1) & 1], b.hist, b.flags, b.sflags, b.st, g.tb,
                                         g.chunk, b.cap_words);

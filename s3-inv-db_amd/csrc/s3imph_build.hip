@@ -442,7 +442,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   const BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
   const double q = 1.0 - std::exp(-0.5);
   const LevelGeom g0 = choose_geom(n, c->target_tiles0, c->target_chunks, kRegTileMaxBits);
-  launch_init_state(c->d_st, n, n, s);
+  launch_init_state(c->d_st, n, n, s, offsets);
   ev_mark(c, s, "init");
   const Grids gr = level_grids(n, 64 * level_words(n), g0);
   if (!conservative && c->l0_mode && g0.tb <= kRegTileMaxBits) {

@@ -78,6 +78,40 @@ static __device__ __forceinline__ void fnv_both_loop(const uint8_t* __restrict__
   fnv_words(w, nw, (unsigned)(b0 & 7) * 8, b1 - b0, ha, hb);
 }
 
+// FNV-1a + FNV-1 of blob[b0, b1) with the aligned-word loads software-pipelined two
+// words ahead: word q+2 is requested while word q is hashed, so a lane's dependent
+// load latency overlaps its own multiply chain.  Never reads past the key's last
+// aligned word.
+static __device__ __forceinline__ void fnv_both_pf(const uint8_t* __restrict__ blob, uint64_t b0, uint64_t b1,
+                                                   uint64_t& ha, uint64_t& hb) {
+  uint64_t a = kFnvOffset, b = kFnvOffset;
+  if (b1 > b0) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(blob + (b0 & ~7ull));
+    const uint64_t nw = ((b1 - 1) >> 3) - (b0 >> 3) + 1;  // aligned words overlapping the key
+    const unsigned sh = (unsigned)(b0 & 7) * 8;
+    const uint64_t len = b1 - b0;
+    const uint64_t nfull = len >> 3;
+    uint64_t cur = w[0];
+    uint64_t nxt = nw > 1 ? w[1] : 0;
+    for (uint64_t q = 0; q < nfull; ++q) {
+      const uint64_t nn = (q + 2 < nw) ? w[q + 2] : 0;
+      const uint64_t v = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
+      fnv_8(a, b, v);
+      cur = nxt;
+      nxt = nn;
+    }
+    const unsigned rem = (unsigned)(len & 7);
+    if (rem) {
+      const uint64_t v = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
+#pragma unroll
+      for (unsigned t = 0; t < 7; ++t)
+        if (t < rem) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
+    }
+  }
+  ha = a;
+  hb = b;
+}
+
 // FNV-1a (key hash) and FNV-1 (fingerprint) of blob[b0, b1) in one pass.  The key's
 // aligned words are loaded 8 at a time (all 8 loads in flight before the first use);
 // stream word q = bytes [8q, 8q+8) of the key = funnel(w[q], w[q+1]) by the key's

@@ -23,7 +23,7 @@ struct LevelState {
   unsigned int nlevels;
   unsigned int status;                       // kSt* flags
   unsigned int tail_first;                   // first level run by the single-workgroup tail
-  unsigned int pad;
+  unsigned int skew;                         // sampled key lengths are skewed: hash length-sorted
   // Binned pipeline (s3imph_binned.hip).
   unsigned long long lvl_base[kMaxLevels + 2];  // set bits in all levels < L (= ranks[L] - 1)
   unsigned long long ntiles[kMaxLevels + 2];    // position tiles of level L
@@ -129,7 +129,8 @@ constexpr int kTailLdsWords32 = 2 * 2 * ((kGammaNum * kTailKeys + 63) / 64);  //
 struct KernelArgs;  // fwd
 
 // ---- launchers (s3imph_kernels.hip) -------------------------------------------
-void launch_init_state(LevelState* st, uint64_t n, uint64_t out_cap, hipStream_t s);
+void launch_init_state(LevelState* st, uint64_t n, uint64_t out_cap, hipStream_t s,
+                       const uint64_t* offsets = nullptr);
 void launch_rank_scan(const uint64_t* bits, uint64_t cap_words, uint64_t* rank_base,
                       unsigned long long* block_sums, uint64_t max_blocks, LevelState* st,
                       hipStream_t s);

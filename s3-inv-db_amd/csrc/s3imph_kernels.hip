@@ -21,9 +21,32 @@ namespace {
 constexpr int kBlock = 256;
 
 // ----------------------------------------------------------------------------------
-__global__ void k_init_state(LevelState* st, uint64_t n, uint64_t out_cap) {
+// Also samples kSkewSamples evenly spaced key lengths (when offsets are given): a set
+// whose longest sampled key exceeds twice the mean + 16 B is hashed length-sorted
+// (st->skew), since a wave runs as long as its longest key.
+constexpr int kSkewSamples = 4096;
+__global__ void k_init_state(LevelState* st, uint64_t n, uint64_t out_cap, const uint64_t* offsets) {
+  __shared__ unsigned long long s_max[kBlock / 64], s_sum[kBlock / 64];
   unsigned long long* p = reinterpret_cast<unsigned long long*>(st);
   for (size_t i = threadIdx.x; i < sizeof(LevelState) / 8; i += blockDim.x) p[i] = 0;
+  unsigned long long mx = 0, sm = 0;
+  if (offsets && n) {
+    for (int q = threadIdx.x; q < kSkewSamples; q += blockDim.x) {
+      const uint64_t i = (uint64_t)q * n / kSkewSamples;
+      const unsigned long long len = offsets[i + 1] - offsets[i];
+      mx = max(mx, len);
+      sm += len;
+    }
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    mx = max(mx, (unsigned long long)__shfl_xor(mx, d));
+    sm += __shfl_xor(sm, d);
+  }
+  if (lane_id() == 0) {
+    s_max[threadIdx.x >> 6] = mx;
+    s_sum[threadIdx.x >> 6] = sm;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint64_t w = level_words(n);
@@ -33,6 +56,12 @@ __global__ void k_init_state(LevelState* st, uint64_t n, uint64_t out_cap) {
     st->woff[1] = w;
     st->magic[0] = level_magic(w);
     st->out_cap = out_cap;
+    unsigned long long gm = 0, gs = 0;
+    for (int k = 0; k < kBlock / 64; ++k) {
+      gm = max(gm, s_max[k]);
+      gs += s_sum[k];
+    }
+    st->skew = offsets && n && gm * kSkewSamples > 2 * gs + 16ull * kSkewSamples;
   }
 }
 
@@ -186,8 +215,8 @@ int default_grid(uint64_t work, int block) {
   return (int)g;
 }
 
-void launch_init_state(LevelState* st, uint64_t n, uint64_t out_cap, hipStream_t s) {
-  k_init_state<<<1, 256, 0, s>>>(st, n, out_cap);
+void launch_init_state(LevelState* st, uint64_t n, uint64_t out_cap, hipStream_t s, const uint64_t* offsets) {
+  k_init_state<<<1, kBlock, 0, s>>>(st, n, out_cap, offsets);
 }
 
 void launch_rank_scan(const uint64_t* bits, uint64_t cap_words, uint64_t* rank_base,
