@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include "s3imph_device.h"
+#include <algorithm>
 #include <cstdlib>
 
 #include "s3imph_internal.h"
@@ -1541,9 +1542,10 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       const char* e = std::getenv("S3IMPH_HASH_MODE");
       return e ? std::atoi(e) : 0;
     }();
+    // the length-sorted variant holds one 1024-thread block per CU (its VGPRs): launch that many
 #define S3_HASH(KS, KV, GATE)                                                                                   \
-  k_hash_count0<KS, KV><<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st, \
-                                                    g.tb, g.chunk, b.tcnt, GATE)
+  k_hash_count0<KS, KV><<<KS ? std::min(grid_chunks, 256) : grid_chunks, kCB, 0, s>>>(                         \
+      blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, GATE)
     switch (mode) {
       case 1: S3_HASH(false, 1, -1); break;
       case 2: S3_HASH(true, 0, -1); break;

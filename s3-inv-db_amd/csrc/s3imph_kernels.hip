@@ -24,18 +24,24 @@ constexpr int kBlock = 256;
 // Also samples kSkewSamples evenly spaced key lengths (when offsets are given): a set
 // whose longest sampled key exceeds twice the mean + 16 B is hashed length-sorted
 // (st->skew), since a wave runs as long as its longest key.
-constexpr int kSkewSamples = 4096;
+constexpr int kSkewSamples = 1024;  // 4 per thread, all loads in flight together
 __global__ void k_init_state(LevelState* st, uint64_t n, uint64_t out_cap, const uint64_t* offsets) {
   __shared__ unsigned long long s_max[kBlock / 64], s_sum[kBlock / 64];
   unsigned long long* p = reinterpret_cast<unsigned long long*>(st);
   for (size_t i = threadIdx.x; i < sizeof(LevelState) / 8; i += blockDim.x) p[i] = 0;
   unsigned long long mx = 0, sm = 0;
   if (offsets && n) {
-    for (int q = threadIdx.x; q < kSkewSamples; q += blockDim.x) {
-      const uint64_t i = (uint64_t)q * n / kSkewSamples;
-      const unsigned long long len = offsets[i + 1] - offsets[i];
-      mx = max(mx, len);
-      sm += len;
+    unsigned long long a[kSkewSamples / kBlock], b[kSkewSamples / kBlock];
+#pragma unroll
+    for (int u = 0; u < kSkewSamples / kBlock; ++u) {
+      const uint64_t i = (uint64_t)(threadIdx.x + u * kBlock) * n / kSkewSamples;
+      a[u] = offsets[i];
+      b[u] = offsets[i + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < kSkewSamples / kBlock; ++u) {
+      mx = max(mx, b[u] - a[u]);
+      sm += b[u] - a[u];
     }
   }
 #pragma unroll
