@@ -36,8 +36,8 @@ constexpr int kCB = 1024;             // count block
 constexpr int kSB = 1024;             // scatter block
 constexpr int kTailT = 1024;          // tail block
 constexpr unsigned kLenBuckets = 256;  // key-length classes (4 B each) of the level-0 hash sort
-constexpr uint64_t kTcntWords = (uint64_t)kResLevels * kMaxTiles * kResShards;
-constexpr uint64_t kLdsTiles = kMaxTiles;  // histogram / cursor entries in LDS
+constexpr uint64_t kTcntWords = (uint64_t)kResLevels * kScatterTiles * kResShards;
+constexpr uint64_t kLdsTiles = kScatterTiles;  // count / start / cursor entries of the LDS-staged scatters
 constexpr unsigned long long kGate = kTailKeys;
 constexpr int kTailW32 = (int)(2 * ((kGammaNum * kTailKeys + 63) / 64));  // A/C words of the largest tail level
 constexpr unsigned long long kFlagAgg = 1ull << 62;
@@ -88,7 +88,7 @@ __device__ __forceinline__ uint64_t block_exscan(uint64_t v, uint64_t* total) {
 }
 
 __device__ __forceinline__ bool geom_ok(LevelState* st, uint64_t T, uint64_t B) {
-  if (T > kLdsTiles || T * B > kHistCap) {
+  if (T > kMaxTiles || T * B > kHistCap) {
     if (threadIdx.x == 0) atomicOr(&st->status, kStGeometry);
     return false;
   }
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__
                                                      unsigned long long* __restrict__ sflags, LevelState* st,
                                                      unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt,
                                                      int gate) {
-  __shared__ unsigned sh[kLdsTiles];
+  __shared__ unsigned sh[kMaxTiles];
   __shared__ unsigned lcnt[kLenBuckets];
   __shared__ unsigned short sidx[kCB];
   __shared__ uint64_t sb0[kCB], sb1[kCB], sh1[kCB], sh2[kCB];
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(kCB) void k_count(int level, const Rec* __restrict_
                                                unsigned long long* __restrict__ flags,
                                                unsigned long long* __restrict__ sflags, LevelState* st,
                                                unsigned tb, uint64_t chunk, uint64_t cap_words) {
-  __shared__ unsigned sh[kLdsTiles];
+  __shared__ unsigned sh[kMaxTiles];
   const int p = level - 1;
   const bool preset = st->preset[level] != 0;
   if (!preset && p > 0 && !st->preset[p] && st->n[p] <= kGate) return;  // previous level ran in the tail
@@ -328,6 +328,10 @@ __global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __re
   const uint64_t n = st->n[level];
   const uint64_t words = st->words[level], magic = st->magic[level];
   const uint64_t T = st->ntiles[level], B = st->nchunks[level];
+  if (T > kLdsTiles) {  // the host predicted fewer tiles: rerun (k_scatter_direct takes any T)
+    if (threadIdx.x == 0) atomicOr(&st->status, kStGeometry);
+    return;
+  }
   const uint64_t plo = level_range(st, level, words).plo;
   const uint64_t seed = level_seed(level);
   // Blocks b, b+8, b+16, ... (one XCD under round-robin dispatch) share one contiguous
@@ -433,6 +437,50 @@ __global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __re
       for (uint64_t t = tid; t < T; t += kSB) {
         cur[t] += cnt[t];
         cnt[t] = 0;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------ direct scatter -------
+// The counted scatter without the LDS staging: each chunk's per-tile cursors live in
+// LDS and every record goes straight to its slot (S3IMPH_SCATTER_DIRECT=1).  Measured
+// with 12k tiles of 2^14 positions on C3's level 0 it was 1.8x slower than the staged
+// scatter over 3k tiles of 2^16 positions, so it is a tested alternative, not a path.
+constexpr int kDU = 4;  // records in flight per thread
+__global__ __launch_bounds__(kSB) void k_scatter_direct(int level, const uint64_t* __restrict__ ik,
+                                                        const uint64_t* __restrict__ ifp,
+                                                        const uint64_t* __restrict__ ipos, uint64_t pos_base,
+                                                        const Rec* __restrict__ ilist,
+                                                        const unsigned* __restrict__ off, Rec* __restrict__ bucket,
+                                                        LevelState* st, unsigned tb, uint64_t chunk) {
+  __shared__ unsigned cur[kMaxTiles];
+  if (!level_active(level, st)) return;
+  const uint64_t n = st->n[level];
+  const uint64_t words = st->words[level], magic = st->magic[level];
+  const uint64_t T = st->ntiles[level], B = st->nchunks[level];
+  const uint64_t plo = level_range(st, level, words).plo;
+  const uint64_t seed = level_seed(level);
+  const unsigned tid = threadIdx.x;
+  for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    for (uint64_t t = tid; t < T; t += kSB) cur[t] = off[t * B + b];
+    __syncthreads();
+    const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
+    for (uint64_t i0 = lo + tid; i0 < hi; i0 += (uint64_t)kSB * kDU) {
+      Rec r[kDU];
+#pragma unroll
+      for (int u = 0; u < kDU; ++u) {
+        const uint64_t i = i0 + (uint64_t)u * kSB;
+        if (i < hi) r[u] = ilist ? ilist[i] : Rec{ik[i], ifp[i], ipos ? ipos[i] : pos_base + i};
+      }
+#pragma unroll
+      for (int u = 0; u < kDU; ++u) {
+        const uint64_t i = i0 + (uint64_t)u * kSB;
+        if (i < hi) {
+          const unsigned t = (unsigned)((bb_index(seed, r[u].k, words, magic) - plo) >> tb);
+          bucket[atomicAdd(&cur[t], 1u)] = r[u];
+        }
       }
     }
     __syncthreads();
@@ -718,11 +766,15 @@ size_t hash_scatter0_lds_bytes(int R, uint64_t T) {
 // --------------------------------------------------------------------- tile --------
 // dyn LDS: A[tpw], C[tpw] u32 (C becomes the per-word rank prefix after finalize);
 // for tiles of <= 2^kCacheBits positions also loc[kCache] u16 (each record's
-// in-tile position), ridx[kCache] u16 (rank -> record) and a redo bitmask.
-constexpr unsigned kCacheBits = 15;
+// in-tile position), ridx[kRank] u16 (rank -> record) and a redo bitmask.
+constexpr unsigned kCacheBits = 16;
 // Records cached per tile: a tile of 2^tb positions holds 2^tb / 2 keys on average
 // (gamma = 2), so 5/8 of 2^tb covers it with > 30 sigma to spare.
 __host__ __device__ constexpr unsigned cache_keys(unsigned tb) { return (5u << tb) / 8; }
+// Rank table entries: every cached record up to 2^15-position tiles; for 2^16 (149 KiB of
+// LDS in all) 3/8 of 2^tb, against ~0.30 x 2^tb settled keys (a tile that settles more
+// writes its outputs in record order instead).
+__host__ __device__ constexpr unsigned rank_keys(unsigned tb) { return tb < 16 ? cache_keys(tb) : (3u << tb) / 8; }
 constexpr int kTU = 4;                         // loads in flight per lane
 
 // Decoupled look-back run by one wave: lane i inspects tile (t-1-i) of the current
@@ -844,9 +896,10 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
   uint32_t* sC = dyn + tpw;
   const bool small = tb <= kCacheBits && mode == 0;
   const unsigned kcap = small ? cache_keys(tb) : 0;
+  const unsigned rcap = small ? rank_keys(tb) : 0;
   unsigned short* sloc = reinterpret_cast<unsigned short*>(dyn + 2 * tpw);
   unsigned short* sridx = sloc + kcap;
-  uint64_t* srm = reinterpret_cast<uint64_t*>(sridx + kcap);  // kcap / 64 words
+  uint64_t* srm = reinterpret_cast<uint64_t*>(sridx + rcap);  // kcap / 64 words
   uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[level] + rg.plo / 64);
   const uint64_t seed = level_seed(level);
   const uint64_t lvl_base = st->lvl_base[level];
@@ -936,7 +989,33 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
     TPROF(3);
     const uint64_t base = lvl_base + s_prefix;
     unsigned wc = 0;
-    if (cached) {
+    if (cached && pop > rcap) {
+      // ---- more settled keys than the rank table holds: outputs in record order from the
+      // cached locs (no rehash), redo bitmask by ballot
+      if (base + pop > N && out_on) bad = true;
+      const bool wr = out_on && base + pop <= N;
+      for (uint64_t jb = wave * 64; jb < nk; jb += NT) {
+        const uint64_t j = jb + lane;
+        bool redo = false;
+        if (j < nk) {
+          const unsigned loc = sloc[j];
+          const uint32_t wv = sA[loc >> 5];
+          const uint32_t bit = 1u << (loc & 31);
+          if (wv & bit) {
+            if (wr) {
+              const uint64_t p = base + sC[loc >> 5] + __popc(wv & (bit - 1));
+              fp_out[p] = rb[j].f;
+              pos_out[p] = rb[j].p;
+            }
+          } else {
+            redo = true;
+          }
+        }
+        const uint64_t m = __ballot(redo);
+        if (lane == 0) srm[jb >> 6] = m;
+        wc += __popcll(m);
+      }
+    } else if (cached) {
       // ---- rank pass (LDS only): rank -> record index; redo bitmask by ballot
       for (uint64_t jb = wave * 64; jb < nk; jb += NT) {
         const uint64_t j = jb + lane;
@@ -1511,7 +1590,8 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
 size_t tile_lds_bytes(unsigned tb) {
   const size_t ac = 2ull * (1ull << (tb - 5)) * sizeof(uint32_t);
   const size_t kc = cache_keys(tb);
-  return tb <= kCacheBits ? ac + 2 * kc * sizeof(unsigned short) + (kc / 64 + 1) * sizeof(uint64_t) : ac;
+  if (tb <= kCacheBits) return ac + (kc + rank_keys(tb)) * sizeof(unsigned short) + (kc / 64 + 1) * sizeof(uint64_t);
+  return ac;
 }
 
 }  // namespace
@@ -1522,9 +1602,9 @@ void binned_set_lds_limits() {
   (void)hipFuncSetAttribute((const void*)k_hash_scatter0<1024, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)hash_scatter0_lds_bytes(2048, kLdsTiles));
   (void)hipFuncSetAttribute((const void*)k_tile<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)tile_lds_bytes(kTileMaxBits));
+                            (int)std::max(tile_lds_bytes(kTileMaxBits), tile_lds_bytes(kCacheBits)));
   (void)hipFuncSetAttribute((const void*)k_tile<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)tile_lds_bytes(kTileMaxBits));
+                            (int)std::max(tile_lds_bytes(kTileMaxBits), tile_lds_bytes(kCacheBits)));
   (void)hipFuncSetAttribute((const void*)k_tile_reg<512, 20, 2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)tile_reg_lds_bytes(kRegMaxBits));
   (void)hipFuncSetAttribute((const void*)k_tile_reg<512, 20, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1568,8 +1648,17 @@ void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s)
   k_hscan<<<grid, kHST, 0, s>>>(level, b.hist, b.off, b.tile_start, b.sflags, b.st);
 }
 
-void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s) {
+void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s, bool direct) {
   const Rec* il = level == 0 && !b.dist ? nullptr : b.list[(level - 1) & 1];
+  static const bool force_direct = [] {  // test knob: every counted level scatters directly
+    const char* e = std::getenv("S3IMPH_SCATTER_DIRECT");
+    return e && e[0] == '1';
+  }();
+  if (direct || force_direct) {
+    k_scatter_direct<<<512, kSB, 0, s>>>(level, b.kh, b.fp, b.pos, b.pos_base, il, b.off, b.bucket, b.st, g.tb,
+                                         g.chunk);
+    return;
+  }
   k_scatter<<<256, kSB, 0, s>>>(level, b.kh, b.fp, b.pos, b.pos_base, il, b.off, b.bucket, b.st, g.tb, g.chunk);
 }
 
@@ -1577,7 +1666,7 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
   if (b.tile_mode == 0 && g.tb <= kRegMaxBits) {
     // records per tile ~2^(tb-1): pick the variant whose NT x R covers it with margin
     // (lighter variants keep several tiles resident per CU)
-    const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kMaxTiles * kResShards : nullptr;
+    const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kScatterTiles * kResShards : nullptr;
     const size_t lds = tile_reg_lds_bytes(g.tb);
 #define S3_TILE_REG(NT_, R_, W_)                                                                             \
   (tc ? k_tile_reg<NT_, R_, W_, true> : k_tile_reg<NT_, R_, W_, false>)<<<grid_tiles, NT_, lds, s>>>(level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags, \
@@ -1611,7 +1700,7 @@ void launch_hash_scatter0(const uint8_t* blob, const uint64_t* offsets, uint64_t
 }
 
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s) {
-  k_scatter_res<<<grid, kSB, 0, s>>>(level, b.list[(level - 1) & 1], b.tcnt + (uint64_t)level * kMaxTiles * kResShards,
+  k_scatter_res<<<grid, kSB, 0, s>>>(level, b.list[(level - 1) & 1], b.tcnt + (uint64_t)level * kScatterTiles * kResShards,
                                      b.bucket, b.bucket_cap, b.flags, b.st, g.tb, b.cap_words, b.tile_prof);
 }
 

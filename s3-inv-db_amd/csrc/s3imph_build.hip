@@ -106,7 +106,7 @@ struct s3imph_ctx {
   unsigned *hist = nullptr, *hoff = nullptr, *tile_start = nullptr, *scan_sums = nullptr;
   unsigned long long* flags = nullptr;
   unsigned long long* sflags = nullptr;
-  unsigned* tcnt = nullptr;  // reservation-path shard fills, kResLevels x kMaxTiles x kResShards
+  unsigned* tcnt = nullptr;  // reservation-path shard fills, kResLevels x kScatterTiles x kResShards
   int tile_mode = 0;
   int tile_block = 1024;
   uint64_t target_tiles = kTargetTiles, target_tiles0 = kTargetTiles0, target_chunks = kTargetChunks;
@@ -228,7 +228,7 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   dalloc(c->scan_sums, kHistCap / 2048 + 2);
   dalloc(c->flags, kMaxTiles + 2);
   dalloc(c->sflags, kHistCap / kScanSeg + 2);
-  dalloc(c->tcnt, (uint64_t)kResLevels * kMaxTiles * kResShards);
+  dalloc(c->tcnt, (uint64_t)kResLevels * kScatterTiles * kResShards);
   alloc_common(c, cap);
   dalloc(c->bits, c->cap_words);
   dalloc(c->rank_base, c->cap_words);
@@ -445,9 +445,10 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   launch_init_state(c->d_st, n, n, s, offsets);
   ev_mark(c, s, "init");
   const Grids gr = level_grids(n, 64 * level_words(n), g0);
-  if (!conservative && c->l0_mode && g0.tb <= kRegTileMaxBits) {
+  if (!conservative && c->l0_mode && g0.tb <= kRegTileMaxBits &&
+      ((64 * level_words(n) + (1ull << g0.tb) - 1) >> g0.tb) <= kScatterTiles) {
     // fused level 0: hash straight into reservation slots, then the sharded tile kernel
-    HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kMaxTiles * kResShards * sizeof(unsigned), s));
+    HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kScatterTiles * kResShards * sizeof(unsigned), s));
     launch_hash_scatter0(blob, offsets, n, b, g0, c->l0_mode - 1, s);
     ev_mark(c, s, "hash_scatter0");
     launch_binned_tile(0, b, g0, gr.gt, s, true);
@@ -724,7 +725,7 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
   dalloc(c->scan_sums, kHistCap / 2048 + 2);
   dalloc(c->flags, kMaxTiles + 2);
   dalloc(c->sflags, kHistCap / kScanSeg + 2);
-  dalloc(c->tcnt, (uint64_t)kResLevels * kMaxTiles * kResShards);
+  dalloc(c->tcnt, (uint64_t)kResLevels * kScatterTiles * kResShards);
   c->cap_words = capw;
   dalloc(c->bits, capw);
   dalloc(c->rank_base, capw);
@@ -761,7 +762,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   const BinBuffers b = make_bufs(c, nullptr, fp_out, pos_out, s);
   const double q = 1.0 - std::exp(-0.5);
   launch_init_state(st, 0, out_cap, s);
-  HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kMaxTiles * kResShards * sizeof(unsigned), s));
+  HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kScatterTiles * kResShards * sizeof(unsigned), s));
   launch_dist_setup(st, 0, nullptr, N, R, P, s);
   ev_mark(c, s, "init");
   std::vector<uint64_t> hw, hS;  // words and per-rank range of each distributed level

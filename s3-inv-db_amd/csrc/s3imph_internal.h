@@ -66,7 +66,8 @@ __device__ __forceinline__ bool level_out_on(const LevelState* st, int L) {
 // per-tile buckets in chunks of `chunk` keys.
 constexpr unsigned kTileMaxBits = 19;                 // 2 x 64 KiB LDS bit vectors
 constexpr unsigned kTileMinBits = 10;
-constexpr uint64_t kMaxTiles = 4096;                  // LDS histogram bound (16 KiB)
+constexpr uint64_t kMaxTiles = 4096;                  // tiles per level (LDS histogram / scatter cursors)
+constexpr uint64_t kScatterTiles = kMaxTiles;         // LDS-staged scatters (count/start/cursor per tile)
 constexpr uint64_t kTargetTiles0 = 2048;              // level 0: 2^14-position tiles at 10M keys
 constexpr uint64_t kTargetTiles = 1024;               // levels >= 1 on the counted path
 constexpr uint64_t kTargetTilesRes = 256;             // reservation-path levels: ~1 tile per CU
@@ -158,7 +159,7 @@ struct BinBuffers {
   unsigned* scan_sums;                  // scan block sums
   unsigned long long* flags;            // decoupled look-back words, one per tile
   unsigned long long* sflags;           // look-back words of the histogram scan
-  unsigned* tcnt;                       // reservation-path shard fills, kResLevels x kMaxTiles x kResShards
+  unsigned* tcnt;                       // reservation-path shard fills, kResLevels x kScatterTiles x kResShards
   uint64_t bucket_cap;                  // bucket capacity in records
   int tile_mode;
   int tile_block;                       // tile workgroup size (512 or 1024)
@@ -174,7 +175,7 @@ void binned_set_lds_limits();
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s);
 void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s);
-void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s);
+void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s, bool direct = false);
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s,
                         bool reserved = false);
 void launch_hash_scatter0(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,

@@ -309,3 +309,39 @@ def test_level0_variants_bit_exact(s3, oracle_lib, monkeypatch, l0, n, kind, avg
         assert np.array_equal(gpo, po)
     finally:
         c.close()
+
+
+def test_big_tiles_bit_exact(s3, oracle_lib):
+    """70M keys: level 0 needs 2^16-position tiles to stay within 4096 tiles, so it runs
+    the generic tile kernel with only the in-tile positions cached in LDS; level 1
+    (2^15-position tiles) the fully cached one.  Bit-exact with the oracle."""
+    c = s3.DeviceBuilder(0)
+    try:
+        n = 70_000_000
+        blob, offs = s3.gen_keys(0, 31, 12, 0, n)
+        st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)
+        assert st == 0
+        gfp, gpo, gmph, info = _device_build(s3, c, blob, offs)
+        assert gmph == mph
+        assert np.array_equal(gfp, fp) and np.array_equal(gpo, po)
+    finally:
+        c.close()
+
+
+def test_direct_scatter_forced_small(s3, oracle_lib, monkeypatch):
+    """The direct scatter on every counted level (S3IMPH_SCATTER_DIRECT=1), small sets."""
+    monkeypatch.setenv("S3IMPH_SCATTER_DIRECT", "1")
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path[:0]=[%r, %r]\n"
+        "import numpy as np, torch, s3imph, oracle as O\n"
+        "for n, kind, avg in [(300_000, 0, 24), (2_500_000, 1, 0)]:\n"
+        "    blob, offs = s3imph.gen_keys(kind, 3, avg, 0, n)\n"
+        "    st, fp, po, mph = O.lib().build(blob[: offs[-1]], offs)\n"
+        "    g = s3imph.build_host(blob, offs)\n"
+        "    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po), n\n"
+        "print('ok')\n"
+    ) % (os.path.join(os.path.dirname(GOLDEN), "..", "s3-inv-db_amd"), os.path.join(os.path.dirname(GOLDEN), "..", "oracle"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
