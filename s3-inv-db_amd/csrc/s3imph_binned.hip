@@ -114,8 +114,9 @@ __device__ __forceinline__ void hash_key(const uint8_t* blob, uint64_t b0, uint6
 
 // gate >= 0: run only if st->skew == gate (k_init_state sampled the key lengths), so the
 // direct and the length-sorted variant are both enqueued and the device picks one.
+// gate == -2: sort every group, skewed or not.
 template <bool kSort, int kBatched>
-__global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__ blob,
+__global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restrict__ blob,
                                                      const uint64_t* __restrict__ offsets, uint64_t n,
                                                      uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
                                                      unsigned* __restrict__ hist,
@@ -190,7 +191,7 @@ __global__ __launch_bounds__(kCB) void k_hash_count0(const uint8_t* __restrict__
         gsum += s_lsum[w];
       }
       const uint64_t gcnt = min<uint64_t>(kCB, hi - g);
-      if (gmax * gcnt <= 2 * gsum + 16 * gcnt) {
+      if (gate != -2 && gmax * gcnt <= 2 * gsum + 16 * gcnt) {
         if (i < hi) {
           uint64_t h1, h2;
           hash_key<kBatched>(blob, b0, b1, h1, h2);
@@ -1622,9 +1623,8 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       const char* e = std::getenv("S3IMPH_HASH_MODE");
       return e ? std::atoi(e) : 0;
     }();
-    // the length-sorted variant holds one 1024-thread block per CU (its VGPRs): launch that many
 #define S3_HASH(KS, KV, GATE)                                                                                   \
-  k_hash_count0<KS, KV><<<KS ? std::min(grid_chunks, 256) : grid_chunks, kCB, 0, s>>>(                         \
+  k_hash_count0<KS, KV><<<grid_chunks, kCB, 0, s>>>(                                                       \
       blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, GATE)
     switch (mode) {
       case 1: S3_HASH(false, 1, -1); break;
@@ -1633,6 +1633,8 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       case 4: S3_HASH(true, 1, -1); break;
       case 7: S3_HASH(false, 2, -1); break;
       case 8: S3_HASH(true, 2, -1); break;
+      case 9: S3_HASH(true, 2, -2); break;
+      case 10: S3_HASH(true, 0, -2); break;
       default:
         S3_HASH(false, 2, 0);
         S3_HASH(true, 1, 1);

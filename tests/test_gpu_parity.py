@@ -328,6 +328,27 @@ def test_big_tiles_bit_exact(s3, oracle_lib):
         c.close()
 
 
+@pytest.mark.parametrize("mode", ["1", "3", "4", "8", "9"])
+def test_hash_variants_bit_exact(s3, oracle_lib, monkeypatch, mode):
+    """Every level-0 hash variant (S3IMPH_HASH_MODE: batched / single loads, length-sorted,
+    forced sort) on ragged sets: bit-exact."""
+    monkeypatch.setenv("S3IMPH_HASH_MODE", mode)
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path[:0]=[%r, %r]\n"
+        "import numpy as np, torch, s3imph, oracle as O\n"
+        "for n, kind, avg in [(1, 0, 8), (3000, 0, 40), (300_000, 0, 64), (2_500_000, 1, 0)]:\n"
+        "    blob, offs = s3imph.gen_keys(kind, 7, avg, 0, n)\n"
+        "    st, fp, po, mph = O.lib().build(blob[: offs[-1]], offs)\n"
+        "    g = s3imph.build_host(blob, offs)\n"
+        "    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po), n\n"
+        "print('ok')\n"
+    ) % (os.path.join(os.path.dirname(GOLDEN), "..", "s3-inv-db_amd"), os.path.join(os.path.dirname(GOLDEN), "..", "oracle"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
 def test_direct_scatter_forced_small(s3, oracle_lib, monkeypatch):
     """The direct scatter on every counted level (S3IMPH_SCATTER_DIRECT=1), small sets."""
     monkeypatch.setenv("S3IMPH_SCATTER_DIRECT", "1")

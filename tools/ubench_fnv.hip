@@ -1,0 +1,62 @@
+// Microbenchmark: VALU cost of the FNV-1a + FNV-1 byte step on gfx950, from registers
+// only (no memory traffic), at full occupancy.  Prints ns and cycles per byte-step
+// per lane, so the level-0 hash kernel's compute floor can be priced.
+//   hipcc -O3 --offload-arch=gfx950 tools/ubench_fnv.hip -o /tmp/ubench_fnv
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+constexpr uint64_t kP = 0x100000001b3ull;
+
+template <int kMode>
+__global__ __launch_bounds__(256) void k_fnv(uint64_t* out, int iters, uint64_t seed) {
+  uint64_t a = seed ^ (threadIdx.x + 977ull * blockIdx.x), b = a * 3;
+  uint64_t v = a * 0x9e3779b97f4a7c15ull;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const uint32_t byte = (uint32_t)(v >> (8 * t)) & 0xffu;
+      if (kMode == 0) {  // both hashes (the build's step)
+        a = (a ^ byte) * kP;
+        b = (b * kP) ^ byte;
+      } else if (kMode == 1) {  // FNV-1a only
+        a = (a ^ byte) * kP;
+      } else {  // calibration: same chain shape with 64-bit adds instead of multiplies
+        a = (a ^ byte) + kP;
+        b = (b + kP) ^ byte;
+      }
+    }
+    v += 0x632be59bd9b4e019ull;
+  }
+  if ((a ^ b) == 0x1234567) out[0] = a + b;
+}
+
+int main() {
+  uint64_t* d;
+  hipMalloc(&d, 64);
+  const int blocks = 256 * 8, iters = 4096;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  int clk = 0;
+  hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, 0);
+  for (int mode = 0; mode < 3; ++mode) {
+    for (int rep = 0; rep < 3; ++rep) {
+      hipEventRecord(e0);
+      if (mode == 0) k_fnv<0><<<blocks, 256>>>(d, iters, rep);
+      else if (mode == 1) k_fnv<1><<<blocks, 256>>>(d, iters, rep);
+      else k_fnv<2><<<blocks, 256>>>(d, iters, rep);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms;
+      hipEventElapsedTime(&ms, e0, e1);
+      const double steps = (double)blocks * 256 * iters * 8;  // byte-steps over all lanes
+      const double lane_steps_per_s = steps / (ms * 1e-3);
+      // 256 CUs x 4 SIMDs; a full-rate wave64 VALU op = 64 lane-ops per SIMD per (1 or 2) cycles
+      printf("mode %d rep %d: %.3f ms, %.2f T byte-steps/s, %.3f SIMD-cycles per wave byte-step (clk %d kHz)\n",
+             mode, rep, ms, lane_steps_per_s * 1e-12,
+             (ms * 1e-3) * (clk * 1e3) * 1024.0 / (steps / 64.0), clk);
+    }
+  }
+  return 0;
+}
