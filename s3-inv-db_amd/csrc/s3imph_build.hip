@@ -113,6 +113,9 @@ struct s3imph_ctx {
   uint64_t res_max_keys = kResMaxKeys;
   int l0_mode = 0;  // level 0: 0 hash+count / scan / scatter; 1, 2 fused hash+scatter (4096 / 2048-key rounds)
   uint64_t target_tiles_res = kTargetTilesRes;
+  // reservation slots hold >= 4x a tile's mean fill, 2x on levels above kResSmallKeys
+  // (full 256-block grids: every XCD shard of a slot then fills evenly)
+  uint64_t res_fill = 2;
   bool debug = false;
   unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps
   bool lds_attr_set = false;
@@ -392,7 +395,7 @@ Grids level_grids(uint64_t nk, uint64_t size, LevelGeom g) {
 void enqueue_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, uint64_t size, bool conservative,
                         const LevelGeom* force, hipStream_t s) {
   // reservation slots are bucket_cap / T records per tile: keep them >= 4x the mean fill
-  const bool res = !conservative && nb <= c->res_max_keys && nb * 4 <= c->bucket_cap && L < kResLevels &&
+  const bool res = !conservative && nb <= c->res_max_keys && nb * (nb > kResSmallKeys ? c->res_fill : 4) <= c->bucket_cap && L < kResLevels &&
                    c->tile_mode == 0;
   const LevelGeom g = force ? *force
                       : res ? choose_geom_sz(nb, size, c->target_tiles_res, c->target_chunks, kRegTileMaxBits)
@@ -1222,6 +1225,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     if (const char* m = std::getenv("S3IMPH_CHUNKS")) c->target_chunks = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_RES_MAX")) c->res_max_keys = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_TARGET_TILES_RES")) c->target_tiles_res = std::strtoull(m, nullptr, 10);
+    if (const char* m = std::getenv("S3IMPH_RES_FILL")) c->res_fill = std::strtoull(m, nullptr, 10);
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     if (const char* m = std::getenv("S3IMPH_TILE_BLOCK")) c->tile_block = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);

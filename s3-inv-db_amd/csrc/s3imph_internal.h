@@ -91,7 +91,8 @@ struct LevelGeom {
 // chunk count is sized to fill the resident blocks in one round), few enough that
 // tiles x chunks stays under kHistCap.
 constexpr uint64_t kChunkGran = 1024;
-constexpr uint64_t kResMaxKeys = 2ull << 20;  // levels up to this size use the reservation scatter
+constexpr uint64_t kResMaxKeys = 64ull << 20;  // levels up to this size use the reservation scatter
+constexpr uint64_t kResSmallKeys = 2ull << 20;  // ... with 4x slot headroom up to this size, 2x above
 constexpr int kResShards = 8;                 // per-tile reservation counters (one per XCD)
 constexpr int kResLevels = 32;                // levels that may use the reservation path
 constexpr double kTailMargin = 1.1;
