@@ -1431,18 +1431,26 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
 }
 
 // --------------------------------------------------------------------- tail --------
-// Every remaining level in one workgroup: A/C and the rank prefix in LDS, outputs
-// written directly, collided records compacted into the other list.
+// Every remaining level in one workgroup, with the live records in LDS: the first tail
+// level's key hashes (and their input indices) are loaded once; each level marks A/C
+// in LDS, finalizes and ranks, writes the settled records' outputs in rank order (f, p
+// fetched from the first tail level's input list through an LDS rank -> index table)
+// and compacts the collided records in place for the next level.  No level after the
+// first reads or writes a record list.
 __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_launched, Rec* list0, Rec* list1, uint64_t* bits,
                                                      uint64_t cap_words, uint64_t* __restrict__ fp_out,
                                                      uint64_t* __restrict__ pos_out, LevelState* st,
                                                      unsigned long long* __restrict__ prof) {
+  __shared__ uint64_t ck[kTailKeys];           // live keys, as mix64(key hash)
+  __shared__ unsigned short cj[kTailKeys];     // ... and their index in the input list
+  __shared__ unsigned short srank[kTailKeys];  // settled rank -> input index
   __shared__ uint32_t sA[kTailW32];
   __shared__ uint32_t sC[kTailW32];
   __shared__ uint32_t spre[kTailW32];
-  __shared__ unsigned long long s_n, s_next;
+  __shared__ unsigned s_wc[kTailT / 64];
+  __shared__ unsigned long long s_n;
   __shared__ int s_level;
-  const unsigned tid = threadIdx.x, lane = lane_id();
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   if (tid == 0) {
     int L = first_level > 1 ? first_level : 1;
     while (L <= big_launched && st->n[L] > kGate) ++L;
@@ -1458,49 +1466,60 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
   __syncthreads();
   const uint64_t N = st->out_cap;
   bool bad = false;
+  const Rec* in = (s_level & 1) ? list0 : list1;  // written by the level before
+  {
+    constexpr int kR = (int)((kTailKeys + kTailT - 1) / kTailT);
+    const unsigned n0 = (unsigned)s_n;
+    uint64_t k[kR];
+#pragma unroll
+    for (int u = 0; u < kR; ++u) {  // every load in flight before the first LDS store
+      const unsigned i = tid + u * kTailT;
+      k[u] = i < n0 ? in[i].k : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kR; ++u) {
+      const unsigned i = tid + u * kTailT;
+      if (i < n0) {
+        ck[i] = mix64(k[u]);  // the level-independent half of key_mix, once
+        cj[i] = (unsigned short)i;
+      }
+    }
+  }
+  __syncthreads();
   for (;;) {
     const int L = s_level;
-    const uint64_t n = s_n;
+    const unsigned n = (unsigned)s_n;
     // debug: level start times in the last prof row
     if (prof && tid == 0 && L < kMaxLevels) prof[(uint64_t)(kMaxLevels - 1) * kMaxTiles * 8 + L] = wall_clock64();
     if (n == 0) break;
     if (L >= kMaxLevels) {
+      // level budget exhausted: leave the unplaced keys in level L's list, where the host
+      // looks for duplicates (as mix64(key hash): a bijection, so duplicates are preserved)
       if (tid == 0) atomicOr(&st->status, kStTooManyLevels);
+      Rec* out = (L & 1) ? list0 : list1;
+      for (unsigned i = tid; i < n; i += kTailT) out[i] = Rec{ck[i], 0, 0};
       break;
     }
     const uint64_t words = st->words[L], magic = st->magic[L], woff = st->woff[L];
     const uint64_t base = st->lvl_base[L];
     const unsigned w32 = (unsigned)(2 * words);
-    const Rec* in = (L & 1) ? list0 : list1;  // level L's records were written by level L-1
-    Rec* out = (L & 1) ? list1 : list0;
     for (unsigned w = tid; w < w32; w += kTailT) {
       sA[w] = 0;
       sC[w] = 0;
     }
-    if (tid == 0) s_next = 0;
     __syncthreads();
     const uint64_t seed = level_seed(L);
-    for (uint64_t j0 = tid; j0 < n; j0 += (uint64_t)kTailT * kTU) {
-      uint64_t k[kTU];
-#pragma unroll
-      for (int u = 0; u < kTU; ++u) {
-        const uint64_t j = j0 + (uint64_t)u * kTailT;
-        k[u] = j < n ? in[j].k : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < kTU; ++u) {
-        if (j0 + (uint64_t)u * kTailT < n) {
-          const uint64_t x = bb_index(seed, k[u], words, magic);
-          const uint32_t bit = 1u << (x & 31);
-          const uint32_t old = atomicOr(&sA[x >> 5], bit);
-          if (old & bit) atomicOr(&sC[x >> 5], bit);
-        }
-      }
+    for (unsigned i = tid; i < n; i += kTailT) {
+      const uint32_t x = (uint32_t)bb_index_mk(seed, ck[i], words, magic);
+      const uint32_t bit = 1u << (x & 31);
+      const uint32_t old = atomicOr(&sA[x >> 5], bit);
+      if (old & bit) atomicOr(&sC[x >> 5], bit);
     }
     __syncthreads();
-    constexpr unsigned kPer = kTailW32 / kTailT;
+    constexpr unsigned kPer = (kTailW32 + kTailT - 1) / kTailT;
     uint64_t cnt = 0;
     uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + woff);
+#pragma unroll
     for (unsigned q = 0; q < kPer; ++q) {
       const unsigned w = tid * kPer + q;
       if (w < w32) {
@@ -1512,6 +1531,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
     }
     uint64_t tot;
     uint64_t run = block_exscan<kTailT>(cnt, &tot);
+#pragma unroll
     for (unsigned q = 0; q < kPer; ++q) {
       const unsigned w = tid * kPer + q;
       if (w < w32) {
@@ -1520,52 +1540,52 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
       }
     }
     __syncthreads();
-    for (uint64_t jb0 = tid & ~63u; jb0 < n; jb0 += (uint64_t)kTailT * kTU) {
-      uint64_t ck[kTU], cf[kTU], cp[kTU];
-#pragma unroll
-      for (int u = 0; u < kTU; ++u) {
-        const uint64_t j = jb0 + (uint64_t)u * kTailT + lane;
-        ck[u] = cf[u] = cp[u] = 0;
-        if (j < n) {
-          ck[u] = in[j].k;
-          cf[u] = in[j].f;
-          cp[u] = in[j].p;
-        }
+    // settled -> rank table; collided -> compacted in place, one block-wide segment of
+    // kTailT records at a time (a record only moves down, never past its segment's end)
+    unsigned n1 = 0;
+    for (unsigned i0 = 0; i0 < n; i0 += kTailT) {
+      const unsigned i = i0 + tid;
+      bool coll = false;
+      uint64_t k = 0;
+      unsigned j = 0;
+      if (i < n) {
+        k = ck[i];
+        j = cj[i];
+        const uint32_t x = (uint32_t)bb_index_mk(seed, k, words, magic);
+        const uint32_t wv = sA[x >> 5];
+        const uint32_t bit = 1u << (x & 31);
+        if (wv & bit) srank[spre[x >> 5] + __popc(wv & (bit - 1))] = (unsigned short)j;
+        else coll = true;
       }
+      const uint64_t m = __ballot(coll);
+      if (lane == 0) s_wc[wave] = (unsigned)__popcll(m);
+      __syncthreads();  // also: every read of this segment precedes the writes below
+      unsigned pre = n1, all = 0;
 #pragma unroll
-      for (int u = 0; u < kTU; ++u) {
-        const uint64_t j = jb0 + (uint64_t)u * kTailT + lane;
-        bool r = false;
-        if (j < n) {
-          const uint64_t x = bb_index(seed, ck[u], words, magic);
-          const uint32_t wv = sA[x >> 5];
-          const uint32_t bit = 1u << (x & 31);
-          if (wv & bit) {
-            const uint64_t q = base + spre[x >> 5] + __popc(wv & (bit - 1));
-            if (q < N) {
-              if (level_out_on(st, L)) {
-                fp_out[q] = cf[u];
-                pos_out[q] = cp[u];
-              }
-            } else if (level_out_on(st, L)) {
-              bad = true;
-            }
-          } else {
-            r = true;
-          }
-        }
-        const uint64_t m = __ballot(r);
-        if (m) {
-          unsigned long long o = 0;
-          if (lane == 0) o = atomicAdd(&s_next, (unsigned long long)__popcll(m));
-          o = __shfl(o, 0);
-          if (r) out[o + __popcll(m & lanemask_lt())] = Rec{ck[u], cf[u], cp[u]};
-        }
+      for (int w = 0; w < kTailT / 64; ++w) {
+        pre += (unsigned)w < wave ? s_wc[w] : 0u;
+        all += s_wc[w];
+      }
+      if (coll) {
+        const unsigned d = pre + (unsigned)__popcll(m & lanemask_lt());
+        ck[d] = k;
+        cj[d] = (unsigned short)j;
+      }
+      n1 += all;
+      __syncthreads();
+    }
+    if (level_out_on(st, L)) {
+      if (base + tot > N) bad = true;
+      const uint64_t m = base + tot <= N ? tot : 0;
+#pragma unroll 4
+      for (uint64_t i = tid; i < m; i += kTailT) {
+        const Rec* src = in + srank[i];
+        fp_out[base + i] = src->f;
+        pos_out[base + i] = src->p;
       }
     }
     __syncthreads();
     if (tid == 0) {
-      const uint64_t n1 = s_next;
       const uint64_t w1 = n1 ? level_words(n1) : 0;
       st->n[L + 1] = n1;
       st->words[L + 1] = w1;

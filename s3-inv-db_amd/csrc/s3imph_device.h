@@ -28,6 +28,18 @@ static __device__ __forceinline__ uint64_t bb_index(uint64_t seed, uint64_t key,
   return (r << 6) | (h & 63);
 }
 
+// bb_index with the level-independent half of key_mix already applied (mk = mix64(key)),
+// for code that revisits the same key at several levels.
+static __device__ __forceinline__ uint64_t bb_index_mk(uint64_t seed, uint64_t mk, uint64_t words,
+                                                     uint64_t magic) {
+  uint64_t h = mix64((seed ^ mk) * kHashM);
+  uint64_t q = h >> 6;
+  uint64_t qe = __umul64hi(q, magic);
+  uint64_t r = q - qe * words;
+  if (r >= words) r -= words;
+  return (r << 6) | (h & 63);
+}
+
 static __device__ __forceinline__ void fnv_step(uint64_t& a, uint64_t& b, uint32_t byte) {
   a = (a ^ byte) * kFnvPrime;  // FNV-1a (hashBytes)
   b = (b * kFnvPrime) ^ byte;  // FNV-1  (computeFingerprintBytes)

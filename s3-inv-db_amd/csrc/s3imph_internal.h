@@ -124,7 +124,7 @@ constexpr unsigned kStRouteOverflow = 256u;  // a multi-GPU send region overflow
 
 // Levels whose active-key count is at most this run inside one workgroup with
 // LDS-resident bit vectors (k_tail); larger levels run as full-grid kernels.
-constexpr unsigned long long kTailKeys = 16384;
+constexpr unsigned long long kTailKeys = 12288;
 constexpr int kTailThreads = 1024;
 constexpr int kTailLdsWords32 = 2 * 2 * ((kGammaNum * kTailKeys + 63) / 64);  // A and C, u32 words
 
