@@ -104,11 +104,12 @@ __device__ __forceinline__ bool level_active(int level, const LevelState* st) {
 // Hash every key (FNV-1a key hash + FNV-1 fingerprint, one pass over the bytes),
 // store both in key order, and histogram the level-0 tiles per chunk.
 // kVar: 0 one load per word (fnv_both_loop), 1 batched 8-word loads (fnv_both),
-// 2 loads pipelined two words ahead (fnv_both_pf).
+// 2 loads pipelined two words ahead (fnv_both_pf), 3 16-byte loads (fnv_both_16).
 template <int kVar>
 __device__ __forceinline__ void hash_key(const uint8_t* blob, uint64_t b0, uint64_t b1, uint64_t& h1, uint64_t& h2) {
   if (kVar == 1) fnv_both(blob, b0, b1, h1, h2);
   else if (kVar == 2) fnv_both_pf(blob, b0, b1, h1, h2);
+  else if (kVar == 3) fnv_both_16(blob, b0, b1, h1, h2);
   else fnv_both_loop(blob, b0, b1, h1, h2);
 }
 
@@ -1636,10 +1637,12 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
                          LevelGeom g, int grid_chunks, hipStream_t s) {
   if (level == 0 && !b.dist) {
     static const int mode = [] {
-      // A/B knob: 0 auto (default: 7 for near-uniform lengths, 4 for skewed ones, picked
+      // A/B knob: 0 auto (default: 7 for near-uniform lengths, 14 for skewed ones, picked
       // on the device from sampled lengths); 1 direct, batched 8-word loads; 2 length-
       // sorted, one load per word; 3 direct, one load per word; 4 length-sorted, batched;
-      // 7 direct, loads two words ahead; 8 length-sorted, loads two words ahead.
+      // 7 direct, loads two words ahead; 8 length-sorted, loads two words ahead; 9 / 10
+      // sort every group (two ahead / one load per word); 13 / 14 direct / length-sorted
+      // with 16-byte loads.
       const char* e = std::getenv("S3IMPH_HASH_MODE");
       return e ? std::atoi(e) : 0;
     }();
@@ -1654,10 +1657,12 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       case 7: S3_HASH(false, 2, -1); break;
       case 8: S3_HASH(true, 2, -1); break;
       case 9: S3_HASH(true, 2, -2); break;
+      case 13: S3_HASH(false, 3, -1); break;
+      case 14: S3_HASH(true, 3, -1); break;
       case 10: S3_HASH(true, 0, -2); break;
       default:
         S3_HASH(false, 2, 0);
-        S3_HASH(true, 1, 1);
+        S3_HASH(true, 3, 1);
     }
 #undef S3_HASH
   } else {

@@ -124,6 +124,83 @@ static __device__ __forceinline__ void fnv_both_pf(const uint8_t* __restrict__ b
   hb = b;
 }
 
+// FNV-1a + FNV-1 of blob[b0, b1) from 16-byte aligned loads (half the load
+// instructions of the 8-byte variants), software-pipelined one chunk ahead.  Stream
+// chunk c = bytes [b0 + 16c, b0 + 16c + 16) = the 128-bit funnel of aligned chunks
+// C[c], C[c+1] by (b0 & 15) bytes.  Reads stay inside the 16-byte chunks overlapping
+// the key, and the last one is read as 8 bytes when the key ends in its low half, so
+// nothing past the key's last aligned 8-byte word is touched.
+struct U128 {
+  uint64_t lo, hi;
+};
+static __device__ __forceinline__ U128 ld_chunk(const uint8_t* p, bool full) {
+  U128 r;
+  if (full) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    r.lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    r.hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  } else {
+    r.lo = *reinterpret_cast<const uint64_t*>(p);
+    r.hi = 0;
+  }
+  return r;
+}
+static __device__ __forceinline__ void fnv_both_16(const uint8_t* __restrict__ blob, uint64_t b0, uint64_t b1,
+                                                   uint64_t& ha, uint64_t& hb) {
+  uint64_t a = kFnvOffset, b = kFnvOffset;
+  if (b1 > b0) {
+    const uint64_t c0 = b0 & ~15ull;
+    const uint8_t* base = blob + c0;
+    const uint64_t nc = ((b1 - 1) >> 4) - (b0 >> 4) + 1;  // 16-byte chunks overlapping the key
+    const bool last_full = ((b1 - 1) & 8) != 0;            // key ends in the last chunk's high half
+    const unsigned d = (unsigned)(b0 & 15) * 8;             // funnel shift in bits, 0..120
+    const uint64_t len = b1 - b0;
+    const uint64_t nfull = len >> 4;                        // whole 16-byte stream chunks
+    U128 cur = ld_chunk(base, nc > 1 || last_full);
+    U128 nxt = nc > 1 ? ld_chunk(base + 16, nc > 2 || last_full) : U128{0, 0};
+    auto funnel = [&](const U128& x, const U128& y, uint64_t& lo, uint64_t& hi) {
+      if (d == 0) {
+        lo = x.lo;
+        hi = x.hi;
+      } else if (d < 64) {
+        lo = (x.lo >> d) | (x.hi << (64 - d));
+        hi = (x.hi >> d) | (y.lo << (64 - d));
+      } else if (d == 64) {
+        lo = x.hi;
+        hi = y.lo;
+      } else {
+        lo = (x.hi >> (d - 64)) | (y.lo << (128 - d));
+        hi = (y.lo >> (d - 64)) | (y.hi << (128 - d));
+      }
+    };
+    for (uint64_t c = 0; c < nfull; ++c) {
+      const U128 nn = c + 2 < nc ? ld_chunk(base + 16 * (c + 2), c + 3 < nc || last_full) : U128{0, 0};
+      uint64_t lo, hi;
+      funnel(cur, nxt, lo, hi);
+      fnv_8(a, b, lo);
+      fnv_8(a, b, hi);
+      cur = nxt;
+      nxt = nn;
+    }
+    const unsigned rem = (unsigned)(len & 15);
+    if (rem) {
+      uint64_t lo, hi;
+      funnel(cur, nxt, lo, hi);
+      uint64_t v = lo;
+      if (rem >= 8) {
+        fnv_8(a, b, lo);
+        v = hi;
+      }
+      const unsigned r8 = rem & 7;
+#pragma unroll
+      for (unsigned t = 0; t < 7; ++t)
+        if (t < r8) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
+    }
+  }
+  ha = a;
+  hb = b;
+}
+
 // FNV-1a (key hash) and FNV-1 (fingerprint) of blob[b0, b1) in one pass.  The key's
 // aligned words are loaded 8 at a time (all 8 loads in flight before the first use);
 // stream word q = bytes [8q, 8q+8) of the key = funnel(w[q], w[q+1]) by the key's

@@ -328,7 +328,7 @@ def test_big_tiles_bit_exact(s3, oracle_lib):
         c.close()
 
 
-@pytest.mark.parametrize("mode", ["1", "3", "4", "8", "9"])
+@pytest.mark.parametrize("mode", ["1", "3", "4", "8", "9", "13", "14"])
 def test_hash_variants_bit_exact(s3, oracle_lib, monkeypatch, mode):
     """Every level-0 hash variant (S3IMPH_HASH_MODE: batched / single loads, length-sorted,
     forced sort) on ragged sets: bit-exact."""

@@ -1,7 +1,8 @@
 set -e
 mkdir -p gpurun_out/sw
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "hash_variants or unaligned or ragged" > gpurun_out/sw/pytest.log 2>&1
 for cfg in c2 c3 c5; do
-  for rm in 2097152 8388608 16777216 50331648; do
-    S3IMPH_RES_MAX=$rm S3IMPH_RES_FILL=2 timeout -k 10 120 python bench.py --no-cpu-baseline --config $cfg --steps 20 --warmup 3 > gpurun_out/sw/$cfg.res$rm.log 2>&1
+  for hm in 0 13 14; do
+    S3IMPH_HASH_MODE=$hm timeout -k 10 120 python bench.py --no-cpu-baseline --config $cfg --steps 10 --warmup 2 > gpurun_out/sw/$cfg.hm$hm.log 2>&1
   done
 done
