@@ -1,8 +1,10 @@
 set -e
 mkdir -p gpurun_out/sw
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "hash_variants or unaligned or ragged" > gpurun_out/sw/pytest.log 2>&1
-for cfg in c2 c3 c5; do
-  for hm in 0 13 14; do
-    S3IMPH_HASH_MODE=$hm timeout -k 10 120 python bench.py --no-cpu-baseline --config $cfg --steps 10 --warmup 2 > gpurun_out/sw/$cfg.hm$hm.log 2>&1
+for t0 in 2048 4096; do
+  for t in 1024 2048; do
+    S3IMPH_TARGET_TILES0=$t0 S3IMPH_TARGET_TILES=$t timeout -k 10 120 python bench.py --no-cpu-baseline --config c2 --steps 30 --warmup 3 > gpurun_out/sw/c2.t$t0.$t.log 2>&1
   done
+done
+for tr in 128 256 512; do
+  S3IMPH_TARGET_TILES_RES=$tr timeout -k 10 120 python bench.py --no-cpu-baseline --config c2 --steps 30 --warmup 3 > gpurun_out/sw/c2.tr$tr.log 2>&1
 done
