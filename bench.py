@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "s3-inv-db_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+FNV_STEP_PEAK_T = 3.49  # FNV-1a + FNV-1 byte steps per second (x1e12), tools/ubench_fnv.hip on MI355X
 
 CONFIGS = {
     "c2": dict(kind=0, avg=32, keys_per_gpu=10_000_000,
@@ -206,6 +207,13 @@ def main() -> None:
         result["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS,
                               "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
                               "alg_bytes": alg, "avg_ms": stages[dom]}
+        if dom == "hash_count0":
+            # The hash is bounded by VALU before HBM: every key byte is one FNV-1a + FNV-1 step
+            # (two 64-bit multiplies by the FNV prime); tools/ubench_fnv.hip measured the chip's
+            # ceiling for that step from registers.
+            steps_per_s = key_bytes_local / (stages[dom] / 1e3)
+            result["roofline"]["valu"] = {"achieved": steps_per_s / 1e12, "peak": FNV_STEP_PEAK_T,
+                                          "unit": "T byte-steps/s", "frac": steps_per_s / 1e12 / FNV_STEP_PEAK_T}
         result["dominant_stage"] = max(stages, key=stages.get)
     if world == 1:
         result["host_e2e"] = host_e2e(s3imph, blob, offs, local_rank)

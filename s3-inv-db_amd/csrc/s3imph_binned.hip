@@ -1658,8 +1658,6 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       case 8: S3_HASH(true, 2, -1); break;
       case 9: S3_HASH(true, 2, -2); break;
       case 13: S3_HASH(false, 3, -1); break;
-      case 14: S3_HASH(true, 3, -1); break;
-      case 10: S3_HASH(true, 0, -2); break;
       default:
         S3_HASH(false, 2, 0);
         S3_HASH(true, 3, 1);

@@ -30,7 +30,7 @@ def main():
     g = torch.Generator(device="cuda")
     g.manual_seed(1)
     ctx = s3imph.DeviceBuilder(0)
-    blob = torch.randint(0, 256, (n * 64 + 64,), dtype=torch.uint8, device="cuda", generator=g)
+    blob = torch.randint(0, 256, (n * 96 + 64,), dtype=torch.uint8, device="cuda", generator=g)
     offs = torch.arange(0, n + 1, dtype=torch.int64, device="cuda") * 64
     run(ctx, blob, offs, n, "fixed64  ")
     for lo, hi in [(56, 72), (48, 80), (32, 96)]:
