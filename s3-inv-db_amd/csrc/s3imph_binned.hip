@@ -113,10 +113,10 @@ __device__ __forceinline__ void hash_key(const uint8_t* blob, uint64_t b0, uint6
   else fnv_both_loop(blob, b0, b1, h1, h2);
 }
 
-// gate >= 0: run only if st->skew == gate (k_init_state sampled the key lengths), so the
-// direct and the length-sorted variant are both enqueued and the device picks one.
-// gate == -2: sort every group, skewed or not.
-template <bool kSort, int kBatched>
+// smode: 0 direct (hash_key<kVD>); 1 length-sorted groups (hash_key<kVS>), a group that is
+// not skewed hashed directly; 2 sort every group; 3 pick 1 or 0 from st->skew (k_init_state
+// sampled the key lengths) — one launch whatever the set.
+template <int kVD, int kVS>
 __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restrict__ blob,
                                                      const uint64_t* __restrict__ offsets, uint64_t n,
                                                      uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
@@ -124,13 +124,13 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
                                                      unsigned long long* __restrict__ flags,
                                                      unsigned long long* __restrict__ sflags, LevelState* st,
                                                      unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt,
-                                                     int gate) {
+                                                     int smode) {
   __shared__ unsigned sh[kMaxTiles];
   __shared__ unsigned lcnt[kLenBuckets];
   __shared__ unsigned short sidx[kCB];
   __shared__ uint64_t sb0[kCB], sb1[kCB], sh1[kCB], sh2[kCB];
   __shared__ uint64_t s_lmax[kCB / 64], s_lsum[kCB / 64];
-  if (gate >= 0 && (int)st->skew != gate) return;
+  const bool sort = smode == 1 || smode == 2 || (smode == 3 && st->skew);
   const uint64_t words = st->words[0], magic = st->magic[0];
   const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
   if (!geom_ok(st, T, B)) return;
@@ -148,11 +148,11 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
   for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
     for (uint64_t t = tid; t < T; t += kCB) sh[t] = 0;
     const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
-    if (!kSort) {
+    if (!sort) {
       __syncthreads();
       for (uint64_t i = lo + tid; i < hi; i += kCB) {
         uint64_t h1, h2;
-        hash_key<kBatched>(blob, offsets[i], offsets[i + 1], h1, h2);
+        hash_key<kVD>(blob, offsets[i], offsets[i + 1], h1, h2);
         kh[i] = h1;
         fp[i] = h2;
         zero |= (h1 == 0);
@@ -192,10 +192,10 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
         gsum += s_lsum[w];
       }
       const uint64_t gcnt = min<uint64_t>(kCB, hi - g);
-      if (gate != -2 && gmax * gcnt <= 2 * gsum + 16 * gcnt) {
+      if (smode != 2 && gmax * gcnt <= 2 * gsum + 16 * gcnt) {
         if (i < hi) {
           uint64_t h1, h2;
-          hash_key<kBatched>(blob, b0, b1, h1, h2);
+          hash_key<kVS>(blob, b0, b1, h1, h2);
           kh[i] = h1;
           fp[i] = h2;
           zero |= (h1 == 0);
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
       const unsigned j = sidx[tid];
       if (g + j < hi) {
         uint64_t h1, h2;
-        hash_key<kBatched>(blob, sb0[tid], sb1[tid], h1, h2);
+        hash_key<kVS>(blob, sb0[tid], sb1[tid], h1, h2);
         sh1[j] = h1;
         sh2[j] = h2;
         zero |= (h1 == 0);
@@ -243,9 +243,8 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
 // Size level L from the redo count the previous level produced and carry its word
 // offset (the rank base lvl_base[L] was published by the previous level's last tile).
 // Runs only after a big level (the tail sizes its own levels).
-__global__ void k_level_setup(int level, LevelState* st) {
+__device__ void level_setup(int level, LevelState* st) {
   const int p = level - 1;
-  if (threadIdx.x != 0) return;
   if (p > 0 && !st->preset[p] && st->n[p] <= kGate) return;
   if (st->status & (kStGeometry | kStOverflow | kStLookback)) return;
   const uint64_t n = st->n[level];
@@ -1453,6 +1452,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
   __shared__ int s_level;
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   if (tid == 0) {
+    level_setup(big_launched + 1, st);  // size the level after the last big one
     int L = first_level > 1 ? first_level : 1;
     while (L <= big_launched && st->n[L] > kGate) ++L;
     s_level = L;
@@ -1646,21 +1646,21 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       const char* e = std::getenv("S3IMPH_HASH_MODE");
       return e ? std::atoi(e) : 0;
     }();
-#define S3_HASH(KS, KV, GATE)                                                                                   \
-  k_hash_count0<KS, KV><<<grid_chunks, kCB, 0, s>>>(                                                       \
-      blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, GATE)
+#define S3_HASH(KVD, KVS, SMODE)                                                                              \
+  k_hash_count0<KVD, KVS><<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st, \
+                                                      g.tb, g.chunk, b.tcnt, SMODE)
     switch (mode) {
-      case 1: S3_HASH(false, 1, -1); break;
-      case 2: S3_HASH(true, 0, -1); break;
-      case 3: S3_HASH(false, 0, -1); break;
-      case 4: S3_HASH(true, 1, -1); break;
-      case 7: S3_HASH(false, 2, -1); break;
-      case 8: S3_HASH(true, 2, -1); break;
-      case 9: S3_HASH(true, 2, -2); break;
-      case 13: S3_HASH(false, 3, -1); break;
-      default:
-        S3_HASH(false, 2, 0);
-        S3_HASH(true, 3, 1);
+      case 1: S3_HASH(1, 1, 0); break;
+      case 2: S3_HASH(0, 0, 1); break;
+      case 3: S3_HASH(0, 0, 0); break;
+      case 4: S3_HASH(1, 1, 1); break;
+      case 7: S3_HASH(2, 2, 0); break;
+      case 8: S3_HASH(2, 2, 1); break;
+      case 9: S3_HASH(2, 2, 2); break;
+      case 10: S3_HASH(0, 0, 2); break;
+      case 13: S3_HASH(3, 3, 0); break;
+      case 14: S3_HASH(3, 3, 1); break;
+      default: S3_HASH(2, 3, 3);
     }
 #undef S3_HASH
   } else {
@@ -1730,7 +1730,6 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
 }
 
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s) {
-  k_level_setup<<<1, 64, 0, s>>>(big_launched + 1, b.st);
   k_bin_tail<<<1, kTailT, 0, s>>>(first_level, big_launched, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out, b.pos_out,
                                   b.st, b.tile_prof);
 }
