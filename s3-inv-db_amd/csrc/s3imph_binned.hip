@@ -922,16 +922,36 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
     if (tp && tid == 0) tp[i] = wall_clock64(); \
   } while (0)
     TPROF(0);
-    // bucket range: from the histogram scan, or (reservation path) a fixed slot per tile
-    uint64_t lo, nk;
+    // bucket range: from the histogram scan, or (reservation path) the kResShards shard
+    // ranges of the tile's fixed slot; record j lives at rb[RB(j)]
+    uint64_t lo, nk, shcap = 0;
+    unsigned pre[kResShards];
     if (tcnt) {
-      lo = t * (bucket_cap / T);
-      nk = tcnt[t];
+      const uint64_t cap = bucket_cap / T;
+      shcap = cap / kResShards;
+      lo = t * cap;
+      unsigned acc = 0;
+#pragma unroll
+      for (int x = 0; x < kResShards; ++x) {
+        pre[x] = acc;
+        acc += tcnt[t * kResShards + x];
+      }
+      nk = acc;
     } else {
       lo = tile_start[t];
       nk = tile_start[t + 1] - lo;
+#pragma unroll
+      for (int x = 0; x < kResShards; ++x) pre[x] = x ? 0xffffffffu : 0u;
     }
     const Rec* rb = bucket + lo;
+    auto shard_off = [&](uint64_t j) -> uint64_t {
+      uint64_t o = j;
+#pragma unroll
+      for (int x = 1; x < kResShards; ++x)
+        if (j >= pre[x]) o = (uint64_t)x * shcap + (j - pre[x]);
+      return o;
+    };
+#define RB(j) rb[shard_off(j)]
     const uint64_t tbase = rg.plo + (t << tb);
     const bool cached = small && nk <= kcap;
     // ---- mark: A/C in LDS (and each record's in-tile position, when cached)
@@ -940,7 +960,7 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
 #pragma unroll
       for (int u = 0; u < kTU; ++u) {
         const uint64_t j = j0 + (uint64_t)u * NT;
-        k[u] = j < nk ? rb[j].k : 0;
+        k[u] = j < nk ? RB(j).k : 0;
       }
 #pragma unroll
       for (int u = 0; u < kTU; ++u) {
@@ -1005,8 +1025,8 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
           if (wv & bit) {
             if (wr) {
               const uint64_t p = base + sC[loc >> 5] + __popc(wv & (bit - 1));
-              fp_out[p] = rb[j].f;
-              pos_out[p] = rb[j].p;
+              fp_out[p] = RB(j).f;
+              pos_out[p] = RB(j).p;
             }
           } else {
             redo = true;
@@ -1046,7 +1066,7 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
           const uint64_t r = r0 + (uint64_t)u * NT;
           cf[u] = cp[u] = 0;
           if (r < pop) {
-            const Rec* src = rb + sridx[r];
+            const Rec* src = &RB(sridx[r]);
             cf[u] = src->f;
             cp[u] = src->p;
           }
@@ -1066,7 +1086,7 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
         const uint64_t j = jb + lane;
         bool redo = false;
         if (j < nk) {
-          const Rec rc = rb[j];
+          const Rec rc = RB(j);
           const unsigned loc = (unsigned)(bb_index(seed, rc.k, words, magic) - tbase);
           const uint32_t wv = sA[loc >> 5];
           const uint32_t bit = 1u << (loc & 31);
@@ -1117,9 +1137,10 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
             m[u] = jb < nk ? srm[jb >> 6] : 0ull;
             ck[u] = cf[u] = cp[u] = 0;
             if ((m[u] >> lane) & 1ull) {
-              ck[u] = rb[jb + lane].k;
-              cf[u] = rb[jb + lane].f;
-              cp[u] = rb[jb + lane].p;
+              const Rec* q = &RB(jb + lane);
+              ck[u] = q->k;
+              cf[u] = q->f;
+              cp[u] = q->p;
             }
           }
 #pragma unroll
@@ -1134,18 +1155,19 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
           bool redo = false;
           uint64_t ck = 0;
           if (j < nk) {
-            ck = rb[j].k;
+            ck = RB(j).k;
             const unsigned loc = (unsigned)(bb_index(seed, ck, words, magic) - tbase);
             redo = !((sA[loc >> 5] >> (loc & 31)) & 1u);
           }
           const uint64_t m = __ballot(redo);
-          if (redo) next[o + __popcll(m & lt)] = Rec{ck, rb[j].f, rb[j].p};
+          if (redo) next[o + __popcll(m & lt)] = Rec{ck, RB(j).f, RB(j).p};
           o += __popcll(m);
         }
       }
     }
     __syncthreads();
     TPROF(7);
+#undef RB
 #undef TPROF
   }
   if (bad) atomicOr(&st->status, kStRank);
@@ -1706,8 +1728,9 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
   }
   const size_t lds = b.tile_mode == 0 ? tile_lds_bytes(g.tb) : 2ull * (1ull << (g.tb - 5)) * sizeof(uint32_t);
   auto kern = b.tile_block == 512 ? k_tile<512> : k_tile<1024>;
+  const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kScatterTiles * kResShards : nullptr;
   kern<<<grid_tiles, b.tile_block == 512 ? 512 : 1024, lds, s>>>(
-      level, b.bucket, b.tile_start, nullptr, b.bucket_cap,
+      level, b.bucket, b.tile_start, tc, b.bucket_cap,
       b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.tile_mode, b.tile_prof);
 }
 

@@ -401,7 +401,7 @@ void enqueue_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, 
                       : res ? choose_geom_sz(nb, size, c->target_tiles_res, c->target_chunks, kRegTileMaxBits)
                             : choose_geom_sz(nb, size, c->target_tiles, c->target_chunks, kRegTileMaxBits);
   const Grids gr = level_grids(nb, size, g);
-  if (res && g.tb <= kRegTileMaxBits) {
+  if (res) {
     const int gsr = (int)std::min<uint64_t>((nb + kSubRound - 1) / kSubRound, 256);
     launch_binned_scatter_res(L, b, g, std::max(gsr, 1), s);
     launch_binned_tile(L, b, g, gr.gt, s, true);
