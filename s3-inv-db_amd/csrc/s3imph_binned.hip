@@ -496,6 +496,8 @@ __global__ __launch_bounds__(kSB) void k_scatter_direct(int level, const uint64_
 // arbitrary, which nothing downstream depends on (ranks come from positions).  A slot
 // overflow sets kStOverflow and the build reruns on the counted path.
 __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __restrict__ ilist,
+                                                     const uint64_t* __restrict__ ik, const uint64_t* __restrict__ ifp,
+                                                     const uint64_t* __restrict__ ipos, uint64_t pos_base,
                                                      unsigned* __restrict__ tcnt, Rec* __restrict__ bucket,
                                                      uint64_t bucket_cap, unsigned long long* __restrict__ flags,
                                                      LevelState* st, unsigned tb, uint64_t cap_words,
@@ -513,7 +515,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   const uint64_t n = st->n[level];
   const unsigned tid = threadIdx.x;
   uint64_t words, magic, woff;
-  if (preset) {  // sized by the multi-GPU build: global words, this rank's records
+  if (level == 0 || preset) {  // level 0: sized by k_init_state; preset: by the multi-GPU build
     words = st->words[level];
     magic = st->magic[level];
     woff = st->woff[level];
@@ -559,17 +561,25 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     if (tp && tid == 0 && round == 0) tp[i] = wall_clock64(); \
   } while (0)
   SPROF(0);
-  // records as three scalar arrays: a conditionally loaded Rec[] would live in scratch
+  // records as three scalar arrays: a conditionally loaded Rec[] would live in scratch.
+  // Level 0 reads the hash kernel's key-order arrays instead of a record list.
   uint64_t rk_[kScatterKPT], rf_[kScatterKPT], rp_[kScatterKPT];
+  auto load = [&](uint64_t i, int q) {
+    if (ilist) {
+      rk_[q] = ilist[i].k;
+      rf_[q] = ilist[i].f;
+      rp_[q] = ilist[i].p;
+    } else {
+      rk_[q] = ik[i];
+      rf_[q] = ifp[i];
+      rp_[q] = ipos ? ipos[i] : pos_base + i;
+    }
+  };
 #pragma unroll
   for (int q = 0; q < kScatterKPT; ++q) {
     const uint64_t i = r0 + (uint64_t)q * kSB + tid;
     rk_[q] = rf_[q] = rp_[q] = 0;
-    if (i < n) {
-      rk_[q] = ilist[i].k;
-      rf_[q] = ilist[i].f;
-      rp_[q] = ilist[i].p;
-    }
+    if (i < n) load(i, q);
   }
   for (uint64_t t = tid; t < T; t += kSB) cnt[t] = 0;
   if (tid == 0) s_over = 0;
@@ -628,11 +638,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
 #pragma unroll
     for (int q = 0; q < kScatterKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
-      if (i < n) {
-        rk_[q] = ilist[i].k;
-        rf_[q] = ilist[i].f;
-        rp_[q] = ilist[i].p;
-      }
+      if (i < n) load(i, q);
     }
     __syncthreads();
     SPROF(3);
@@ -1748,7 +1754,9 @@ void launch_hash_scatter0(const uint8_t* blob, const uint64_t* offsets, uint64_t
 }
 
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s) {
-  k_scatter_res<<<grid, kSB, 0, s>>>(level, b.list[(level - 1) & 1], b.tcnt + (uint64_t)level * kScatterTiles * kResShards,
+  const bool l0 = level == 0 && !b.dist;
+  k_scatter_res<<<grid, kSB, 0, s>>>(level, l0 ? nullptr : b.list[(level - 1) & 1], b.kh, b.fp, b.pos, b.pos_base,
+                                     b.tcnt + (uint64_t)level * kScatterTiles * kResShards,
                                      b.bucket, b.bucket_cap, b.flags, b.st, g.tb, b.cap_words, b.tile_prof);
 }
 

@@ -116,6 +116,7 @@ struct s3imph_ctx {
   // reservation slots hold >= 4x a tile's mean fill, 2x on levels above kResSmallKeys
   // (full 256-block grids: every XCD shard of a slot then fills evenly)
   uint64_t res_fill = 2;
+  int res0 = 1;  // level 0 through the reservation scatter when its tiles are large
   bool debug = false;
   unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps
   bool lds_attr_set = false;
@@ -461,6 +462,17 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   }
   launch_binned_count(0, blob, offsets, n, b, g0, gr.gc, s);
   ev_mark(c, s, "hash_count0");
+  // Level 0 through the reservation scatter when its tiles are big enough that every
+  // (tile, XCD shard) slot's 1.25x headroom (bucket_cap = 1.25 n) is > 10 sigma of its fill
+  const uint64_t T0 = (64 * level_words(n) + (1ull << g0.tb) - 1) >> g0.tb;
+  if (!conservative && c->res0 && T0 <= kScatterTiles && n >= 2048ull * kResShards * T0) {
+    launch_binned_scatter_res(0, b, g0, 256, s);
+    ev_mark(c, s, "scatter0");
+    launch_binned_tile(0, b, g0, gr.gt, s, true);
+    ev_mark(c, s, "tile0");
+    enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
+    return;
+  }
   launch_binned_scan(0, b, gr.gs, s);
   ev_mark(c, s, "hscan0");
   launch_binned_scatter(0, b, g0, s);
@@ -1226,6 +1238,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     if (const char* m = std::getenv("S3IMPH_RES_MAX")) c->res_max_keys = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_TARGET_TILES_RES")) c->target_tiles_res = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_RES_FILL")) c->res_fill = std::strtoull(m, nullptr, 10);
+    if (const char* m = std::getenv("S3IMPH_RES0")) c->res0 = std::atoi(m);
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     if (const char* m = std::getenv("S3IMPH_TILE_BLOCK")) c->tile_block = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);
