@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
         kh[i] = h1;
         fp[i] = h2;
         zero |= (h1 == 0);
-        atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
+        if (hist) atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
       }
     } else {
     for (uint64_t g = lo; g < hi; g += kCB) {
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
           kh[i] = h1;
           fp[i] = h2;
           zero |= (h1 == 0);
-          atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
+          if (hist) atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
         }
         __syncthreads();
         continue;
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
         sh1[j] = h1;
         sh2[j] = h2;
         zero |= (h1 == 0);
-        atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
+        if (hist) atomicAdd(&sh[bb_index(seed, h1, words, magic) >> tb], 1u);
       }
       __syncthreads();
       if (i < hi) {
@@ -233,7 +233,8 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
     }
     }
     __syncthreads();
-    for (uint64_t t = tid; t < T; t += kCB) hist[t * B + b] = sh[t];
+    if (hist)
+      for (uint64_t t = tid; t < T; t += kCB) hist[t * B + b] = sh[t];
     __syncthreads();
   }
   if (zero) atomicOr(&st->status, kStKeyZero);
@@ -1662,7 +1663,7 @@ void binned_set_lds_limits() {
 }
 
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
-                         LevelGeom g, int grid_chunks, hipStream_t s) {
+                         LevelGeom g, int grid_chunks, hipStream_t s, bool histogram) {
   if (level == 0 && !b.dist) {
     static const int mode = [] {
       // A/B knob: 0 auto (default: 7 for near-uniform lengths, 14 for skewed ones, picked
@@ -1675,7 +1676,8 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       return e ? std::atoi(e) : 0;
     }();
 #define S3_HASH(KVD, KVS, SMODE)                                                                              \
-  k_hash_count0<KVD, KVS><<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.hist, b.flags, b.sflags, b.st, \
+  k_hash_count0<KVD, KVS><<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, histogram ? b.hist : nullptr,   \
+                                                      b.flags, b.sflags, b.st,                                         \
                                                       g.tb, g.chunk, b.tcnt, SMODE)
     switch (mode) {
       case 1: S3_HASH(1, 1, 0); break;

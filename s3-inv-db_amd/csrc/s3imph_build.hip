@@ -460,13 +460,14 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
     enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
     return;
   }
-  launch_binned_count(0, blob, offsets, n, b, g0, gr.gc, s);
-  ev_mark(c, s, "hash_count0");
   // Level 0 through the reservation scatter when its tiles are big enough that every
   // (tile, XCD shard) slot's 1.25x headroom (bucket_cap = 1.25 n) is >= 6.9 sigma of its
   // mean fill of >= 768 keys (an overflow is caught on the device and rerun counted)
   const uint64_t T0 = (64 * level_words(n) + (1ull << g0.tb) - 1) >> g0.tb;
-  if (!conservative && c->res0 && T0 <= kScatterTiles && (n >= 768ull * kResShards * T0 || c->res0 == 2)) {
+  const bool res0 = !conservative && c->res0 && T0 <= kScatterTiles && (n >= 768ull * kResShards * T0 || c->res0 == 2);
+  launch_binned_count(0, blob, offsets, n, b, g0, gr.gc, s, !res0);  // no histogram for the reservation path
+  ev_mark(c, s, "hash_count0");
+  if (res0) {
     launch_binned_scatter_res(0, b, g0, 256, s);
     ev_mark(c, s, "scatter0");
     launch_binned_tile(0, b, g0, gr.gt, s, true);

@@ -174,7 +174,7 @@ struct BinBuffers {
 };
 void binned_set_lds_limits();
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
-                         LevelGeom g, int grid_chunks, hipStream_t s);
+                         LevelGeom g, int grid_chunks, hipStream_t s, bool histogram = true);
 void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s);
 void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s, bool direct = false);
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s,
