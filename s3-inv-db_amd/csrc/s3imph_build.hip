@@ -391,12 +391,25 @@ Grids level_grids(uint64_t nk, uint64_t size, LevelGeom g) {
   return r;
 }
 
+// Do reservation slots (bucket_cap / T records per tile, cut into kResShards shards)
+// hold a level of about nb records over `size` positions?  Small levels keep 4x the mean
+// fill; larger ones res_fill x; and tiles so large that a shard's mean fill m is >= 768
+// need only 1 + 7/sqrt(m) (7 sigma of a Poisson fill) plus 2 % for the size estimate.
+// An overflow is caught on the device and the build reruns on the counted path.
+bool res_fits(const s3imph_ctx* c, uint64_t nb, uint64_t size) {
+  if (nb * (nb > kResSmallKeys ? c->res_fill : 4) <= c->bucket_cap) return true;
+  const LevelGeom g = choose_geom_sz(nb, size, c->target_tiles_res, c->target_chunks, kRegTileMaxBits);
+  const double T = (double)((size + (1ull << g.tb) - 1) >> g.tb);
+  const double m = (double)nb / (T * kResShards);
+  return m >= 768.0 && (double)c->bucket_cap >= (double)nb * (1.02 + 7.0 / std::sqrt(m));
+}
+
 // One list-input level L (records in list[(L-1)&1]): about nb records over `size`
 // positions.  Small levels take the reservation scatter (no count / histogram scan).
 void enqueue_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, uint64_t size, bool conservative,
                         const LevelGeom* force, hipStream_t s) {
   // reservation slots are bucket_cap / T records per tile: keep them >= 4x the mean fill
-  const bool res = !conservative && nb <= c->res_max_keys && nb * (nb > kResSmallKeys ? c->res_fill : 4) <= c->bucket_cap && L < kResLevels &&
+  const bool res = !conservative && nb <= c->res_max_keys && res_fits(c, nb, size) && L < kResLevels &&
                    c->tile_mode == 0;
   const LevelGeom g = force ? *force
                       : res ? choose_geom_sz(nb, size, c->target_tiles_res, c->target_chunks, kRegTileMaxBits)
@@ -731,10 +744,12 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
   const uint64_t capw = cap_words_for(std::max<uint64_t>(n_global, 1024)) + stagew;
   if (capl <= d.cap_list && caps <= d.cap_send && stagew <= d.cap_stage_words && capw <= c->cap_words && c->hist)
     return;
-  dalloc(c->bucket, capl);
+  // the bucket gets 1.3x the list capacity: reservation slots need headroom over the mean fill
+  const uint64_t capb = capl + capl * 3 / 10;
+  dalloc(c->bucket, capb);
   dalloc(c->list[0], capl);
   dalloc(c->list[1], capl);
-  c->bucket_cap = capl;
+  c->bucket_cap = capb;
   c->cap_keys = capl;
   dalloc(c->hist, kHistCap);
   dalloc(c->hoff, kHistCap);
@@ -824,9 +839,9 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
     const uint64_t lo = std::min<uint64_t>((uint64_t)R * S, w), rw = std::min<uint64_t>(S, w - lo);
     hw.push_back(w);
     hS.push_back(S);
-    if (m > c->bucket_cap) {
+    if (m > d.cap_list) {
       *msg = "build MPHF: rank " + std::to_string(R) + " received " + std::to_string(m) + " records (capacity " +
-             std::to_string(c->bucket_cap) + ")";
+             std::to_string(d.cap_list) + ")";
       return S3IMPH_ERR_NOMEM;
     }
     // ---- exchange: the received records become this level's list, list[(L-1)&1]
@@ -863,7 +878,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
     total += cnt[r];
     maxc = std::max(maxc, cnt[r]);
   }
-  if (total > c->bucket_cap) {
+  if (total > d.cap_list) {
     *msg = "build MPHF: replicated level of " + std::to_string(total) + " records exceeds the workspace";
     return S3IMPH_ERR_NOMEM;
   }
