@@ -496,6 +496,10 @@ __global__ __launch_bounds__(kSB) void k_scatter_direct(int level, const uint64_
 // block reserves its run in its shard of a tile with one atomic per (round, tile).  Record order inside a tile is then
 // arbitrary, which nothing downstream depends on (ranks come from positions).  A slot
 // overflow sets kStOverflow and the build reruns on the counted path.
+// kR records per round, at most kT tiles (<4096, 4096>: one block per CU, 152 KiB of LDS).
+// <2048, 2048> (two blocks per CU, so one block's atomics and barriers overlap the other's
+// memory phases) measured slower on C2: level-0 scatter 0.156 -> 0.214 ms.
+template <int kR, int kT>
 __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __restrict__ ilist,
                                                      const uint64_t* __restrict__ ik, const uint64_t* __restrict__ ifp,
                                                      const uint64_t* __restrict__ ipos, uint64_t pos_base,
@@ -503,11 +507,12 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
                                                      uint64_t bucket_cap, unsigned long long* __restrict__ flags,
                                                      LevelState* st, unsigned tb, uint64_t cap_words,
                                                      unsigned long long* __restrict__ prof) {
-  __shared__ Rec stage[kSubRound];
-  __shared__ unsigned short stile[kSubRound];
-  __shared__ unsigned cnt[kLdsTiles];
-  __shared__ unsigned start[kLdsTiles];
-  __shared__ unsigned cur[kLdsTiles];  // bucket indices fit u32 (n < 2^32 per GPU)
+  constexpr int kKPT = kR / kSB;
+  __shared__ Rec stage[kR];
+  __shared__ unsigned short stile[kR];
+  __shared__ unsigned cnt[kT];
+  __shared__ unsigned start[kT];
+  __shared__ unsigned cur[kT];  // bucket indices fit u32 (n < 2^32 per GPU)
   __shared__ unsigned s_over;
   const int p = level - 1;
   const bool preset = st->preset[level] != 0;
@@ -535,7 +540,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   }
   const LevelRange rg = level_range(st, level, words);
   const uint64_t T = ntiles_of(rg.rw, tb);
-  if (T > kLdsTiles) {
+  if (T > kT) {
     if (tid == 0) atomicOr(&st->status, kStGeometry);
     return;
   }
@@ -550,8 +555,8 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
   const unsigned shard = blockIdx.x % kResShards;
   const uint64_t seed = level_seed(level);
-  const uint64_t stride = (uint64_t)gridDim.x * kSubRound;
-  uint64_t r0 = (uint64_t)blockIdx.x * kSubRound;
+  const uint64_t stride = (uint64_t)gridDim.x * kR;
+  uint64_t r0 = (uint64_t)blockIdx.x * kR;
   if (r0 >= n) return;
   // debug: round-0 phase timestamps of this block in prof row 32 + level
   unsigned long long* tp =
@@ -564,7 +569,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   SPROF(0);
   // records as three scalar arrays: a conditionally loaded Rec[] would live in scratch.
   // Level 0 reads the hash kernel's key-order arrays instead of a record list.
-  uint64_t rk_[kScatterKPT], rf_[kScatterKPT], rp_[kScatterKPT];
+  uint64_t rk_[kKPT], rf_[kKPT], rp_[kKPT];
   auto load = [&](uint64_t i, int q) {
     if (ilist) {
       rk_[q] = ilist[i].k;
@@ -577,7 +582,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     }
   };
 #pragma unroll
-  for (int q = 0; q < kScatterKPT; ++q) {
+  for (int q = 0; q < kKPT; ++q) {
     const uint64_t i = r0 + (uint64_t)q * kSB + tid;
     rk_[q] = rf_[q] = rp_[q] = 0;
     if (i < n) load(i, q);
@@ -586,9 +591,9 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   if (tid == 0) s_over = 0;
   __syncthreads();
   for (;;) {
-    unsigned tt[kScatterKPT], rk[kScatterKPT];
+    unsigned tt[kKPT], rk[kKPT];
 #pragma unroll
-    for (int q = 0; q < kScatterKPT; ++q) {
+    for (int q = 0; q < kKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < n) {
         tt[q] = (unsigned)((bb_index(seed, rk_[q], words, magic) - rg.plo) >> tb);
@@ -597,7 +602,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     }
     __syncthreads();
     SPROF(1);
-    constexpr int kTPT = (int)(kLdsTiles / kSB);
+    constexpr int kTPT = (int)(kT / kSB);
     const uint64_t t0 = (uint64_t)kTPT * tid;
     unsigned a[kTPT];
     uint64_t sum = 0;
@@ -625,7 +630,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     __syncthreads();
     SPROF(2);
 #pragma unroll
-    for (int q = 0; q < kScatterKPT; ++q) {
+    for (int q = 0; q < kKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < n) {
         const unsigned slot = start[tt[q]] + rk[q];
@@ -633,11 +638,11 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
         stile[slot] = (unsigned short)tt[q];
       }
     }
-    const unsigned m = (unsigned)min<uint64_t>(kSubRound, n - r0);
+    const unsigned m = (unsigned)min<uint64_t>(kR, n - r0);
     r0 += stride;
     const bool more = r0 < n;
 #pragma unroll
-    for (int q = 0; q < kScatterKPT; ++q) {
+    for (int q = 0; q < kKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < n) load(i, q);
     }
@@ -1757,9 +1762,11 @@ void launch_hash_scatter0(const uint8_t* blob, const uint64_t* offsets, uint64_t
 
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s) {
   const bool l0 = level == 0 && !b.dist;
-  k_scatter_res<<<grid, kSB, 0, s>>>(level, l0 ? nullptr : b.list[(level - 1) & 1], b.kh, b.fp, b.pos, b.pos_base,
-                                     b.tcnt + (uint64_t)level * kScatterTiles * kResShards,
-                                     b.bucket, b.bucket_cap, b.flags, b.st, g.tb, b.cap_words, b.tile_prof);
+  const Rec* il = l0 ? nullptr : b.list[(level - 1) & 1];
+  unsigned* tc = b.tcnt + (uint64_t)level * kScatterTiles * kResShards;
+  k_scatter_res<kSubRound, kLdsTiles><<<grid, kSB, 0, s>>>(level, il, b.kh, b.fp, b.pos, b.pos_base, tc, b.bucket,
+                                                           b.bucket_cap, b.flags, b.st, g.tb, b.cap_words,
+                                                           b.tile_prof);
 }
 
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s) {
