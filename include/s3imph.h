@@ -138,7 +138,8 @@ int s3imph_build_device(s3imph_ctx *ctx, const uint8_t *d_blob, const uint64_t *
 int s3imph_ctx_mph_bin(s3imph_ctx *ctx, uint8_t *out, uint64_t cap, uint64_t *len);
 
 /* Per-stage device times of the last build (ms), recorded with HIP events on the
- * build stream when profiling is on.  names: comma-separated stage names. */
+ * build stream when profiling is on (on = 1: every stage; on = 2: only the level-0
+ * hash / route stage, two events per build).  names: comma-separated stage names. */
 int s3imph_ctx_set_profiling(s3imph_ctx *ctx, int on);
 int s3imph_ctx_stage_times(s3imph_ctx *ctx, float *ms, int cap, int *count, char *names, size_t names_len);
 

@@ -132,7 +132,7 @@ struct s3imph_ctx {
   uint64_t last_n = 0;
   s3imph_build_info info{};
 
-  bool profiling = false;
+  int profiling = 0;  // 0 off, 1 every stage, 2 the level-0 hash (or route) stage only
   std::vector<hipEvent_t> events;
   std::vector<std::string> ev_names;
   int ev_used = 0;
@@ -280,6 +280,9 @@ void ev_begin(s3imph_ctx* c) {
 }
 void ev_mark(s3imph_ctx* c, hipStream_t s, const char* name) {
   if (!c->profiling) return;
+  if (c->profiling == 2 && std::strcmp(name, "init") != 0 && std::strcmp(name, "hash_count0") != 0 &&
+      std::strcmp(name, "route0") != 0)
+    return;  // light mode: two events per build, around the dominant kernel
   if (c->ev_used >= (int)c->events.size()) {
     hipEvent_t e;
     HIPCHECK(hipEventCreate(&e));
@@ -1346,7 +1349,7 @@ int s3imph_ctx_mph_bin(s3imph_ctx* c, uint8_t* out, uint64_t cap, uint64_t* len)
 
 int s3imph_ctx_set_profiling(s3imph_ctx* c, int on) {
   if (!c) return S3IMPH_ERR_INVALID;
-  c->profiling = on != 0;
+  c->profiling = on < 0 ? 0 : on > 2 ? 1 : on;
   return S3IMPH_OK;
 }
 

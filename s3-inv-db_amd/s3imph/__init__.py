@@ -290,8 +290,9 @@ class DeviceBuilder:
     def reserve(self, max_keys: int, max_global_keys: int = 0) -> None:
         _check(LIB.s3imph_ctx_reserve(self._h, max_keys, max_global_keys), None, "reserve")
 
-    def set_profiling(self, on: bool) -> None:
-        LIB.s3imph_ctx_set_profiling(self._h, 1 if on else 0)
+    def set_profiling(self, on) -> None:
+        """False/0 off, True/1 every stage, 2 the level-0 hash (or route) stage only."""
+        LIB.s3imph_ctx_set_profiling(self._h, int(on))
 
     def stage_times(self) -> dict:
         ms = (ctypes.c_float * 64)()
