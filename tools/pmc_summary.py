@@ -50,7 +50,9 @@ def main():
         for o in out:
             first.setdefault(o["kernel"], o)
         ent = tr.setdefault(cfg, {})
-        for stage, kern in (("hash_count0", "k_hash_count0"), ("scatter0", "k_scatter"), ("tile0", "k_tile_reg"),
+        scatter0 = "k_scatter_res" if "k_scatter_res" in first and "k_hscan" not in first else "k_scatter"
+        tile0 = next((o["kernel"] for o in out if o["kernel"] in ("k_tile_reg", "k_tile")), "k_tile_reg")
+        for stage, kern in (("hash_count0", "k_hash_count0"), ("scatter0", scatter0), ("tile0", tile0),
                             ("hash_scatter0", "k_hash_scatter0")):
             if kern in first:
                 o = first[kern]
