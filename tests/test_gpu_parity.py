@@ -329,40 +329,49 @@ def test_big_tiles_bit_exact(s3, oracle_lib):
 
 
 @pytest.mark.parametrize("mode", ["1", "3", "4", "8", "9", "13", "14"])
-def test_hash_variants_bit_exact(s3, oracle_lib, monkeypatch, mode):
+def test_hash_variants_bit_exact(s3, oracle_lib, mode):
     """Every level-0 hash variant (S3IMPH_HASH_MODE: batched / single loads, length-sorted,
-    forced sort) on ragged sets: bit-exact."""
-    monkeypatch.setenv("S3IMPH_HASH_MODE", mode)
+    forced sort) on ragged sets, the 10M-key one on the reservation path: bit-exact."""
+    _parity_subprocess({"S3IMPH_HASH_MODE": mode},
+                       [(1, 0, 8), (3000, 0, 40), (300_000, 0, 64), (2_500_000, 1, 0), (10_000_000, 0, 32)])
+
+
+def _parity_subprocess(env: dict, cases) -> None:
+    """Build `cases` (n, kind, avg) through s3imph.build_host in a fresh process with
+    `env` set (the library reads its A/B knobs once per process): bit-exact vs the oracle."""
     import subprocess
     import sys
     code = (
         "import sys; sys.path[:0]=[%r, %r]\n"
         "import numpy as np, torch, s3imph, oracle as O\n"
-        "for n, kind, avg in [(1, 0, 8), (3000, 0, 40), (300_000, 0, 64), (2_500_000, 1, 0)]:\n"
-        "    blob, offs = s3imph.gen_keys(kind, 7, avg, 0, n)\n"
-        "    st, fp, po, mph = O.lib().build(blob[: offs[-1]], offs)\n"
-        "    g = s3imph.build_host(blob, offs)\n"
-        "    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po), n\n"
-        "print('ok')\n"
-    ) % (os.path.join(os.path.dirname(GOLDEN), "..", "s3-inv-db_amd"), os.path.join(os.path.dirname(GOLDEN), "..", "oracle"))
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
-
-
-def test_direct_scatter_forced_small(s3, oracle_lib, monkeypatch):
-    """The direct scatter on every counted level (S3IMPH_SCATTER_DIRECT=1), small sets."""
-    monkeypatch.setenv("S3IMPH_SCATTER_DIRECT", "1")
-    import subprocess
-    import sys
-    code = (
-        "import sys; sys.path[:0]=[%r, %r]\n"
-        "import numpy as np, torch, s3imph, oracle as O\n"
-        "for n, kind, avg in [(300_000, 0, 24), (2_500_000, 1, 0)]:\n"
+        "for n, kind, avg in %r:\n"
         "    blob, offs = s3imph.gen_keys(kind, 3, avg, 0, n)\n"
         "    st, fp, po, mph = O.lib().build(blob[: offs[-1]], offs)\n"
         "    g = s3imph.build_host(blob, offs)\n"
         "    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po), n\n"
         "print('ok')\n"
-    ) % (os.path.join(os.path.dirname(GOLDEN), "..", "s3-inv-db_amd"), os.path.join(os.path.dirname(GOLDEN), "..", "oracle"))
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    ) % (os.path.join(os.path.dirname(GOLDEN), "..", "s3-inv-db_amd"), os.path.join(os.path.dirname(GOLDEN), "..", "oracle"),
+         list(cases))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=280,
+                       env={**os.environ, **env})
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_direct_scatter_forced_small(s3, oracle_lib):
+    """The direct scatter on every counted level (S3IMPH_SCATTER_DIRECT=1), small sets."""
+    _parity_subprocess({"S3IMPH_SCATTER_DIRECT": "1"}, [(300_000, 0, 24), (2_500_000, 1, 0)])
+
+
+def test_counted_path_every_level(s3, oracle_lib):
+    """With the reservation scatter off (S3IMPH_RES_MAX=0, S3IMPH_RES0=0) every level runs
+    count -> histogram scan -> counted scatter -> tile: bit-exact."""
+    _parity_subprocess({"S3IMPH_RES_MAX": "0", "S3IMPH_RES0": "0"},
+                       [(300_000, 0, 24), (2_500_000, 1, 0), (10_000_000, 0, 32)])
+
+
+def test_reservation_overflow_reruns(s3, oracle_lib):
+    """Reservation slots forced too small (level 0 forced onto the reservation path for
+    sets whose shard fills are tiny, list-level slots at 1x the mean fill): the device
+    flags the overflow, the build reruns on the counted path, outputs stay bit-exact."""
+    _parity_subprocess({"S3IMPH_RES0": "2", "S3IMPH_RES_FILL": "1"},
+                       [(3000, 0, 40), (300_000, 0, 24), (2_500_000, 1, 0)])
