@@ -395,15 +395,20 @@ Grids level_grids(uint64_t nk, uint64_t size, LevelGeom g) {
 }
 
 // Do reservation slots (bucket_cap / T records per tile, cut into kResShards shards)
-// hold a level of about nb records over `size` positions?  Small levels keep 4x the mean
-// fill; larger ones res_fill x; and tiles so large that a shard's mean fill m is >= 768
-// need only 1 + 7/sqrt(m) (7 sigma of a Poisson fill) plus 2 % for the size estimate.
-// An overflow is caught on the device and the build reruns on the counted path.
-bool res_fits(const s3imph_ctx* c, uint64_t nb, uint64_t size) {
+// hold a level of about nb records over `size` positions (T tiles; 0: the list-level
+// geometry)?  Small levels keep 4x the mean fill; larger ones res_fill x; and tiles so
+// large that a shard's mean fill m is >= 768 need only 1 + 7/sqrt(m) (7 sigma of a
+// Poisson fill) plus 2 % for the size estimate (1.24x at m = 1024: level 0 of 10M keys).
+// Shards follow the XCDs (blockIdx % 8): 16 shards measured far slower (C3 level-0
+// scatter 1.60 -> 2.87 ms), the runs of an XCD's blocks no longer meet in its L2.  An overflow is caught on the device and
+// the build reruns on the counted path.
+bool res_fits(const s3imph_ctx* c, uint64_t nb, uint64_t size, uint64_t T = 0) {
   if (nb * (nb > kResSmallKeys ? c->res_fill : 4) <= c->bucket_cap) return true;
-  const LevelGeom g = choose_geom_sz(nb, size, c->target_tiles_res, c->target_chunks, kRegTileMaxBits);
-  const double T = (double)((size + (1ull << g.tb) - 1) >> g.tb);
-  const double m = (double)nb / (T * kResShards);
+  if (T == 0) {
+    const LevelGeom g = choose_geom_sz(nb, size, c->target_tiles_res, c->target_chunks, kRegTileMaxBits);
+    T = (size + (1ull << g.tb) - 1) >> g.tb;
+  }
+  const double m = (double)nb / ((double)T * kResShards);
   return m >= 768.0 && (double)c->bucket_cap >= (double)nb * (1.02 + 7.0 / std::sqrt(m));
 }
 
@@ -477,10 +482,9 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
     return;
   }
   // Level 0 through the reservation scatter when its tiles are big enough that every
-  // (tile, XCD shard) slot's 1.25x headroom (bucket_cap = 1.25 n) is >= 6.9 sigma of its
-  // mean fill of >= 768 keys (an overflow is caught on the device and rerun counted)
+  // (tile, shard) slot's headroom (bucket_cap = 1.25 n) covers 7 sigma of its fill
   const uint64_t T0 = (64 * level_words(n) + (1ull << g0.tb) - 1) >> g0.tb;
-  const bool res0 = !conservative && c->res0 && T0 <= kScatterTiles && (n >= 768ull * kResShards * T0 || c->res0 == 2);
+  const bool res0 = !conservative && c->res0 && T0 <= kScatterTiles && (res_fits(c, n, 64 * level_words(n), T0) || c->res0 == 2);
   launch_binned_count(0, blob, offsets, n, b, g0, gr.gc, s, !res0);  // no histogram for the reservation path
   ev_mark(c, s, "hash_count0");
   if (res0) {

@@ -1,3 +1,6 @@
 set -e
 mkdir -p gpurun_out/sw
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "hash_variants or counted_path or overflow_reruns or direct_scatter" > gpurun_out/sw/pytest.log 2>&1
+for cfg in c2 c3 c5; do
+  timeout -k 10 120 python bench.py --no-cpu-baseline --config $cfg --steps 20 --warmup 3 > gpurun_out/sw/$cfg.log 2>&1
+done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/sw/pytest.log 2>&1
