@@ -1210,9 +1210,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
                                                   uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
                                                   unsigned long long* __restrict__ prof) {
   extern __shared__ uint64_t dyn64[];
-  __shared__ unsigned long long s_t, s_prefix;
+  __shared__ unsigned long long s_t, s_prefix, s_b0;
   __shared__ unsigned s_wc[NT / 64];
-  __shared__ unsigned long long s_wbase[NT / 64];
   if (!level_active(level, st)) return;
   const uint64_t N = st->out_cap;
   const bool out_on = level_out_on(st, level);
@@ -1343,7 +1342,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
         run += __popc(sA[w]);
       }
     }
+    __syncthreads();  // every word's A & ~C and rank prefix in LDS before any record reads them
     TPROF(2);
+    // Every record settles or collides, so the tile's collided count nk - pop is known
+    // now: wave 1 reserves the next list's slots while wave 0 runs the look-back, and
+    // every wave classifies its records (neither needs the tile's rank prefix).
+    if (tid == 64) s_b0 = nk > pop ? atomicAdd(&st->n[level + 1], (unsigned long long)(nk - pop)) : 0ull;
     if (wave == 0) {
       const uint64_t excl = look_back_wave(flags, t, pop, st);
       if (lane == 0) {
@@ -1351,13 +1355,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
         s_prefix = excl;
       }
     }
-    __syncthreads();
-    TPROF(3);
-    const uint64_t base = lvl_base + s_prefix;
-    const bool ok = base + pop <= N;
-    if (!ok && out_on) bad = true;
-    // ---- classify: settled -> stage[rank] (or direct past the stage); collided -> count
+    // ---- classify: settled -> stage[rank] (ranks past the stage are written below);
+    // collided -> counted per wave
     unsigned wc = 0;
+    uint32_t late = 0;  // bit r: settled with a rank past the stage
     if (fits) {
 #pragma unroll
       for (int r = 0; r < kRegR; ++r) {
@@ -1372,9 +1373,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
             if (rank < scap) {
               sf[rank] = f[r];
               sp[rank] = p[r];
-            } else if (ok && out_on) {
-              fp_out[base + rank] = f[r];
-              pos_out[base + rank] = p[r];
+            } else {
+              late |= 1u << r;
             }
           } else {
             redo = true;
@@ -1387,42 +1387,26 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
         const uint64_t j = jb + lane;
         bool redo = false;
         if (j < nk) {
-          const Rec* q = rb + shard_off((unsigned)j);
-          const unsigned x = (unsigned)(bb_index(seed, q->k, words, magic) - tbase);
-          const uint32_t wv = sA[x >> 5];
-          const uint32_t bit = 1u << (x & 31);
-          if (wv & bit) {
-            const unsigned rank = sC[x >> 5] + __popc(wv & (bit - 1));
-            if (ok && out_on) {
-              fp_out[base + rank] = q->f;
-              pos_out[base + rank] = q->p;
-            }
-          } else {
-            redo = true;
-          }
+          const unsigned x = (unsigned)(bb_index(seed, rb[shard_off((unsigned)j)].k, words, magic) - tbase);
+          redo = !((sA[x >> 5] >> (x & 31)) & 1u);
         }
         wc += __popcll(__ballot(redo));
       }
     }
-    TPROF(4);
+    TPROF(3);
     if (lane == 0) s_wc[wave] = wc;
     __syncthreads();
+    TPROF(4);
+    const uint64_t base = lvl_base + s_prefix;
+    const bool ok = base + pop <= N;
+    if (!ok && out_on) bad = true;
     TPROF(5);
-    if (tid == 0) {
-      unsigned tot = 0;
-      for (int w = 0; w < NT / 64; ++w) tot += s_wc[w];
-      unsigned long long b0 = tot ? atomicAdd(&st->n[level + 1], (unsigned long long)tot) : 0;
-      for (int w = 0; w < NT / 64; ++w) {
-        s_wbase[w] = b0;
-        b0 += s_wc[w];
-      }
-    }
-    __syncthreads();
     TPROF(6);
-    // ---- collided records -> next level; staged settled records -> outputs
-    if (wc) {
-      uint64_t o = s_wbase[wave];
-      if (fits) {
+    // ---- collided records -> next level; settled records -> outputs
+    uint64_t o = s_b0;
+    for (unsigned w = 0; w < wave; ++w) o += s_wc[w];
+    if (fits) {
+      if (wc) {
 #pragma unroll
         for (int r = 0; r < kRegR; ++r) {
           const unsigned j = r * NT + tid;
@@ -1432,28 +1416,50 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
           if (redo) next[o + __popcll(m & lt)] = Rec{k[r], f[r], p[r]};
           o += __popcll(m);
         }
-      } else {
-        for (uint64_t jb = wave * 64; jb < nk; jb += NT) {
-          const uint64_t j = jb + lane;
-          bool redo = false;
-          uint64_t ck = 0;
-          const Rec* q = rb + shard_off((unsigned)j);
-          if (j < nk) {
-            ck = q->k;
-            const unsigned x = (unsigned)(bb_index(seed, ck, words, magic) - tbase);
-            redo = !((sA[x >> 5] >> (x & 31)) & 1u);
+      }
+      if (late && ok && out_on) {
+#pragma unroll
+        for (int r = 0; r < kRegR; ++r) {
+          if ((late >> r) & 1u) {
+            const unsigned x = LOC(r);
+            const uint32_t wv = sA[x >> 5];
+            const uint64_t q = base + sC[x >> 5] + __popc(wv & ((1u << (x & 31)) - 1));
+            fp_out[q] = f[r];
+            pos_out[q] = p[r];
           }
-          const uint64_t m = __ballot(redo);
-          if (redo) next[o + __popcll(m & lt)] = Rec{ck, q->f, q->p};
-          o += __popcll(m);
         }
       }
-    }
-    if (ok && fits && out_on) {
-      const uint64_t ns = min<uint64_t>(pop, scap);
-      for (uint64_t i = tid; i < ns; i += NT) {
-        fp_out[base + i] = sf[i];
-        pos_out[base + i] = sp[i];
+      if (ok && out_on) {
+        const uint64_t ns = min<uint64_t>(pop, scap);
+        for (uint64_t i = tid; i < ns; i += NT) {
+          fp_out[base + i] = sf[i];
+          pos_out[base + i] = sp[i];
+        }
+      }
+    } else {
+      for (uint64_t jb = wave * 64; jb < nk; jb += NT) {
+        const uint64_t j = jb + lane;
+        bool redo = false;
+        const Rec* q = rb + shard_off((unsigned)j);
+        uint64_t ck = 0;
+        if (j < nk) {
+          ck = q->k;
+          const unsigned x = (unsigned)(bb_index(seed, ck, words, magic) - tbase);
+          const uint32_t wv = sA[x >> 5];
+          const uint32_t bit = 1u << (x & 31);
+          if (wv & bit) {
+            if (ok && out_on) {
+              const uint64_t rank = sC[x >> 5] + __popc(wv & (bit - 1));
+              fp_out[base + rank] = q->f;
+              pos_out[base + rank] = q->p;
+            }
+          } else {
+            redo = true;
+          }
+        }
+        const uint64_t m = __ballot(redo);
+        if (redo) next[o + __popcll(m & lt)] = Rec{ck, q->f, q->p};
+        o += __popcll(m);
       }
     }
     __syncthreads();

@@ -336,6 +336,28 @@ def test_hash_variants_bit_exact(s3, oracle_lib, mode):
                        [(1, 0, 8), (3000, 0, 40), (300_000, 0, 64), (2_500_000, 1, 0), (10_000_000, 0, 32)])
 
 
+@pytest.mark.parametrize("kind,avg", [(0, 32), (1, 0)])
+def test_repeated_builds_identical(s3, oracle_lib, ctx, kind, avg):
+    """Schedule-dependent races show up as a build that differs from the others: 12
+    device builds of one 10M-key set (level 0 and levels 1..7 on the reservation path)
+    each equal the oracle's outputs byte for byte (tools/flake_probe.py runs more)."""
+    import torch
+    n = 10_000_000
+    blob, offs = s3.gen_keys(kind, 3, avg, 0, n)
+    st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)
+    assert st == 0
+    d_blob, d_offs = to_dev(blob), to_dev(offs)
+    d_fp = torch.zeros(n, dtype=torch.int64, device="cuda")
+    d_po = torch.zeros(n, dtype=torch.int64, device="cuda")
+    for r in range(12):
+        d_fp.zero_()
+        d_po.zero_()
+        ctx.build(d_blob, d_offs, n, d_fp, d_po)
+        assert ctx.mph_bin() == mph, r
+        assert np.array_equal(from_dev(d_fp), fp), r
+        assert np.array_equal(from_dev(d_po), po), r
+
+
 def _parity_subprocess(env: dict, cases) -> None:
     """Build `cases` (n, kind, avg) through s3imph.build_host in a fresh process with
     `env` set (the library reads its A/B knobs once per process): bit-exact vs the oracle."""
