@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restr
       if (i < n) {
         if (kHash) {
           uint64_t h1, h2;
-          fnv_both_loop(blob, offsets[i], offsets[i + 1], h1, h2);
+          fnv_both_pf(blob, offsets[i], offsets[i + 1], h1, h2);
           zero |= (h1 == 0);
           rec[q] = Rec{h1, h2, ipos ? ipos[i] : pos_base + i};
         } else {
