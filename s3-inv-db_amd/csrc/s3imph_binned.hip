@@ -1710,6 +1710,12 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
   }
 }
 
+void launch_hash0_only(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
+                       int grid, hipStream_t s) {
+  k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
+                                           g.chunk, b.tcnt, 3);
+}
+
 void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s) {
   k_hscan<<<grid, kHST, 0, s>>>(level, b.hist, b.off, b.tile_start, b.sflags, b.st);
 }

@@ -756,6 +756,8 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
   dalloc(c->bucket, capb);
   dalloc(c->list[0], capl);
   dalloc(c->list[1], capl);
+  dalloc(c->kh, capl);  // level-0 hashes of this rank's keys (capl >= n_local)
+  dalloc(c->fp, capl);
   c->bucket_cap = capb;
   c->cap_keys = capl;
   dalloc(c->hist, kHistCap);
@@ -804,6 +806,12 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kScatterTiles * kResShards * sizeof(unsigned), s));
   launch_dist_setup(st, 0, nullptr, N, R, P, s);
   ev_mark(c, s, "init");
+  // level 0's key hashes and fingerprints, once (the routing below may be retried)
+  if (n_local) {
+    const LevelGeom gh = choose_geom_sz(n_local, 64 * level_words(N), c->target_tiles0, c->target_chunks, kTileMaxBits);
+    launch_hash0_only(blob, offsets, n_local, b, gh, level_grids(n_local, 64 * level_words(N), gh).gc, s);
+  }
+  ev_mark(c, s, "hash_count0");
   std::vector<uint64_t> hw, hS;  // words and per-rank range of each distributed level
   std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
   double src_pred = (double)n_local;  // records this rank routes at the current level
@@ -820,7 +828,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
       }
       HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
       if (L == 0)
-        launch_route0(blob, offsets, pos, key_base, n_local, d.send, C, d.scnt, st, P, s);
+        launch_route0_arrays(c->kh, c->fp, pos, key_base, n_local, d.send, C, d.scnt, st, P, s);
       else
         launch_route(L, c->list[(L - 1) & 1], (uint64_t)src_pred, d.send, C, d.scnt, st, P, s);
       launch_route_flag(st, d.scnt, P, s);

@@ -37,16 +37,17 @@ __device__ __forceinline__ unsigned owner_of(uint64_t w, uint64_t S, uint64_t mS
   return (unsigned)d;
 }
 
-// Route this rank's records of level `level` to their owners.  kHash: level 0, the
+// Route this rank's records of level `level` to their owners.  kSrc 0: level 0, the
 // records are made here from the keys (FNV-1a key hash + FNV-1 fingerprint, one pass
-// over the bytes, as StreamingMPHFBuilder.Add does); otherwise they are the collided
-// records list[0..n[level]).  Each round of kRRound records is counting-sorted by owner
+// over the bytes, as StreamingMPHFBuilder.Add does); 2: level 0 from the hash kernel's
+// key-order kh / fp arrays; 1: the collided records list[0..n[level]).  Each round of kRRound records is counting-sorted by owner
 // in LDS; one atomic per (round, owner) reserves its run in the owner's send region
 // [d*cap, (d+1)*cap), and the runs are written out coalesced.  A region overflow sets
 // kStRouteOverflow (the host re-routes with larger regions; bytes are unaffected).
-template <bool kHash>
+template <int kSrc>
 __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restrict__ blob,
                                                const uint64_t* __restrict__ offsets,
+                                               const uint64_t* __restrict__ ikh, const uint64_t* __restrict__ ifp,
                                                const uint64_t* __restrict__ ipos, uint64_t pos_base,
                                                uint64_t n_keys, const Rec* __restrict__ ilist,
                                                Rec* __restrict__ send, uint64_t cap,
@@ -58,7 +59,7 @@ __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restr
   __shared__ unsigned s_over;
   const unsigned tid = threadIdx.x;
   if (tid == 0) s_over = 0;
-  const uint64_t n = kHash ? n_keys : st->n[level];
+  const uint64_t n = kSrc != 1 ? n_keys : st->n[level];
   const uint64_t words = st->words[level], magic = st->magic[level];
   const uint64_t S = st->dS[level], mS = st->dmagic[level];
   const uint64_t seed = level_seed(level);
@@ -73,11 +74,13 @@ __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restr
       const uint64_t i = r0 + (uint64_t)q * kRT + tid;
       d[q] = rk[q] = 0;
       if (i < n) {
-        if (kHash) {
+        if (kSrc == 0) {
           uint64_t h1, h2;
           fnv_both_pf(blob, offsets[i], offsets[i + 1], h1, h2);
           zero |= (h1 == 0);
           rec[q] = Rec{h1, h2, ipos ? ipos[i] : pos_base + i};
+        } else if (kSrc == 2) {
+          rec[q] = Rec{ikh[i], ifp[i], ipos ? ipos[i] : pos_base + i};
         } else {
           rec[q] = ilist[i];
         }
@@ -180,13 +183,20 @@ void launch_route_flag(LevelState* st, unsigned long long* scnt, int P, hipStrea
 void launch_route0(const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t pos_base, uint64_t n,
                    Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + kRRound - 1) / kRRound, 2048));
-  k_route<true><<<grid, kRT, 0, s>>>(0, blob, offsets, pos, pos_base, n, nullptr, send, cap, scnt, st, P);
+  k_route<0><<<grid, kRT, 0, s>>>(0, blob, offsets, nullptr, nullptr, pos, pos_base, n, nullptr, send, cap, scnt, st, P);
+}
+
+void launch_route0_arrays(const uint64_t* kh, const uint64_t* fp, const uint64_t* pos, uint64_t pos_base, uint64_t n,
+                          Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, hipStream_t s) {
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + kRRound - 1) / kRRound, 2048));
+  k_route<2><<<grid, kRT, 0, s>>>(0, nullptr, nullptr, kh, fp, pos, pos_base, n, nullptr, send, cap, scnt, st, P);
 }
 
 void launch_route(int level, const Rec* list, uint64_t n_pred, Rec* send, uint64_t cap, unsigned long long* scnt,
                   LevelState* st, int P, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n_pred + kRRound - 1) / kRRound + 8, 2048));
-  k_route<false><<<grid, kRT, 0, s>>>(level, nullptr, nullptr, nullptr, 0, 0, list, send, cap, scnt, st, P);
+  k_route<1><<<grid, kRT, 0, s>>>(level, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, list, send, cap, scnt, st,
+                                   P);
 }
 
 void launch_dist_setup(LevelState* st, int L, const unsigned long long* gcount, uint64_t n_value, int rank, int P,
