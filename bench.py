@@ -229,6 +229,8 @@ def main() -> None:
             result["roofline"]["valu"] = {"achieved": steps_per_s / 1e12, "peak": FNV_STEP_PEAK_T,
                                           "unit": "T byte-steps/s", "frac": steps_per_s / 1e12 / FNV_STEP_PEAK_T}
         result["dominant_stage"] = max(stages, key=stages.get)
+    if world == 1 and not use_dist:
+        result["lookup"] = lookup_rate(ctx, d_blob, d_offs, n, d_fp, d_po)
     if world == 1:
         result["host_e2e"] = host_e2e(s3imph, blob, offs, local_rank)
     if world == 1 and not args.no_cpu_baseline:
@@ -237,6 +239,24 @@ def main() -> None:
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def lookup_rate(ctx, d_blob, d_offs, n: int, d_fp, d_po, reps: int = 5) -> dict:
+    """Batched MPHF.Lookup of every member (VerifyMPHF, mphf.go:372-393) against the build
+    just timed, device-resident: FNV of each key, level probes, fingerprint check, pos.
+    Reported beside `value`; the first call also builds the word-rank table."""
+    import torch
+    res = torch.empty(n, dtype=torch.int64, device=d_fp.device)
+    ctx.lookup(d_blob, d_offs, n, d_fp, d_po, n, res)  # rank table + warm-up
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(res, torch.arange(n, dtype=torch.int64, device=res.device)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.lookup(d_blob, d_offs, n, d_fp, d_po, n, res)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    return {"keys_per_s": n / dt, "ms": dt * 1e3, "all_members_found": ok,
+            "note": "every member looked up against the last build (device-resident)"}
 
 
 def host_e2e(s3imph, blob, offs, device: int, reps: int = 3) -> dict:
