@@ -235,7 +235,7 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   dalloc(c->tcnt, (uint64_t)kResLevels * kScatterTiles * kResShards);
   alloc_common(c, cap);
   dalloc(c->bits, c->cap_words);
-  dalloc(c->rank_base, c->cap_words);
+  dalloc(c->rank_base, 2 * c->cap_words);  // rank directory: (word, rank) pairs
   c->cap_blocks = (c->cap_words + 2047) / 2048 + 1;
   dalloc(c->block_sums, c->cap_blocks);
   c->cap_keys = cap;
@@ -769,7 +769,7 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
   dalloc(c->tcnt, (uint64_t)kResLevels * kScatterTiles * kResShards);
   c->cap_words = capw;
   dalloc(c->bits, capw);
-  dalloc(c->rank_base, capw);
+  dalloc(c->rank_base, 2 * capw);  // rank directory: (word, rank) pairs
   c->cap_blocks = (capw + 2047) / 2048 + 1;
   dalloc(c->block_sums, c->cap_blocks);
   dalloc(d.send, caps);

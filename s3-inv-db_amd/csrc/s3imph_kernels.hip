@@ -175,12 +175,27 @@ __global__ __launch_bounds__(kBlock) void k_scan_down(const uint64_t* __restrict
 #pragma unroll
   for (int t = 0; t < kScanPerThread; ++t) {
     const uint64_t w = w0 + t;
-    if (w < W) rank_base[w] = run;
+    if (w < W) {  // rank directory: (word, rank before it) side by side, one 16-byte read per probe
+      rank_base[2 * w] = v[t];
+      rank_base[2 * w + 1] = run;
+    }
     run += __popcll(v[t]);
   }
 }
 
 // Batched MPHF.Lookup: FNV-1a -> Find -> p -> range check -> FNV-1 == fp[p] -> pos[p].
+// Each thread takes two keys at a time (i and i + kBlock, so a wave's offsets stay
+// coalesced) and walks their level probes side by side: each probe is one 16-byte read
+// of the (word, rank) directory, and the two keys' dependent reads are in flight together.
+__device__ __forceinline__ bool probe(const ulonglong2* __restrict__ dir, const LevelState* __restrict__ st,
+                                      unsigned L, uint64_t h1, uint64_t& p) {
+  const uint64_t x = bb_index(level_seed(L), h1, st->words[L], st->magic[L]);
+  const ulonglong2 e = dir[st->woff[L] + (x >> 6)];
+  if (!((e.x >> (x & 63)) & 1ull)) return false;
+  p = e.y + __popcll(e.x & ((1ull << (x & 63)) - 1));
+  return true;
+}
+
 __global__ __launch_bounds__(kBlock) void k_lookup(const uint8_t* __restrict__ blob,
                                                    const uint64_t* __restrict__ offsets, uint64_t n,
                                                    const uint64_t* __restrict__ bits,
@@ -189,25 +204,36 @@ __global__ __launch_bounds__(kBlock) void k_lookup(const uint8_t* __restrict__ b
                                                    const uint64_t* __restrict__ fp,
                                                    const uint64_t* __restrict__ pos, uint64_t count,
                                                    uint64_t* __restrict__ result) {
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  const ulonglong2* dir = reinterpret_cast<const ulonglong2*>(rank_base);  // (word, rank) per level word
+  const uint64_t stride = 2ull * gridDim.x * kBlock;
   const unsigned nl = st->nlevels;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-    uint64_t h1, h2;
-    fnv_both(blob, offsets[i], offsets[i + 1], h1, h2);
-    uint64_t out = ~0ull;
-    if (count != 0) {
-      for (unsigned L = 0; L < nl; ++L) {
-        const uint64_t x = bb_index(level_seed(L), h1, st->words[L], st->magic[L]);
-        const uint64_t gw = st->woff[L] + (x >> 6);
-        const uint64_t word = bits[gw];
-        if ((word >> (x & 63)) & 1ull) {
-          const uint64_t p = rank_base[gw] + __popcll(word & ((1ull << (x & 63)) - 1));
-          if (p < count && fp[p] == h2) out = pos[p];
-          break;
-        }
+  for (uint64_t i0 = 2ull * blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += stride) {
+    const uint64_t i1 = i0 + kBlock;
+    const bool v1 = i1 < n;
+    uint64_t a1, a2, b1 = 0, b2 = 0;
+    fnv_both_pf(blob, offsets[i0], offsets[i0 + 1], a1, a2);
+    if (v1) fnv_both_pf(blob, offsets[i1], offsets[i1 + 1], b1, b2);
+    uint64_t pa = ~0ull, pb = ~0ull;
+    bool da = count == 0, db = count == 0 || !v1;  // done: found, or nothing to look in
+    for (unsigned L = 0; L < nl && !(da && db); ++L) {
+      uint64_t qa = 0, qb = 0;
+      const bool fa = !da && probe(dir, st, L, a1, qa);
+      const bool fb = !db && probe(dir, st, L, b1, qb);
+      if (fa) {
+        pa = qa;
+        da = true;
+      }
+      if (fb) {
+        pb = qb;
+        db = true;
       }
     }
-    result[i] = out;
+    const bool ha = pa < count, hb = pb < count;
+    const uint64_t fa = ha ? fp[pa] : 0, fb = hb ? fp[pb] : 0;
+    const uint64_t oa = ha && fa == a2 ? pos[pa] : ~0ull;
+    const uint64_t ob = hb && fb == b2 ? pos[pb] : ~0ull;
+    result[i0] = oa;
+    if (v1) result[i1] = ob;
   }
 }
 
