@@ -1,6 +1,5 @@
 set -e
 mkdir -p gpurun_out/sw
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "lookup or c3 or dist or golden" > gpurun_out/sw/pytest.log 2>&1
-for cfg in c2 c3; do
-  timeout -k 10 200 python bench.py --no-cpu-baseline --config $cfg > gpurun_out/sw/$cfg.log 2>&1
-done
+timeout -k 10 300 python -u tools/flake_probe.py 100 300000 > gpurun_out/sw/flake300k.log 2>&1
+timeout -k 10 300 python -u tools/flake_probe.py 60 2500000 > gpurun_out/sw/flake2m5.log 2>&1
+timeout -k 10 300 python -u tools/flake_probe.py 30 25000000 > gpurun_out/sw/flake25m.log 2>&1
