@@ -1744,10 +1744,19 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
   (tc ? k_tile_reg<NT_, R_, W_, true> : k_tile_reg<NT_, R_, W_, false>)<<<grid_tiles, NT_, lds, s>>>(level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags, \
                                                    b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb,  \
                                                    b.tile_prof)
-    if (g.tb == 14) S3_TILE_REG(512, 20, 2);       // 1 tile per CU
-    else if (g.tb == 13) S3_TILE_REG(256, 20, 2);  // 2 tiles per CU
-    else if (g.tb == 12) S3_TILE_REG(256, 10, 3);  // 3 tiles per CU
-    else S3_TILE_REG(256, 5, 5);                   // 5 tiles per CU
+    // A level with no more tiles than CUs runs one round whatever the variant, so it
+    // takes twice the threads per tile (half the records per thread: a shorter chain).
+    static const bool wide_small = [] {
+      const char* e = std::getenv("S3IMPH_TILE_WIDE");
+      return !e || e[0] != '0';
+    }();
+    const bool one_round = wide_small && grid_tiles <= 256;
+    if (g.tb == 14) S3_TILE_REG(512, 20, 2);                     // 1 tile per CU
+    else if (g.tb == 13 && one_round) S3_TILE_REG(512, 10, 2);
+    else if (g.tb == 13) S3_TILE_REG(256, 20, 2);                // 2 tiles per CU
+    else if (g.tb == 12 && one_round) S3_TILE_REG(512, 5, 2);
+    else if (g.tb == 12) S3_TILE_REG(256, 10, 3);                // 3 tiles per CU
+    else S3_TILE_REG(256, 5, 5);                                 // 5 tiles per CU
 #undef S3_TILE_REG
     return;
   }

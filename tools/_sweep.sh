@@ -1,8 +1,10 @@
 set -e
 mkdir -p gpurun_out/sw
-for cfg in c2 c3; do
-  timeout -k 10 120 python bench.py --no-cpu-baseline --config $cfg --steps 30 --warmup 3 > gpurun_out/sw/$cfg.log 2>&1
+for i in 1 2; do
+for w in 0 1; do
+  for cfg in c2 c5; do
+    S3IMPH_TILE_WIDE=$w timeout -k 10 120 python bench.py --no-cpu-baseline --config $cfg --steps 30 --warmup 3 > gpurun_out/sw/$cfg.w$w.$i.log 2>&1
+  done
 done
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/sw/pmc_write -o run -- python3 bench.py --config c2 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/sw/pmcw.log 2>&1
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/sw/pmc_fetch -o run -- python3 bench.py --config c2 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/sw/pmcf.log 2>&1
+done
+timeout -k 10 300 python -u tools/flake_probe.py 40 > gpurun_out/sw/flake.log 2>&1
