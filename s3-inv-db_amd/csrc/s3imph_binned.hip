@@ -1756,6 +1756,8 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
     else if (g.tb == 13) S3_TILE_REG(256, 20, 2);                // 2 tiles per CU
     else if (g.tb == 12 && one_round) S3_TILE_REG(512, 5, 2);
     else if (g.tb == 12) S3_TILE_REG(256, 10, 3);                // 3 tiles per CU
+    else if (g.tb == 11 && one_round) S3_TILE_REG(512, 3, 2);
+    else if (one_round) S3_TILE_REG(512, 2, 2);
     else S3_TILE_REG(256, 5, 5);                                 // 5 tiles per CU
 #undef S3_TILE_REG
     return;
