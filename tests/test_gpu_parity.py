@@ -146,6 +146,18 @@ def test_ragged_lengths_0_to_1024(s3, oracle_lib, ctx):
     _check_vs_oracle(oracle_lib, s3, ctx, sorted(keys))
 
 
+def test_very_long_keys_mixed(s3, oracle_lib, ctx):
+    """A few 16-200 KiB keys among short ones (the sampled-skew path and the per-lane
+    word chains at extreme lengths), and one key of exactly 2^16 bytes: bit-exact."""
+    rng = np.random.default_rng(11)
+    keys = set()
+    for L in [65536] + [int(x) for x in rng.integers(16 << 10, 200 << 10, 40)]:
+        keys.add(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+    while len(keys) < 20000:
+        keys.add(rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8).tobytes())
+    _check_vs_oracle(oracle_lib, s3, ctx, sorted(keys))
+
+
 def test_unaligned_blob_offsets(s3, oracle_lib, ctx):
     """Keys starting at every byte phase, including a non-zero offsets[0]."""
     keys = [bytes([65 + (i % 26)] * (i % 19)) + b"%d/" % i for i in range(5000)]
