@@ -33,6 +33,7 @@ namespace s3imph {
 namespace {
 
 constexpr int kCB = 1024;             // count block
+constexpr int kHR = 256;              // pipelined level-0 hash block
 constexpr int kSB = 1024;             // scatter block
 constexpr int kTailT = 1024;          // tail block
 constexpr unsigned kLenBuckets = 256;  // key-length classes (4 B each) of the level-0 hash sort
@@ -130,7 +131,8 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
   __shared__ unsigned short sidx[kCB];
   __shared__ uint64_t sb0[kCB], sb1[kCB], sh1[kCB], sh2[kCB];
   __shared__ uint64_t s_lmax[kCB / 64], s_lsum[kCB / 64];
-  const bool sort = smode == 1 || smode == 2 || (smode == 3 && st->skew);
+  if (smode == 4 && !st->skew) return;  // pipelined level 0: k_hash0_range hashes this set
+  const bool sort = smode == 1 || smode == 2 || ((smode == 3 || smode == 4) && st->skew);
   const uint64_t words = st->words[0], magic = st->magic[0];
   const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
   if (!geom_ok(st, T, B)) return;
@@ -238,6 +240,30 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
     __syncthreads();
   }
   if (zero) atomicOr(&st->status, kStKeyZero);
+}
+
+// --------------------------------------------------- pipelined level-0 hash ---------
+// FNV-1a + FNV-1 of keys [lo, hi) into kh / fp (key order), one key per thread, loads two
+// words ahead, no LDS: its blocks fit beside a k_scatter_res block (152 KiB of LDS) on
+// the same CU, so the hash of chunk k+1 (VALU-bound) runs while chunk k is scattered
+// (atomics, LDS and memory latency) on the other stream.  Near-uniform sets only: a
+// skewed set was hashed length-sorted by k_hash_count0 (smode 4) and this returns.
+__global__ __launch_bounds__(kHR) void k_hash0_range(const uint8_t* __restrict__ blob,
+                                                     const uint64_t* __restrict__ offsets, uint64_t lo, uint64_t hi,
+                                                     uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
+                                                     LevelState* st, unsigned* __restrict__ tcnt) {
+  // chunk 0 clears every level's reservation counters (k_hash_count0's job otherwise)
+  if (tcnt)
+    for (uint64_t q = (uint64_t)blockIdx.x * kHR + threadIdx.x; q < kTcntWords; q += (uint64_t)gridDim.x * kHR)
+      tcnt[q] = 0;
+  if (st->skew) return;
+  const uint64_t i = lo + (uint64_t)blockIdx.x * kHR + threadIdx.x;
+  if (i >= hi) return;
+  uint64_t h1, h2;
+  hash_key<2>(blob, offsets[i], offsets[i + 1], h1, h2);
+  kh[i] = h1;
+  fp[i] = h2;
+  if (h1 == 0) atomicOr(&st->status, kStKeyZero);
 }
 
 // ------------------------------------------------------------- level L setup ---------
@@ -506,7 +532,8 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
                                                      unsigned* __restrict__ tcnt, Rec* __restrict__ bucket,
                                                      uint64_t bucket_cap, unsigned long long* __restrict__ flags,
                                                      LevelState* st, unsigned tb, uint64_t cap_words,
-                                                     unsigned long long* __restrict__ prof) {
+                                                     unsigned long long* __restrict__ prof, uint64_t i_lo,
+                                                     uint64_t i_hi) {
   constexpr int kKPT = kR / kSB;
   __shared__ Rec stage[kR];
   __shared__ unsigned short stile[kR];
@@ -518,7 +545,8 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   const bool preset = st->preset[level] != 0;
   if (!preset && p > 0 && !st->preset[p] && st->n[p] <= kGate) return;  // previous level ran in the tail
   if (st->status & (kStGeometry | kStOverflow | kStLookback)) return;
-  const uint64_t n = st->n[level];
+  // [i_lo, i_hi): one chunk of level 0's key-order arrays (pipelined level 0); else all
+  const uint64_t n = i_hi ? min<uint64_t>(st->n[level], i_hi) : st->n[level];
   const unsigned tid = threadIdx.x;
   uint64_t words, magic, woff;
   if (level == 0 || preset) {  // level 0: sized by k_init_state; preset: by the multi-GPU build
@@ -556,7 +584,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   const unsigned shard = blockIdx.x % kResShards;
   const uint64_t seed = level_seed(level);
   const uint64_t stride = (uint64_t)gridDim.x * kR;
-  uint64_t r0 = (uint64_t)blockIdx.x * kR;
+  uint64_t r0 = i_lo + (uint64_t)blockIdx.x * kR;
   if (r0 >= n) return;
   // debug: round-0 phase timestamps of this block in prof row 32 + level
   unsigned long long* tp =
@@ -1783,13 +1811,27 @@ void launch_hash_scatter0(const uint8_t* blob, const uint64_t* offsets, uint64_t
   }
 }
 
-void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s) {
+void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s, uint64_t i_lo,
+                               uint64_t i_hi) {
   const bool l0 = level == 0 && !b.dist;
   const Rec* il = l0 ? nullptr : b.list[(level - 1) & 1];
   unsigned* tc = b.tcnt + (uint64_t)level * kScatterTiles * kResShards;
   k_scatter_res<kSubRound, kLdsTiles><<<grid, kSB, 0, s>>>(level, il, b.kh, b.fp, b.pos, b.pos_base, tc, b.bucket,
                                                            b.bucket_cap, b.flags, b.st, g.tb, b.cap_words,
-                                                           b.tile_prof);
+                                                           b.tile_prof, i_lo, i_hi);
+}
+
+void launch_hash0_range(const uint8_t* blob, const uint64_t* offsets, uint64_t lo, uint64_t hi, const BinBuffers& b,
+                        hipStream_t s) {
+  if (hi <= lo) return;
+  const uint64_t grid = (hi - lo + kHR - 1) / kHR;
+  k_hash0_range<<<(unsigned)grid, kHR, 0, s>>>(blob, offsets, lo, hi, b.kh, b.fp, b.st, lo == 0 ? b.tcnt : nullptr);
+}
+
+void launch_hash0_skewed(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
+                         int grid, hipStream_t s) {
+  k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
+                                           g.chunk, b.tcnt, 4);
 }
 
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s) {

@@ -117,6 +117,12 @@ struct s3imph_ctx {
   // (full 256-block grids: every XCD shard of a slot then fills evenly)
   uint64_t res_fill = 2;
   int res0 = 1;  // level 0 through the reservation scatter when its tiles are large
+  // level 0 in pipe0 chunks: the hash of chunk k+1 (aux stream) overlaps the reservation
+  // scatter of chunk k (build stream); 0 / 1: one hash launch, then one scatter launch
+  int pipe0 = 0;
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_chunk[kPipe0MaxChunks] = {};
   bool debug = false;
   unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps
   bool lds_attr_set = false;
@@ -459,6 +465,14 @@ int enqueue_levels_from(s3imph_ctx* c, const BinBuffers& b, int L0, uint64_t n0,
   return launched;
 }
 
+// The pipelined level 0's second stream and its fork / per-chunk events, made on first use.
+void ensure_aux(s3imph_ctx* c) {
+  if (c->aux) return;
+  HIPCHECK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+  HIPCHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+  for (auto& e : c->ev_chunk) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+}
+
 // Enqueue one attempt of the binned pipeline.  `conservative` sizes every level with
 // the level-0 geometry (always inside the workspace bounds) and runs every level that
 // is still big as a full-grid level; the default predicts each level's size.
@@ -485,6 +499,32 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   // (tile, shard) slot's headroom (bucket_cap = 1.25 n) covers 7 sigma of its fill
   const uint64_t T0 = (64 * level_words(n) + (1ull << g0.tb) - 1) >> g0.tb;
   const bool res0 = !conservative && c->res0 && T0 <= kScatterTiles && (res_fits(c, n, 64 * level_words(n), T0) || c->res0 == 2);
+  if (res0 && c->pipe0 > 1 && n >= kPipe0MinKeys) {
+    // Level 0 pipelined over K chunks: the aux stream hashes chunk k+1 while the build
+    // stream scatters chunk k; the two kernels share CUs (the hash uses no LDS).
+    ensure_aux(c);  // (chunk 0's hash clears the reservation counters of every level)
+    HIPCHECK(hipEventRecord(c->ev_fork, s));
+    HIPCHECK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    launch_hash0_skewed(blob, offsets, n, b, g0, gr.gc, c->aux);  // returns unless lengths are skewed
+    const int K = std::min(c->pipe0, kPipe0MaxChunks);
+    uint64_t lo = 0;
+    for (int k = 0; k < K; ++k) {
+      uint64_t hi = n;
+      if (k + 1 < K) hi = std::min<uint64_t>(n, (n * (k + 1) / K + kSubRound - 1) / kSubRound * kSubRound);
+      launch_hash0_range(blob, offsets, lo, hi, b, c->aux);  // returns if skewed
+      HIPCHECK(hipEventRecord(c->ev_chunk[k], c->aux));
+      HIPCHECK(hipStreamWaitEvent(s, c->ev_chunk[k], 0));
+      if (hi > lo)
+        launch_binned_scatter_res(0, b, g0, (int)std::min<uint64_t>(256, (hi - lo + kSubRound - 1) / kSubRound), s,
+                                  lo, hi);
+      lo = hi;
+    }
+    ev_mark(c, s, "hash_scatter0");
+    launch_binned_tile(0, b, g0, gr.gt, s, true);
+    ev_mark(c, s, "tile0");
+    enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
+    return;
+  }
   launch_binned_count(0, blob, offsets, n, b, g0, gr.gc, s, !res0);  // no histogram for the reservation path
   ev_mark(c, s, "hash_count0");
   if (res0) {
@@ -1275,6 +1315,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     if (const char* m = std::getenv("S3IMPH_TILE_BLOCK")) c->tile_block = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_L0")) c->l0_mode = std::atoi(m);
+    if (const char* m = std::getenv("S3IMPH_PIPE0")) c->pipe0 = std::atoi(m);
     // A blocking stream: implicitly ordered with the legacy NULL stream, so work a
     // caller queued there (e.g. torch's default stream) completes before ours starts.
     HIPCHECK(hipStreamCreate(&c->own_stream));
@@ -1304,6 +1345,12 @@ int s3imph_ctx_destroy(s3imph_ctx* c) {
   delete c->d.comm;
   c->d.comm = nullptr;
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->aux) {
+    (void)hipStreamSynchronize(c->aux);
+    (void)hipStreamDestroy(c->aux);
+    (void)hipEventDestroy(c->ev_fork);
+    for (auto e : c->ev_chunk) (void)hipEventDestroy(e);
+  }
   delete c;
   return S3IMPH_OK;
 }

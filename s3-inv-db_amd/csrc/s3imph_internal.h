@@ -96,6 +96,8 @@ constexpr uint64_t kResSmallKeys = 2ull << 20;  // ... with 4x slot headroom up 
 constexpr int kResShards = 8;                 // per-tile reservation counters (one per XCD)
 constexpr int kResLevels = 32;                // levels that may use the reservation path
 constexpr double kTailMargin = 1.1;
+constexpr int kPipe0MaxChunks = 16;              // pipelined level 0: most chunks
+constexpr uint64_t kPipe0MinKeys = 1ull << 20;   // ... and fewest keys it runs on
 constexpr uint64_t kTargetChunks = 768;  // 3 resident 1024-thread count blocks x 256 CUs
 // n records over `size` positions (64 * level_words(n) for a whole level).
 inline LevelGeom choose_geom_sz(uint64_t n, uint64_t size, uint64_t target_tiles = kTargetTiles,
@@ -181,7 +183,14 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
                         bool reserved = false);
 void launch_hash_scatter0(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                           int variant, hipStream_t s);
-void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s);
+void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s,
+                               uint64_t i_lo = 0, uint64_t i_hi = 0);
+// pipelined level 0: keys [lo, hi) hashed into kh / fp (near-uniform sets; returns on a
+// skewed one), and the length-sorted hash of a skewed set (returns on a near-uniform one)
+void launch_hash0_range(const uint8_t* blob, const uint64_t* offsets, uint64_t lo, uint64_t hi, const BinBuffers& b,
+                        hipStream_t s);
+void launch_hash0_skewed(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
+                         int grid, hipStream_t s);
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s);
 
 // ---- multi-GPU launchers (s3imph_dist.hip) ------------------------------------------

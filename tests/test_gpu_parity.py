@@ -391,6 +391,14 @@ def _parity_subprocess(env: dict, cases) -> None:
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
+def test_pipelined_level0(s3, oracle_lib):
+    """Level 0 in 4 chunks whose hash (aux stream) overlaps the previous chunk's reservation
+    scatter (S3IMPH_PIPE0=4, off by default): near-uniform and skewed sets, and builds
+    repeated on one context (chunk 0 clears every level's reservation counters)."""
+    _parity_subprocess({"S3IMPH_PIPE0": "4"},
+                       [(2_500_000, 0, 32), (2_500_000, 1, 0), (10_000_000, 0, 32), (10_000_000, 0, 32)])
+
+
 def test_direct_scatter_forced_small(s3, oracle_lib):
     """The direct scatter on every counted level (S3IMPH_SCATTER_DIRECT=1), small sets."""
     _parity_subprocess({"S3IMPH_SCATTER_DIRECT": "1"}, [(300_000, 0, 24), (2_500_000, 1, 0)])

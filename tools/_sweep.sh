@@ -1,10 +1,12 @@
 set -e
-mkdir -p gpurun_out/sw
+O=gpurun_out/pipe
+mkdir -p $O
+S3IMPH_PIPE0=4 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_pipe4.log 2>&1
 for i in 1 2; do
-for w in 0 1; do
-  for cfg in c2 c5; do
-    S3IMPH_TILE_WIDE=$w timeout -k 10 120 python bench.py --no-cpu-baseline --config $cfg --steps 30 --warmup 3 > gpurun_out/sw/$cfg.w$w.$i.log 2>&1
+for k in 0 2 4 8; do
+  for cfg in c2 c3 c5; do
+    S3IMPH_PIPE0=$k timeout -k 10 120 python bench.py --no-cpu-baseline --config $cfg --steps 20 --warmup 3 > $O/$cfg.k$k.$i.log 2>&1
   done
 done
 done
-timeout -k 10 300 python -u tools/flake_probe.py 40 > gpurun_out/sw/flake.log 2>&1
+echo done > $O/DONE
