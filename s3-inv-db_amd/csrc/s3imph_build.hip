@@ -110,6 +110,7 @@ struct s3imph_ctx {
   int tile_mode = 0;
   int tile_block = 1024;
   uint64_t target_tiles = kTargetTiles, target_tiles0 = kTargetTiles0, target_chunks = kTargetChunks;
+  bool chunks_set = false;  // S3IMPH_CHUNKS given: level 0 uses it too
   uint64_t res_max_keys = kResMaxKeys;
   int l0_mode = 0;  // level 0: 0 hash+count / scan / scatter; 1, 2 fused hash+scatter (4096 / 2048-key rounds)
   uint64_t target_tiles_res = kTargetTilesRes;
@@ -473,6 +474,15 @@ void ensure_aux(s3imph_ctx* c) {
   for (auto& e : c->ev_chunk) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 }
 
+// Chunks (hash blocks) of the level-0 hash over n keys.  Blocks are scheduled as they
+// free up, so more, smaller chunks even out long-key chunks on big sets; on small ones
+// each block's fixed cost wins (S3IMPH_CHUNKS sweep, hash_count0 ms at 768 / 1536
+// chunks: C2 0.229 / 0.243, C3 3.89 / 3.75, C5 4.28 / 4.05).
+uint64_t chunks0(const s3imph_ctx* c, uint64_t n) {
+  if (c->chunks_set) return c->target_chunks;
+  return n >= kBigChunksKeys ? 2 * kTargetChunks : kTargetChunks;
+}
+
 // Enqueue one attempt of the binned pipeline.  `conservative` sizes every level with
 // the level-0 geometry (always inside the workspace bounds) and runs every level that
 // is still big as a full-grid level; the default predicts each level's size.
@@ -480,7 +490,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
   const BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
   const double q = 1.0 - std::exp(-0.5);
-  const LevelGeom g0 = choose_geom(n, c->target_tiles0, c->target_chunks, kRegTileMaxBits);
+  const LevelGeom g0 = choose_geom(n, c->target_tiles0, chunks0(c, n), kRegTileMaxBits);
   launch_init_state(c->d_st, n, n, s, offsets);
   ev_mark(c, s, "init");
   const Grids gr = level_grids(n, 64 * level_words(n), g0);
@@ -848,7 +858,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   ev_mark(c, s, "init");
   // level 0's key hashes and fingerprints, once (the routing below may be retried)
   if (n_local) {
-    const LevelGeom gh = choose_geom_sz(n_local, 64 * level_words(N), c->target_tiles0, c->target_chunks, kTileMaxBits);
+    const LevelGeom gh = choose_geom_sz(n_local, 64 * level_words(N), c->target_tiles0, chunks0(c, n_local), kTileMaxBits);
     launch_hash0_only(blob, offsets, n_local, b, gh, level_grids(n_local, 64 * level_words(N), gh).gc, s);
   }
   ev_mark(c, s, "hash_count0");
@@ -1306,7 +1316,10 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     if (const char* m = std::getenv("S3IMPH_TILE_MODE")) c->tile_mode = std::atoi(m);  // A/B knobs
     if (const char* m = std::getenv("S3IMPH_TARGET_TILES")) c->target_tiles = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_TARGET_TILES0")) c->target_tiles0 = std::strtoull(m, nullptr, 10);
-    if (const char* m = std::getenv("S3IMPH_CHUNKS")) c->target_chunks = std::strtoull(m, nullptr, 10);
+    if (const char* m = std::getenv("S3IMPH_CHUNKS")) {
+      c->target_chunks = std::strtoull(m, nullptr, 10);
+      c->chunks_set = true;
+    }
     if (const char* m = std::getenv("S3IMPH_RES_MAX")) c->res_max_keys = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_TARGET_TILES_RES")) c->target_tiles_res = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_RES_FILL")) c->res_fill = std::strtoull(m, nullptr, 10);

@@ -99,6 +99,7 @@ constexpr double kTailMargin = 1.1;
 constexpr int kPipe0MaxChunks = 16;              // pipelined level 0: most chunks
 constexpr uint64_t kPipe0MinKeys = 1ull << 20;   // ... and fewest keys it runs on
 constexpr uint64_t kTargetChunks = 768;  // 3 resident 1024-thread count blocks x 256 CUs
+constexpr uint64_t kBigChunksKeys = 20ull << 20;  // level-0 hash of this many keys or more: 2x the chunks
 // n records over `size` positions (64 * level_words(n) for a whole level).
 inline LevelGeom choose_geom_sz(uint64_t n, uint64_t size, uint64_t target_tiles = kTargetTiles,
                                 uint64_t target_chunks = kTargetChunks, unsigned max_tb = kTileMaxBits) {
