@@ -7,7 +7,8 @@ os.environ["S3IMPH_DEBUG"] = "1"
 import numpy as np, torch
 import s3imph
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
-blob, offs = s3imph.gen_keys(0, 42, 32, 0, n)
+avg = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+blob, offs = s3imph.gen_keys(0, 42, avg, 0, n)
 ctx = s3imph.DeviceBuilder(0)
 d_blob = torch.from_numpy(blob).cuda(); d_offs = torch.from_numpy(offs.view(np.int64)).cuda()
 d_fp = torch.zeros(n, dtype=torch.int64, device="cuda"); d_po = torch.zeros(n, dtype=torch.int64, device="cuda")
