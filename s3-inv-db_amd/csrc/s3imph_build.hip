@@ -119,7 +119,8 @@ struct s3imph_ctx {
   uint64_t res_fill = 2;
   int res0 = 1;  // level 0 through the reservation scatter when its tiles are large
   // level 0 in pipe0 chunks: the hash of chunk k+1 (aux stream) overlaps the reservation
-  // scatter of chunk k (build stream); 0 / 1: one hash launch, then one scatter launch
+  // scatter of chunk k (build stream); 1: k_hash0_range over every key, then one scatter;
+  // 0: k_hash_count0, then one scatter
   int pipe0 = 0;
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr;
@@ -509,7 +510,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   // (tile, shard) slot's headroom (bucket_cap = 1.25 n) covers 7 sigma of its fill
   const uint64_t T0 = (64 * level_words(n) + (1ull << g0.tb) - 1) >> g0.tb;
   const bool res0 = !conservative && c->res0 && T0 <= kScatterTiles && (res_fits(c, n, 64 * level_words(n), T0) || c->res0 == 2);
-  if (res0 && c->pipe0 > 1 && n >= kPipe0MinKeys) {
+  if (res0 && c->pipe0 >= 1 && n >= kPipe0MinKeys) {
     // Level 0 pipelined over K chunks: the aux stream hashes chunk k+1 while the build
     // stream scatters chunk k; the two kernels share CUs (the hash uses no LDS).
     ensure_aux(c);  // (chunk 0's hash clears the reservation counters of every level)
