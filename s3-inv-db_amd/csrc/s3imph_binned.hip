@@ -1511,7 +1511,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
                                                      unsigned long long* __restrict__ prof) {
   __shared__ uint64_t ck[kTailKeys];           // live keys, as mix64(key hash)
   __shared__ unsigned short cj[kTailKeys];     // ... and their index in the input list
-  __shared__ unsigned short srank[kTailKeys];  // settled rank -> input index
+  __shared__ unsigned short srank[kTailKeys];  // tail rank (every tail level) -> input index
   __shared__ uint32_t sA[kTailW32];
   __shared__ uint32_t sC[kTailW32];
   __shared__ uint32_t spre[kTailW32];
@@ -1555,6 +1555,11 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
     }
   }
   __syncthreads();
+  // Outputs of every tail level go out in one pass after the last level: the tail's ranks
+  // are contiguous from the first tail level's base, so one rank -> input-index table
+  // covers them all and the (f, p) gathers from `in` pay one memory round trip, not one
+  // per level.  Levels with outputs on are a prefix of the tail (out_skip_from).
+  uint64_t base0 = ~0ull, out_end = 0;
   for (;;) {
     const int L = s_level;
     const unsigned n = (unsigned)s_n;
@@ -1571,6 +1576,8 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
     }
     const uint64_t words = st->words[L], magic = st->magic[L], woff = st->woff[L];
     const uint64_t base = st->lvl_base[L];
+    if (base0 == ~0ull) base0 = base;
+    const unsigned rb0 = (unsigned)(base - base0);  // this level's first slot in srank
     const unsigned w32 = (unsigned)(2 * words);
     for (unsigned w = tid; w < w32; w += kTailT) {
       sA[w] = 0;
@@ -1623,7 +1630,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
         const uint32_t x = (uint32_t)bb_index_mk(seed, k, words, magic);
         const uint32_t wv = sA[x >> 5];
         const uint32_t bit = 1u << (x & 31);
-        if (wv & bit) srank[spre[x >> 5] + __popc(wv & (bit - 1))] = (unsigned short)j;
+        if (wv & bit) srank[rb0 + spre[x >> 5] + __popc(wv & (bit - 1))] = (unsigned short)j;
         else coll = true;
       }
       const uint64_t m = __ballot(coll);
@@ -1643,17 +1650,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
       n1 += all;
       __syncthreads();
     }
-    if (level_out_on(st, L)) {
-      if (base + tot > N) bad = true;
-      const uint64_t m = base + tot <= N ? tot : 0;
-#pragma unroll 4
-      for (uint64_t i = tid; i < m; i += kTailT) {
-        const Rec* src = in + srank[i];
-        fp_out[base + i] = src->f;
-        pos_out[base + i] = src->p;
-      }
-    }
-    __syncthreads();
+    if (level_out_on(st, L)) out_end = rb0 + tot;
     if (tid == 0) {
       const uint64_t w1 = n1 ? level_words(n1) : 0;
       st->n[L + 1] = n1;
@@ -1672,6 +1669,18 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
       s_level = L + 1;
     }
     __syncthreads();
+  }
+  if (out_end) {
+    if (base0 + out_end > N) {
+      bad = true;
+    } else {
+#pragma unroll 4
+      for (uint64_t i = tid; i < out_end; i += kTailT) {
+        const Rec* src = in + srank[i];
+        fp_out[base0 + i] = src->f;
+        pos_out[base0 + i] = src->p;
+      }
+    }
   }
   if (bad) atomicOr(&st->status, kStRank);
   if (tid == 0) st->rank_total = st->lvl_base[s_level];
