@@ -1501,9 +1501,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
 // --------------------------------------------------------------------- tail --------
 // Every remaining level in one workgroup, with the live records in LDS: the first tail
 // level's key hashes (and their input indices) are loaded once; each level marks A/C
-// in LDS, finalizes and ranks, writes the settled records' outputs in rank order (f, p
-// fetched from the first tail level's input list through an LDS rank -> index table)
-// and compacts the collided records in place for the next level.  No level after the
+// in LDS, finalizes and ranks, records each settled key's input index at its rank in an
+// LDS table shared by all tail levels, and compacts the collided records in place for the
+// next level; the outputs of every tail level go out in one rank-order pass at the end
+// (f, p fetched from the first tail level's input list through that table).  No level after the
 // first reads or writes a record list.
 __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_launched, Rec* list0, Rec* list1, uint64_t* bits,
                                                      uint64_t cap_words, uint64_t* __restrict__ fp_out,
