@@ -1499,6 +1499,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
 }
 
 // --------------------------------------------------------------------- tail --------
+constexpr unsigned kWaveKeys = 64;  // tail levels this small run in one wave
+
+// Orders one wave's LDS accesses across lanes (a wave's LDS operations execute in order;
+// this keeps the compiler from moving them across the point).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Every remaining level in one workgroup, with the live records in LDS: the first tail
 // level's key hashes (and their input indices) are loaded once; each level marks A/C
 // in LDS, finalizes and ranks, records each settled key's input index at its rank in an
@@ -1518,6 +1528,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
   __shared__ uint32_t spre[kTailW32];
   __shared__ unsigned s_wc[kTailT / 64];
   __shared__ unsigned long long s_n;
+  __shared__ unsigned long long s_wbase0, s_wout;  // wave-level tail: base0 / out_end for the block
   __shared__ int s_level;
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   if (tid == 0) {
@@ -1561,6 +1572,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
   // covers them all and the (f, p) gathers from `in` pay one memory round trip, not one
   // per level.  Levels with outputs on are a prefix of the tail (out_skip_from).
   uint64_t base0 = ~0ull, out_end = 0;
+  bool wave_levels = false;
   for (;;) {
     const int L = s_level;
     const unsigned n = (unsigned)s_n;
@@ -1573,6 +1585,10 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
       if (tid == 0) atomicOr(&st->status, kStTooManyLevels);
       Rec* out = (L & 1) ? list0 : list1;
       for (unsigned i = tid; i < n; i += kTailT) out[i] = Rec{ck[i], 0, 0};
+      break;
+    }
+    if (n <= kWaveKeys) {  // the rest runs in wave 0 alone, below
+      wave_levels = true;
       break;
     }
     const uint64_t words = st->words[L], magic = st->magic[L], woff = st->woff[L];
@@ -1670,6 +1686,99 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
       s_level = L + 1;
     }
     __syncthreads();
+  }
+  // Levels of at most kWaveKeys keys: wave 0 alone, lane i holding key i, so a level costs
+  // wave-local LDS ops and ballots instead of the block's barriers (~3 us per level).
+  // Level parameters are carried in registers (the same values the block path writes).
+  if (wave_levels) {
+    if (wave == 0) {
+      int L = s_level;
+      unsigned n = (unsigned)s_n;
+      uint64_t words = st->words[L], magic = st->magic[L], woff = st->woff[L], base = st->lvl_base[L];
+      if (base0 == ~0ull) base0 = base;
+      uint32_t* g32 = nullptr;
+      for (;;) {
+        if (prof && lane == 0 && L < kMaxLevels) prof[(uint64_t)(kMaxLevels - 1) * kMaxTiles * 8 + L] = wall_clock64();
+        if (n == 0) break;
+        const bool act = lane < n;
+        if (L >= kMaxLevels) {  // as in the block path
+          if (lane == 0) atomicOr(&st->status, kStTooManyLevels);
+          Rec* out = (L & 1) ? list0 : list1;
+          if (act) out[lane] = Rec{ck[lane], 0, 0};
+          break;
+        }
+        const uint64_t k = act ? ck[lane] : 0;
+        const unsigned short j = act ? cj[lane] : (unsigned short)0;
+        const unsigned w32 = (unsigned)(2 * words);  // <= 4 for <= 64 keys
+        const unsigned rb0 = (unsigned)(base - base0);
+        if (lane < w32) {
+          sA[lane] = 0;
+          sC[lane] = 0;
+        }
+        wave_lds_sync();
+        uint32_t x = 0;
+        if (act) {
+          x = (uint32_t)bb_index_mk(level_seed(L), k, words, magic);
+          const uint32_t bit = 1u << (x & 31);
+          const uint32_t old = atomicOr(&sA[x >> 5], bit);
+          if (old & bit) atomicOr(&sC[x >> 5], bit);
+        }
+        wave_lds_sync();
+        g32 = reinterpret_cast<uint32_t*>(bits + woff);
+        uint32_t v = 0;
+        if (lane < w32) {
+          v = sA[lane] & ~sC[lane];
+          g32[lane] = v;
+        }
+        unsigned tot = 0, pre = 0;
+        uint32_t vx = 0;
+        for (unsigned q = 0; q < w32; ++q) {
+          const uint32_t vq = (uint32_t)__shfl((int)v, (int)q);
+          tot += __popc(vq);
+          if (q < (x >> 5)) pre += __popc(vq);
+          if (q == (x >> 5)) vx = vq;
+        }
+        const uint32_t bit = 1u << (x & 31);
+        const bool settled = act && (vx & bit);
+        if (settled) srank[rb0 + pre + __popc(vx & (bit - 1))] = j;
+        const uint64_t cm = __ballot(act && !settled);
+        const unsigned n1 = (unsigned)__popcll(cm);
+        wave_lds_sync();
+        if (act && !settled) {
+          const unsigned d = (unsigned)__popcll(cm & lanemask_lt());
+          ck[d] = k;
+          cj[d] = j;
+        }
+        wave_lds_sync();
+        if (level_out_on(st, L)) out_end = rb0 + tot;
+        const uint64_t w1 = n1 ? level_words(n1) : 0;
+        const bool over = woff + words + w1 > cap_words;
+        if (lane == 0) {
+          st->n[L + 1] = n1;
+          st->words[L + 1] = w1;
+          st->magic[L + 1] = level_magic(w1);
+          st->woff[L + 1] = woff + words;
+          st->woff[L + 2] = woff + words + w1;
+          st->lvl_base[L + 1] = base + tot;
+          st->nlevels = L + 1;
+          if (over) atomicOr(&st->status, kStOverflow);
+        }
+        woff += words;
+        words = w1;
+        magic = level_magic(w1);
+        base += tot;
+        n = over ? 0 : n1;
+        ++L;
+      }
+      if (lane == 0) {
+        s_level = L;
+        s_wbase0 = base0;
+        s_wout = out_end;
+      }
+    }
+    __syncthreads();
+    base0 = s_wbase0;
+    out_end = s_wout;
   }
   if (out_end) {
     if (base0 + out_end > N) {
