@@ -6,13 +6,15 @@ in HBM: FNV-1a key hashes + FNV-1 fingerprints, every BBHash level, level ranks,
 the mph_fp / mph_pos placement — the work of StreamingMPHFBuilder.Build minus file
 I/O (/root/reference/pkg/format/mphf_streaming.go:122-213).
 
-  python bench.py [--gpus N --steps K --warmup W --config c2]
+  python bench.py [--gpus N --steps K --warmup W --config c3]
   N > 1: torchrun --nproc-per-node N bench.py --gpus N ...  (one process per GPU;
          RCCL communicator owned by libs3imph; torch.distributed/gloo only for the
          rendezvous, barriers and the max-over-ranks time).
 
-Workload (BASELINE.json configs[1]): 10M synthetic prefixes per GPU, avg key 32 B
-(weak scaling: N GPUs build one MPHF over N x 10M keys).
+Workload: BASELINE.json configs[2] (C3), the largest single-GPU configuration:
+100M synthetic prefixes per GPU, avg key 64 B (weak scaling: N GPUs build one MPHF over
+N x 100M keys).  At N = 1 a C2 line (configs[1], 10M keys, avg 32 B) rides beside it
+as `secondary` (never `value`).
 """
 from __future__ import annotations
 
@@ -37,7 +39,7 @@ CONFIGS = {
     "c4": dict(kind=0, avg=32, keys_per_gpu=125_000_000,
                workload="C4: 125M synthetic prefixes per GPU (1B on 8 GPUs), avg key 32 B"),
     "c5": dict(kind=1, avg=0, keys_per_gpu=25_000_000,
-               workload="C5: 25M prefixes per GPU (200M on 8 GPUs), key length log-uniform 10-1024 B"),
+               workload="C5: 25M prefixes per GPU (200M on 8 GPUs), key length log-uniform 1-1024 B"),
 }
 
 
@@ -59,14 +61,14 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist", action="store_true", help="use the multi-GPU build path even at N=1")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
                     help="N>1 collectives: RCCL over xGMI (default), or host copies over gloo — a rehearsal "
                          "mode that lets several ranks share one GPU (not a measurement)")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C2 line beside the C3 headline")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC summary (HBM bytes per launch) to attach as roofline.traffic")
     args = ap.parse_args()
@@ -217,24 +219,30 @@ def main() -> None:
                 traffic = ent["hbm_bytes_per_launch"]
         except (OSError, ValueError):
             pass
-        result["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS,
-                              "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
-                              "alg_bytes": alg, "avg_ms": dom_ms,
-                              "timed_region_events": dom in timed_stages}
+        hbm = {"achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS}
+        result["roofline"] = {"kernel": dom, "bound": "hbm", **hbm, "traffic": traffic, "alg_bytes": alg,
+                              "avg_ms": dom_ms, "timed_region_events": dom in timed_stages}
         if dom == "hash_count0":
             # The hash is bounded by VALU before HBM: every key byte is one FNV-1a + FNV-1 step
             # (two 64-bit multiplies by the FNV prime); tools/ubench_fnv.hip measured the chip's
-            # ceiling for that step from registers.
+            # ceiling for that step from registers.  Its HBM rate rides
+            # along in roofline.hbm.
             steps_per_s = key_bytes_local / (dom_ms / 1e3)
-            result["roofline"]["valu"] = {"achieved": steps_per_s / 1e12, "peak": FNV_STEP_PEAK_T,
-                                          "unit": "T byte-steps/s", "frac": steps_per_s / 1e12 / FNV_STEP_PEAK_T}
+            result["roofline"].update({"bound": "valu", "achieved": steps_per_s / 1e12, "peak": FNV_STEP_PEAK_T,
+                                       "unit": "T byte-steps/s", "frac": steps_per_s / 1e12 / FNV_STEP_PEAK_T,
+                                       "hbm": hbm})
         result["dominant_stage"] = max(stages, key=stages.get)
     if world == 1 and not use_dist:
         result["lookup"] = lookup_rate(ctx, d_blob, d_offs, n, d_fp, d_po)
     if world == 1:
         result["host_e2e"] = host_e2e(s3imph, blob, offs, local_rank)
     if world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(blob, offs, args.cpu_baseline_seconds)
+        result["cpu_baseline"] = cpu_baseline(s3imph, cfg, args.seed)
+    if world == 1 and not use_dist and args.config != "c2" and not args.no_secondary:
+        del d_blob, d_offs, d_fp, d_po
+        ctx.close()
+        torch.cuda.empty_cache()
+        result["secondary"] = {"c2": secondary_line(s3imph, local_rank, args.seed, args.steps, args.warmup)}
     print(json.dumps(result), flush=True)
     if dist is not None:
         dist.barrier()
@@ -278,24 +286,113 @@ def host_e2e(s3imph, blob, offs, device: int, reps: int = 3) -> dict:
                     "pinned chunk staging (8 workers), mph.bin marshal; output arrays reused"}
 
 
-def cpu_baseline(blob, offs, seconds: float) -> dict:
-    """The oracle's C restatement of the reference algorithm (single thread, like the
-    reference's sequential bbhash.New), timed on this host over the same workload."""
+def secondary_line(s3imph, device: int, seed: int, steps: int, warmup: int) -> dict:
+    """C2 (BASELINE configs[1]: 10M keys, avg 32 B) on the same GPU: ms/step and keys/s,
+    device-resident, same step as the headline.  Reported beside `value`, never as it."""
+    import numpy as np
+    import torch
+    cfg = CONFIGS["c2"]
+    n = cfg["keys_per_gpu"]
+    blob, offs = s3imph.gen_keys(cfg["kind"], seed, cfg["avg"], 0, n)
+    dev = f"cuda:{device}"
+    d_blob = torch.from_numpy(blob).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_fp = torch.empty(n, dtype=torch.int64, device=dev)
+    d_po = torch.empty(n, dtype=torch.int64, device=dev)
+    ctx = s3imph.DeviceBuilder(device)
+    ctx.reserve(n)
+    for _ in range(warmup):
+        ctx.build(d_blob, d_offs, n, d_fp, d_po)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.build(d_blob, d_offs, n, d_fp, d_po)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    ctx.set_profiling(1)
+    ctx.build(d_blob, d_offs, n, d_fp, d_po)
+    stages = {k: round(v, 4) for k, v in ctx.stage_times().items()}
+    ctx.close()
+    return {"workload": cfg["workload"], "keys": n, "ms_per_step": dt * 1e3, "keys_per_s": n / dt,
+            "key_bytes_GBps": int(offs[-1]) / dt / 1e9, "stages_ms": stages}
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_cores() -> int:
+    """Threads this job may use: the box's CPU share (16 on the GPU pool; os.cpu_count()
+    there shows the whole machine) or the affinity mask, whichever is smaller."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+
+
+def cpu_baseline(s3imph, cfg: dict, seed: int) -> dict:
+    """The reference algorithm restated in C (oracle/bbhash_oracle.c), timed on this host.
+
+    - `value`: orc_build_revmap, shaped like StreamingMPHFBuilder.Build (serial FNV Add,
+      sequential bbhash.New levels with a reverse map, the Go-map position pass and the
+      scatter, mphf_streaming.go:68-261), ONE thread like the reference, on a bounded
+      sample of the bench workload: its first 10M keys (~5 s).
+    - `all_core`: orc_build_mt on `cores` threads (FNV and placement parallel; the levels
+      stay sequential as in bbhash.New without Parallel()), same sample.
+    - `sets`: both variants on C1 (wide_single_level 100k -> 100 002 prefixes, the
+      reference's benchutil shape) and the reference's 1M bench set
+      (generateRealisticPrefixes(1_000_000), mphf_bench_test.go:12-27).
+    A reported baseline, not the optimisation target (the GPU kernels' roofline is)."""
+    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import keysets
     import oracle as O
     lib = O.lib()
-    n = len(offs) - 1
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        st, _, _, _ = lib.build(blob[: int(offs[-1])], offs)
-        assert st == 0
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": n * reps / el, "unit": "keys/s", "cores": 1, "kind": "port",
-            "sample": f"full workload ({n} keys) x {reps} builds, {el:.1f} s, oracle/bbhash_oracle.c "
-                      f"(FNV + sequential BBHash levels + Find-per-key scatter), host CPU {os.cpu_count()} threads visible"}
+    cores = _cpu_cores()
+
+    def timed(blob, offs, reps_min_s: float = 1.0) -> dict:
+        n = len(offs) - 1
+        out = {}
+        for name, fn in (("1_thread", lambda: lib.build_revmap(blob, offs)[0]),
+                         ("all_core", lambda: lib.build_mt(blob, offs, threads=cores)[0])):
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                assert fn() == 0
+                reps += 1
+                el = time.perf_counter() - t0
+                if el >= reps_min_s:
+                    break
+            out[name] = n * reps / el
+        return out
+
+    sample_n = min(cfg["keys_per_gpu"], 10_000_000)
+    blob, offs = s3imph.gen_keys(cfg["kind"], seed, cfg["avg"], 0, sample_n)
+    main = timed(blob[: int(offs[-1])], offs)
+    del blob, offs
+    sets = {}
+    for name, keys in (("c1_wide_single_level_100k", keysets.wide_single_level_prefixes()),
+                       ("realistic_1m", keysets.realistic_prefixes(1_000_000))):
+        b, o = O.keys_to_blob([k.encode() for k in keys])
+        r = timed(b, o, 0.5)
+        sets[name] = {"keys": len(o) - 1, "avg_key_B": round(float(o[-1]) / (len(o) - 1), 2),
+                      "1_thread_keys_per_s": r["1_thread"], "all_core_keys_per_s": r["all_core"]}
+    return {"value": main["1_thread"], "unit": "keys/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample_n} keys of the bench workload ({cfg['workload']}), "
+                      f"oracle/bbhash_oracle.c orc_build_revmap: serial FNV, sequential levels + reverse map, "
+                      f"hash-map positions, scatter (mphf_streaming.go:68-261)",
+            "cpu_model": _cpu_model(),
+            "all_core": {"value": main["all_core"], "unit": "keys/s", "cores": cores,
+                         "note": "orc_build_mt: FNV + placement on all cores, levels sequential"},
+            "sets": sets}
 
 
 if __name__ == "__main__":

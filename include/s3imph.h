@@ -210,9 +210,12 @@ int s3imph_lookup_device(s3imph_ctx *ctx, const uint8_t *d_blob, const uint64_t 
 
 /* ------------------------------------------------------------------------
  * 6. Deterministic synthetic prefix sets (bench/test support, not on the path).
- *    kind: 0 = s3-like, lengths uniform in [avg/2, 3avg/2];
- *          1 = lengths log-uniform in [8, 1024] (C5, min 8 keeps keys distinct).
- *    Keys are distinct, byte-sorted, key 0 = "" when lo == 0.  Generate keys
+ *    kind: 0 = s3-like, lengths uniform in [max(10, avg/2), 3avg/2],
+ *              distinct and byte-sorted;
+ *          1 = lengths log-uniform in [1, 1024] (C5), each raised to the base-64 digit
+ *              count of its index where that is longer (4 bytes hold 16.7M keys), so
+ *              keys stay distinct; not byte-sorted.
+ *    Key 0 = "" when lo == 0 (the root prefix).  Generate keys
  *    [lo, lo+n) of the global sequence: call once with blob == NULL to get the
  *    byte count, then again to fill.  offsets are relative to the shard start.
  * ------------------------------------------------------------------------ */

@@ -24,6 +24,7 @@
  *
  * Build: oracle/Makefile -> oracle/_build/liboracle.so (plain gcc, no GPU).
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -308,4 +309,192 @@ int orc_lookup(const orc_mphf *m, const uint64_t *fp_arr, const uint64_t *pos_ar
     if (fp_arr[hp] != orc_fnv1_64(key, len)) return 0;
     *pos_out = pos_arr[hp];
     return 1;
+}
+
+/* ------------------------------------------------------- threaded helpers ---- */
+
+typedef struct {
+    void (*fn)(void *, uint64_t, uint64_t);
+    void *arg;
+    uint64_t lo, hi;
+} orc_range_task;
+
+static void *orc_range_main(void *p) {
+    orc_range_task *t = (orc_range_task *)p;
+    t->fn(t->arg, t->lo, t->hi);
+    return NULL;
+}
+
+/* fn(arg, lo, hi) over [0, n) cut into nt contiguous ranges, one pthread each. */
+static void orc_par_for(uint64_t n, int nt, void (*fn)(void *, uint64_t, uint64_t), void *arg) {
+    if (nt < 1) nt = 1;
+    if (nt > 256) nt = 256;
+    if (nt == 1 || n < 4096) { fn(arg, 0, n); return; }
+    pthread_t th[256];
+    orc_range_task tk[256];
+    for (int t = 0; t < nt; t++) {
+        tk[t].fn = fn; tk[t].arg = arg;
+        tk[t].lo = n * (uint64_t)t / (uint64_t)nt;
+        tk[t].hi = n * (uint64_t)(t + 1) / (uint64_t)nt;
+        if (t && pthread_create(&th[t], NULL, orc_range_main, &tk[t]) != 0) { fn(arg, tk[t].lo, tk[t].hi); th[t] = 0; }
+    }
+    fn(arg, tk[0].lo, tk[0].hi);
+    for (int t = 1; t < nt; t++) if (th[t]) pthread_join(th[t], NULL);
+}
+
+typedef struct {
+    const uint8_t *blob; const uint64_t *offsets; uint64_t *kh, *fp;
+    const orc_mphf *m; const uint64_t *pos; uint64_t *fp_out, *pos_out; uint64_t n;
+    int bad;
+} orc_mt_ctx;
+
+static void orc_mt_hash(void *p, uint64_t lo, uint64_t hi) {
+    orc_mt_ctx *c = (orc_mt_ctx *)p;
+    for (uint64_t i = lo; i < hi; i++) {
+        const uint8_t *k = c->blob + c->offsets[i];
+        uint64_t len = c->offsets[i + 1] - c->offsets[i];
+        c->kh[i] = orc_fnv1a64(k, len);
+        c->fp[i] = orc_fnv1_64(k, len);
+    }
+}
+
+static void orc_mt_place(void *p, uint64_t lo, uint64_t hi) {
+    orc_mt_ctx *c = (orc_mt_ctx *)p;
+    for (uint64_t i = lo; i < hi; i++) {
+        uint64_t v = orc_find(c->m, c->kh[i]);
+        if (v == 0 || v > c->n) { c->bad = 1; continue; }
+        c->fp_out[v - 1] = c->fp[i];
+        c->pos_out[v - 1] = c->pos ? c->pos[i] : i;
+    }
+}
+
+/*
+ * orc_build with the embarrassingly parallel parts on `nthreads` threads: the FNV pass
+ * (StreamingMPHFBuilder.Add, mphf_streaming.go:73,80) and the per-key placement; the
+ * BBHash level loop stays sequential, as bbhash.New runs without bbhash.Parallel()
+ * (mphf_streaming.go:141).  Same outputs as orc_build.  Used by the tests to check big
+ * sets quickly and by bench.py's all-core CPU baseline.
+ */
+int orc_build_mt(const uint8_t *blob, const uint64_t *offsets, const uint64_t *pos, uint64_t n, int nthreads,
+                 uint64_t *fp_out, uint64_t *pos_out, orc_mphf **mph_out) {
+    *mph_out = NULL;
+    if (n == 0) return ORC_OK;
+    orc_mt_ctx c;
+    memset(&c, 0, sizeof c);
+    c.blob = blob; c.offsets = offsets; c.n = n; c.pos = pos; c.fp_out = fp_out; c.pos_out = pos_out;
+    c.kh = (uint64_t *)malloc(n * sizeof(uint64_t));
+    c.fp = (uint64_t *)malloc(n * sizeof(uint64_t));
+    orc_par_for(n, nthreads, orc_mt_hash, &c);
+    for (uint64_t i = 0; i < n; i++)
+        if (c.kh[i] == 0) { free(c.kh); free(c.fp); return ORC_ERR_KEY_ZERO; }
+    orc_mphf *m = NULL;
+    int st = orc_bbhash_new(c.kh, n, &m);
+    if (st != ORC_OK) { free(c.kh); free(c.fp); return st; }
+    c.m = m;
+    orc_par_for(n, nthreads, orc_mt_place, &c);
+    free(c.kh);
+    free(c.fp);
+    if (c.bad) { orc_free(m); return ORC_ERR_INTERNAL; }
+    *mph_out = m;
+    return ORC_OK;
+}
+
+/* ------------------------------------------- reference-shaped CPU baseline ---- */
+
+/* Open-addressing u64 -> u64 table: the Go map[uint64]int of
+ * computeHashPositionsReverseMap (mphf_streaming.go:239-243). */
+typedef struct { uint64_t *k, *v; uint64_t mask; } orc_map;
+
+static void orc_map_init(orc_map *m, uint64_t n) {
+    uint64_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    m->k = (uint64_t *)calloc(cap, sizeof(uint64_t));
+    m->v = (uint64_t *)malloc(cap * sizeof(uint64_t));
+    m->mask = cap - 1;
+}
+static inline uint64_t orc_map_slot(uint64_t k) { return orc_mix(k); }
+static void orc_map_put(orc_map *m, uint64_t k, uint64_t v) { /* k != 0 (checked by the caller) */
+    uint64_t i = orc_map_slot(k) & m->mask;
+    while (m->k[i] && m->k[i] != k) i = (i + 1) & m->mask;
+    m->k[i] = k;
+    m->v[i] = v;
+}
+static int orc_map_get(const orc_map *m, uint64_t k, uint64_t *v) {
+    uint64_t i = orc_map_slot(k) & m->mask;
+    while (m->k[i]) {
+        if (m->k[i] == k) { *v = m->v[i]; return 1; }
+        i = (i + 1) & m->mask;
+    }
+    return 0;
+}
+
+/*
+ * StreamingMPHFBuilder.Build shaped like the reference, single-threaded:
+ *   Add: FNV-1a + FNV-1 per key, serially (mphf_streaming.go:68-97);
+ *   bbhash.New(.., WithReverseMap()): the level loop, and per level a pass recording each
+ *     settled key at its rank (the reverse map behind BBHash2.Key);
+ *   computeHashPositionsReverseMap (:237-261): a hash -> input-index map of N entries, then
+ *     for mphPos = 1..N: key = Key(mphPos), idx = map[key], hashPositions[idx] = mphPos-1;
+ *   the mapping loop (:197-204): fp_out[p] = fp[i], pos_out[p] = pos[i].
+ * Outputs equal orc_build's.  This is what bench.py times as the "port" CPU baseline.
+ */
+int orc_build_revmap(const uint8_t *blob, const uint64_t *offsets, const uint64_t *pos, uint64_t n,
+                     uint64_t *fp_out, uint64_t *pos_out) {
+    if (n == 0) return ORC_OK;
+    uint64_t *kh = (uint64_t *)malloc(n * sizeof(uint64_t));
+    uint64_t *fp = (uint64_t *)malloc(n * sizeof(uint64_t));
+    orc_hash_keys(blob, offsets, n, kh, fp);
+    int status = ORC_OK;
+    for (uint64_t i = 0; i < n; i++) if (kh[i] == 0) { status = ORC_ERR_KEY_ZERO; break; }
+    uint64_t *rev = (uint64_t *)malloc(n * sizeof(uint64_t));   /* rank -> key hash */
+    uint64_t *cur = (uint64_t *)malloc(n * sizeof(uint64_t));
+    uint64_t *nxt = (uint64_t *)malloc(n * sizeof(uint64_t));
+    uint64_t wmax = orc_level_words(n);
+    uint64_t *A = (uint64_t *)malloc(wmax * sizeof(uint64_t));
+    uint64_t *C = (uint64_t *)malloc(wmax * sizeof(uint64_t));
+    uint64_t *R = (uint64_t *)malloc(wmax * sizeof(uint64_t));    /* per-word rank prefix */
+    memcpy(cur, kh, n * sizeof(uint64_t));
+    uint64_t ncur = n, rank_base = 0;
+    for (uint32_t lvl = 0; status == ORC_OK && ncur > 0; lvl++) {
+        if (lvl >= ORC_MAX_LEVELS) { status = ORC_ERR_TOO_MANY_LEVELS; break; }
+        uint64_t w = orc_level_words(ncur), size = w * 64, lh = orc_level_hash(lvl);
+        memset(A, 0, w * sizeof(uint64_t));
+        memset(C, 0, w * sizeof(uint64_t));
+        for (uint64_t j = 0; j < ncur; j++) {
+            uint64_t i = orc_key_hash(lh, cur[j]) % size, bit = 1ULL << (i & 63);
+            if (C[i >> 6] & bit) continue;
+            if (A[i >> 6] & bit) { C[i >> 6] |= bit; continue; }
+            A[i >> 6] |= bit;
+        }
+        uint64_t acc = 0;
+        for (uint64_t q = 0; q < w; q++) { A[q] &= ~C[q]; R[q] = acc; acc += (uint64_t)__builtin_popcountll(A[q]); }
+        uint64_t nn = 0;
+        for (uint64_t j = 0; j < ncur; j++) {
+            uint64_t i = orc_key_hash(lh, cur[j]) % size, bit = 1ULL << (i & 63);
+            if (A[i >> 6] & bit) rev[rank_base + R[i >> 6] + (uint64_t)__builtin_popcountll(A[i >> 6] & (bit - 1))] = cur[j];
+            else nxt[nn++] = cur[j];
+        }
+        rank_base += acc;
+        uint64_t *t = cur; cur = nxt; nxt = t;
+        ncur = nn;
+    }
+    if (status == ORC_OK) {
+        orc_map mp;
+        orc_map_init(&mp, n);
+        for (uint64_t i = 0; i < n; i++) orc_map_put(&mp, kh[i], i);
+        uint64_t *hpos = cur; /* reuse: hashPositions[orig] */
+        for (uint64_t p = 0; p < n && status == ORC_OK; p++) {
+            uint64_t idx;
+            if (!orc_map_get(&mp, rev[p], &idx)) status = ORC_ERR_INTERNAL;
+            else hpos[idx] = p;
+        }
+        for (uint64_t i = 0; status == ORC_OK && i < n; i++) {
+            fp_out[hpos[i]] = fp[i];
+            pos_out[hpos[i]] = pos ? pos[i] : i;
+        }
+        free(mp.k);
+        free(mp.v);
+    }
+    free(kh); free(fp); free(rev); free(cur); free(nxt); free(A); free(C); free(R);
+    return status;
 }

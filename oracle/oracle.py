@@ -111,6 +111,10 @@ class OracleLib:
         lib.orc_free.argtypes = [vp]
         lib.orc_build.restype = ctypes.c_int
         lib.orc_build.argtypes = [vp, vp, vp, u64, vp, vp, ctypes.POINTER(vp)]
+        lib.orc_build_mt.restype = ctypes.c_int
+        lib.orc_build_mt.argtypes = [vp, vp, vp, u64, ctypes.c_int, vp, vp, ctypes.POINTER(vp)]
+        lib.orc_build_revmap.restype = ctypes.c_int
+        lib.orc_build_revmap.argtypes = [vp, vp, vp, u64, vp, vp]
         lib.orc_lookup.restype = ctypes.c_int
         lib.orc_lookup.argtypes = [vp, vp, vp, u64, ctypes.c_char_p, u64, u64p]
         lib.orc_level_hash.restype = u64
@@ -169,6 +173,34 @@ class OracleLib:
             return st, fp_out, pos_out, b""
         m = OracleMPHF(self, h)
         return st, fp_out, pos_out, m.marshal()
+
+    def build_mt(self, blob: np.ndarray, offsets: np.ndarray, pos: np.ndarray | None = None, threads: int = 8):
+        """orc_build with the FNV pass and the placement on `threads` threads (same outputs)."""
+        n = len(offsets) - 1
+        blob = np.ascontiguousarray(blob, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        fp_out = np.zeros(n, np.uint64)
+        pos_out = np.zeros(n, np.uint64)
+        posp = None if pos is None else _ptr(np.ascontiguousarray(pos, np.uint64))
+        h = ctypes.c_void_p()
+        st = self.lib.orc_build_mt(_ptr(blob), _ptr(offsets), posp, n, threads, _ptr(fp_out), _ptr(pos_out),
+                                   ctypes.byref(h))
+        if st != ORC_OK:
+            return st, None, None, None
+        if n == 0:
+            return st, fp_out, pos_out, b""
+        return st, fp_out, pos_out, OracleMPHF(self, h).marshal()
+
+    def build_revmap(self, blob: np.ndarray, offsets: np.ndarray, pos: np.ndarray | None = None):
+        """The reference-shaped single-thread build (reverse map + hash map): (status, fp_out, pos_out)."""
+        n = len(offsets) - 1
+        blob = np.ascontiguousarray(blob, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        fp_out = np.zeros(n, np.uint64)
+        pos_out = np.zeros(n, np.uint64)
+        posp = None if pos is None else _ptr(np.ascontiguousarray(pos, np.uint64))
+        st = self.lib.orc_build_revmap(_ptr(blob), _ptr(offsets), posp, n, _ptr(fp_out), _ptr(pos_out))
+        return st, fp_out, pos_out
 
     def lookup(self, mph: OracleMPHF | None, fp_arr: np.ndarray, pos_arr: np.ndarray, key: bytes):
         out = ctypes.c_uint64()

@@ -1500,6 +1500,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
 
 // --------------------------------------------------------------------- tail --------
 constexpr unsigned kWaveKeys = 64;  // tail levels this small run in one wave
+// The wave tail holds key i in lane i, compacts with 64-bit ballots and reads the level's
+// A/C words (<= level_words(64) * 2 u32) with lane shuffles: all of it is wave64-only.
+static_assert(kWaveKeys == 64, "the wave tail assumes one key per lane of a 64-lane wave");
+static_assert(2 * ((kGammaNum * kWaveKeys + 63) / 64) <= kWaveKeys, "wave tail: A/C words must fit one per lane");
 
 // Orders one wave's LDS accesses across lanes (a wave's LDS operations execute in order;
 // this keeps the compiler from moving them across the point).
@@ -1692,6 +1696,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
   // Level parameters are carried in registers (the same values the block path writes).
   if (wave_levels) {
     if (wave == 0) {
+      if (__builtin_amdgcn_wavefrontsize() != 64) __builtin_trap();  // gfx950 only: wave64
       int L = s_level;
       unsigned n = (unsigned)s_n;
       uint64_t words = st->words[L], magic = st->magic[L], woff = st->woff[L], base = st->lvl_base[L];
@@ -1780,6 +1785,9 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
     base0 = s_wbase0;
     out_end = s_wout;
   }
+  // On kStTooManyLevels the unplaced keys were written over a record list (possibly `in`):
+  // the build fails and fp_out / pos_out are undefined, so nothing is gathered.
+  if (st->status & kStTooManyLevels) out_end = 0;
   if (out_end) {
     if (base0 + out_end > N) {
       bad = true;

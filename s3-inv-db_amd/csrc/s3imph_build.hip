@@ -1394,12 +1394,14 @@ int s3imph_build_device(s3imph_ctx* c, const uint8_t* d_blob, const uint64_t* d_
   try {
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
+    c->last_msg.clear();
     int rc = c->dist ? S3IMPH_ERR_STATE
                      : build_single(c, d_blob, d_offsets, d_pos, n, d_fp_out, d_pos_out, s, info, &msg);
     c->last_msg = msg;
     info->status = rc;
     return rc;
   } catch (const Fail& f) {
+    c->last_msg = f.msg;
     info->status = f.code;
     return f.code;
   } catch (const std::bad_alloc&) {
@@ -1505,6 +1507,7 @@ int s3imph_build_device_dist(s3imph_ctx* c, const uint8_t* d_blob, const uint64_
   try {
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
+    c->last_msg.clear();
     int rc = build_dist(c, d_blob, d_offsets, d_pos, n_local, key_base, d_fp_out, d_pos_out, out_cap, out_n, s,
                         info, &msg);
     c->last_msg = msg;

@@ -215,11 +215,13 @@ int s3imph_builder_add(s3imph_builder* b, const uint8_t* prefix, uint64_t len, u
 
 int s3imph_builder_add_batch(s3imph_builder* b, const uint8_t* blob, const uint64_t* offsets,
                              const uint64_t* pos, uint64_t n, char* err, size_t errlen) {
-  if (!b || (n && (!blob || !offsets))) return S3IMPH_ERR_INVALID;
+  if (!b) return S3IMPH_ERR_INVALID;
   if (b->built) {
     set_err(err, errlen, "add to MPHF builder: builder already built");
     return S3IMPH_ERR_STATE;
   }
+  if (n == 0) return S3IMPH_OK;  // an empty batch may pass NULL blob / offsets
+  if (!blob || !offsets) return S3IMPH_ERR_INVALID;
   try {
     const uint64_t base = offsets[0], nbytes = offsets[n] - base, shift = b->blob.size();
     b->blob.insert(b->blob.end(), blob + base, blob + base + nbytes);
@@ -298,10 +300,16 @@ int s3imph_write_index_files(const char* out_dir, const uint8_t* mph_bin, uint64
 }
 
 // ------------------------------------------------------------ synthetic prefixes ----
-// Key g of the global sequence: g == 0 -> "" (the root prefix, aggregator.go:48);
-// g >= 1 -> 9 lowercase hex digits of g-1, '/', then pseudo-random [a-z0-5] segments
-// separated by '/' every 12 bytes, ending in '/'.  The fixed-width hex head makes the
-// sequence byte-sorted and distinct by construction.
+// kind 0 (C2/C3/C4): key g of the global sequence: g == 0 -> "" (the root prefix,
+// aggregator.go:48); g >= 1 -> 9 lowercase hex digits of g-1, '/', then pseudo-random
+// [a-z0-5] segments separated by '/' every 12 bytes, ending in '/'.  The fixed-width hex
+// head makes the sequence byte-sorted and distinct by construction.
+// kind 1 (C5): g == 0 -> ""; g >= 1 -> a length L drawn log-uniform on [1, 1024], raised
+// to the base-64 digit count of g-1 where that is longer (so short keys stay distinct:
+// 64^4 = 16.7M keys fit in 4 bytes, 64^5 in 5).  Keys of <= 11 bytes are g-1 in exactly
+// L base-64 digits; longer keys start with g-1 in 11 digits and continue as kind 0's
+// segments.  Equal lengths therefore mean distinct digit strings: distinct by
+// construction, not byte-sorted.
 static inline uint64_t splitmix64(uint64_t x) {
   x += 0x9e3779b97f4a7c15ull;
   x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -309,29 +317,35 @@ static inline uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
+static const char kB64[] = "0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ-_";
+constexpr uint32_t kHeadDigits = 11;  // 64^11 = 2^66 > any index
+
+static uint32_t b64_digits(uint64_t j) {
+  uint32_t d = 1;
+  while (d < kHeadDigits && (j >> (6 * d)) != 0) ++d;
+  return d;
+}
+
 static uint32_t gen_len(int kind, uint64_t seed, uint32_t avg, uint64_t g) {
   if (g == 0) return 0;
   const uint64_t r = splitmix64(seed * 0x9e3779b97f4a7c15ull ^ (g * 0xd1b54a32d192ed03ull));
   if (kind == 1) {
-    const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);
-    uint32_t L = (uint32_t)std::floor(10.0 * std::pow(1024.0 / 10.0, u));
-    return std::min<uint32_t>(std::max<uint32_t>(L, 10), 1024);
+    const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);  // [0, 1)
+    uint32_t L = (uint32_t)std::floor(std::exp(u * std::log(1025.0)));
+    L = std::min<uint32_t>(std::max<uint32_t>(L, 1), 1024);
+    return std::max(L, b64_digits(g - 1));
   }
   uint32_t lo = std::max<uint32_t>(10, avg / 2), hi = std::max<uint32_t>(lo, avg + avg / 2);
   return lo + (uint32_t)(r % (uint64_t)(hi - lo + 1));
 }
 
-static void gen_fill(uint64_t seed, uint64_t g, uint32_t L, uint8_t* out) {
-  static const char kHex[] = "0123456789abcdef";
+// kind 0's tail: pseudo-random [a-z0-5] segments with '/' every 12 bytes and at the end
+static void gen_segments(uint64_t seed, uint64_t g, uint32_t from, uint32_t L, uint8_t* out) {
   static const char kAlpha[] = "abcdefghijklmnopqrstuvwxyz012345";
-  if (L == 0) return;
-  const uint64_t j = g - 1;
-  for (int d = 0; d < 9; ++d) out[d] = (uint8_t)kHex[(j >> (4 * (8 - d))) & 0xf];
-  out[9] = '/';
   uint64_t state = splitmix64(splitmix64(seed) ^ (g * 0xd6e8feb86659fd93ull));
   uint64_t r = 0;
   int avail = 0;
-  for (uint32_t i = 10; i < L; ++i) {
+  for (uint32_t i = from; i < L; ++i) {
     if (i + 1 == L || i % 12 == 11) {
       out[i] = '/';
       continue;
@@ -345,6 +359,24 @@ static void gen_fill(uint64_t seed, uint64_t g, uint32_t L, uint8_t* out) {
     r >>= 5;
     --avail;
   }
+}
+
+static void gen_fill(int kind, uint64_t seed, uint64_t g, uint32_t L, uint8_t* out) {
+  static const char kHex[] = "0123456789abcdef";
+  if (L == 0) return;
+  const uint64_t j = g - 1;
+  if (kind == 1) {
+    const uint32_t d = std::min(L, kHeadDigits);
+    for (uint32_t i = 0; i < d; ++i) {
+      const uint32_t sh = 6 * (d - 1 - i);
+      out[i] = (uint8_t)kB64[sh < 64 ? (j >> sh) & 63 : 0];
+    }
+    if (L > kHeadDigits) gen_segments(seed, g, kHeadDigits, L, out);
+    return;
+  }
+  for (int d = 0; d < 9; ++d) out[d] = (uint8_t)kHex[(j >> (4 * (8 - d))) & 0xf];
+  out[9] = '/';
+  gen_segments(seed, g, 10, L, out);
 }
 
 int s3imph_gen_keys(int kind, uint64_t seed, uint32_t avg_len, uint64_t lo, uint64_t n, uint8_t* blob,
@@ -375,7 +407,7 @@ int s3imph_gen_keys(int kind, uint64_t seed, uint32_t avg_len, uint64_t lo, uint
     uint64_t acc = part[t];
     for (uint64_t i = a; i < b; ++i) {
       const uint64_t L = offsets[i + 1];
-      if (blob) gen_fill(seed, lo + i, (uint32_t)L, blob + acc);
+      if (blob) gen_fill(kind, seed, lo + i, (uint32_t)L, blob + acc);
       acc += L;
       offsets[i + 1] = acc;
     }

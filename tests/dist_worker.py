@@ -11,7 +11,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def rank_main(rank, world, port, shards, n_global, switch, result_q):
+def rank_main(rank, world, port, shard, n_global, switch, result_q):
     try:
         for d in (os.path.join(ROOT, "s3-inv-db_amd"), os.path.join(ROOT, "oracle")):
             if d not in sys.path:
@@ -22,7 +22,7 @@ def rank_main(rank, world, port, shards, n_global, switch, result_q):
         import torch.distributed as dist
         import s3imph
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        blob, offs, pos, key_base = shards[rank]
+        blob, offs, pos, key_base = shard
         n = len(offs) - 1
         ctx = s3imph.DistBuilder(0, None, rank, world, host_comm=True)
         cap = ctx.out_cap(n_global)

@@ -113,9 +113,15 @@ def test_generator_sorted_distinct_and_shardable():
     b2, o2 = s3imph.gen_keys(0, 42, 32, 12345, 100)
     for i in range(100):
         assert bytes(b2[o2[i]:o2[i + 1]]) == keys[12345 + i]
+    # C5's kind 1: lengths log-uniform on [1, 1024] (raised to the digits a distinct key
+    # needs), distinct, reproducible by shard
     b3, o3 = s3imph.gen_keys(1, 42, 0, 0, 20000)
     l3 = np.diff(o3.astype(np.int64))[1:]
-    assert l3.min() >= 10 and l3.max() <= 1024
+    assert l3.min() == 1 and l3.max() == 1024 and 130 < l3.mean() < 170
+    k3 = [bytes(b3[o3[i]:o3[i + 1]]) for i in range(20000)]
+    assert len(set(k3)) == 20000
+    b4, o4 = s3imph.gen_keys(1, 42, 0, 777, 50)
+    assert [bytes(b4[o4[i]:o4[i + 1]]) for i in range(50)] == k3[777:827]
     assert hashlib.sha256(blob[: offs[-1]].tobytes()).hexdigest() == \
         hashlib.sha256(s3imph.gen_keys(0, 42, 32, 0, 50000)[0][: offs[-1]].tobytes()).hexdigest()
 
@@ -126,3 +132,13 @@ def test_shard_plan_covers_everything():
             plans = [s3imph.ShardPlan(r, p, n) for r in range(p)]
             assert sum(x.n_local for x in plans) == n
             assert all(plans[r].hi == plans[r + 1].lo for r in range(p - 1))
+
+
+def test_builder_add_batch_empty_null_pointers(tmp_path):
+    """An empty batch may pass NULL blob/offsets (a cgo caller's nil slices): a no-op."""
+    b = s3imph.StreamingMPHFBuilder(str(tmp_path))
+    err = ctypes.create_string_buffer(64)
+    assert s3imph.LIB.s3imph_builder_add_batch(b._h, None, None, None, 0, err, 64) == s3imph.OK
+    assert b.count() == 0
+    assert s3imph.LIB.s3imph_builder_add_batch(b._h, None, None, None, 3, err, 64) == s3imph.ERR_INVALID
+    b.close()

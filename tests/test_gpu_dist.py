@@ -43,7 +43,7 @@ def _run(world, shards, n, switch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=dist_worker.rank_main, args=(r, world, port, shards, n, switch, q))
+    procs = [ctx.Process(target=dist_worker.rank_main, args=(r, world, port, shards[r], n, switch, q))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -82,7 +82,7 @@ def test_dist_host_comm_matches_oracle(world, n, switch, oracle_lib):
 def test_dist_unbalanced_shards_custom_pos(oracle_lib):
     import s3imph
     n, world = 90_000, 3
-    blob, offs = s3imph.gen_keys(1, 3, 0, 0, n)  # ragged lengths 10-1024 B
+    blob, offs = s3imph.gen_keys(1, 3, 0, 0, n)  # ragged lengths 1-1024 B
     blob = blob[: int(offs[-1])]
     pos = (np.random.default_rng(1).permutation(n).astype(np.uint64) + np.uint64(7_000_000))
     st, fp, po, mph = oracle_lib.build(blob, offs, pos)

@@ -6,18 +6,18 @@
 set -e
 TAG=${1:-run}
 PYT=${2:-pytest}
-CFG=${3:-c2}
+CFG=${3:-c3}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 if [ "$PYT" = pytest ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 fi
-timeout -k 10 300 python bench.py --config $CFG > $OUT/bench.log 2>&1
+timeout -k 10 400 python bench.py --config $CFG > $OUT/bench.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
-  python3 bench.py --config $CFG --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof.log 2>&1
+  python3 bench.py --config $CFG --steps 10 --warmup 2 --no-cpu-baseline --no-secondary > $OUT/bench_prof.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \
-  python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1
+  python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-secondary > $OUT/pmc_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- \
-  python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmc_write.log 2>&1
+  python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-secondary > $OUT/pmc_write.log 2>&1
 echo done > $OUT/DONE
