@@ -78,6 +78,11 @@ uint64_t s3imph_builder_count(const s3imph_builder *b);
  * Count()==0 writes the empty set (writeEmpty, :506-541). On failure mph.bin is removed (:159-168). */
 int s3imph_builder_build(s3imph_builder *b, const char *out_dir, char *err, size_t errlen);
 
+/* Build on several GPUs (s3imph_build_host_multi's num_gpus / devices / flags); the
+ * default is the one device given to s3imph_builder_new.  No reference counterpart (the
+ * reference builds on one CPU thread, mphf_streaming.go:141). */
+int s3imph_builder_set_gpus(s3imph_builder *b, int num_gpus, const int *devices, unsigned flags);
+
 /* Close() — mphf_streaming.go:105-114. Frees everything; b is invalid afterwards. */
 int s3imph_builder_close(s3imph_builder *b);
 
@@ -94,6 +99,21 @@ int s3imph_build_host(int device, const uint8_t *blob, const uint64_t *offsets, 
                       uint64_t *mph_len, char *err, size_t errlen);
 
 void s3imph_free(void *p);
+
+/* Multi-GPU host-memory build for ONE calling process (the reference's caller is one
+ * process: indexbuild.go:506-518 -> Build).  num_gpus host threads, one per GPU, each
+ * run the sharded rank build of section 4 on a contiguous key shard of about equal key
+ * bytes; collectives are RCCL communicators made in-process (ncclCommInitAll, xGMI) or,
+ * when `devices` repeat or S3IMPH_MULTI_HOST_TRANSPORT is set, in-process host copies.
+ * Each rank writes its output segments straight to their global offsets in fp_out /
+ * pos_out; mph.bin comes from rank 0 (identical on every rank).  devices may be NULL
+ * (GPUs 0 .. num_gpus-1).  num_gpus == 1 without S3IMPH_MULTI_FORCE_SHARDED is
+ * s3imph_build_host.  Outputs equal s3imph_build_host's byte for byte. */
+#define S3IMPH_MULTI_FORCE_SHARDED 1u   /* the sharded (multi-GPU) build even for one GPU */
+#define S3IMPH_MULTI_HOST_TRANSPORT 2u  /* host-copy collectives instead of RCCL */
+int s3imph_build_host_multi(int num_gpus, const int *devices, unsigned flags, const uint8_t *blob,
+                            const uint64_t *offsets, const uint64_t *pos, uint64_t n, uint64_t *fp_out,
+                            uint64_t *pos_out, uint8_t **mph_bin, uint64_t *mph_len, char *err, size_t errlen);
 
 /* Emit the 5 files of the MPHF stage with the reference's framing:
  * mph.bin raw (mphf_streaming.go:152-169), mph_fp.u64 / mph_pos.u64 as S3ID

@@ -33,7 +33,6 @@ namespace s3imph {
 namespace {
 
 constexpr int kCB = 1024;             // count block
-constexpr int kHR = 256;              // pipelined level-0 hash block
 constexpr int kSB = 1024;             // scatter block
 constexpr int kTailT = 1024;          // tail block
 constexpr unsigned kLenBuckets = 256;  // key-length classes (4 B each) of the level-0 hash sort
@@ -131,8 +130,7 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
   __shared__ unsigned short sidx[kCB];
   __shared__ uint64_t sb0[kCB], sb1[kCB], sh1[kCB], sh2[kCB];
   __shared__ uint64_t s_lmax[kCB / 64], s_lsum[kCB / 64];
-  if (smode == 4 && !st->skew) return;  // pipelined level 0: k_hash0_range hashes this set
-  const bool sort = smode == 1 || smode == 2 || ((smode == 3 || smode == 4) && st->skew);
+  const bool sort = smode == 1 || smode == 2 || (smode == 3 && st->skew);
   const uint64_t words = st->words[0], magic = st->magic[0];
   const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
   if (!geom_ok(st, T, B)) return;
@@ -240,30 +238,6 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
     __syncthreads();
   }
   if (zero) atomicOr(&st->status, kStKeyZero);
-}
-
-// --------------------------------------------------- pipelined level-0 hash ---------
-// FNV-1a + FNV-1 of keys [lo, hi) into kh / fp (key order), one key per thread, loads two
-// words ahead, no LDS: its blocks fit beside a k_scatter_res block (152 KiB of LDS) on
-// the same CU, so the hash of chunk k+1 (VALU-bound) runs while chunk k is scattered
-// (atomics, LDS and memory latency) on the other stream.  Near-uniform sets only: a
-// skewed set was hashed length-sorted by k_hash_count0 (smode 4) and this returns.
-__global__ __launch_bounds__(kHR) void k_hash0_range(const uint8_t* __restrict__ blob,
-                                                     const uint64_t* __restrict__ offsets, uint64_t lo, uint64_t hi,
-                                                     uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
-                                                     LevelState* st, unsigned* __restrict__ tcnt) {
-  // chunk 0 clears every level's reservation counters (k_hash_count0's job otherwise)
-  if (tcnt)
-    for (uint64_t q = (uint64_t)blockIdx.x * kHR + threadIdx.x; q < kTcntWords; q += (uint64_t)gridDim.x * kHR)
-      tcnt[q] = 0;
-  if (st->skew) return;
-  const uint64_t i = lo + (uint64_t)blockIdx.x * kHR + threadIdx.x;
-  if (i >= hi) return;
-  uint64_t h1, h2;
-  hash_key<2>(blob, offsets[i], offsets[i + 1], h1, h2);
-  kh[i] = h1;
-  fp[i] = h2;
-  if (h1 == 0) atomicOr(&st->status, kStKeyZero);
 }
 
 // ------------------------------------------------------------- level L setup ---------
@@ -471,50 +445,6 @@ __global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __re
   }
 }
 
-// ------------------------------------------------------------ direct scatter -------
-// The counted scatter without the LDS staging: each chunk's per-tile cursors live in
-// LDS and every record goes straight to its slot (S3IMPH_SCATTER_DIRECT=1).  Measured
-// with 12k tiles of 2^14 positions on C3's level 0 it was 1.8x slower than the staged
-// scatter over 3k tiles of 2^16 positions, so it is a tested alternative, not a path.
-constexpr int kDU = 4;  // records in flight per thread
-__global__ __launch_bounds__(kSB) void k_scatter_direct(int level, const uint64_t* __restrict__ ik,
-                                                        const uint64_t* __restrict__ ifp,
-                                                        const uint64_t* __restrict__ ipos, uint64_t pos_base,
-                                                        const Rec* __restrict__ ilist,
-                                                        const unsigned* __restrict__ off, Rec* __restrict__ bucket,
-                                                        LevelState* st, unsigned tb, uint64_t chunk) {
-  __shared__ unsigned cur[kMaxTiles];
-  if (!level_active(level, st)) return;
-  const uint64_t n = st->n[level];
-  const uint64_t words = st->words[level], magic = st->magic[level];
-  const uint64_t T = st->ntiles[level], B = st->nchunks[level];
-  const uint64_t plo = level_range(st, level, words).plo;
-  const uint64_t seed = level_seed(level);
-  const unsigned tid = threadIdx.x;
-  for (uint64_t b = blockIdx.x; b < B; b += gridDim.x) {
-    for (uint64_t t = tid; t < T; t += kSB) cur[t] = off[t * B + b];
-    __syncthreads();
-    const uint64_t lo = b * chunk, hi = min(n, lo + chunk);
-    for (uint64_t i0 = lo + tid; i0 < hi; i0 += (uint64_t)kSB * kDU) {
-      Rec r[kDU];
-#pragma unroll
-      for (int u = 0; u < kDU; ++u) {
-        const uint64_t i = i0 + (uint64_t)u * kSB;
-        if (i < hi) r[u] = ilist ? ilist[i] : Rec{ik[i], ifp[i], ipos ? ipos[i] : pos_base + i};
-      }
-#pragma unroll
-      for (int u = 0; u < kDU; ++u) {
-        const uint64_t i = i0 + (uint64_t)u * kSB;
-        if (i < hi) {
-          const unsigned t = (unsigned)((bb_index(seed, r[u].k, words, magic) - plo) >> tb);
-          bucket[atomicAdd(&cur[t], 1u)] = r[u];
-        }
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------- reservation scatter ------
 // Small levels (a few 10^5 .. 10^6 keys) skip the count and histogram-scan kernels:
 // tile t owns the fixed bucket slot [t * cap, (t + 1) * cap), cap = bucket_cap / T
@@ -693,117 +623,6 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
 #undef SPROF
 }
 
-// ------------------------------------------------------- fused level-0 hash + scatter ----
-// Level 0 in one pass over the key bytes: FNV-1a + FNV-1 of each key (one pass over its
-// bytes, StreamingMPHFBuilder.Add, mphf_streaming.go:73,80), its level-0 tile, and the
-// record (kh, fp, pos) written straight into the tile's reservation slot (the layout of
-// k_scatter_res: tile t owns [t cap, (t+1) cap), cut into kResShards shards, one per
-// XCD).  Each round of NT*KPT keys is counting-sorted by tile in LDS; one atomic per
-// (round, tile) reserves the run.  No kh/fp arrays, no histogram scan.  A slot
-// overflow sets kStResOverflow and the build reruns on the counted path.
-// dyn LDS: stage Rec[R], stile u16[R], cnt/start/cur u32[T].
-template <int NT, int KPT>
-__global__ __launch_bounds__(NT) void k_hash_scatter0(const uint8_t* __restrict__ blob,
-                                                      const uint64_t* __restrict__ offsets, uint64_t n,
-                                                      const uint64_t* __restrict__ ipos, uint64_t pos_base,
-                                                      unsigned* __restrict__ tcnt, Rec* __restrict__ bucket,
-                                                      uint64_t bucket_cap, unsigned long long* __restrict__ flags,
-                                                      LevelState* st, unsigned tb) {
-  constexpr int R = NT * KPT;
-  extern __shared__ uint64_t dyn64[];
-  __shared__ unsigned s_over;
-  Rec* stage = reinterpret_cast<Rec*>(dyn64);
-  unsigned short* stile = reinterpret_cast<unsigned short*>(stage + R);
-  unsigned* cnt = reinterpret_cast<unsigned*>(stile + R);
-  const uint64_t words = st->words[0], magic = st->magic[0];
-  const uint64_t T = ntiles_of(words, tb);
-  unsigned* start = cnt + T;
-  unsigned* cur = start + T;
-  const unsigned tid = threadIdx.x;
-  if (T > kLdsTiles) {
-    if (tid == 0) atomicOr(&st->status, kStGeometry);
-    return;
-  }
-  if (blockIdx.x == 0 && tid == 0) {
-    st->ntiles[0] = T;
-    st->nchunks[0] = 0;
-  }
-  for (uint64_t t = (uint64_t)blockIdx.x * NT + tid; t < T; t += (uint64_t)gridDim.x * NT) flags[t] = 0;
-  const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
-  const unsigned shard = blockIdx.x % kResShards;
-  const uint64_t seed = level_seed(0);
-  if (tid == 0) s_over = 0;
-  for (uint64_t t = tid; t < T; t += NT) cnt[t] = 0;
-  __syncthreads();
-  bool zero = false;
-  for (uint64_t r0 = (uint64_t)blockIdx.x * R; r0 < n; r0 += (uint64_t)gridDim.x * R) {
-    uint64_t rk_[KPT], rf_[KPT];
-    unsigned tt[KPT], rk[KPT];
-#pragma unroll
-    for (int q = 0; q < KPT; ++q) {
-      const uint64_t i = r0 + (uint64_t)q * NT + tid;
-      if (i < n) {
-        fnv_both_loop(blob, offsets[i], offsets[i + 1], rk_[q], rf_[q]);
-        zero |= (rk_[q] == 0);
-        tt[q] = (unsigned)(bb_index(seed, rk_[q], words, magic) >> tb);
-        rk[q] = atomicAdd(&cnt[tt[q]], 1u);
-      }
-    }
-    __syncthreads();
-    // exclusive scan of the round's per-tile counts
-    constexpr int kTPT = (int)(kLdsTiles / NT);
-    const uint64_t t0 = (uint64_t)kTPT * tid;
-    unsigned a[kTPT];
-    uint64_t sum = 0;
-#pragma unroll
-    for (int q = 0; q < kTPT; ++q) {
-      a[q] = t0 + q < T ? cnt[t0 + q] : 0u;
-      sum += a[q];
-    }
-    uint64_t tot;
-    uint64_t ex = block_exscan<NT>(sum, &tot);
-#pragma unroll
-    for (int q = 0; q < kTPT; ++q) {
-      if (t0 + q < T) start[t0 + q] = (unsigned)ex;
-      ex += a[q];
-    }
-    // reservations: every touched tile's atomic in flight at once
-    for (uint64_t t = tid; t < T; t += NT) {
-      const unsigned c = cnt[t];
-      if (c) {
-        const uint64_t at = atomicAdd(&tcnt[t * kResShards + shard], c);
-        if (at + c > scap) s_over = 1;
-        cur[t] = (unsigned)(t * cap + shard * scap + at);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < KPT; ++q) {
-      const uint64_t i = r0 + (uint64_t)q * NT + tid;
-      if (i < n) {
-        const unsigned slot = start[tt[q]] + rk[q];
-        stage[slot] = Rec{rk_[q], rf_[q], ipos ? ipos[i] : pos_base + i};
-        stile[slot] = (unsigned short)tt[q];
-      }
-    }
-    __syncthreads();
-    if (s_over) break;
-    const unsigned m = (unsigned)min<uint64_t>(R, n - r0);
-    for (unsigned j = tid; j < m; j += NT) {
-      const unsigned t = stile[j];
-      bucket[cur[t] + (j - start[t])] = stage[j];
-    }
-    for (uint64_t t = tid; t < T; t += NT) cnt[t] = 0;
-    __syncthreads();
-  }
-  if (zero) atomicOr(&st->status, kStKeyZero);
-  if (s_over && tid == 0) atomicOr(&st->status, kStOverflow | kStResOverflow);
-}
-
-size_t hash_scatter0_lds_bytes(int R, uint64_t T) {
-  return (size_t)R * (sizeof(Rec) + sizeof(unsigned short)) + 3 * T * sizeof(unsigned);
-}
-
 // --------------------------------------------------------------------- tile --------
 // dyn LDS: A[tpw], C[tpw] u32 (C becomes the per-word rank prefix after finalize);
 // for tiles of <= 2^kCacheBits positions also loc[kCache] u16 (each record's
@@ -919,7 +738,7 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
                                               unsigned long long* flags, uint64_t* __restrict__ bits,
                                               Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
                                               uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
-                                              int mode, unsigned long long* __restrict__ prof) {
+                                              unsigned long long* __restrict__ prof) {
   extern __shared__ uint32_t dyn[];
   __shared__ unsigned long long s_t, s_prefix;
   __shared__ unsigned s_wc[NT / 64];
@@ -935,7 +754,7 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
   const unsigned per = (tpw + NT - 1) / NT;
   uint32_t* sA = dyn;
   uint32_t* sC = dyn + tpw;
-  const bool small = tb <= kCacheBits && mode == 0;
+  const bool small = tb <= kCacheBits;
   const unsigned kcap = small ? cache_keys(tb) : 0;
   const unsigned rcap = small ? rank_keys(tb) : 0;
   unsigned short* sloc = reinterpret_cast<unsigned short*>(dyn + 2 * tpw);
@@ -1814,13 +1633,7 @@ size_t tile_lds_bytes(unsigned tb) {
 }  // namespace
 
 void binned_set_lds_limits() {
-  (void)hipFuncSetAttribute((const void*)k_hash_scatter0<1024, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)hash_scatter0_lds_bytes(4096, kLdsTiles));
-  (void)hipFuncSetAttribute((const void*)k_hash_scatter0<1024, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)hash_scatter0_lds_bytes(2048, kLdsTiles));
   (void)hipFuncSetAttribute((const void*)k_tile<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)std::max(tile_lds_bytes(kTileMaxBits), tile_lds_bytes(kCacheBits)));
-  (void)hipFuncSetAttribute((const void*)k_tile<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)std::max(tile_lds_bytes(kTileMaxBits), tile_lds_bytes(kCacheBits)));
   (void)hipFuncSetAttribute((const void*)k_tile_reg<512, 20, 2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)tile_reg_lds_bytes(kRegMaxBits));
@@ -1831,34 +1644,10 @@ void binned_set_lds_limits() {
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s, bool histogram) {
   if (level == 0 && !b.dist) {
-    static const int mode = [] {
-      // A/B knob: 0 auto (default: 7 for near-uniform lengths, 14 for skewed ones, picked
-      // on the device from sampled lengths); 1 direct, batched 8-word loads; 2 length-
-      // sorted, one load per word; 3 direct, one load per word; 4 length-sorted, batched;
-      // 7 direct, loads two words ahead; 8 length-sorted, loads two words ahead; 9 / 10
-      // sort every group (two ahead / one load per word); 13 / 14 direct / length-sorted
-      // with 16-byte loads.
-      const char* e = std::getenv("S3IMPH_HASH_MODE");
-      return e ? std::atoi(e) : 0;
-    }();
-#define S3_HASH(KVD, KVS, SMODE)                                                                              \
-  k_hash_count0<KVD, KVS><<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, histogram ? b.hist : nullptr,   \
-                                                      b.flags, b.sflags, b.st,                                         \
-                                                      g.tb, g.chunk, b.tcnt, SMODE)
-    switch (mode) {
-      case 1: S3_HASH(1, 1, 0); break;
-      case 2: S3_HASH(0, 0, 1); break;
-      case 3: S3_HASH(0, 0, 0); break;
-      case 4: S3_HASH(1, 1, 1); break;
-      case 7: S3_HASH(2, 2, 0); break;
-      case 8: S3_HASH(2, 2, 1); break;
-      case 9: S3_HASH(2, 2, 2); break;
-      case 10: S3_HASH(0, 0, 2); break;
-      case 13: S3_HASH(3, 3, 0); break;
-      case 14: S3_HASH(3, 3, 1); break;
-      default: S3_HASH(2, 3, 3);
-    }
-#undef S3_HASH
+    // near-uniform lengths hash directly (loads two words ahead); a set whose sampled
+    // lengths are skewed (k_init_state) hashes 1024-key groups length-sorted (16-byte loads)
+    k_hash_count0<2, 3><<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, histogram ? b.hist : nullptr,
+                                                  b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, 3);
   } else {
     k_count<<<grid_chunks, kCB, 0, s>>>(level, b.list[(level - 1) & 1], b.hist, b.flags, b.sflags, b.st, g.tb,
                                         g.chunk, b.cap_words);
@@ -1875,22 +1664,13 @@ void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s)
   k_hscan<<<grid, kHST, 0, s>>>(level, b.hist, b.off, b.tile_start, b.sflags, b.st);
 }
 
-void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s, bool direct) {
+void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s) {
   const Rec* il = level == 0 && !b.dist ? nullptr : b.list[(level - 1) & 1];
-  static const bool force_direct = [] {  // test knob: every counted level scatters directly
-    const char* e = std::getenv("S3IMPH_SCATTER_DIRECT");
-    return e && e[0] == '1';
-  }();
-  if (direct || force_direct) {
-    k_scatter_direct<<<512, kSB, 0, s>>>(level, b.kh, b.fp, b.pos, b.pos_base, il, b.off, b.bucket, b.st, g.tb,
-                                         g.chunk);
-    return;
-  }
   k_scatter<<<256, kSB, 0, s>>>(level, b.kh, b.fp, b.pos, b.pos_base, il, b.off, b.bucket, b.st, g.tb, g.chunk);
 }
 
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s, bool reserved) {
-  if (b.tile_mode == 0 && g.tb <= kRegMaxBits) {
+  if (g.tb <= kRegMaxBits) {
     // records per tile ~2^(tb-1): pick the variant whose NT x R covers it with margin
     // (lighter variants keep several tiles resident per CU)
     const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kScatterTiles * kResShards : nullptr;
@@ -1901,11 +1681,7 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
                                                    b.tile_prof)
     // A level with no more tiles than CUs runs one round whatever the variant, so it
     // takes twice the threads per tile (half the records per thread: a shorter chain).
-    static const bool wide_small = [] {
-      const char* e = std::getenv("S3IMPH_TILE_WIDE");
-      return !e || e[0] != '0';
-    }();
-    const bool one_round = wide_small && grid_tiles <= 256;
+    const bool one_round = grid_tiles <= 256;
     if (g.tb == 14) S3_TILE_REG(512, 20, 2);                     // 1 tile per CU
     else if (g.tb == 13 && one_round) S3_TILE_REG(512, 10, 2);
     else if (g.tb == 13) S3_TILE_REG(256, 20, 2);                // 2 tiles per CU
@@ -1917,25 +1693,10 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
 #undef S3_TILE_REG
     return;
   }
-  const size_t lds = b.tile_mode == 0 ? tile_lds_bytes(g.tb) : 2ull * (1ull << (g.tb - 5)) * sizeof(uint32_t);
-  auto kern = b.tile_block == 512 ? k_tile<512> : k_tile<1024>;
   const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kScatterTiles * kResShards : nullptr;
-  kern<<<grid_tiles, b.tile_block == 512 ? 512 : 1024, lds, s>>>(
-      level, b.bucket, b.tile_start, tc, b.bucket_cap,
-      b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.tile_mode, b.tile_prof);
-}
-
-void launch_hash_scatter0(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
-                          int variant, hipStream_t s) {
-  const uint64_t T = ntiles_of(level_words(n ? n : 1), g.tb);
-  const int cus = 256;
-  if (variant == 1) {  // 2 x 2048-key rounds resident per CU
-    k_hash_scatter0<1024, 2><<<2 * cus, 1024, hash_scatter0_lds_bytes(2048, T), s>>>(
-        blob, offsets, n, b.pos, b.pos_base, b.tcnt, b.bucket, b.bucket_cap, b.flags, b.st, g.tb);
-  } else {  // one 4096-key round per CU
-    k_hash_scatter0<1024, 4><<<cus, 1024, hash_scatter0_lds_bytes(4096, T), s>>>(
-        blob, offsets, n, b.pos, b.pos_base, b.tcnt, b.bucket, b.bucket_cap, b.flags, b.st, g.tb);
-  }
+  k_tile<1024><<<grid_tiles, 1024, tile_lds_bytes(g.tb), s>>>(level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags,
+                                                          b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb,
+                                                          b.tile_prof);
 }
 
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s, uint64_t i_lo,
@@ -1946,19 +1707,6 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
   k_scatter_res<kSubRound, kLdsTiles><<<grid, kSB, 0, s>>>(level, il, b.kh, b.fp, b.pos, b.pos_base, tc, b.bucket,
                                                            b.bucket_cap, b.flags, b.st, g.tb, b.cap_words,
                                                            b.tile_prof, i_lo, i_hi);
-}
-
-void launch_hash0_range(const uint8_t* blob, const uint64_t* offsets, uint64_t lo, uint64_t hi, const BinBuffers& b,
-                        hipStream_t s) {
-  if (hi <= lo) return;
-  const uint64_t grid = (hi - lo + kHR - 1) / kHR;
-  k_hash0_range<<<(unsigned)grid, kHR, 0, s>>>(blob, offsets, lo, hi, b.kh, b.fp, b.st, lo == 0 ? b.tcnt : nullptr);
-}
-
-void launch_hash0_skewed(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
-                         int grid, hipStream_t s) {
-  k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
-                                           g.chunk, b.tcnt, 4);
 }
 
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s) {

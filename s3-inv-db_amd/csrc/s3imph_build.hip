@@ -29,131 +29,11 @@
 #include <thread>
 #include <vector>
 
-#include "s3imph.h"
-#include "s3imph_internal.h"
+#include "s3imph_ctx.h"
 
 using namespace s3imph;
 
-namespace {
-
-// Collectives of the multi-GPU build, on device buffers, ordered on stream s.
-struct Comm {
-  int rank = 0, nranks = 1;
-  virtual ~Comm() = default;
-  // d_recv[r * bytes ..) <- rank r's d_send[0 .. bytes)
-  virtual void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) = 0;
-  // element-wise u64 sum over ranks
-  virtual void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
-                             hipStream_t s) = 0;
-  // d_send + soff[q] (sbytes[q] bytes) -> rank q; rank q's bytes -> d_recv + roff[q] (rbytes[q]); host arrays
-  virtual void alltoallv(const void* d_send, const uint64_t* soff, const uint64_t* sbytes, void* d_recv,
-                         const uint64_t* roff, const uint64_t* rbytes, hipStream_t s) = 0;
-};
-
-constexpr uint64_t kDistSwitchKeysDefault = 2ull << 20;  // levels below this run replicated
-
-struct DistState {
-  Comm* comm = nullptr;
-  int rank = 0, nranks = 1;
-  uint64_t cap_list = 0, cap_send = 0, cap_stage_words = 0;
-  Rec* send = nullptr;                       // per-owner send regions / replicated gather staging
-  uint64_t* stage_bits = nullptr;            // level bit-vector all-gather staging
-  unsigned long long* scnt = nullptr;        // per-owner send counts (nranks)
-  unsigned long long* mat = nullptr;         // all-gathered send counts (nranks x nranks)
-  unsigned long long* gslot = nullptr;       // per-level global counts (kMaxLevels + 2)
-  unsigned long long* small = nullptr;       // scratch for tiny collectives (2 x 64 x 64)
-  unsigned long long* h_pinned = nullptr;    // host staging (64 x 64 + 256 u64)
-  std::vector<uint64_t> seg;                 // last build: (p_lo, count, local_off) triples
-  uint64_t out_n = 0;
-};
-
-}  // namespace
-
-namespace {
-
-// Pinned staging for host-memory builds (the Go caller's buffers are pageable):
-// kStageWorkers threads, each with its own pinned chunk buffer and stream, move the
-// data through pinned memory, so the CPU copies of one worker overlap the DMA of the
-// others and the PCIe link runs at its pinned rate.
-constexpr int kStageWorkers = 8;
-constexpr uint64_t kStageChunk = 8ull << 20;
-
-struct Stager {
-  void* pin[kStageWorkers][2] = {};  // double-buffered: one chunk in DMA while the other is copied
-  hipStream_t st[kStageWorkers] = {};
-  hipEvent_t ev[kStageWorkers][2] = {};
-  bool ready = false;
-};
-
-}  // namespace
-
-struct s3imph_ctx {
-  int device = 0;
-  hipStream_t own_stream = nullptr;
-  std::mutex mu;
-
-  uint64_t cap_keys = 0, cap_words = 0, cap_blocks = 0;
-  uint64_t *kh = nullptr, *fp = nullptr, *bits = nullptr, *rank_base = nullptr;
-  unsigned long long* block_sums = nullptr;
-  LevelState* d_st = nullptr;
-  LevelState* h_st = nullptr;
-  bool rank_valid = false;                   // rank_base matches the last build
-
-  // single-GPU binned pipeline (s3imph_binned.hip)
-  Rec* bucket = nullptr;
-  Rec* list[2] = {nullptr, nullptr};
-  uint64_t bucket_cap = 0;                   // records in bucket / each list
-  unsigned *hist = nullptr, *hoff = nullptr, *tile_start = nullptr, *scan_sums = nullptr;
-  unsigned long long* flags = nullptr;
-  unsigned long long* sflags = nullptr;
-  unsigned* tcnt = nullptr;  // reservation-path shard fills, kResLevels x kScatterTiles x kResShards
-  int tile_mode = 0;
-  int tile_block = 1024;
-  uint64_t target_tiles = kTargetTiles, target_tiles0 = kTargetTiles0, target_chunks = kTargetChunks;
-  bool chunks_set = false;  // S3IMPH_CHUNKS given: level 0 uses it too
-  uint64_t res_max_keys = kResMaxKeys;
-  int l0_mode = 0;  // level 0: 0 hash+count / scan / scatter; 1, 2 fused hash+scatter (4096 / 2048-key rounds)
-  uint64_t target_tiles_res = kTargetTilesRes;
-  // reservation slots hold >= 4x a tile's mean fill, 2x on levels above kResSmallKeys
-  // (full 256-block grids: every XCD shard of a slot then fills evenly)
-  uint64_t res_fill = 2;
-  int res0 = 1;  // level 0 through the reservation scatter when its tiles are large
-  // level 0 in pipe0 chunks: the hash of chunk k+1 (aux stream) overlaps the reservation
-  // scatter of chunk k (build stream); 1: k_hash0_range over every key, then one scatter;
-  // 0: k_hash_count0, then one scatter
-  int pipe0 = 0;
-  hipStream_t aux = nullptr;
-  hipEvent_t ev_fork = nullptr;
-  hipEvent_t ev_chunk[kPipe0MaxChunks] = {};
-  bool debug = false;
-  unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps
-  bool lds_attr_set = false;
-
-  // staging for host-memory builds
-  uint8_t* s_blob = nullptr;
-  uint64_t s_blob_cap = 0;
-  uint64_t *s_offsets = nullptr, *s_pos = nullptr, *s_fp = nullptr, *s_posout = nullptr;
-  uint64_t s_cap = 0;
-  Stager stager;
-
-  bool have_build = false;
-  uint64_t last_n = 0;
-  s3imph_build_info info{};
-
-  int profiling = 0;  // 0 off, 1 every stage, 2 the level-0 hash (or route) stage only
-  std::vector<hipEvent_t> events;
-  std::vector<std::string> ev_names;
-  int ev_used = 0;
-  std::vector<float> stage_ms;
-  std::vector<std::string> stage_names;
-
-  std::string last_msg;  // message of the last failed device-resident call
-  bool dist = false;
-  uint64_t dist_switch = kDistSwitchKeysDefault;  // global keys below which levels run replicated
-  DistState d;
-};
-
-namespace {
+namespace s3imph {
 
 constexpr uint64_t kU32Limit = 0xffffffffull;
 
@@ -173,40 +53,6 @@ const char* status_name(int s) {
     case S3IMPH_ERR_STATE: return "invalid state";
     default: return "unknown status";
   }
-}
-
-struct Fail {
-  int code;
-  std::string msg;
-};
-
-#define HIPCHECK(x)                                                                           \
-  do {                                                                                        \
-    hipError_t e_ = (x);                                                                      \
-    if (e_ != hipSuccess)                                                                     \
-      throw Fail{e_ == hipErrorOutOfMemory ? S3IMPH_ERR_NOMEM : S3IMPH_ERR_HIP,               \
-                 std::string(#x) + ": " + hipGetErrorString(e_)};                             \
-  } while (0)
-
-#define NCCLCHECK(x)                                                                          \
-  do {                                                                                        \
-    ncclResult_t r_ = (x);                                                                    \
-    if (r_ != ncclSuccess)                                                                    \
-      throw Fail{S3IMPH_ERR_RCCL, std::string(#x) + ": " + ncclGetErrorString(r_)};           \
-  } while (0)
-
-template <typename T>
-void dfree(T*& p) {
-  if (p) (void)hipFree(p);
-  p = nullptr;
-}
-
-template <typename T>
-void dalloc(T*& p, uint64_t count) {
-  dfree(p);
-  void* v = nullptr;
-  HIPCHECK(hipMalloc(&v, std::max<uint64_t>(count, 1) * sizeof(T)));
-  p = static_cast<T*>(v);
 }
 
 uint64_t cap_words_for(uint64_t n) {
@@ -369,8 +215,6 @@ BinBuffers make_bufs(s3imph_ctx* c, const uint64_t* pos, uint64_t* fp_out, uint6
   b.sflags = c->sflags;
   b.tcnt = c->tcnt;
   b.bucket_cap = c->bucket_cap;
-  b.tile_mode = c->tile_mode;
-  b.tile_block = c->tile_block;
   b.tile_prof = nullptr;
   if (c->debug) {
     const size_t nprof = (size_t)kMaxLevels * kMaxTiles * 8;
@@ -413,7 +257,7 @@ Grids level_grids(uint64_t nk, uint64_t size, LevelGeom g) {
 bool res_fits(const s3imph_ctx* c, uint64_t nb, uint64_t size, uint64_t T = 0) {
   if (nb * (nb > kResSmallKeys ? c->res_fill : 4) <= c->bucket_cap) return true;
   if (T == 0) {
-    const LevelGeom g = choose_geom_sz(nb, size, c->target_tiles_res, c->target_chunks, kRegTileMaxBits);
+    const LevelGeom g = choose_geom_sz(nb, size, kTargetTilesRes, kTargetChunks, kRegTileMaxBits);
     T = (size + (1ull << g.tb) - 1) >> g.tb;
   }
   const double m = (double)nb / ((double)T * kResShards);
@@ -425,11 +269,10 @@ bool res_fits(const s3imph_ctx* c, uint64_t nb, uint64_t size, uint64_t T = 0) {
 void enqueue_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, uint64_t size, bool conservative,
                         const LevelGeom* force, hipStream_t s) {
   // reservation slots are bucket_cap / T records per tile: keep them >= 4x the mean fill
-  const bool res = !conservative && nb <= c->res_max_keys && res_fits(c, nb, size) && L < kResLevels &&
-                   c->tile_mode == 0;
+  const bool res = !conservative && nb <= c->res_max_keys && res_fits(c, nb, size) && L < kResLevels;
   const LevelGeom g = force ? *force
-                      : res ? choose_geom_sz(nb, size, c->target_tiles_res, c->target_chunks, kRegTileMaxBits)
-                            : choose_geom_sz(nb, size, c->target_tiles, c->target_chunks, kRegTileMaxBits);
+                      : res ? choose_geom_sz(nb, size, kTargetTilesRes, kTargetChunks, kRegTileMaxBits)
+                            : choose_geom_sz(nb, size, kTargetTiles, kTargetChunks, kRegTileMaxBits);
   const Grids gr = level_grids(nb, size, g);
   if (res) {
     const int gsr = (int)std::min<uint64_t>((nb + kSubRound - 1) / kSubRound, 256);
@@ -467,20 +310,11 @@ int enqueue_levels_from(s3imph_ctx* c, const BinBuffers& b, int L0, uint64_t n0,
   return launched;
 }
 
-// The pipelined level 0's second stream and its fork / per-chunk events, made on first use.
-void ensure_aux(s3imph_ctx* c) {
-  if (c->aux) return;
-  HIPCHECK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-  HIPCHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-  for (auto& e : c->ev_chunk) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-}
-
 // Chunks (hash blocks) of the level-0 hash over n keys.  Blocks are scheduled as they
 // free up, so more, smaller chunks even out long-key chunks on big sets; on small ones
 // each block's fixed cost wins (S3IMPH_CHUNKS sweep, hash_count0 ms at 768 / 1536
 // chunks: C2 0.229 / 0.243, C3 3.89 / 3.75, C5 4.28 / 4.05).
-uint64_t chunks0(const s3imph_ctx* c, uint64_t n) {
-  if (c->chunks_set) return c->target_chunks;
+uint64_t chunks0(uint64_t n) {
   return n >= kBigChunksKeys ? 2 * kTargetChunks : kTargetChunks;
 }
 
@@ -491,51 +325,14 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
   const BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
   const double q = 1.0 - std::exp(-0.5);
-  const LevelGeom g0 = choose_geom(n, c->target_tiles0, chunks0(c, n), kRegTileMaxBits);
+  const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
   launch_init_state(c->d_st, n, n, s, offsets);
   ev_mark(c, s, "init");
   const Grids gr = level_grids(n, 64 * level_words(n), g0);
-  if (!conservative && c->l0_mode && g0.tb <= kRegTileMaxBits &&
-      ((64 * level_words(n) + (1ull << g0.tb) - 1) >> g0.tb) <= kScatterTiles) {
-    // fused level 0: hash straight into reservation slots, then the sharded tile kernel
-    HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kScatterTiles * kResShards * sizeof(unsigned), s));
-    launch_hash_scatter0(blob, offsets, n, b, g0, c->l0_mode - 1, s);
-    ev_mark(c, s, "hash_scatter0");
-    launch_binned_tile(0, b, g0, gr.gt, s, true);
-    ev_mark(c, s, "tile0");
-    enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
-    return;
-  }
   // Level 0 through the reservation scatter when its tiles are big enough that every
   // (tile, shard) slot's headroom (bucket_cap = 1.25 n) covers 7 sigma of its fill
   const uint64_t T0 = (64 * level_words(n) + (1ull << g0.tb) - 1) >> g0.tb;
   const bool res0 = !conservative && c->res0 && T0 <= kScatterTiles && (res_fits(c, n, 64 * level_words(n), T0) || c->res0 == 2);
-  if (res0 && c->pipe0 >= 1 && n >= kPipe0MinKeys) {
-    // Level 0 pipelined over K chunks: the aux stream hashes chunk k+1 while the build
-    // stream scatters chunk k; the two kernels share CUs (the hash uses no LDS).
-    ensure_aux(c);  // (chunk 0's hash clears the reservation counters of every level)
-    HIPCHECK(hipEventRecord(c->ev_fork, s));
-    HIPCHECK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-    launch_hash0_skewed(blob, offsets, n, b, g0, gr.gc, c->aux);  // returns unless lengths are skewed
-    const int K = std::min(c->pipe0, kPipe0MaxChunks);
-    uint64_t lo = 0;
-    for (int k = 0; k < K; ++k) {
-      uint64_t hi = n;
-      if (k + 1 < K) hi = std::min<uint64_t>(n, (n * (k + 1) / K + kSubRound - 1) / kSubRound * kSubRound);
-      launch_hash0_range(blob, offsets, lo, hi, b, c->aux);  // returns if skewed
-      HIPCHECK(hipEventRecord(c->ev_chunk[k], c->aux));
-      HIPCHECK(hipStreamWaitEvent(s, c->ev_chunk[k], 0));
-      if (hi > lo)
-        launch_binned_scatter_res(0, b, g0, (int)std::min<uint64_t>(256, (hi - lo + kSubRound - 1) / kSubRound), s,
-                                  lo, hi);
-      lo = hi;
-    }
-    ev_mark(c, s, "hash_scatter0");
-    launch_binned_tile(0, b, g0, gr.gt, s, true);
-    ev_mark(c, s, "tile0");
-    enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
-    return;
-  }
   launch_binned_count(0, blob, offsets, n, b, g0, gr.gc, s, !res0);  // no histogram for the reservation path
   ev_mark(c, s, "hash_count0");
   if (res0) {
@@ -670,37 +467,6 @@ int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
 }
 
 // -------------------------------------------------------------------- distributed ----
-// RCCL over xGMI: all-to-all as grouped point-to-point send/recv (xGMI is a full mesh
-// of point-to-point links, so every pair streams on its own link), all-gathers and
-// all-reduces as RCCL collectives; the rank's own share is a device-to-device copy.
-struct RcclComm final : Comm {
-  ncclComm_t comm = nullptr;
-  ~RcclComm() override {
-    if (comm) (void)ncclCommDestroy(comm);
-  }
-  void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
-    NCCLCHECK(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, s));
-  }
-  void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
-                     hipStream_t s) override {
-    NCCLCHECK(ncclAllReduce(d_in, d_out, count, ncclUint64, ncclSum, comm, s));
-  }
-  void alltoallv(const void* d_send, const uint64_t* soff, const uint64_t* sbytes, void* d_recv,
-                 const uint64_t* roff, const uint64_t* rbytes, hipStream_t s) override {
-    const char* sb = static_cast<const char*>(d_send);
-    char* rb = static_cast<char*>(d_recv);
-    NCCLCHECK(ncclGroupStart());
-    for (int q = 0; q < nranks; ++q) {
-      if (q == rank) continue;
-      if (sbytes[q]) NCCLCHECK(ncclSend(sb + soff[q], sbytes[q], ncclUint8, q, comm, s));
-      if (rbytes[q]) NCCLCHECK(ncclRecv(rb + roff[q], rbytes[q], ncclUint8, q, comm, s));
-    }
-    NCCLCHECK(ncclGroupEnd());
-    if (sbytes[rank])
-      HIPCHECK(hipMemcpyAsync(rb + roff[rank], sb + soff[rank], sbytes[rank], hipMemcpyDeviceToDevice, s));
-  }
-};
-
 // Host-callback transport (s3imph_host_comm): the test harness's collectives (e.g.
 // torch.distributed/gloo) on host copies.  Lets several ranks share one GPU.
 struct HostComm final : Comm {
@@ -859,7 +625,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   ev_mark(c, s, "init");
   // level 0's key hashes and fingerprints, once (the routing below may be retried)
   if (n_local) {
-    const LevelGeom gh = choose_geom_sz(n_local, 64 * level_words(N), c->target_tiles0, chunks0(c, n_local), kTileMaxBits);
+    const LevelGeom gh = choose_geom_sz(n_local, 64 * level_words(N), kTargetTiles0, chunks0(n_local), kTileMaxBits);
     launch_hash0_only(blob, offsets, n_local, b, gh, level_grids(n_local, 64 * level_words(N), gh).gc, s);
   }
   ev_mark(c, s, "hash_count0");
@@ -964,7 +730,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   }
   launch_dist_replicate(st, Ls, total, R == 0 ? 0 : (uint64_t)Ls, s);
   ev_mark(c, s, "gather");
-  const LevelGeom gcons = choose_geom(std::max<uint64_t>(total, 1), c->target_tiles, c->target_chunks, kRegTileMaxBits);
+  const LevelGeom gcons = choose_geom(std::max<uint64_t>(total, 1), kTargetTiles, kTargetChunks, kRegTileMaxBits);
   enqueue_levels_from(c, b, Ls, total, gcons, conservative, s);
   // ---- level bit vectors of the distributed levels: all-gather each rank's word range
   uint64_t woff = 0;
@@ -1098,7 +864,7 @@ int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
 s3imph_ctx* g_default[64] = {nullptr};
 std::mutex g_default_mu;
 
-}  // namespace
+}  // namespace s3imph
 
 namespace s3imph {
 int marshal_locked(s3imph_ctx* c, uint8_t* out, uint64_t cap, uint64_t* len, std::string* msg);
@@ -1137,16 +903,11 @@ void stager_init(s3imph_ctx* c) {
 // Chunked copy between pageable host memory and the device through the pinned
 // buffers.  h2d: device dst <- host src; with `bias`, src holds u64 words and each is
 // stored minus bias (offsets rebased to a blob that starts at offsets[0]).
-void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias = 0) {
+void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias) {
   if (!bytes) return;
   // Pageable H2D through the runtime already runs at the PCIe rate (C2: 400 MB in
   // 7.4 ms, 54 GB/s); pageable D2H does not (17 GB/s), and neither does rebasing.
-  // S3IMPH_STAGE=0 / =2 force the runtime / staged path for every copy (A/B).
-  static const int mode = [] {
-    const char* e = std::getenv("S3IMPH_STAGE");
-    return e ? std::atoi(e) : 1;
-  }();
-  if (!bias && (mode == 0 || (mode == 1 && h2d))) {
+  if (!bias && h2d) {
     HIPCHECK(hipMemcpy(dst, src, bytes, h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost));
     return;
   }
@@ -1314,22 +1075,11 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     HIPCHECK(hipSetDevice(device));
     c = new s3imph_ctx();
     c->device = device;
-    if (const char* m = std::getenv("S3IMPH_TILE_MODE")) c->tile_mode = std::atoi(m);  // A/B knobs
-    if (const char* m = std::getenv("S3IMPH_TARGET_TILES")) c->target_tiles = std::strtoull(m, nullptr, 10);
-    if (const char* m = std::getenv("S3IMPH_TARGET_TILES0")) c->target_tiles0 = std::strtoull(m, nullptr, 10);
-    if (const char* m = std::getenv("S3IMPH_CHUNKS")) {
-      c->target_chunks = std::strtoull(m, nullptr, 10);
-      c->chunks_set = true;
-    }
     if (const char* m = std::getenv("S3IMPH_RES_MAX")) c->res_max_keys = std::strtoull(m, nullptr, 10);
-    if (const char* m = std::getenv("S3IMPH_TARGET_TILES_RES")) c->target_tiles_res = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_RES_FILL")) c->res_fill = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_RES0")) c->res0 = std::atoi(m);
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
-    if (const char* m = std::getenv("S3IMPH_TILE_BLOCK")) c->tile_block = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);
-    if (const char* m = std::getenv("S3IMPH_L0")) c->l0_mode = std::atoi(m);
-    if (const char* m = std::getenv("S3IMPH_PIPE0")) c->pipe0 = std::atoi(m);
     // A blocking stream: implicitly ordered with the legacy NULL stream, so work a
     // caller queued there (e.g. torch's default stream) completes before ours starts.
     HIPCHECK(hipStreamCreate(&c->own_stream));
@@ -1359,12 +1109,6 @@ int s3imph_ctx_destroy(s3imph_ctx* c) {
   delete c->d.comm;
   c->d.comm = nullptr;
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
-  if (c->aux) {
-    (void)hipStreamSynchronize(c->aux);
-    (void)hipStreamDestroy(c->aux);
-    (void)hipEventDestroy(c->ev_fork);
-    for (auto e : c->ev_chunk) (void)hipEventDestroy(e);
-  }
   delete c;
   return S3IMPH_OK;
 }

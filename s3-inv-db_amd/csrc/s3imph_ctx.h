@@ -1,0 +1,207 @@
+// s3imph_ctx.h — the device context and the pieces of the build orchestration shared by
+// s3imph_build.hip (single-GPU and per-rank builds, the device-side C ABI) and
+// s3imph_multi.hip (multi-GPU builds behind the host-memory boundary).  Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "s3imph.h"
+#include "s3imph_internal.h"
+
+namespace s3imph {
+
+struct Fail {
+  int code;
+  std::string msg;
+};
+
+#define HIPCHECK(x)                                                                           \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess)                                                                     \
+      throw Fail{e_ == hipErrorOutOfMemory ? S3IMPH_ERR_NOMEM : S3IMPH_ERR_HIP,               \
+                 std::string(#x) + ": " + hipGetErrorString(e_)};                             \
+  } while (0)
+
+#define NCCLCHECK(x)                                                                          \
+  do {                                                                                        \
+    ncclResult_t r_ = (x);                                                                    \
+    if (r_ != ncclSuccess)                                                                    \
+      throw Fail{S3IMPH_ERR_RCCL, std::string(#x) + ": " + ncclGetErrorString(r_)};           \
+  } while (0)
+
+template <typename T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+template <typename T>
+void dalloc(T*& p, uint64_t count) {
+  dfree(p);
+  void* v = nullptr;
+  HIPCHECK(hipMalloc(&v, std::max<uint64_t>(count, 1) * sizeof(T)));
+  p = static_cast<T*>(v);
+}
+
+// Collectives of the multi-GPU build, on device buffers, ordered on stream s.
+struct Comm {
+  int rank = 0, nranks = 1;
+  virtual ~Comm() = default;
+  // d_recv[r * bytes ..) <- rank r's d_send[0 .. bytes)
+  virtual void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) = 0;
+  // element-wise u64 sum over ranks
+  virtual void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
+                             hipStream_t s) = 0;
+  // d_send + soff[q] (sbytes[q] bytes) -> rank q; rank q's bytes -> d_recv + roff[q] (rbytes[q]); host arrays
+  virtual void alltoallv(const void* d_send, const uint64_t* soff, const uint64_t* sbytes, void* d_recv,
+                         const uint64_t* roff, const uint64_t* rbytes, hipStream_t s) = 0;
+};
+
+constexpr uint64_t kDistSwitchKeysDefault = 2ull << 20;  // levels below this run replicated
+
+struct DistState {
+  Comm* comm = nullptr;
+  int rank = 0, nranks = 1;
+  uint64_t cap_list = 0, cap_send = 0, cap_stage_words = 0;
+  Rec* send = nullptr;                       // per-owner send regions / replicated gather staging
+  uint64_t* stage_bits = nullptr;            // level bit-vector all-gather staging
+  unsigned long long* scnt = nullptr;        // per-owner send counts (nranks)
+  unsigned long long* mat = nullptr;         // all-gathered send counts (nranks x nranks)
+  unsigned long long* gslot = nullptr;       // per-level global counts (kMaxLevels + 2)
+  unsigned long long* small = nullptr;       // scratch for tiny collectives (2 x 64 x 64)
+  unsigned long long* h_pinned = nullptr;    // host staging (64 x 64 + 256 u64)
+  std::vector<uint64_t> seg;                 // last build: (p_lo, count, local_off) triples
+  uint64_t out_n = 0;
+};
+
+// RCCL over xGMI: all-to-all as grouped point-to-point send/recv (xGMI is a full mesh
+// of point-to-point links, so every pair streams on its own link), all-gathers and
+// all-reduces as RCCL collectives; the rank's own share is a device-to-device copy.
+struct RcclComm final : Comm {
+  ncclComm_t comm = nullptr;
+  ~RcclComm() override {
+    if (comm) (void)ncclCommDestroy(comm);
+  }
+  void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
+    NCCLCHECK(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, s));
+  }
+  void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
+                     hipStream_t s) override {
+    NCCLCHECK(ncclAllReduce(d_in, d_out, count, ncclUint64, ncclSum, comm, s));
+  }
+  void alltoallv(const void* d_send, const uint64_t* soff, const uint64_t* sbytes, void* d_recv,
+                 const uint64_t* roff, const uint64_t* rbytes, hipStream_t s) override {
+    const char* sb = static_cast<const char*>(d_send);
+    char* rb = static_cast<char*>(d_recv);
+    NCCLCHECK(ncclGroupStart());
+    for (int q = 0; q < nranks; ++q) {
+      if (q == rank) continue;
+      if (sbytes[q]) NCCLCHECK(ncclSend(sb + soff[q], sbytes[q], ncclUint8, q, comm, s));
+      if (rbytes[q]) NCCLCHECK(ncclRecv(rb + roff[q], rbytes[q], ncclUint8, q, comm, s));
+    }
+    NCCLCHECK(ncclGroupEnd());
+    if (sbytes[rank])
+      HIPCHECK(hipMemcpyAsync(rb + roff[rank], sb + soff[rank], sbytes[rank], hipMemcpyDeviceToDevice, s));
+  }
+};
+
+// Pinned staging for host-memory builds (the Go caller's buffers are pageable):
+// kStageWorkers threads, each with its own pinned chunk buffer and stream, move the
+// data through pinned memory, so the CPU copies of one worker overlap the DMA of the
+// others and the PCIe link runs at its pinned rate.
+constexpr int kStageWorkers = 8;
+constexpr uint64_t kStageChunk = 8ull << 20;
+
+struct Stager {
+  void* pin[kStageWorkers][2] = {};  // double-buffered: one chunk in DMA while the other is copied
+  hipStream_t st[kStageWorkers] = {};
+  hipEvent_t ev[kStageWorkers][2] = {};
+  bool ready = false;
+};
+
+}  // namespace s3imph
+
+using s3imph::DistState;
+using s3imph::LevelState;
+using s3imph::Rec;
+using s3imph::Stager;
+
+struct s3imph_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  std::mutex mu;
+
+  uint64_t cap_keys = 0, cap_words = 0, cap_blocks = 0;
+  uint64_t *kh = nullptr, *fp = nullptr, *bits = nullptr, *rank_base = nullptr;
+  unsigned long long* block_sums = nullptr;
+  LevelState* d_st = nullptr;
+  LevelState* h_st = nullptr;
+  bool rank_valid = false;                   // rank_base matches the last build
+
+  // single-GPU binned pipeline (s3imph_binned.hip)
+  Rec* bucket = nullptr;
+  Rec* list[2] = {nullptr, nullptr};
+  uint64_t bucket_cap = 0;                   // records in bucket / each list
+  unsigned *hist = nullptr, *hoff = nullptr, *tile_start = nullptr, *scan_sums = nullptr;
+  unsigned long long* flags = nullptr;
+  unsigned long long* sflags = nullptr;
+  unsigned* tcnt = nullptr;  // reservation-path shard fills, kResLevels x kScatterTiles x kResShards
+  uint64_t res_max_keys = s3imph::kResMaxKeys;
+  // reservation slots hold >= 4x a tile's mean fill, 2x on levels above kResSmallKeys
+  // (full 256-block grids: every XCD shard of a slot then fills evenly)
+  uint64_t res_fill = 2;
+  // test knobs (S3IMPH_RES_MAX / S3IMPH_RES0 / S3IMPH_RES_FILL) that force the fallback paths:
+  // res0 = 0 puts level 0 on the counted path, 2 on the reservation path whatever its fill
+  int res0 = 1;  // level 0 through the reservation scatter when its tiles are large
+  bool debug = false;
+  unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps
+  bool lds_attr_set = false;
+
+  // staging for host-memory builds
+  uint8_t* s_blob = nullptr;
+  uint64_t s_blob_cap = 0;
+  uint64_t *s_offsets = nullptr, *s_pos = nullptr, *s_fp = nullptr, *s_posout = nullptr;
+  uint64_t s_cap = 0;
+  Stager stager;
+
+  bool have_build = false;
+  uint64_t last_n = 0;
+  s3imph_build_info info{};
+
+  int profiling = 0;  // 0 off, 1 every stage, 2 the level-0 hash (or route) stage only
+  std::vector<hipEvent_t> events;
+  std::vector<std::string> ev_names;
+  int ev_used = 0;
+  std::vector<float> stage_ms;
+  std::vector<std::string> stage_names;
+
+  std::string last_msg;  // message of the last failed device-resident call
+  bool dist = false;
+  uint64_t dist_switch = s3imph::kDistSwitchKeysDefault;  // global keys below which levels run replicated
+  DistState d;
+};
+
+namespace s3imph {
+
+// Builds (s3imph_build.hip).  Both return an s3imph_status and throw Fail on HIP/RCCL errors.
+int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t n,
+                 uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, s3imph_build_info* info, std::string* msg);
+int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t n_local,
+               uint64_t key_base, uint64_t* fp_out, uint64_t* pos_out, uint64_t out_cap, uint64_t* out_n,
+               hipStream_t s, s3imph_build_info* info, std::string* msg);
+uint64_t dist_out_cap(const s3imph_ctx* c, uint64_t n_global);
+// Chunked host <-> device copy through the ctx's pinned stager (h2d: device dst <- host src;
+// with `bias`, src holds u64 words stored minus bias).
+void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias = 0);
+int marshal_locked(s3imph_ctx* c, uint8_t* out, uint64_t cap, uint64_t* len, std::string* msg);
+// A context (s3imph_ctx_create) whose multi-GPU collectives go through `comm` (owned).
+s3imph_ctx* make_dist_ctx(int device, Comm* comm, int rank, int nranks, std::string* msg);
+
+}  // namespace s3imph

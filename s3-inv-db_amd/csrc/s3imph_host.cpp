@@ -21,10 +21,6 @@
 
 namespace s3imph {
 
-int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
-                    uint64_t n, uint64_t* fp_out, uint64_t* pos_out, std::vector<uint8_t>* mph,
-                    std::string* msg);
-
 void set_err(char* err, size_t errlen, const std::string& msg) {
   if (!err || errlen == 0) return;
   size_t k = std::min(errlen - 1, msg.size());
@@ -164,6 +160,8 @@ using namespace s3imph;
 // --------------------------------------------------------------- builder mirror ----
 struct s3imph_builder {
   int device = 0;
+  std::vector<int> devices;  // s3imph_builder_set_gpus (empty: `device` alone)
+  unsigned multi_flags = 0;
   std::string temp_dir;
   std::vector<uint8_t> blob;
   std::vector<uint64_t> offsets{0};
@@ -258,8 +256,11 @@ int s3imph_builder_build(s3imph_builder* b, const char* out_dir, char* err, size
     std::vector<uint64_t> fp(n), pos_out(n);
     std::vector<uint8_t> mph;
     if (n) {
-      int rc = build_from_host(b->device, b->blob.data(), b->offsets.data(), b->pos.data(), n, fp.data(),
-                               pos_out.data(), &mph, &msg);
+      int rc = b->devices.empty()
+                   ? build_from_host(b->device, b->blob.data(), b->offsets.data(), b->pos.data(), n, fp.data(),
+                                     pos_out.data(), &mph, &msg)
+                   : build_from_host_multi(b->devices, b->multi_flags, b->blob.data(), b->offsets.data(),
+                                           b->pos.data(), n, fp.data(), pos_out.data(), &mph, &msg);
       if (rc != S3IMPH_OK) {
         set_err(err, errlen, msg);
         return rc;
@@ -277,6 +278,15 @@ int s3imph_builder_build(s3imph_builder* b, const char* out_dir, char* err, size
     set_err(err, errlen, "build MPHF: out of host memory");
     return S3IMPH_ERR_NOMEM;
   }
+}
+
+int s3imph_builder_set_gpus(s3imph_builder* b, int num_gpus, const int* devices, unsigned flags) {
+  if (!b || num_gpus < 1 || num_gpus > 64) return S3IMPH_ERR_INVALID;
+  if (b->built) return S3IMPH_ERR_STATE;
+  b->devices.resize(num_gpus);
+  for (int r = 0; r < num_gpus; ++r) b->devices[r] = devices ? devices[r] : r;
+  b->multi_flags = flags;
+  return S3IMPH_OK;
 }
 
 int s3imph_builder_close(s3imph_builder* b) {

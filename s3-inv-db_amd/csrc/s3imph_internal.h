@@ -96,8 +96,6 @@ constexpr uint64_t kResSmallKeys = 2ull << 20;  // ... with 4x slot headroom up 
 constexpr int kResShards = 8;                 // per-tile reservation counters (one per XCD)
 constexpr int kResLevels = 32;                // levels that may use the reservation path
 constexpr double kTailMargin = 1.1;
-constexpr int kPipe0MaxChunks = 16;              // pipelined level 0: most chunks
-constexpr uint64_t kPipe0MinKeys = 1ull << 20;   // ... and fewest keys it runs on
 constexpr uint64_t kTargetChunks = 768;  // 3 resident 1024-thread count blocks x 256 CUs
 constexpr uint64_t kBigChunksKeys = 20ull << 20;  // level-0 hash of this many keys or more: 2x the chunks
 // n records over `size` positions (64 * level_words(n) for a whole level).
@@ -165,9 +163,7 @@ struct BinBuffers {
   unsigned long long* sflags;           // look-back words of the histogram scan
   unsigned* tcnt;                       // reservation-path shard fills, kResLevels x kScatterTiles x kResShards
   uint64_t bucket_cap;                  // bucket capacity in records
-  int tile_mode;
-  int tile_block;                       // tile workgroup size (512 or 1024)
-  unsigned long long* tile_prof;        // debug: per (level, tile) phase timestamps, or null                        // 0: rank-order gather, 1: in-order with window writes
+  unsigned long long* tile_prof;        // debug: per (level, tile) phase timestamps, or null
   uint64_t* bits;
   uint64_t cap_words;
   uint64_t* fp_out;
@@ -179,19 +175,11 @@ void binned_set_lds_limits();
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s, bool histogram = true);
 void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s);
-void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s, bool direct = false);
+void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s);
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s,
                         bool reserved = false);
-void launch_hash_scatter0(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
-                          int variant, hipStream_t s);
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s,
                                uint64_t i_lo = 0, uint64_t i_hi = 0);
-// pipelined level 0: keys [lo, hi) hashed into kh / fp (near-uniform sets; returns on a
-// skewed one), and the length-sorted hash of a skewed set (returns on a near-uniform one)
-void launch_hash0_range(const uint8_t* blob, const uint64_t* offsets, uint64_t lo, uint64_t hi, const BinBuffers& b,
-                        hipStream_t s);
-void launch_hash0_skewed(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
-                         int grid, hipStream_t s);
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s);
 
 // ---- multi-GPU launchers (s3imph_dist.hip) ------------------------------------------
@@ -211,6 +199,13 @@ void launch_dist_setup(LevelState* st, int L, const unsigned long long* gcount, 
 void launch_set_u64(unsigned long long* p, uint64_t v, hipStream_t s);
 void launch_route_flag(LevelState* st, unsigned long long* scnt, int P, hipStream_t s);
 void launch_dist_replicate(LevelState* st, int L, uint64_t n_all, uint64_t skip_from, hipStream_t s);
+
+// ---- host-memory builds (s3imph_build.hip, s3imph_multi.hip) -------------------------
+int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t n,
+                    uint64_t* fp_out, uint64_t* pos_out, std::vector<uint8_t>* mph, std::string* msg);
+int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const uint8_t* blob, const uint64_t* offsets,
+                          const uint64_t* pos, uint64_t n, uint64_t* fp_out, uint64_t* pos_out,
+                          std::vector<uint8_t>* mph, std::string* msg);
 
 // ---- host helpers (s3imph_host.cpp) -------------------------------------------
 void set_err(char* err, size_t errlen, const std::string& msg);

@@ -45,12 +45,16 @@ ERR_FORMAT = 9
 ERR_INTERNAL = 10
 ERR_STATE = 11
 
+MULTI_FORCE_SHARDED = 1   # the sharded (multi-GPU) build even for one GPU
+MULTI_HOST_TRANSPORT = 2  # in-process host-copy collectives instead of RCCL
+
 # Every entry point include/s3imph.h declares (checked by tests/test_capi.py).
 EXPORTS = (
     "s3imph_abi_version", "s3imph_status_string",
     "s3imph_builder_new", "s3imph_builder_add", "s3imph_builder_add_batch", "s3imph_builder_count",
     "s3imph_builder_build", "s3imph_builder_close",
-    "s3imph_build_host", "s3imph_free", "s3imph_write_index_files",
+    "s3imph_build_host", "s3imph_build_host_multi", "s3imph_builder_set_gpus", "s3imph_free",
+    "s3imph_write_index_files",
     "s3imph_ctx_create", "s3imph_ctx_destroy", "s3imph_ctx_reserve", "s3imph_build_device",
     "s3imph_ctx_mph_bin", "s3imph_ctx_set_profiling", "s3imph_ctx_stage_times",
     "s3imph_dist_unique_id", "s3imph_ctx_create_dist", "s3imph_ctx_create_dist_host", "s3imph_build_device_dist",
@@ -109,6 +113,8 @@ def _load():
         "s3imph_builder_build": (i32, [vp, cp, cp, sz]),
         "s3imph_builder_close": (i32, [vp]),
         "s3imph_build_host": (i32, [i32, vp, vp, vp, u64, vp, vp, P(vp), P(u64), cp, sz]),
+        "s3imph_build_host_multi": (i32, [i32, vp, ctypes.c_uint, vp, vp, vp, u64, vp, vp, P(vp), P(u64), cp, sz]),
+        "s3imph_builder_set_gpus": (i32, [vp, i32, vp, ctypes.c_uint]),
         "s3imph_free": (None, [vp]),
         "s3imph_write_index_files": (i32, [cp, vp, u64, vp, vp, u64, vp, vp, cp, sz]),
         "s3imph_ctx_create": (i32, [i32, P(vp), cp, sz]),
@@ -201,6 +207,11 @@ class StreamingMPHFBuilder:
     def count(self) -> int:
         return LIB.s3imph_builder_count(self._h)
 
+    def set_gpus(self, num_gpus: int, devices=None, flags: int = 0) -> None:
+        """Build on `num_gpus` GPUs (s3imph_builder_set_gpus; see build_host)."""
+        devs = None if devices is None else (ctypes.c_int * num_gpus)(*devices)
+        _check(LIB.s3imph_builder_set_gpus(self._h, num_gpus, devs, flags), None, "set_gpus")
+
     def build(self, out_dir: str) -> None:
         err = ctypes.create_string_buffer(1024)
         _check(LIB.s3imph_builder_build(self._h, out_dir.encode(), err, 1024), err)
@@ -224,9 +235,12 @@ class StreamingMPHFBuilder:
 
 
 def build_host(blob: np.ndarray, offsets: np.ndarray, pos: np.ndarray | None = None, device: int = 0,
-               out: tuple[np.ndarray, np.ndarray] | None = None):
+               out: tuple[np.ndarray, np.ndarray] | None = None, num_gpus: int = 1, devices=None, flags: int = 0):
     """One-shot build from host memory: (fp_out u64[N], pos_out u64[N], mph_bin bytes).
-    `out` may supply the two output arrays (u64, N each) to be filled in place."""
+    `out` may supply the two output arrays (u64, N each) to be filled in place.
+    num_gpus > 1 (or `devices`, or `flags`) runs s3imph_build_host_multi: one host thread
+    per GPU, RCCL between them (or in-process host copies when devices repeat or flags
+    has MULTI_HOST_TRANSPORT)."""
     blob = np.ascontiguousarray(blob, np.uint8)
     offsets = np.ascontiguousarray(offsets, np.uint64)
     n = len(offsets) - 1
@@ -243,8 +257,16 @@ def build_host(blob: np.ndarray, offsets: np.ndarray, pos: np.ndarray | None = N
     mp = ctypes.c_void_p()
     ml = ctypes.c_uint64()
     err = ctypes.create_string_buffer(1024)
-    rc = LIB.s3imph_build_host(device, _np_ptr(blob), _np_ptr(offsets), _np_ptr(pos), n, _np_ptr(fp_out),
-                               _np_ptr(pos_out), ctypes.byref(mp), ctypes.byref(ml), err, 1024)
+    if num_gpus == 1 and devices is None and not flags:
+        rc = LIB.s3imph_build_host(device, _np_ptr(blob), _np_ptr(offsets), _np_ptr(pos), n, _np_ptr(fp_out),
+                                   _np_ptr(pos_out), ctypes.byref(mp), ctypes.byref(ml), err, 1024)
+    else:
+        if devices is not None:
+            num_gpus = len(devices)
+        devs = None if devices is None else (ctypes.c_int * num_gpus)(*devices)
+        rc = LIB.s3imph_build_host_multi(num_gpus, devs, flags, _np_ptr(blob), _np_ptr(offsets), _np_ptr(pos), n,
+                                         _np_ptr(fp_out), _np_ptr(pos_out), ctypes.byref(mp), ctypes.byref(ml), err,
+                                         1024)
     _check(rc, err)
     mph = ctypes.string_at(mp.value, ml.value) if ml.value else b""
     if mp.value:

@@ -1,0 +1,110 @@
+"""Multi-GPU builds behind the host-memory boundary (s3imph_build_host_multi and the
+builder's set_gpus): one calling process, one host thread per rank.
+
+The box has one GPU, so the ranks of the thread-per-rank logic share it through the
+in-process host-copy transport (devices = [0] * P); the RCCL path runs with one rank
+made by ncclCommInitAll.  S3IMPH_DIST_SWITCH lowers the replicated-tail threshold so
+that small sets still route several levels between ranks.  Every result is compared
+byte for byte with the oracle (mph.bin, mph_fp, mph_pos).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def s3():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    import s3imph
+    return s3imph
+
+
+def _expect(oracle_lib, blob, offs, pos=None):
+    st, fp, po, mph = oracle_lib.build_mt(blob[: int(offs[-1])], offs, pos, threads=16)
+    assert st == 0
+    return fp, po, mph
+
+
+def test_one_gpu_default_is_the_single_gpu_build(s3, oracle_lib):
+    blob, offs = s3.gen_keys(0, 5, 32, 0, 300_000)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    g = s3.build_host(blob, offs, num_gpus=1)
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+
+
+def test_one_gpu_sharded_over_rccl(s3, oracle_lib, monkeypatch):
+    """num_gpus = 1 forced onto the sharded path: an in-process RCCL communicator
+    (ncclCommInitAll) carries every collective of the routed levels."""
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", "20000")
+    blob, offs = s3.gen_keys(0, 6, 40, 0, 400_000)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    for _ in range(2):  # the second build reuses the cached contexts and communicator
+        g = s3.build_host(blob, offs, num_gpus=1, flags=s3.MULTI_FORCE_SHARDED)
+        assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+
+
+@pytest.mark.parametrize("ranks,kind,avg,n", [(2, 0, 32, 300_000), (3, 1, 0, 400_000), (4, 0, 64, 500_000)])
+def test_thread_per_rank_shared_gpu(s3, oracle_lib, monkeypatch, ranks, kind, avg, n):
+    """2-4 ranks in one process on the one GPU (host-copy transport), shards balanced by
+    key bytes, skewed lengths on one case: bit-exact."""
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", "15000")
+    blob, offs = s3.gen_keys(kind, 8, avg, 0, n)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    g = s3.build_host(blob, offs, devices=[0] * ranks)
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+
+
+def test_thread_per_rank_custom_positions_offset_blob(s3, oracle_lib, monkeypatch):
+    """A blob starting at a non-zero offsets[0] with custom positions, 3 ranks."""
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", "15000")
+    n = 250_000
+    blob, offs = s3.gen_keys(0, 9, 24, 0, n)
+    blob = blob[: int(offs[-1])]
+    pos = np.random.default_rng(2).permutation(n).astype(np.uint64) + np.uint64(10**9)
+    fp, po, mph = _expect(oracle_lib, blob, offs, pos)
+    shifted = np.concatenate([np.frombuffer(b"abcde", np.uint8), blob])
+    g = s3.build_host(shifted, offs + np.uint64(5), pos, devices=[0, 0, 0])
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+
+
+def test_thread_per_rank_tiny_and_duplicate_sets(s3, oracle_lib):
+    keys = [b"", b"a/", b"data/", b"data/2024/", b"root/"]
+    blob, offs = O.keys_to_blob(keys)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    g = s3.build_host(blob, offs, devices=[0, 0, 0, 0])
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+    dup = [b"x/%05d/" % i for i in range(3000)]
+    dup[2500] = dup[10]  # the duplicate lands on another rank's shard
+    b2, o2 = O.keys_to_blob(dup)
+    with pytest.raises(s3.MPHFError) as e:
+        s3.build_host(b2, o2, devices=[0, 0])
+    assert e.value.status == s3.ERR_DUP_KEY_HASH
+    # the cached rank contexts stay usable after the error
+    g = s3.build_host(blob, offs, devices=[0, 0, 0, 0])
+    assert g[2] == mph
+
+
+def test_builder_on_several_gpus_writes_identical_files(s3, oracle_lib, tmp_path, monkeypatch):
+    """StreamingMPHFBuilder mirror with set_gpus: Add x N -> Build(outDir) on 3 ranks ->
+    the 5 files equal the oracle's."""
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", "15000")
+    blob, offs = s3.gen_keys(0, 4, 32, 0, 120_000)
+    keys = [bytes(blob[offs[i]:offs[i + 1]]) for i in range(len(offs) - 1)]
+    b = s3.StreamingMPHFBuilder(str(tmp_path))
+    b.set_gpus(3, [0, 0, 0])
+    for i, k in enumerate(keys):
+        b.add(k, i)
+    out = tmp_path / "idx"
+    out.mkdir()
+    b.build(str(out))
+    b.close()
+    kb, ko = O.keys_to_blob(keys)
+    st, fp, po, mph = oracle_lib.build(kb, ko)
+    want = {"mph.bin": mph, "mph_fp.u64": O.s3id_u64_array(fp), "mph_pos.u64": O.s3id_u64_array(po),
+            "prefix_blob.bin": kb.tobytes(), "prefix_offsets.u64": O.s3id_u64_array(ko)}
+    for name, data in want.items():
+        assert (out / name).read_bytes() == data, name
