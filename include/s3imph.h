@@ -224,6 +224,12 @@ const char *s3imph_ctx_last_error(s3imph_ctx *ctx);
  *    over the last build's levels, for n query keys; result[i] = pos or
  *    UINT64_MAX when not found.  Self-verifies a build (VerifyMPHF, :372-393).
  * ------------------------------------------------------------------------ */
+/* OpenMPHF (pkg/format/mphf.go:186-247): load a marshalled mph.bin (any builder's, e.g.
+ * an index on disk) into ctx in place of its last build, so that s3imph_lookup_device
+ * answers MPHF.Lookup against it.  S3IMPH_ERR_FORMAT (message: s3imph_ctx_last_error)
+ * on a malformed file; len == 0 is the empty MPHF (writeEmpty's 0-byte mph.bin). */
+int s3imph_ctx_load_mph_bin(s3imph_ctx *ctx, const uint8_t *mph_bin, uint64_t len);
+
 int s3imph_lookup_device(s3imph_ctx *ctx, const uint8_t *d_blob, const uint64_t *d_offsets, uint64_t n,
                          const uint64_t *d_fp, const uint64_t *d_pos, uint64_t count,
                          uint64_t *d_result, void *stream);

@@ -335,6 +335,8 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   const bool res0 = !conservative && c->res0 && T0 <= kScatterTiles && (res_fits(c, n, 64 * level_words(n), T0) || c->res0 == 2);
   launch_binned_count(0, blob, offsets, n, b, g0, gr.gc, s, !res0);  // no histogram for the reservation path
   ev_mark(c, s, "hash_count0");
+  static const bool hash_only = std::getenv("S3IMPH_HASH_ONLY") != nullptr;  // TEMPORARY probe knob
+  if (hash_only) return;
   if (res0) {
     launch_binned_scatter_res(0, b, g0, 256, s);
     ev_mark(c, s, "scatter0");
@@ -1283,6 +1285,90 @@ uint64_t s3imph_dist_out_cap(s3imph_ctx* c, uint64_t n_global) {
 }
 
 const char* s3imph_ctx_last_error(s3imph_ctx* c) { return c ? c->last_msg.c_str() : ""; }
+
+int s3imph_ctx_load_mph_bin(s3imph_ctx* c, const uint8_t* mph_bin, uint64_t len) {
+  if (!c || (len && !mph_bin)) return S3IMPH_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  try {
+    HIPCHECK(hipSetDevice(c->device));
+    c->have_build = false;
+    c->rank_valid = false;
+    c->last_msg.clear();
+    LevelState h{};
+    std::vector<uint64_t> words;  // concatenated level words
+    uint64_t keys = 0;
+    if (len) {
+      // MarshalBinary framing (restated): [u64 partitions][u64 levels]
+      // then per level [u64 words][words x u64], little endian; nothing may follow
+      static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "mph.bin words are little-endian");
+      uint64_t at = 0;
+      auto get = [&](uint64_t* v) {
+        if (len - at < 8) return false;
+        std::memcpy(v, mph_bin + at, 8);
+        at += 8;
+        return true;
+      };
+      uint64_t parts = 0, nl = 0;
+      if (!get(&parts) || parts != kPartitions || !get(&nl) || nl == 0 || nl > (uint64_t)kMaxLevels) {
+        c->last_msg = "open MPHF: unmarshal: bad header";
+        return S3IMPH_ERR_FORMAT;
+      }
+      for (uint64_t L = 0; L < nl; ++L) {
+        uint64_t w = 0;
+        if (!get(&w) || w > (len - at) / 8) {
+          c->last_msg = "open MPHF: unmarshal: truncated level " + std::to_string(L);
+          return S3IMPH_ERR_FORMAT;
+        }
+        h.words[L] = w;
+        h.woff[L] = words.size();
+        h.magic[L] = level_magic(w);
+        const size_t o = words.size();
+        words.resize(o + w);
+        std::memcpy(words.data() + o, mph_bin + at, 8 * w);
+        at += 8 * w;
+        for (uint64_t q = 0; q < w; ++q) keys += (uint64_t)__builtin_popcountll(words[o + q]);
+      }
+      if (at != len) {
+        c->last_msg = "open MPHF: unmarshal: trailing bytes";
+        return S3IMPH_ERR_FORMAT;
+      }
+      h.nlevels = (unsigned)nl;
+      h.woff[nl] = words.size();
+      h.rank_total = keys;
+      h.out_cap = keys;
+    }
+    const uint64_t need = std::max<uint64_t>(words.size(), 1);
+    if (need > c->cap_words || !c->bits) {
+      dalloc(c->bits, need);
+      dalloc(c->rank_base, 2 * need);
+      c->cap_blocks = (need + 2047) / 2048 + 1;
+      dalloc(c->block_sums, c->cap_blocks);
+      c->cap_words = need;
+    }
+    if (!c->d_st) dalloc(c->d_st, 1);
+    if (!c->h_st) {
+      void* hp = nullptr;
+      HIPCHECK(hipHostMalloc(&hp, sizeof(LevelState), hipHostMallocDefault));
+      c->h_st = static_cast<LevelState*>(hp);
+    }
+    *c->h_st = h;
+    HIPCHECK(hipMemcpy(c->d_st, c->h_st, sizeof(LevelState), hipMemcpyHostToDevice));
+    if (!words.empty()) HIPCHECK(hipMemcpy(c->bits, words.data(), 8 * words.size(), hipMemcpyHostToDevice));
+    c->info = s3imph_build_info{};
+    c->info.num_levels = h.nlevels;
+    c->info.total_words = words.size();
+    c->info.mph_bin_len = len;
+    c->info.n_keys = keys;
+    c->last_n = keys;
+    c->have_build = true;
+    return S3IMPH_OK;
+  } catch (const Fail& f) {
+    c->last_msg = f.msg;
+    return f.code;
+  } catch (const std::bad_alloc&) {
+    return S3IMPH_ERR_NOMEM;
+  }
+}
 
 int s3imph_lookup_device(s3imph_ctx* c, const uint8_t* d_blob, const uint64_t* d_offsets, uint64_t n,
                          const uint64_t* d_fp, const uint64_t* d_pos, uint64_t count, uint64_t* d_result,

@@ -12,6 +12,13 @@ namespace s3imph {
 
 static __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
+// A wave-uniform 64-bit value moved to scalar registers.
+static __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
 static __device__ __forceinline__ uint64_t lanemask_lt() {
   return (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
 }
@@ -40,18 +47,86 @@ static __device__ __forceinline__ uint64_t bb_index_mk(uint64_t seed, uint64_t m
   return (r << 6) | (h & 63);
 }
 
-static __device__ __forceinline__ void fnv_step(uint64_t& a, uint64_t& b, uint32_t byte) {
-  a = (a ^ byte) * kFnvPrime;  // FNV-1a (hashBytes)
-  b = (b * kFnvPrime) ^ byte;  // FNV-1  (computeFingerprintBytes)
+// ---- FNV-64 multiply by the prime P = 2^40 + 435, on 32-bit halves -----------------
+// x * P mod 2^64 with x = lo + 2^32 hi:
+//   lo' = lo * 435 (low word),  hi' = mulhi(lo, 435) + hi * 435 + (lo << 8)   (mod 2^32).
+// hi * 435 mod 2^32 = hi[23:0] * 435 + ((hi[31:24] * 179) mod 256) << 24  (435 mod 256 = 179):
+// two full-rate 24-bit multiplies (the second one SDWA-selects hi's top byte and writes its
+// low byte to bits 31:24), instead of a quarter-rate v_mul_lo_u32; the (lo << 8) term folds
+// in with v_lshl_add_u32 and the sum rides into v_mad_u64_u32 as its addend's high word.
+// Per byte and hash: 1 quarter-rate + 4 full-rate VALU ops (was 2 + 3).
+constexpr uint32_t kFnvPLow = 435u;
+static_assert(kFnvPrime == (1ull << 40) + kFnvPLow, "fnv_mulP decomposes the FNV-64 prime as 2^40 + 435");
+static __device__ __forceinline__ void fnv_mulP(uint32_t& lo, uint32_t& hi) {
+  const uint32_t c179 = 179u;
+  uint32_t t, u;
+  asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+      : "=v"(t)
+      : "v"(hi), "v"(c179));
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(u) : "v"(hi), "s"(kFnvPLow), "v"(t));
+  const uint32_t x = (lo << 8) + u;
+  uint64_t r, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(lo), "s"(kFnvPLow), "v"((uint64_t)x << 32));
+  lo = (uint32_t)r;
+  hi = (uint32_t)(r >> 32);
 }
 
-// FNV-1a and FNV-1 of blob[b0, b1) in one pass.  The key's bytes are funnel-shifted
-// out of the aligned 8-byte words that overlap it, so every full 8-byte group runs the
-// same unrolled 8-step body whatever the key's alignment; only the last 0-7 bytes run
-// predicated steps.  Reads stay inside the aligned words overlapping [b0, b1).
+// x ^ byte K of w (SDWA byte select: no separate extract)
+#define S3IMPH_XOR_BYTE(K)                                                                                   \
+  static __device__ __forceinline__ uint32_t xor_byte##K(uint32_t x, uint32_t w) {                           \
+    uint32_t r;                                                                                              \
+    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_" #K     \
+        : "=v"(r)                                                                                            \
+        : "v"(x), "v"(w));                                                                                   \
+    return r;                                                                                                \
+  }
+S3IMPH_XOR_BYTE(0)
+S3IMPH_XOR_BYTE(1)
+S3IMPH_XOR_BYTE(2)
+S3IMPH_XOR_BYTE(3)
+#undef S3IMPH_XOR_BYTE
+
+template <int K>
+static __device__ __forceinline__ uint32_t xor_byte(uint32_t x, uint32_t w) {
+  if (K == 0) return xor_byte0(x, w);
+  if (K == 1) return xor_byte1(x, w);
+  if (K == 2) return xor_byte2(x, w);
+  return xor_byte3(x, w);
+}
+
+// One FNV-1a step and one FNV-1 step on byte K of w (K = 0..3)
+template <int K>
+static __device__ __forceinline__ void fnv_step_w(uint32_t& alo, uint32_t& ahi, uint32_t& blo, uint32_t& bhi,
+                                                  uint32_t w) {
+  alo = xor_byte<K>(alo, w);  // FNV-1a (hashBytes): h ^= b; h *= P
+  fnv_mulP(alo, ahi);
+  fnv_mulP(blo, bhi);         // FNV-1 (computeFingerprintBytes): h *= P; h ^= b
+  blo = xor_byte<K>(blo, w);
+}
+
+static __device__ __forceinline__ void fnv_step(uint64_t& a, uint64_t& b, uint32_t byte) {
+  uint32_t alo = (uint32_t)a ^ byte, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
+  fnv_mulP(alo, ahi);
+  fnv_mulP(blo, bhi);
+  blo ^= byte;
+  a = (uint64_t)alo | ((uint64_t)ahi << 32);
+  b = (uint64_t)blo | ((uint64_t)bhi << 32);
+}
+
+// FNV-1a and FNV-1 over the 8 bytes of v, little-endian order.
 static __device__ __forceinline__ void fnv_8(uint64_t& a, uint64_t& b, uint64_t v) {
-#pragma unroll
-  for (int t = 0; t < 8; ++t) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
+  uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
+  const uint32_t w0 = (uint32_t)v, w1 = (uint32_t)(v >> 32);
+  fnv_step_w<0>(alo, ahi, blo, bhi, w0);
+  fnv_step_w<1>(alo, ahi, blo, bhi, w0);
+  fnv_step_w<2>(alo, ahi, blo, bhi, w0);
+  fnv_step_w<3>(alo, ahi, blo, bhi, w0);
+  fnv_step_w<0>(alo, ahi, blo, bhi, w1);
+  fnv_step_w<1>(alo, ahi, blo, bhi, w1);
+  fnv_step_w<2>(alo, ahi, blo, bhi, w1);
+  fnv_step_w<3>(alo, ahi, blo, bhi, w1);
+  a = (uint64_t)alo | ((uint64_t)ahi << 32);
+  b = (uint64_t)blo | ((uint64_t)bhi << 32);
 }
 
 // FNV-1a + FNV-1 over a key whose bytes start `sh` bits into aligned word w[0] and
@@ -80,6 +155,19 @@ static __device__ __forceinline__ void fnv_words(const uint64_t* w, uint64_t nw,
   }
   ha = a;
   hb = b;
+}
+
+// Bytes [s, s + 8) of the 16-byte little-endian concatenation lo:hi (s in 0..7), from
+// 32-bit byte funnels (v_alignbyte_b32): the key stream word of a key that starts s bytes
+// into aligned word `lo`.
+static __device__ __forceinline__ uint64_t funnel_bytes(uint64_t lo, uint64_t hi, unsigned s) {
+  const uint32_t c0 = (uint32_t)lo, c1 = (uint32_t)(lo >> 32), n0 = (uint32_t)hi, n1 = (uint32_t)(hi >> 32);
+  const bool up = s >= 4;
+  const uint32_t x0 = up ? c1 : c0, x1 = up ? n0 : c1, x2 = up ? n1 : n0;
+  const unsigned sb = s & 3u;
+  const uint32_t r0 = __builtin_amdgcn_alignbyte(x1, x0, sb);
+  const uint32_t r1 = __builtin_amdgcn_alignbyte(x2, x1, sb);
+  return (uint64_t)r0 | ((uint64_t)r1 << 32);
 }
 
 // FNV-1a + FNV-1 of blob[b0, b1), one dependent load per aligned word (funnel shifts).

@@ -59,7 +59,7 @@ EXPORTS = (
     "s3imph_ctx_mph_bin", "s3imph_ctx_set_profiling", "s3imph_ctx_stage_times",
     "s3imph_dist_unique_id", "s3imph_ctx_create_dist", "s3imph_ctx_create_dist_host", "s3imph_build_device_dist",
     "s3imph_dist_segments", "s3imph_dist_out_cap", "s3imph_ctx_last_error",
-    "s3imph_lookup_device", "s3imph_gen_keys",
+    "s3imph_ctx_load_mph_bin", "s3imph_lookup_device", "s3imph_gen_keys",
 )
 
 
@@ -131,6 +131,7 @@ def _load():
         "s3imph_dist_segments": (i32, [vp, P(u64), u64, P(u64)]),
         "s3imph_dist_out_cap": (u64, [vp, u64]),
         "s3imph_ctx_last_error": (cp, [vp]),
+        "s3imph_ctx_load_mph_bin": (i32, [vp, vp, u64]),
         "s3imph_lookup_device": (i32, [vp, vp, vp, u64, vp, vp, u64, vp, vp]),
         "s3imph_gen_keys": (i32, [i32, u64, ctypes.c_uint32, u64, u64, vp, vp, P(u64)]),
     }
@@ -344,6 +345,12 @@ class DeviceBuilder:
         _check(LIB.s3imph_ctx_mph_bin(self._h, buf, ln.value, ctypes.byref(ln)), None, "marshal MPHF")
         return buf.raw[: ln.value]
 
+    def load_mph_bin(self, mph: bytes) -> None:
+        """OpenMPHF (mphf.go:186-247): this context's lookups now answer against `mph`."""
+        rc = LIB.s3imph_ctx_load_mph_bin(self._h, mph if mph else None, len(mph))
+        if rc != OK:
+            raise MPHFError(rc, f"open MPHF: {self.last_error() or status_string(rc)}")
+
     def lookup(self, d_blob, d_offsets, n: int, d_fp, d_pos, count: int, d_result, stream=None) -> None:
         _check(LIB.s3imph_lookup_device(self._h, _dev_ptr(d_blob), _dev_ptr(d_offsets), n, _dev_ptr(d_fp),
                                         _dev_ptr(d_pos), count, _dev_ptr(d_result), _stream_ptr(stream)),
@@ -359,6 +366,83 @@ class DeviceBuilder:
             self.close()
         except Exception:
             pass
+
+
+S3ID_MAGIC = 0x53334944  # pkg/format/format.go:6-45
+S3ID_VERSION = 1
+S3ID_HEADER = 20
+
+
+def read_u64_array(path: str) -> np.ndarray:
+    """OpenArray (pkg/format/reader.go:81-119) for width-8 arrays: S3ID header checked,
+    payload returned as little-endian u64 (memory-mapped)."""
+    raw = np.memmap(path, dtype=np.uint8, mode="r")
+    if len(raw) < S3ID_HEADER:
+        raise MPHFError(ERR_FORMAT, f"open array {path}: file too small")
+    hdr = bytes(raw[:S3ID_HEADER])
+    magic, version = int.from_bytes(hdr[0:4], "little"), int.from_bytes(hdr[4:8], "little")
+    count, width = int.from_bytes(hdr[8:16], "little"), int.from_bytes(hdr[16:20], "little")
+    if magic != S3ID_MAGIC or version != S3ID_VERSION or width != 8 or len(raw) != S3ID_HEADER + 8 * count:
+        raise MPHFError(ERR_FORMAT, f"open array {path}: bad header")
+    return raw[S3ID_HEADER:].view("<u8")
+
+
+class MPHF:
+    """format.MPHF on the GPU (OpenMPHF / Lookup / VerifyMPHF, pkg/format/mphf.go:186-302,
+    :372-393): mph.bin loaded into a device context, mph_fp / mph_pos in HBM, batched
+    Lookup; prefix_blob.bin / prefix_offsets.u64 (when present) for VerifyMPHF."""
+
+    def __init__(self, out_dir: str, device: int = 0):
+        import torch
+        mph = open(os.path.join(out_dir, "mph.bin"), "rb").read()
+        self.ctx = DeviceBuilder(device)
+        self.count = 0
+        self.dev = f"cuda:{device}"
+        self.blob = self.offsets = None
+        if mph:
+            fp = read_u64_array(os.path.join(out_dir, "mph_fp.u64"))
+            pos = read_u64_array(os.path.join(out_dir, "mph_pos.u64"))
+            if len(fp) != len(pos):
+                raise MPHFError(ERR_FORMAT, "open MPHF: fingerprint and position arrays differ in length")
+            self.count = len(fp)
+            self.d_fp = torch.from_numpy(np.ascontiguousarray(fp).view(np.int64)).to(self.dev)
+            self.d_pos = torch.from_numpy(np.ascontiguousarray(pos).view(np.int64)).to(self.dev)
+        else:
+            self.d_fp = self.d_pos = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.ctx.load_mph_bin(mph)
+        bp, op = os.path.join(out_dir, "prefix_blob.bin"), os.path.join(out_dir, "prefix_offsets.u64")
+        if os.path.exists(bp):
+            self.offsets = np.ascontiguousarray(read_u64_array(op))
+            self.blob = np.fromfile(bp, dtype=np.uint8)
+
+    def lookup(self, keys) -> np.ndarray:
+        """Lookup (mphf.go:275-302) of a batch: pos per key, or 2^64-1 when not found."""
+        blob, offs = keys_to_blob(keys)
+        return self.lookup_blob(blob, offs)
+
+    def lookup_blob(self, blob: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+        import torch
+        n = len(offsets) - 1
+        pad = np.zeros(((len(blob) + 7) // 8) * 8 + 8, np.uint8)
+        pad[:len(blob)] = blob
+        d_blob = torch.from_numpy(pad).to(self.dev)
+        d_offs = torch.from_numpy(np.ascontiguousarray(offsets, np.uint64).view(np.int64)).to(self.dev)
+        res = torch.empty(max(n, 1), dtype=torch.int64, device=self.dev)
+        self.ctx.lookup(d_blob, d_offs, n, self.d_fp, self.d_pos, self.count, res)
+        return res[:n].cpu().numpy().view(np.uint64)
+
+    def verify(self) -> None:
+        """VerifyMPHF (mphf.go:372-393): every prefix i of the blob looks up to i."""
+        if self.offsets is None:
+            raise MPHFError(ERR_STATE, "prefix blob not loaded")
+        got = self.lookup_blob(self.blob, self.offsets)
+        bad = np.nonzero(got != np.arange(len(got), dtype=np.uint64))[0]
+        if len(bad):
+            i = int(bad[0])
+            raise MPHFError(ERR_INTERNAL, f"lookup returned wrong pos for prefix {i}: got {int(got[i])}, want {i}")
+
+    def close(self) -> None:
+        self.ctx.close()
 
 
 def dist_unique_id() -> bytes:

@@ -142,3 +142,15 @@ def test_builder_add_batch_empty_null_pointers(tmp_path):
     assert b.count() == 0
     assert s3imph.LIB.s3imph_builder_add_batch(b._h, None, None, None, 3, err, 64) == s3imph.ERR_INVALID
     b.close()
+
+
+def test_read_u64_array_checks_the_s3id_header(tmp_path):
+    """OpenArray (reader.go:81-119) restated in the binding: header checked, payload LE u64."""
+    p = tmp_path / "a.u64"
+    p.write_bytes(O.s3id_u64_array([5, 6, 2**64 - 1]))
+    assert list(s3imph.read_u64_array(str(p))) == [5, 6, 2**64 - 1]
+    for bad in (O.s3id_header(3, 4) + b"\0" * 12, O.s3id_header(4) + b"\0" * 24, b"\0" * 28):
+        p.write_bytes(bad)
+        with pytest.raises(s3imph.MPHFError) as e:
+            s3imph.read_u64_array(str(p))
+        assert e.value.status == s3imph.ERR_FORMAT

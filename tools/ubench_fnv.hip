@@ -6,12 +6,22 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include "../s3-inv-db_amd/csrc/s3imph_device.h"  // fnv_8: the product's byte step (mode 3)
+
 constexpr uint64_t kP = 0x100000001b3ull;
 
 template <int kMode>
 __global__ __launch_bounds__(256) void k_fnv(uint64_t* out, int iters, uint64_t seed) {
   uint64_t a = seed ^ (threadIdx.x + 977ull * blockIdx.x), b = a * 3;
   uint64_t v = a * 0x9e3779b97f4a7c15ull;
+  if (kMode == 3) {  // the product's step (24-bit / SDWA multiplies, s3imph_device.h)
+    for (int it = 0; it < iters; ++it) {
+      s3imph::fnv_8(a, b, v);
+      v += 0x632be59bd9b4e019ull;
+    }
+    if ((a ^ b) == 0x1234567) out[0] = a + b;
+    return;
+  }
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
@@ -40,12 +50,13 @@ int main() {
   hipEventCreate(&e1);
   int clk = 0;
   hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, 0);
-  for (int mode = 0; mode < 3; ++mode) {
+  for (int mode = 0; mode < 4; ++mode) {
     for (int rep = 0; rep < 3; ++rep) {
       hipEventRecord(e0);
       if (mode == 0) k_fnv<0><<<blocks, 256>>>(d, iters, rep);
       else if (mode == 1) k_fnv<1><<<blocks, 256>>>(d, iters, rep);
-      else k_fnv<2><<<blocks, 256>>>(d, iters, rep);
+      else if (mode == 2) k_fnv<2><<<blocks, 256>>>(d, iters, rep);
+      else k_fnv<3><<<blocks, 256>>>(d, iters, rep);
       hipEventRecord(e1);
       hipEventSynchronize(e1);
       float ms;
