@@ -100,7 +100,21 @@ __device__ __forceinline__ bool geom_ok(LevelState* st, uint64_t T, uint64_t B) 
 
 __device__ __forceinline__ bool level_active(int level, const LevelState* st) {
   return (st->preset[level] || level == 0 || st->n[level] > kGate) &&
-         !(st->status & (kStGeometry | kStOverflow | kStLookback));
+         !(st->status & kStStop);
+}
+
+// A whole level that placed no key: its keys all collide again at every level (only
+// duplicate key hashes do that at these sizes), so the build stops here instead of
+// running out the level budget; the host then looks for duplicates among the n[level]
+// records left in the level's input list.  (Sharded levels, preset, count this rank's
+// share only and are not judged.)
+__device__ __forceinline__ bool no_progress(LevelState* st, int level, uint64_t n) {
+  if (level < 1 || st->preset[level] || st->preset[level - 1] || n == 0 || n != st->n[level - 1]) return false;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->stop_level = level;
+    atomicOr(&st->status, kStTooManyLevels);
+  }
+  return true;
 }
 
 // ---------------------------------------------------------------- level 0 count ----
@@ -263,7 +277,9 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256) void k_hash0_lds(const ui
                                                   uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
                                                   unsigned long long* __restrict__ flags,
                                                   unsigned long long* __restrict__ sflags, LevelState* st,
-                                                  unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
+                                                  unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt,
+                                                  unsigned long long* __restrict__ prof = nullptr) {
+  unsigned long long pt0 = __builtin_amdgcn_s_memtime(), ph = 0, pw = 0, pm = 0;  // debug phase clock
   constexpr int KW = (BB / 16 + NT - 1) / NT;  // 16-byte window chunks per thread
   constexpr unsigned kLB = 256;                // length classes of the sort
   __shared__ uint64_t sw[BB / 8 + 2];          // the round's window (+ 16 B: a lane may read one word past)
@@ -383,6 +399,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256) void k_hash0_lds(const ui
     const bool more = g < gend;
     if (PF && more) prefetch(g);
     // ---- hash: lane -> the key in its sorted slot, aligned LDS words, byte funnel
+    unsigned long long pta = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (tid < m) {
       uint64_t a = kFnvOffset, b = kFnvOffset, j;
       if (alone) {
@@ -412,7 +429,206 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256) void k_hash0_lds(const ui
       fp[r0 + j] = b;
       zero |= (a == 0);
     }
+    unsigned long long ptb = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (!more) break;
+    __syncthreads();  // every lane is done with sw / sidx before the next round overwrites them
+    if (prof) {
+      const unsigned long long ptc = __builtin_amdgcn_s_memtime();
+      ph += ptb - pta;
+      pw += ptc - ptb;
+      pm += pta - pt0 - (ph - (ptb - pta)) - (pw - (ptc - ptb)) - pm;  // everything else this round
+    }
+  }
+  if (prof && lane_id() == 0) {
+    const unsigned long long tot = __builtin_amdgcn_s_memtime() - pt0;
+    unsigned long long* q = prof + ((uint64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6)) * 4;
+    q[0] = tot;
+    q[1] = ph;
+    q[2] = pw;
+    q[3] = tot - ph - pw;
+  }
+  if (zero) atomicOr(&st->status, kStKeyZero);
+}
+
+// Level-0 hash, LDS-staged rounds of 2 NT keys, two keys per lane: a round's keys are
+// counting-sorted by length and lane t hashes sorted slot t (the shorter half) then slot
+// 2NT - 1 - t (the longer half), so every lane — and so every wave — carries about twice
+// the mean key length: no wave of a round waits behind another at the round's barrier,
+// and within a wave the keys of each half have nearly one length.  Otherwise as
+// k_hash0_lds: coalesced 16-byte window loads staged in LDS, aligned LDS words funnelled
+// per lane, keys past the window budget wait for the next round.
+template <int NT, int BB>
+__global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(const uint8_t* __restrict__ blob,
+                                                  const uint64_t* __restrict__ offsets, uint64_t n,
+                                                  uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
+                                                  unsigned long long* __restrict__ flags,
+                                                  unsigned long long* __restrict__ sflags, LevelState* st,
+                                                  unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
+  constexpr int G = 2 * NT;                    // keys per round
+  constexpr int KW = (BB / 16 + NT - 1) / NT;  // 16-byte window chunks per thread
+  constexpr unsigned kLB = 256;                // length classes of the sort
+  constexpr int NW = NT / 64;
+  __shared__ uint64_t sw[BB / 8 + 2];          // the round's window (+ 16 B: a lane may read one word past)
+  __shared__ unsigned soff[G], slen[G];        // sorted slot -> key's window offset, length
+  __shared__ unsigned short sidx[G];           // sorted slot -> key index in the round
+  __shared__ unsigned lcnt[kLB];
+  __shared__ unsigned s_cnt[NW];
+  if (st->skew) return;  // k_hash_count0 hashes skewed sets (and clears the tile state)
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  {
+    const uint64_t T = ntiles_of(st->words[0], tb), B = (n + chunk - 1) / chunk;
+    const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
+    const uint64_t g0 = (uint64_t)blockIdx.x * NT + tid, gs = (uint64_t)gridDim.x * NT;
+    if (blockIdx.x == 0 && tid == 0) {
+      st->ntiles[0] = T;
+      st->nchunks[0] = B;
+    }
+    for (uint64_t t = g0; t < T; t += gs) flags[t] = 0;
+    for (uint64_t q = g0; q < nseg; q += gs) sflags[q] = 0;
+    for (uint64_t q = g0; q < kTcntWords; q += gs) tcnt[q] = 0;
+  }
+  const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+  uint64_t g = (uint64_t)blockIdx.x * per;
+  const uint64_t gend = min(n, g + per);
+  if (g >= gend) return;
+  const uint64_t end8 = (offsets[n] + 7) & ~7ull;
+  bool zero = false;
+  for (;;) {
+    // ---- the round's keys g + tid and g + NT + tid, and its window [wlo, wend)
+    const uint64_t last = min(gend, g + G);
+    uint64_t kb0[2], kb1[2];
+    bool kin[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t i = g + tid + (unsigned)h * NT;
+      kin[h] = i < last;
+      kb0[h] = kin[h] ? offsets[i] : 0;
+      kb1[h] = kin[h] ? offsets[i + 1] : 0;
+    }
+    const uint64_t wlo = uniform64(offsets[g] & ~15ull);
+    const uint64_t wend = uniform64(min((offsets[last] + 15) & ~15ull, wlo + (uint64_t)BB));
+    {
+      uint4 wr[KW];
+#pragma unroll
+      for (int k = 0; k < KW; ++k) {
+        const uint64_t a = wlo + 16ull * (tid + (unsigned)k * NT);
+        wr[k] = make_uint4(0, 0, 0, 0);
+        if (a < wend) {
+          if (a + 16 <= end8) {
+            wr[k] = *reinterpret_cast<const uint4*>(blob + a);
+          } else {  // the blob's last 8 readable bytes
+            const uint2 hh = *reinterpret_cast<const uint2*>(blob + a);
+            wr[k].x = hh.x;
+            wr[k].y = hh.y;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < KW; ++k) {
+        const unsigned c = tid + (unsigned)k * NT;
+        if (wlo + 16ull * c < wend) {
+          sw[2 * c] = (uint64_t)wr[k].x | ((uint64_t)wr[k].y << 32);
+          sw[2 * c + 1] = (uint64_t)wr[k].z | ((uint64_t)wr[k].w << 32);
+        }
+      }
+    }
+    for (unsigned b = tid; b < kLB; b += NT) lcnt[b] = 0;
+    // keys whose bytes all lie in the window: a prefix of the round (offsets ascend)
+    bool fits[2];
+    unsigned mine = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      fits[h] = kin[h] && kb1[h] - wlo <= (uint64_t)BB;
+      const uint64_t fb = __ballot(fits[h]);
+      mine += (unsigned)__popcll(fb);
+    }
+    if (lane == 0) s_cnt[wave] = mine;
+    __syncthreads();
+    unsigned m = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) m += s_cnt[w];
+    const bool alone = m == 0;  // the round's first key is longer than the window
+    if (alone) m = 1;
+    // ---- counting sort of the round's keys by length
+    unsigned cls[2] = {0, 0}, rk[2] = {0, 0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (fits[h]) {
+        cls[h] = (unsigned)min<uint64_t>(kb1[h] - kb0[h], kLB - 1);
+        rk[h] = atomicAdd(&lcnt[cls[h]], 1u);
+      }
+    __syncthreads();
+    if (tid < 64) {
+      unsigned v[kLB / 64], sum = 0;
+#pragma unroll
+      for (int q = 0; q < (int)(kLB / 64); ++q) {
+        v[q] = lcnt[tid * (kLB / 64) + q];
+        sum += v[q];
+      }
+      unsigned x = sum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned y = __shfl_up(x, d);
+        if (tid >= (unsigned)d) x += y;
+      }
+      unsigned ex = x - sum;
+#pragma unroll
+      for (int q = 0; q < (int)(kLB / 64); ++q) {
+        lcnt[tid * (kLB / 64) + q] = ex;
+        ex += v[q];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (fits[h]) {
+        const unsigned slot = lcnt[cls[h]] + rk[h];
+        sidx[slot] = (unsigned short)(tid + (unsigned)h * NT);
+        soff[slot] = (unsigned)(kb0[h] - wlo);
+        slen[slot] = (unsigned)(kb1[h] - kb0[h]);
+      }
+    __syncthreads();
+    // ---- hash: slot tid (shorter half), then slot m - 1 - tid (longer half)
+    if (alone) {
+      if (tid == 0) {
+        uint64_t a, b;
+        fnv_both_pf(blob, kb0[0], kb1[0], a, b);
+        kh[g] = a;
+        fp[g] = b;
+        zero |= (a == 0);
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const unsigned slot = h == 0 ? tid : m - 1 - tid;
+        if (h == 0 ? tid < (m + 1) / 2 : tid < m / 2) {
+          uint64_t a = kFnvOffset, b = kFnvOffset;
+          const unsigned j = sidx[slot];
+          const unsigned o = soff[slot], len = slen[slot];
+          const uint64_t* w = sw + (o >> 3);
+          const unsigned s = o & 7u;
+          const unsigned nfull = len >> 3;
+          uint64_t cur = w[0];
+          for (unsigned q = 0; q < nfull; ++q) {
+            const uint64_t nxt = w[q + 1];
+            fnv_8(a, b, funnel_bytes(cur, nxt, s));
+            cur = nxt;
+          }
+          const unsigned rem = len & 7u;
+          if (rem) {
+            const uint64_t v = funnel_bytes(cur, w[nfull + 1], s);
+#pragma unroll
+            for (unsigned t = 0; t < 7; ++t)
+              if (t < rem) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
+          }
+          kh[g + j] = a;
+          fp[g + j] = b;
+          zero |= (a == 0);
+        }
+      }
+    }
+    g += m;
+    if (g >= gend) break;
     __syncthreads();  // every lane is done with sw / sidx before the next round overwrites them
   }
   if (zero) atomicOr(&st->status, kStKeyZero);
@@ -636,7 +852,7 @@ __global__ __launch_bounds__(NT) void k_hash0_dma(const uint8_t* __restrict__ bl
 __device__ void level_setup(int level, LevelState* st) {
   const int p = level - 1;
   if (p > 0 && !st->preset[p] && st->n[p] <= kGate) return;
-  if (st->status & (kStGeometry | kStOverflow | kStLookback)) return;
+  if (st->status & kStStop) return;
   const uint64_t n = st->n[level];
   const uint64_t w = n ? level_words(n) : 0;
   st->words[level] = w;
@@ -656,7 +872,7 @@ __global__ __launch_bounds__(kCB) void k_count(int level, const Rec* __restrict_
   const int p = level - 1;
   const bool preset = st->preset[level] != 0;
   if (!preset && p > 0 && !st->preset[p] && st->n[p] <= kGate) return;  // previous level ran in the tail
-  if (st->status & (kStGeometry | kStOverflow | kStLookback)) return;
+  if (st->status & kStStop) return;
   const uint64_t n = st->n[level];
   uint64_t words, magic, woff;
   if (preset) {  // sized by the multi-GPU build: global words, this rank's records
@@ -675,6 +891,7 @@ __global__ __launch_bounds__(kCB) void k_count(int level, const Rec* __restrict_
       st->nlevels = level;
     }
     if (n <= kGate) return;
+    if (no_progress(st, level, n)) return;
   }
   const LevelRange rg = level_range(st, level, words);
   const uint64_t T = ntiles_of(rg.rw, tb), B = (n + chunk - 1) / chunk;
@@ -863,7 +1080,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   const int p = level - 1;
   const bool preset = st->preset[level] != 0;
   if (!preset && p > 0 && !st->preset[p] && st->n[p] <= kGate) return;  // previous level ran in the tail
-  if (st->status & (kStGeometry | kStOverflow | kStLookback)) return;
+  if (st->status & kStStop) return;
   // [i_lo, i_hi): one chunk of level 0's key-order arrays (pipelined level 0); else all
   const uint64_t n = i_hi ? min<uint64_t>(st->n[level], i_hi) : st->n[level];
   const unsigned tid = threadIdx.x;
@@ -884,6 +1101,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
       st->nlevels = level;
     }
     if (n <= kGate) return;
+    if (no_progress(st, level, n)) return;
   }
   const LevelRange rg = level_range(st, level, words);
   const uint64_t T = ntiles_of(rg.rw, tb);
@@ -1749,7 +1967,7 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
     while (L <= big_launched && st->n[L] > kGate) ++L;
     s_level = L;
     s_n = st->n[L];
-    if (st->status & (kStGeometry | kStOverflow | kStLookback)) s_n = 0;
+    if (st->status & kStStop) s_n = 0;
     if (s_n > kTailKeys) {
       atomicOr(&st->status, kStTailOverflow);
       s_n = 0;
@@ -1794,7 +2012,10 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
     if (L >= kMaxLevels) {
       // level budget exhausted: leave the unplaced keys in level L's list, where the host
       // looks for duplicates (as mix64(key hash): a bijection, so duplicates are preserved)
-      if (tid == 0) atomicOr(&st->status, kStTooManyLevels);
+      if (tid == 0) {
+        st->stop_level = L;
+        atomicOr(&st->status, kStTooManyLevels);
+      }
       Rec* out = (L & 1) ? list0 : list1;
       for (unsigned i = tid; i < n; i += kTailT) out[i] = Rec{ck[i], 0, 0};
       break;
@@ -1880,6 +2101,22 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
       __syncthreads();
     }
     if (level_out_on(st, L)) out_end = rb0 + tot;
+    if (tot == 0) {
+      // No key placed: these keys collide again at every level (duplicate hashes); stop and
+      // leave them, as mix64(key hash) (a bijection: duplicates stay duplicates), where the
+      // host looks: list[(stop_level - 1) & 1]
+      Rec* out = (L & 1) ? list1 : list0;
+      for (unsigned i = tid; i < n; i += kTailT) out[i] = Rec{ck[i], 0, 0};
+      if (tid == 0) {
+        st->n[L + 1] = n;
+        st->stop_level = L + 1;
+        atomicOr(&st->status, kStTooManyLevels);
+        s_level = L + 1;
+        s_n = 0;
+      }
+      __syncthreads();
+      break;
+    }
     if (tid == 0) {
       const uint64_t w1 = n1 ? level_words(n1) : 0;
       st->n[L + 1] = n1;
@@ -1915,7 +2152,10 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
         if (n == 0) break;
         const bool act = lane < n;
         if (L >= kMaxLevels) {  // as in the block path
-          if (lane == 0) atomicOr(&st->status, kStTooManyLevels);
+          if (lane == 0) {
+            st->stop_level = L;
+            atomicOr(&st->status, kStTooManyLevels);
+          }
           Rec* out = (L & 1) ? list0 : list1;
           if (act) out[lane] = Rec{ck[lane], 0, 0};
           break;
@@ -1956,6 +2196,26 @@ __global__ __launch_bounds__(kTailT) void k_bin_tail(int first_level, int big_la
         if (settled) srank[rb0 + pre + __popc(vx & (bit - 1))] = j;
         const uint64_t cm = __ballot(act && !settled);
         const unsigned n1 = (unsigned)__popcll(cm);
+        if (n1 == n) {
+          // No key placed.  Stop only if every key has a twin (duplicate hashes never
+          // resolve); distinct keys this few can all collide by chance, and go on.
+          bool twin = false;
+          for (unsigned q = 0; q < n; ++q) {
+            const uint64_t kq = __shfl(k, (int)q);
+            twin |= act && q != lane && kq == k;
+          }
+          if (__ballot(act && !twin) == 0) {
+            Rec* out = (L & 1) ? list1 : list0;  // list[(stop_level - 1) & 1]
+            if (act) out[lane] = Rec{k, 0, 0};
+            if (lane == 0) {
+              st->n[L + 1] = n;
+              st->stop_level = L + 1;
+              atomicOr(&st->status, kStTooManyLevels);
+            }
+            ++L;
+            break;
+          }
+        }
         wave_lds_sync();
         if (act && !settled) {
           const unsigned d = (unsigned)__popcll(cm & lanemask_lt());
@@ -2043,8 +2303,9 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       // near-uniform lengths: LDS-staged, length-sorted rounds; skewed sets (decided on the
       // device from sampled lengths) fall through to k_hash_count0's length-sorted groups
       if (h0 == 1)
-        k_hash0_lds<kH0T, kH0B, false><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
-                                                               g.tb, g.chunk, b.tcnt);
+        k_hash0_lds<kH0T, kH0B, false><<<kH0Grid, kH0T, 0, s>>>(
+            blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt,
+            b.tile_prof ? b.tile_prof + (uint64_t)(kMaxLevels - 2) * kMaxTiles * 8 : nullptr);
       else if (h0 == 2)
         k_hash0_lds<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
                                                               g.tb, g.chunk, b.tcnt);
@@ -2054,6 +2315,12 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       else if (h0 == 8)  // debug: no window loads (sort + hash + stores)
         k_hash0_lds<kH0T, kH0B, false, 2><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags,
                                                                   b.st, g.tb, g.chunk, b.tcnt);
+      else if (h0 == 9)
+        k_hash0_pair<512, 64 << 10><<<512, 512, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb,
+                                                         g.chunk, b.tcnt);
+      else if (h0 == 10)
+        k_hash0_pair<256, 32 << 10><<<1024, 256, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb,
+                                                          g.chunk, b.tcnt);
       else if (h0 == 5)
         k_hash0_dma<1024, 64 << 10><<<256, 1024, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb,
                                                           g.chunk, b.tcnt);

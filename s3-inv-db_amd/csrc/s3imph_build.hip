@@ -176,9 +176,28 @@ bool has_duplicates(const uint64_t* d_keys, uint64_t n) {
   return std::adjacent_find(h.begin(), h.end()) != h.end();
 }
 
+bool records_have_duplicates(const Rec* d_list, uint64_t n) {
+  std::vector<Rec> h(n);
+  if (n) HIPCHECK(hipMemcpy(h.data(), d_list, n * sizeof(Rec), hipMemcpyDeviceToHost));
+  std::vector<uint64_t> k(n);
+  for (uint64_t i = 0; i < n; ++i) k[i] = h[i].k;
+  std::sort(k.begin(), k.end());
+  return std::adjacent_find(k.begin(), k.end()) != k.end();
+}
+
+// Duplicate key hashes, judged from the records the build could not place (the stop
+// level's input list) when it stopped on them, else from every key hash.
+bool stopped_on_duplicates(s3imph_ctx* c, unsigned flags, uint64_t n) {
+  const LevelState& h = *c->h_st;
+  const unsigned S = h.stop_level;
+  if ((flags & kStTooManyLevels) && S >= 1 && S < (unsigned)kMaxLevels + 2 && h.n[S])
+    return records_have_duplicates(c->list[(S - 1) & 1], h.n[S]);
+  return has_duplicates(c->kh, n);
+}
+
 int map_status(s3imph_ctx* c, unsigned flags, uint64_t n, std::string* msg) {
   if (flags & (kStTooManyLevels | kStOverflow)) {
-    if (has_duplicates(c->kh, n)) {
+    if (stopped_on_duplicates(c, flags, n)) {
       *msg = "build MPHF: duplicate FNV-1a key hashes: bbhash cannot place them";
       return S3IMPH_ERR_DUP_KEY_HASH;
     }
@@ -366,6 +385,19 @@ void print_tile_profile(s3imph_ctx* c) {
   if (!c->tile_prof) return;
   std::vector<unsigned long long> h((size_t)kMaxLevels * kMaxTiles * 8);
   HIPCHECK(hipMemcpy(h.data(), c->tile_prof, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  {  // level-0 hash waves (k_hash0_lds debug clock): total / hash / barrier wait after hash / rest
+    const unsigned long long* q = &h[(size_t)(kMaxLevels - 2) * kMaxTiles * 8];
+    double a[4] = {0, 0, 0, 0};
+    int cnt = 0;
+    for (int w = 0; w < (int)(kMaxTiles * 8 / 4); ++w) {
+      if (!q[4 * w]) continue;
+      ++cnt;
+      for (int k = 0; k < 4; ++k) a[k] += (double)q[4 * w + k];
+    }
+    if (cnt)
+      std::fprintf(stderr, "  hash0 waves %d: avg cycles %.0f, hash %.1f%%, barrier wait %.1f%%, rest %.1f%%\n", cnt,
+                   a[0] / cnt, 100 * a[1] / a[0], 100 * a[2] / a[0], 100 * a[3] / a[0]);
+  }
   static const char* names[7] = {"mark", "final", "lookbk", "rank", "output", "redoN", "redoW"};
   {
     const unsigned long long* tl = &h[(size_t)(kMaxLevels - 1) * kMaxTiles * 8];
@@ -598,14 +630,6 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
   d.cap_stage_words = stagew;
 }
 
-bool records_have_duplicates(const Rec* d_list, uint64_t n) {
-  std::vector<Rec> h(n);
-  if (n) HIPCHECK(hipMemcpy(h.data(), d_list, n * sizeof(Rec), hipMemcpyDeviceToHost));
-  std::vector<uint64_t> k(n);
-  for (uint64_t i = 0; i < n; ++i) k[i] = h[i].k;
-  std::sort(k.begin(), k.end());
-  return std::adjacent_find(k.begin(), k.end()) != k.end();
-}
 
 constexpr int kDistRetry = -1;
 
@@ -761,7 +785,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   for (int r = 0; r < P; ++r) flags |= (unsigned)lb(r, Ls + 2);
   if (flags & (kStGeometry | kStTailOverflow | kStResOverflow)) return conservative ? S3IMPH_ERR_INTERNAL : kDistRetry;
   if (flags & kStTooManyLevels) {
-    const unsigned nl = hs.nlevels;
+    const unsigned nl = hs.stop_level ? hs.stop_level : hs.nlevels;
     const uint64_t rem = nl < (unsigned)kMaxLevels + 2 ? hs.n[nl] : 0;
     if (records_have_duplicates(c->list[(nl - 1) & 1], rem)) {
       *msg = "build MPHF: duplicate FNV-1a key hashes: bbhash cannot place them";

@@ -50,65 +50,33 @@ static __device__ __forceinline__ uint64_t bb_index_mk(uint64_t seed, uint64_t m
 // ---- FNV-64 multiply by the prime P = 2^40 + 435, on 32-bit halves -----------------
 // x * P mod 2^64 with x = lo + 2^32 hi:
 //   lo' = lo * 435 (low word),  hi' = mulhi(lo, 435) + hi * 435 + (lo << 8)   (mod 2^32).
-// hi * 435 mod 2^32 = hi[23:0] * 435 + ((hi[31:24] * 179) mod 256) << 24  (435 mod 256 = 179):
-// two full-rate 24-bit multiplies (the second one SDWA-selects hi's top byte and writes its
-// low byte to bits 31:24), instead of a quarter-rate v_mul_lo_u32; the (lo << 8) term folds
-// in with v_lshl_add_u32 and the sum rides into v_mad_u64_u32 as its addend's high word.
-// Per byte and hash: 1 quarter-rate + 4 full-rate VALU ops (was 2 + 3).
+// hi * 435 + (lo << 8) is one v_mul_lo_u32 and one v_lshl_add_u32, and rides into
+// v_mad_u64_u32 (lo * 435) as its addend's high word, so the multiply costs 3 VALU ops
+// (the compiler's own lowering of a 64-bit multiply takes 5).  tools/ubench_fnv.hip
+// prices the FNV-1a + FNV-1 byte step at 36 SIMD-cycles per wave (45 compiler-lowered;
+// 40 with the top byte of hi * 435 taken by an SDWA 24-bit multiply).
 constexpr uint32_t kFnvPLow = 435u;
 static_assert(kFnvPrime == (1ull << 40) + kFnvPLow, "fnv_mulP decomposes the FNV-64 prime as 2^40 + 435");
 static __device__ __forceinline__ void fnv_mulP(uint32_t& lo, uint32_t& hi) {
-  const uint32_t c179 = 179u;
-  uint32_t t, u;
-  asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
-      : "=v"(t)
-      : "v"(hi), "v"(c179));
-  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(u) : "v"(hi), "s"(kFnvPLow), "v"(t));
-  const uint32_t x = (lo << 8) + u;
+  const uint32_t x = (lo << 8) + hi * kFnvPLow;
   uint64_t r, cc;
   asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(lo), "s"(kFnvPLow), "v"((uint64_t)x << 32));
   lo = (uint32_t)r;
   hi = (uint32_t)(r >> 32);
 }
 
-// x ^ byte K of w (SDWA byte select: no separate extract)
-#define S3IMPH_XOR_BYTE(K)                                                                                   \
-  static __device__ __forceinline__ uint32_t xor_byte##K(uint32_t x, uint32_t w) {                           \
-    uint32_t r;                                                                                              \
-    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_" #K     \
-        : "=v"(r)                                                                                            \
-        : "v"(x), "v"(w));                                                                                   \
-    return r;                                                                                                \
-  }
-S3IMPH_XOR_BYTE(0)
-S3IMPH_XOR_BYTE(1)
-S3IMPH_XOR_BYTE(2)
-S3IMPH_XOR_BYTE(3)
-#undef S3IMPH_XOR_BYTE
-
-template <int K>
-static __device__ __forceinline__ uint32_t xor_byte(uint32_t x, uint32_t w) {
-  if (K == 0) return xor_byte0(x, w);
-  if (K == 1) return xor_byte1(x, w);
-  if (K == 2) return xor_byte2(x, w);
-  return xor_byte3(x, w);
-}
-
-// One FNV-1a step and one FNV-1 step on byte K of w (K = 0..3)
-template <int K>
+// One FNV-1a step and one FNV-1 step on byte c
 static __device__ __forceinline__ void fnv_step_w(uint32_t& alo, uint32_t& ahi, uint32_t& blo, uint32_t& bhi,
-                                                  uint32_t w) {
-  alo = xor_byte<K>(alo, w);  // FNV-1a (hashBytes): h ^= b; h *= P
+                                                  uint32_t c) {
+  alo ^= c;  // FNV-1a (hashBytes): h ^= b; h *= P
   fnv_mulP(alo, ahi);
-  fnv_mulP(blo, bhi);         // FNV-1 (computeFingerprintBytes): h *= P; h ^= b
-  blo = xor_byte<K>(blo, w);
+  fnv_mulP(blo, bhi);  // FNV-1 (computeFingerprintBytes): h *= P; h ^= b
+  blo ^= c;
 }
 
 static __device__ __forceinline__ void fnv_step(uint64_t& a, uint64_t& b, uint32_t byte) {
-  uint32_t alo = (uint32_t)a ^ byte, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
-  fnv_mulP(alo, ahi);
-  fnv_mulP(blo, bhi);
-  blo ^= byte;
+  uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
+  fnv_step_w(alo, ahi, blo, bhi, byte);
   a = (uint64_t)alo | ((uint64_t)ahi << 32);
   b = (uint64_t)blo | ((uint64_t)bhi << 32);
 }
@@ -117,14 +85,8 @@ static __device__ __forceinline__ void fnv_step(uint64_t& a, uint64_t& b, uint32
 static __device__ __forceinline__ void fnv_8(uint64_t& a, uint64_t& b, uint64_t v) {
   uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
   const uint32_t w0 = (uint32_t)v, w1 = (uint32_t)(v >> 32);
-  fnv_step_w<0>(alo, ahi, blo, bhi, w0);
-  fnv_step_w<1>(alo, ahi, blo, bhi, w0);
-  fnv_step_w<2>(alo, ahi, blo, bhi, w0);
-  fnv_step_w<3>(alo, ahi, blo, bhi, w0);
-  fnv_step_w<0>(alo, ahi, blo, bhi, w1);
-  fnv_step_w<1>(alo, ahi, blo, bhi, w1);
-  fnv_step_w<2>(alo, ahi, blo, bhi, w1);
-  fnv_step_w<3>(alo, ahi, blo, bhi, w1);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) fnv_step_w(alo, ahi, blo, bhi, ((t < 4 ? w0 : w1) >> (8 * (t & 3))) & 0xffu);
   a = (uint64_t)alo | ((uint64_t)ahi << 32);
   b = (uint64_t)blo | ((uint64_t)bhi << 32);
 }

@@ -24,6 +24,8 @@ struct LevelState {
   unsigned int status;                       // kSt* flags
   unsigned int tail_first;                   // first level run by the single-workgroup tail
   unsigned int skew;                         // sampled key lengths are skewed: hash length-sorted
+  unsigned int stop_level;  // kStTooManyLevels: the level whose n[stop_level] keys could not be
+                            // placed; they are left in list[(stop_level - 1) & 1]
   // Binned pipeline (s3imph_binned.hip).
   unsigned long long lvl_base[kMaxLevels + 2];  // set bits in all levels < L (= ranks[L] - 1)
   unsigned long long ntiles[kMaxLevels + 2];    // position tiles of level L
@@ -122,6 +124,8 @@ constexpr unsigned kStTooManyLevels = 2u;  // level budget exhausted (duplicates
 constexpr unsigned kStOverflow = 4u;       // workspace capacity exceeded
 constexpr unsigned kStRank = 8u;           // a position landed outside [0, N)
 constexpr unsigned kStRouteOverflow = 256u;  // a multi-GPU send region overflowed (rerun bigger)
+// Any of these ends the level pipeline: later kernels return at once.
+constexpr unsigned kStStop = kStGeometry | kStOverflow | kStLookback | kStTooManyLevels;
 
 // Levels whose active-key count is at most this run inside one workgroup with
 // LDS-resident bit vectors (k_tail); larger levels run as full-grid kernels.

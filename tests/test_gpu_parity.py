@@ -202,6 +202,35 @@ def test_duplicate_keys_error_builder(s3, tmp_path):
     assert not (tmp_path / "mph.bin").exists()
 
 
+def test_tiny_distinct_sets_are_never_reported_as_duplicates(s3, oracle_lib, ctx):
+    """A build stops early when a level places no key, but only when every key left has a
+    twin: 3000 two-key sets (about 1 in 64 collide at a level by chance) all build, equal
+    to the oracle."""
+    for i in range(3000):
+        keys = [b"k%d/a" % i, b"k%d/bb" % i]
+        blob, offs = O.keys_to_blob(keys)
+        st, fp, po, mph = oracle_lib.build(blob, offs)
+        gfp, gpo, gmph, info = _device_build(s3, ctx, blob, offs)
+        assert gmph == mph and np.array_equal(gfp, fp) and np.array_equal(gpo, po), i
+
+
+def test_duplicates_stop_the_build_early(s3, ctx):
+    """Keys with duplicate hashes stop the build at the first level that places nothing
+    (the host then finds the twins among the records left): a 1M-key set with 500
+    duplicated keys fails with DUP_KEY_HASH, in about the time of a build."""
+    import time
+    n = 1_000_000
+    blob, offs = s3.gen_keys(0, 21, 32, 0, n)
+    keys = [bytes(blob[offs[i]:offs[i + 1]]) for i in range(n)]
+    keys += keys[1000:1500]
+    blob, offs = O.keys_to_blob(keys)
+    t0 = time.perf_counter()
+    with pytest.raises(s3.MPHFError) as e:
+        _device_build(s3, ctx, blob, offs)
+    assert e.value.status == s3.ERR_DUP_KEY_HASH
+    assert time.perf_counter() - t0 < 5.0
+
+
 def test_duplicate_group_overflowing_a_reservation_slot(s3, ctx):
     """150k copies of one key all land in one tile of every level: the small-level
     reservation slot overflows, the build reruns on the counted path, and the result is
