@@ -33,9 +33,9 @@ namespace s3imph {
 namespace {
 
 constexpr int kCB = 1024;             // count block
-constexpr int kH0T = 1024;            // k_hash0_lds: threads (= keys per round)
-constexpr int kH0B = 64 << 10;        // ... window bytes per round (2 blocks per CU)
-constexpr int kH0Grid = 512;          // ... blocks: 2 per CU, a contiguous key range each
+constexpr int kH0T = 256;             // k_hash0_pair: threads (2 keys each per round)
+constexpr int kH0B = 32 << 10;        // ... window bytes per round (4 blocks per CU)
+constexpr int kH0Grid = 4096;         // ... blocks: 4 per resident slot, a contiguous key range each
 constexpr int kSB = 1024;             // scatter block
 constexpr int kTailT = 1024;          // tail block
 constexpr unsigned kLenBuckets = 256;  // key-length classes (4 B each) of the level-0 hash sort
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
   __shared__ unsigned short sidx[kCB];
   __shared__ uint64_t sb0[kCB], sb1[kCB], sh1[kCB], sh2[kCB];
   __shared__ uint64_t s_lmax[kCB / 64], s_lsum[kCB / 64];
-  if (smode == 5 && !st->skew) return;  // k_hash0_lds hashed this near-uniform set
+  if (smode == 5 && !st->skew) return;  // k_hash0_pair hashed this near-uniform set
   const bool sort = smode == 1 || smode == 2 || ((smode == 3 || smode == 5) && st->skew);
   const uint64_t words = st->words[0], magic = st->magic[0];
   const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
@@ -260,210 +260,32 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
 
 // ------------------------------------------------ level-0 hash, LDS-staged ----------
 // FNV-1a + FNV-1 of every key (StreamingMPHFBuilder.Add, mphf_streaming.go:73,80;
-// mphf.go:349-369) for near-uniform key lengths (st->skew == 0).  A block takes rounds of
-// up to NT consecutive keys: their bytes (one contiguous range of prefix_blob) come in
-// with coalesced 16-byte loads — the NEXT round's loads are issued into registers before
-// the current round is hashed, so their latency hides behind the multiply chains — and
-// are staged in LDS; the round's keys are counting-sorted by length, so the 64 lanes of a
-// wave hash keys of (nearly) one length and finish together; each lane then walks its
-// key's aligned words in LDS.  Compared with one lane per key reading the blob directly
-// (k_hash_count0), every blob line is fetched once and no lane idles behind a longer key
-// of its wave.  A round holds at most BB bytes: keys past that wait for the next round,
-// and a single key longer than BB is hashed from global memory by one lane.
-// (kh, fp) land in key order.  No level-0 histogram (the reservation path needs none).
-template <int NT, int BB, bool PF, int DBG = 0>
-__global__ __launch_bounds__(NT, 2048 / NT * NT / 256) void k_hash0_lds(const uint8_t* __restrict__ blob,
+// mphf.go:349-369) for near-uniform key lengths (st->skew == 0; skewed sets go to
+// k_hash_count0).  A block works through its contiguous key range in rounds of up to 2 NT
+// keys.  A round's bytes — one contiguous range of prefix_blob — come in with coalesced
+// 16-byte loads, issued into registers while the PREVIOUS round is hashed, and are staged
+// in LDS.  The round's keys are counting-sorted by length and lane t hashes sorted slot t
+// (the shorter half), then slot m - 1 - t (the longer half): within a wave the keys of each
+// half have nearly one length (no lane idles behind a longer key), and every lane, so every
+// wave, carries about twice the mean length (no wave waits behind another at the round's
+// barrier).  Each lane walks its key's aligned LDS words through a byte funnel.  Keys past
+// the window budget BB wait for the next round; a key longer than BB is hashed from global
+// memory by one lane.  (kh, fp) land in key order; no level-0 histogram (the reservation
+// path needs none).  The grid is many blocks per resident slot (kH0Grid): a block that
+// finishes early is replaced, so every SIMD keeps its waves to the end instead of running
+// the last blocks' load / sort phases exposed.
+// prof (S3IMPH_DEBUG): per wave, shader cycles total / hashing / barrier wait / rest, and
+// the real-time clock span, for the phase report of print_tile_profile.
+template <int NT, int BB, bool PF>
+__global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(const uint8_t* __restrict__ blob,
                                                   const uint64_t* __restrict__ offsets, uint64_t n,
                                                   uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
                                                   unsigned long long* __restrict__ flags,
                                                   unsigned long long* __restrict__ sflags, LevelState* st,
                                                   unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt,
                                                   unsigned long long* __restrict__ prof = nullptr) {
-  unsigned long long pt0 = __builtin_amdgcn_s_memtime(), ph = 0, pw = 0, pm = 0;  // debug phase clock
-  constexpr int KW = (BB / 16 + NT - 1) / NT;  // 16-byte window chunks per thread
-  constexpr unsigned kLB = 256;                // length classes of the sort
-  __shared__ uint64_t sw[BB / 8 + 2];          // the round's window (+ 16 B: a lane may read one word past)
-  __shared__ unsigned soff[NT], slen[NT];      // sorted slot -> key's window offset, length
-  __shared__ unsigned short sidx[NT];          // sorted slot -> key index in the round
-  __shared__ unsigned lcnt[kLB];
-  if (st->skew) return;  // k_hash_count0 hashes skewed sets (and clears the tile state)
-  const unsigned tid = threadIdx.x;
-  {
-    const uint64_t T = ntiles_of(st->words[0], tb), B = (n + chunk - 1) / chunk;
-    const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
-    const uint64_t g0 = (uint64_t)blockIdx.x * NT + tid, gs = (uint64_t)gridDim.x * NT;
-    if (blockIdx.x == 0 && tid == 0) {
-      st->ntiles[0] = T;
-      st->nchunks[0] = B;
-    }
-    for (uint64_t t = g0; t < T; t += gs) flags[t] = 0;
-    for (uint64_t q = g0; q < nseg; q += gs) sflags[q] = 0;
-    for (uint64_t q = g0; q < kTcntWords; q += gs) tcnt[q] = 0;
-  }
-  // this block's keys [g, gend); the blob is readable up to offsets[n] rounded up to 8
-  const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
-  uint64_t g = (uint64_t)blockIdx.x * per;
-  const uint64_t gend = min(n, g + per);
-  if (g >= gend) return;
-  const uint64_t end8 = (offsets[n] + 7) & ~7ull;
-  bool zero = false;
-  // ---- prefetch state of the round that starts at g: key bounds and window chunks
-  uint64_t kb0 = 0, kb1 = 0, wlo = 0, wend = 0;
-  bool kin = false;  // this thread holds a key of the round
-  uint4 wr[KW];
-  auto prefetch = [&](uint64_t r0) {
-    const uint64_t i = r0 + tid;
-    const uint64_t last = min(gend, r0 + NT);
-    kb0 = kb1 = 0;
-    kin = i < last;
-    if (kin) {
-      kb0 = offsets[i];
-      kb1 = offsets[i + 1];
-    }
-    // uniform over the block: kept in scalar registers
-    wlo = uniform64(offsets[r0] & ~15ull);
-    wend = uniform64(min((offsets[last] + 15) & ~15ull, wlo + (uint64_t)BB));
-#pragma unroll
-    for (int k = 0; k < KW; ++k) {
-      const uint64_t a = wlo + 16ull * (tid + (unsigned)k * NT);
-      wr[k] = make_uint4(0, 0, 0, 0);
-      if (DBG != 2 && a < wend) {
-        if (a + 16 <= end8) {
-          wr[k] = *reinterpret_cast<const uint4*>(blob + a);
-        } else {  // the blob's last 8 readable bytes
-          const uint2 h = *reinterpret_cast<const uint2*>(blob + a);
-          wr[k].x = h.x;
-          wr[k].y = h.y;
-        }
-      }
-    }
-  };
-  if (PF) prefetch(g);
-  for (;;) {
-    if (!PF) prefetch(g);
-    // ---- stage the window in LDS; reset the length classes
-#pragma unroll
-    for (int k = 0; k < KW; ++k) {
-      const unsigned c = tid + (unsigned)k * NT;
-      if (wlo + 16ull * c < wend) {
-        sw[2 * c] = (uint64_t)wr[k].x | ((uint64_t)wr[k].y << 32);
-        sw[2 * c + 1] = (uint64_t)wr[k].z | ((uint64_t)wr[k].w << 32);
-      }
-    }
-    for (unsigned b = tid; b < kLB; b += NT) lcnt[b] = 0;
-    const uint64_t rw = wlo;
-    const uint64_t t_b0 = kb0, t_b1 = kb1;
-    // keys whose bytes all lie in the window (a prefix of the round: offsets ascend)
-    const bool fits = kin && t_b1 - rw <= (uint64_t)BB;
-    unsigned m = (unsigned)__syncthreads_count(fits);
-    const bool alone = m == 0;  // the round's first key is longer than the window
-    if (alone) m = 1;
-    // ---- counting sort of the round's keys by length (LDS atomics, one wave scans)
-    unsigned cls = 0, rk = 0;
-    if (fits) {
-      cls = (unsigned)min<uint64_t>(t_b1 - t_b0, kLB - 1);
-      rk = atomicAdd(&lcnt[cls], 1u);
-    }
-    __syncthreads();
-    if (tid < 64) {
-      unsigned v[kLB / 64], sum = 0;
-#pragma unroll
-      for (int q = 0; q < (int)(kLB / 64); ++q) {
-        v[q] = lcnt[tid * (kLB / 64) + q];
-        sum += v[q];
-      }
-      unsigned x = sum;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const unsigned y = __shfl_up(x, d);
-        if (tid >= (unsigned)d) x += y;
-      }
-      unsigned ex = x - sum;
-#pragma unroll
-      for (int q = 0; q < (int)(kLB / 64); ++q) {
-        lcnt[tid * (kLB / 64) + q] = ex;
-        ex += v[q];
-      }
-    }
-    __syncthreads();
-    if (fits) {
-      const unsigned slot = lcnt[cls] + rk;
-      sidx[slot] = (unsigned short)tid;
-      soff[slot] = (unsigned)(t_b0 - rw);
-      slen[slot] = (unsigned)(t_b1 - t_b0);
-    }
-    __syncthreads();
-    // ---- issue the next round's loads; they land while this round is hashed
-    const uint64_t r0 = g;
-    g += m;
-    const bool more = g < gend;
-    if (PF && more) prefetch(g);
-    // ---- hash: lane -> the key in its sorted slot, aligned LDS words, byte funnel
-    unsigned long long pta = prof ? __builtin_amdgcn_s_memtime() : 0;
-    if (tid < m) {
-      uint64_t a = kFnvOffset, b = kFnvOffset, j;
-      if (alone) {
-        j = 0;
-        fnv_both_pf(blob, t_b0, t_b1, a, b);  // tid 0 holds the round's first key
-      } else {
-        j = sidx[tid];
-        const unsigned o = soff[tid], len = DBG == 1 ? 0u : slen[tid];
-        const uint64_t* w = sw + (o >> 3);
-        const unsigned s = o & 7u;
-        const unsigned nfull = len >> 3;
-        uint64_t cur = w[0];
-        for (unsigned q = 0; q < nfull; ++q) {
-          const uint64_t nxt = w[q + 1];
-          fnv_8(a, b, funnel_bytes(cur, nxt, s));
-          cur = nxt;
-        }
-        const unsigned rem = len & 7u;
-        if (rem) {
-          const uint64_t v = funnel_bytes(cur, w[nfull + 1], s);
-#pragma unroll
-          for (unsigned t = 0; t < 7; ++t)
-            if (t < rem) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
-        }
-      }
-      kh[r0 + j] = a;
-      fp[r0 + j] = b;
-      zero |= (a == 0);
-    }
-    unsigned long long ptb = prof ? __builtin_amdgcn_s_memtime() : 0;
-    if (!more) break;
-    __syncthreads();  // every lane is done with sw / sidx before the next round overwrites them
-    if (prof) {
-      const unsigned long long ptc = __builtin_amdgcn_s_memtime();
-      ph += ptb - pta;
-      pw += ptc - ptb;
-      pm += pta - pt0 - (ph - (ptb - pta)) - (pw - (ptc - ptb)) - pm;  // everything else this round
-    }
-  }
-  if (prof && lane_id() == 0) {
-    const unsigned long long tot = __builtin_amdgcn_s_memtime() - pt0;
-    unsigned long long* q = prof + ((uint64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6)) * 4;
-    q[0] = tot;
-    q[1] = ph;
-    q[2] = pw;
-    q[3] = tot - ph - pw;
-  }
-  if (zero) atomicOr(&st->status, kStKeyZero);
-}
-
-// Level-0 hash, LDS-staged rounds of 2 NT keys, two keys per lane: a round's keys are
-// counting-sorted by length and lane t hashes sorted slot t (the shorter half) then slot
-// 2NT - 1 - t (the longer half), so every lane — and so every wave — carries about twice
-// the mean key length: no wave of a round waits behind another at the round's barrier,
-// and within a wave the keys of each half have nearly one length.  Otherwise as
-// k_hash0_lds: coalesced 16-byte window loads staged in LDS, aligned LDS words funnelled
-// per lane, keys past the window budget wait for the next round.
-template <int NT, int BB>
-__global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(const uint8_t* __restrict__ blob,
-                                                  const uint64_t* __restrict__ offsets, uint64_t n,
-                                                  uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
-                                                  unsigned long long* __restrict__ flags,
-                                                  unsigned long long* __restrict__ sflags, LevelState* st,
-                                                  unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
+  unsigned long long pt0 = __builtin_amdgcn_s_memtime(), ph = 0, pw = 0;  // debug phase clock
+  const unsigned long long prt0 = __builtin_amdgcn_s_memrealtime();
   constexpr int G = 2 * NT;                    // keys per round
   constexpr int KW = (BB / 16 + NT - 1) / NT;  // 16-byte window chunks per thread
   constexpr unsigned kLB = 256;                // length classes of the sort
@@ -493,52 +315,56 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   if (g >= gend) return;
   const uint64_t end8 = (offsets[n] + 7) & ~7ull;
   bool zero = false;
-  for (;;) {
-    // ---- the round's keys g + tid and g + NT + tid, and its window [wlo, wend)
-    const uint64_t last = min(gend, g + G);
-    uint64_t kb0[2], kb1[2];
-    bool kin[2];
+  // ---- the round at r0: keys r0 + tid and r0 + NT + tid, its window [wlo, wend) in wr
+  uint64_t kb0[2], kb1[2], wlo = 0, wend = 0;
+  bool kin[2];
+  uint4 wr[KW];
+  auto prefetch = [&](uint64_t r0) {
+    const uint64_t last = min(gend, r0 + G);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const uint64_t i = g + tid + (unsigned)h * NT;
+      const uint64_t i = r0 + tid + (unsigned)h * NT;
       kin[h] = i < last;
       kb0[h] = kin[h] ? offsets[i] : 0;
       kb1[h] = kin[h] ? offsets[i + 1] : 0;
     }
-    const uint64_t wlo = uniform64(offsets[g] & ~15ull);
-    const uint64_t wend = uniform64(min((offsets[last] + 15) & ~15ull, wlo + (uint64_t)BB));
-    {
-      uint4 wr[KW];
+    wlo = uniform64(offsets[r0] & ~15ull);
+    wend = uniform64(min((offsets[last] + 15) & ~15ull, wlo + (uint64_t)BB));
 #pragma unroll
-      for (int k = 0; k < KW; ++k) {
-        const uint64_t a = wlo + 16ull * (tid + (unsigned)k * NT);
-        wr[k] = make_uint4(0, 0, 0, 0);
-        if (a < wend) {
-          if (a + 16 <= end8) {
-            wr[k] = *reinterpret_cast<const uint4*>(blob + a);
-          } else {  // the blob's last 8 readable bytes
-            const uint2 hh = *reinterpret_cast<const uint2*>(blob + a);
-            wr[k].x = hh.x;
-            wr[k].y = hh.y;
-          }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < KW; ++k) {
-        const unsigned c = tid + (unsigned)k * NT;
-        if (wlo + 16ull * c < wend) {
-          sw[2 * c] = (uint64_t)wr[k].x | ((uint64_t)wr[k].y << 32);
-          sw[2 * c + 1] = (uint64_t)wr[k].z | ((uint64_t)wr[k].w << 32);
+    for (int k = 0; k < KW; ++k) {
+      const uint64_t a = wlo + 16ull * (tid + (unsigned)k * NT);
+      wr[k] = make_uint4(0, 0, 0, 0);
+      if (a < wend) {
+        if (a + 16 <= end8) {
+          wr[k] = *reinterpret_cast<const uint4*>(blob + a);
+        } else {  // the blob's last 8 readable bytes
+          const uint2 hh = *reinterpret_cast<const uint2*>(blob + a);
+          wr[k].x = hh.x;
+          wr[k].y = hh.y;
         }
       }
     }
+  };
+  if (PF) prefetch(g);
+  for (;;) {
+    if (!PF) prefetch(g);
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+      const unsigned c = tid + (unsigned)k * NT;
+      if (wlo + 16ull * c < wend) {
+        sw[2 * c] = (uint64_t)wr[k].x | ((uint64_t)wr[k].y << 32);
+        sw[2 * c + 1] = (uint64_t)wr[k].z | ((uint64_t)wr[k].w << 32);
+      }
+    }
     for (unsigned b = tid; b < kLB; b += NT) lcnt[b] = 0;
+    const uint64_t rw = wlo;
+    const uint64_t t_b0[2] = {kb0[0], kb0[1]}, t_b1[2] = {kb1[0], kb1[1]};
     // keys whose bytes all lie in the window: a prefix of the round (offsets ascend)
     bool fits[2];
     unsigned mine = 0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      fits[h] = kin[h] && kb1[h] - wlo <= (uint64_t)BB;
+      fits[h] = kin[h] && t_b1[h] - rw <= (uint64_t)BB;
       const uint64_t fb = __ballot(fits[h]);
       mine += (unsigned)__popcll(fb);
     }
@@ -554,7 +380,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       if (fits[h]) {
-        cls[h] = (unsigned)min<uint64_t>(kb1[h] - kb0[h], kLB - 1);
+        cls[h] = (unsigned)min<uint64_t>(t_b1[h] - t_b0[h], kLB - 1);
         rk[h] = atomicAdd(&lcnt[cls[h]], 1u);
       }
     __syncthreads();
@@ -584,17 +410,22 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
       if (fits[h]) {
         const unsigned slot = lcnt[cls[h]] + rk[h];
         sidx[slot] = (unsigned short)(tid + (unsigned)h * NT);
-        soff[slot] = (unsigned)(kb0[h] - wlo);
-        slen[slot] = (unsigned)(kb1[h] - kb0[h]);
+        soff[slot] = (unsigned)(t_b0[h] - rw);
+        slen[slot] = (unsigned)(t_b1[h] - t_b0[h]);
       }
     __syncthreads();
+    const uint64_t r0 = g;
+    g += m;
+    const bool more = g < gend;
+    if (PF && more) prefetch(g);  // the next round's loads land while this one is hashed
+    unsigned long long pta = prof ? __builtin_amdgcn_s_memtime() : 0;
     // ---- hash: slot tid (shorter half), then slot m - 1 - tid (longer half)
     if (alone) {
       if (tid == 0) {
         uint64_t a, b;
-        fnv_both_pf(blob, kb0[0], kb1[0], a, b);
-        kh[g] = a;
-        fp[g] = b;
+        fnv_both_pf(blob, t_b0[0], t_b1[0], a, b);
+        kh[r0] = a;
+        fp[r0] = b;
         zero |= (a == 0);
       }
     } else {
@@ -621,226 +452,31 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
             for (unsigned t = 0; t < 7; ++t)
               if (t < rem) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
           }
-          kh[g + j] = a;
-          fp[g + j] = b;
+          kh[r0 + j] = a;
+          fp[r0 + j] = b;
           zero |= (a == 0);
         }
       }
     }
-    g += m;
-    if (g >= gend) break;
-    __syncthreads();  // every lane is done with sw / sidx before the next round overwrites them
-  }
-  if (zero) atomicOr(&st->status, kStKeyZero);
-}
-
-// Level-0 hash with the window pipeline on LDS-DMA (global_load_lds_dwordx4): one block
-// per CU keeps two window buffers; while round k is hashed from one, the DMA engine fills
-// the other with round k+1's bytes (no VGPRs hold them, nothing waits for them until the
-// round ends).  Same rounds, sort and per-lane hash as k_hash0_lds.  Round k's hashes go
-// to LDS and are stored, coalesced, early in round k+1 — before its DMA is issued — so no
-// vector-memory op is pending behind the DMA while a round is hashed and the end-of-round
-// wait retires only loads that have had the whole hash phase to land.  All LDS lives in
-// one array and the loop uses raw s_barrier (a __syncthreads() would drain the DMA).
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-template <int NT, int BB>
-__global__ __launch_bounds__(NT) void k_hash0_dma(const uint8_t* __restrict__ blob,
-                                                  const uint64_t* __restrict__ offsets, uint64_t n,
-                                                  uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
-                                                  unsigned long long* __restrict__ flags,
-                                                  unsigned long long* __restrict__ sflags, LevelState* st,
-                                                  unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
-  typedef __attribute__((address_space(3))) void* lds_vp;
-  typedef __attribute__((address_space(1))) void* gbl_vp;
-  constexpr int KW = (BB / 16 + NT - 1) / NT;  // window chunks (16 B) per thread
-  constexpr int WW = BB / 8 + 2;               // u64 words per window buffer (+16 B read slack)
-  constexpr unsigned kLB = 256;                // length classes of the sort
-  constexpr int NW = NT / 64;
-  static_assert(BB % (16 * 64) == 0, "window = whole 1 KiB DMA pieces");
-  // [win0 | win1 | res_a u64[NT] | res_b u64[NT] | soff u32[NT] | slen u32[NT] | sidx u16[NT] | lcnt u32[kLB] | s_cnt u32[NW]]
-  __shared__ uint64_t smem[2 * WW + 2 * NT + (8 * NT + 2 * NT + 4 * kLB + 4 * NW) / 8 + 1];
-  uint64_t* res_a = smem + 2 * WW;
-  uint64_t* res_b = res_a + NT;
-  unsigned* soff = reinterpret_cast<unsigned*>(res_b + NT);
-  unsigned* slen = soff + NT;
-  unsigned short* sidx = reinterpret_cast<unsigned short*>(slen + NT);
-  unsigned* lcnt = reinterpret_cast<unsigned*>(sidx + NT);
-  unsigned* s_cnt = lcnt + kLB;
-  if (st->skew) return;  // k_hash_count0 hashes skewed sets (and clears the tile state)
-  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  {
-    const uint64_t T = ntiles_of(st->words[0], tb), B = (n + chunk - 1) / chunk;
-    const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
-    const uint64_t g0 = (uint64_t)blockIdx.x * NT + tid, gs = (uint64_t)gridDim.x * NT;
-    if (blockIdx.x == 0 && tid == 0) {
-      st->ntiles[0] = T;
-      st->nchunks[0] = B;
-    }
-    for (uint64_t t = g0; t < T; t += gs) flags[t] = 0;
-    for (uint64_t q = g0; q < nseg; q += gs) sflags[q] = 0;
-    for (uint64_t q = g0; q < kTcntWords; q += gs) tcnt[q] = 0;
-  }
-  const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
-  uint64_t g = (uint64_t)blockIdx.x * per;
-  const uint64_t gend = min(n, g + per);
-  if (g >= gend) return;
-  const uint64_t end8 = (offsets[n] + 7) & ~7ull;  // the blob is readable up to here
-  // round bounds: this thread's key [b0, b1) and the window [lo, hi)
-  auto bounds = [&](uint64_t r0, uint64_t& b0, uint64_t& b1, bool& in, uint64_t& lo, uint64_t& hi) {
-    const uint64_t i = r0 + tid, last = min(gend, r0 + NT);
-    in = i < last;
-    b0 = in ? offsets[i] : 0;
-    b1 = in ? offsets[i + 1] : 0;
-    lo = uniform64(offsets[r0] & ~15ull);
-    hi = uniform64(min((offsets[last] + 15) & ~15ull, lo + (uint64_t)BB));
-  };
-  // window [lo, hi) -> buffer w: 1 KiB DMA pieces, lane-linear; the blob's last 16-byte
-  // chunk (only 8 bytes readable) goes through a register instead
-  auto fill = [&](uint64_t lo, uint64_t hi, uint64_t* w) {
-    if (hi + 8 > end8) {
-#pragma unroll
-      for (int k = 0; k < KW; ++k) {
-        const unsigned c = (unsigned)k * NT + tid;
-        const uint64_t a = lo + 16ull * c;
-        if (a < hi && a + 16 > end8) w[2 * c] = *reinterpret_cast<const uint64_t*>(blob + a);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < KW; ++k) {
-      const unsigned c = (unsigned)k * NT + tid;
-      const uint64_t a = lo + 16ull * c;
-      if (lo + 16ull * ((unsigned)k * NT + wave * 64) < hi) {  // any lane of this wave's piece
-        if (a < hi && a + 16 <= end8)
-          __builtin_amdgcn_global_load_lds((gbl_vp)(blob + a), (lds_vp)(w + 2 * ((unsigned)k * NT + wave * 64)), 16, 0, 0);
-      }
-    }
-  };
-  uint64_t kb0, kb1, wlo, wend;
-  bool kin;
-  bounds(g, kb0, kb1, kin, wlo, wend);
-  fill(wlo, wend, smem);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
-  int buf = 0;
-  bool zero = false;
-  uint64_t p0 = 0;   // first key of the previous round (its hashes wait in res_a / res_b)
-  unsigned pm = 0;   // ... and its key count
-  for (;;) {
-    const uint64_t* sw = smem + buf * WW;
-    // ---- keys whose bytes all lie in the window (a prefix of the round)
-    const bool fits = kin && kb1 - wlo <= (uint64_t)BB;
-    if (tid < kLB) lcnt[tid] = 0;
-    const uint64_t fb = __ballot(fits);
-    if (lane == 0) s_cnt[wave] = (unsigned)__popcll(fb);
-    lds_barrier();
-    unsigned m = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) m += s_cnt[w];
-    const bool alone = m == 0;  // the round's first key is longer than the window
-    if (alone) m = 1;
-    const uint64_t r0 = g;
-    const uint64_t g1 = g + m;
-    const bool more = g1 < gend;
-    // ---- next round's bounds (plain loads, consumed after the sort)
-    uint64_t nb0 = 0, nb1 = 0, nlo = 0, nhi = 0;
-    bool nin = false;
-    if (more) bounds(g1, nb0, nb1, nin, nlo, nhi);
-    // ---- counting sort of the round's keys by length
-    unsigned cls = 0, rk = 0;
-    if (fits) {
-      cls = (unsigned)min<uint64_t>(kb1 - kb0, kLB - 1);
-      rk = atomicAdd(&lcnt[cls], 1u);
-    }
-    lds_barrier();
-    if (tid < 64) {
-      unsigned v[kLB / 64], sum = 0;
-#pragma unroll
-      for (int q = 0; q < (int)(kLB / 64); ++q) {
-        v[q] = lcnt[tid * (kLB / 64) + q];
-        sum += v[q];
-      }
-      unsigned x = sum;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const unsigned y = __shfl_up(x, d);
-        if (tid >= (unsigned)d) x += y;
-      }
-      unsigned ex = x - sum;
-#pragma unroll
-      for (int q = 0; q < (int)(kLB / 64); ++q) {
-        lcnt[tid * (kLB / 64) + q] = ex;
-        ex += v[q];
-      }
-    }
-    lds_barrier();
-    if (fits) {
-      const unsigned slot = lcnt[cls] + rk;
-      sidx[slot] = (unsigned short)tid;
-      soff[slot] = (unsigned)(kb0 - wlo);
-      slen[slot] = (unsigned)(kb1 - kb0);
-    }
-    // the next round's bounds are consumed here, before the stores and the DMA: a first
-    // use behind either would make the compiler wait vmcnt(0) there
-    if (more) asm volatile("" ::"v"(nb0), "v"(nb1));
-    // ---- the previous round's hashes (LDS) -> kh / fp, coalesced
-    if (tid < pm) {
-      const uint64_t a = res_a[tid];
-      kh[p0 + tid] = a;
-      fp[p0 + tid] = res_b[tid];
-      zero |= (a == 0);
-    }
-    lds_barrier();  // sidx / soff / slen written; res_a / res_b read
-    // ---- the next window streams into the other buffer while this one is hashed
-    if (more) fill(nlo, nhi, smem + (buf ^ 1) * WW);
-    if (tid < m) {
-      uint64_t a = kFnvOffset, b = kFnvOffset;
-      unsigned j = 0;
-      if (alone) {
-        fnv_both_pf(blob, kb0, kb1, a, b);  // tid 0: a key longer than the window
-      } else {
-        j = sidx[tid];
-        const unsigned o = soff[tid], len = slen[tid];
-        const uint64_t* w = sw + (o >> 3);
-        const unsigned s = o & 7u;
-        const unsigned nfull = len >> 3;
-        uint64_t cur = w[0];
-        for (unsigned q = 0; q < nfull; ++q) {
-          const uint64_t nxt = w[q + 1];
-          fnv_8(a, b, funnel_bytes(cur, nxt, s));
-          cur = nxt;
-        }
-        const unsigned rem = len & 7u;
-        if (rem) {
-          const uint64_t v = funnel_bytes(cur, w[nfull + 1], s);
-#pragma unroll
-          for (unsigned t = 0; t < 7; ++t)
-            if (t < rem) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
-        }
-      }
-      res_a[j] = a;
-      res_b[j] = b;
-    }
-    p0 = r0;
-    pm = m;
-    // ---- the next window has landed (this wave's pieces, then every wave's), and every
-    // lane is done with sw / soff / sidx / res
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
+    unsigned long long ptb = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (!more) break;
-    kb0 = nb0;
-    kb1 = nb1;
-    kin = nin;
-    wlo = nlo;
-    wend = nhi;
-    g = g1;
-    buf ^= 1;
+    __syncthreads();  // every lane is done with sw / sidx before the next round overwrites them
+    if (prof) {
+      ph += ptb - pta;
+      pw += __builtin_amdgcn_s_memtime() - ptb;
+    }
   }
-  if (tid < pm) {
-    const uint64_t a = res_a[tid];
-    kh[p0 + tid] = a;
-    fp[p0 + tid] = res_b[tid];
-    zero |= (a == 0);
+  if (prof && lane == 0 && (uint64_t)blockIdx.x * NW + wave < 8192) {
+    const unsigned long long tot = __builtin_amdgcn_s_memtime() - pt0;
+    unsigned long long* q = prof + ((uint64_t)blockIdx.x * NW + wave) * 8;
+    q[0] = tot;
+    q[1] = ph;
+    q[2] = pw;
+    q[3] = tot - ph - pw;
+    const unsigned long long prt1 = __builtin_amdgcn_s_memrealtime();
+    q[4] = prt1 - prt0;
+    q[5] = prt0;
+    q[6] = prt1;
   }
   if (zero) atomicOr(&st->status, kStKeyZero);
 }
@@ -2293,46 +1929,14 @@ void binned_set_lds_limits() {
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s, bool histogram) {
   if (level == 0 && !b.dist) {
-    // near-uniform lengths hash directly (loads two words ahead); a set whose sampled
-    // lengths are skewed (k_init_state) hashes 1024-key groups length-sorted (16-byte loads)
-    static const int h0 = [] {  // TEMPORARY A/B knob (round-2 hash sweep)
-      const char* e = std::getenv("S3IMPH_H0");
-      return e ? std::atoi(e) : 1;
-    }();
-    if (!histogram && ((uintptr_t)blob & 15) == 0 && h0) {
+    // a set whose sampled lengths are skewed (k_init_state) hashes 1024-key groups
+    // length-sorted in k_hash_count0 (16-byte loads); so does a caller's unaligned blob
+    if (!histogram && ((uintptr_t)blob & 15) == 0) {
       // near-uniform lengths: LDS-staged, length-sorted rounds; skewed sets (decided on the
       // device from sampled lengths) fall through to k_hash_count0's length-sorted groups
-      if (h0 == 1)
-        k_hash0_lds<kH0T, kH0B, false><<<kH0Grid, kH0T, 0, s>>>(
-            blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt,
-            b.tile_prof ? b.tile_prof + (uint64_t)(kMaxLevels - 2) * kMaxTiles * 8 : nullptr);
-      else if (h0 == 2)
-        k_hash0_lds<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
-                                                              g.tb, g.chunk, b.tcnt);
-      else if (h0 == 7)  // debug: no hashing (skeleton: loads, sort, stores)
-        k_hash0_lds<kH0T, kH0B, false, 1><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags,
-                                                                  b.st, g.tb, g.chunk, b.tcnt);
-      else if (h0 == 8)  // debug: no window loads (sort + hash + stores)
-        k_hash0_lds<kH0T, kH0B, false, 2><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags,
-                                                                  b.st, g.tb, g.chunk, b.tcnt);
-      else if (h0 == 9)
-        k_hash0_pair<512, 64 << 10><<<512, 512, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb,
-                                                         g.chunk, b.tcnt);
-      else if (h0 == 10)
-        k_hash0_pair<256, 32 << 10><<<1024, 256, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb,
-                                                          g.chunk, b.tcnt);
-      else if (h0 == 5)
-        k_hash0_dma<1024, 64 << 10><<<256, 1024, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb,
-                                                          g.chunk, b.tcnt);
-      else if (h0 == 6)
-        k_hash0_dma<512, 32 << 10><<<512, 512, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb,
-                                                        g.chunk, b.tcnt);
-      else if (h0 == 3)
-        k_hash0_lds<512, 32 << 10, false><<<2 * kH0Grid, 512, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags,
-                                                                     b.st, g.tb, g.chunk, b.tcnt);
-      else
-        k_hash0_lds<512, 32 << 10, true><<<2 * kH0Grid, 512, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags,
-                                                                    b.st, g.tb, g.chunk, b.tcnt);
+      unsigned long long* prof = b.tile_prof ? b.tile_prof + (uint64_t)(kMaxLevels - 3) * kMaxTiles * 8 : nullptr;
+      k_hash0_pair<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
+                                                             g.tb, g.chunk, b.tcnt, prof);
       k_hash_count0<2, 3><<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st,
                                                       g.tb, g.chunk, b.tcnt, 5);
       return;

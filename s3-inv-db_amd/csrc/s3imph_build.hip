@@ -385,18 +385,54 @@ void print_tile_profile(s3imph_ctx* c) {
   if (!c->tile_prof) return;
   std::vector<unsigned long long> h((size_t)kMaxLevels * kMaxTiles * 8);
   HIPCHECK(hipMemcpy(h.data(), c->tile_prof, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-  {  // level-0 hash waves (k_hash0_lds debug clock): total / hash / barrier wait after hash / rest
-    const unsigned long long* q = &h[(size_t)(kMaxLevels - 2) * kMaxTiles * 8];
-    double a[4] = {0, 0, 0, 0};
+  {  // level-0 hash waves (k_hash0_pair debug clock, first 8192 waves): total / hash / barrier wait after hash / rest
+    const unsigned long long* q = &h[(size_t)(kMaxLevels - 3) * kMaxTiles * 8];  // two rows: 8 words per wave
+    double a[5] = {0, 0, 0, 0, 0};
     int cnt = 0;
-    for (int w = 0; w < (int)(kMaxTiles * 8 / 4); ++w) {
-      if (!q[4 * w]) continue;
+    for (int w = 0; w < (int)(2 * kMaxTiles * 8 / 8); ++w) {
+      if (!q[8 * w]) continue;
       ++cnt;
-      for (int k = 0; k < 4; ++k) a[k] += (double)q[4 * w + k];
+      for (int k = 0; k < 5; ++k) a[k] += (double)q[8 * w + k];
+    }
+    if (cnt) {  // wave start / end spread (100 MHz real-time counter)
+      std::vector<double> st, en;
+      for (int w = 0; w < (int)(2 * kMaxTiles * 8 / 8); ++w)
+        if (q[8 * w]) {
+          st.push_back((double)q[8 * w + 5]);
+          en.push_back((double)q[8 * w + 6]);
+        }
+      std::sort(st.begin(), st.end());
+      std::sort(en.begin(), en.end());
+      const double t0 = st[0];
+      auto pc = [&](const std::vector<double>& v, double f) { return (v[(size_t)(f * (v.size() - 1))] - t0) / 100.0; };
+      {  // by XCD (block % 8) and by block-index decile: mean end (us) and shader clock (MHz)
+        const int nw = (int)st.size(), wpb = 4, nb = nw / wpb;  // k_hash0_pair: 4 waves per block
+        double xe[8] = {0}, xc[8] = {0}, xn[8] = {0}, de[10] = {0}, dn[10] = {0};
+        for (int w = 0; w < (int)(2 * kMaxTiles * 8 / 8); ++w) {
+          if (!q[8 * w]) continue;
+          const int blk = w / wpb, x = blk % 8, d = std::min(9, blk * 10 / std::max(1, nb));
+          const double e = ((double)q[8 * w + 6] - t0) / 100.0;
+          xe[x] += e;
+          xc[x] += 100.0 * (double)q[8 * w] / (double)q[8 * w + 4];
+          xn[x] += 1;
+          de[d] += e;
+          dn[d] += 1;
+        }
+        std::fprintf(stderr, "  hash0 by xcd (end us / MHz):");
+        for (int x = 0; x < 8; ++x) std::fprintf(stderr, " %.0f/%.0f", xe[x] / std::max(1.0, xn[x]), xc[x] / std::max(1.0, xn[x]));
+        std::fprintf(stderr, "\n  hash0 by block decile (end us):");
+        for (int d = 0; d < 10; ++d) std::fprintf(stderr, " %.0f", de[d] / std::max(1.0, dn[d]));
+        std::fprintf(stderr, "\n");
+      }
+      std::fprintf(stderr, "  hash0 wave starts (us) p50 %.1f p90 %.1f max %.1f; ends min %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f\n",
+                   pc(st, 0.5), pc(st, 0.9), pc(st, 1.0), pc(en, 0.0), pc(en, 0.1), pc(en, 0.5), pc(en, 0.9), pc(en, 1.0));
     }
     if (cnt)
-      std::fprintf(stderr, "  hash0 waves %d: avg cycles %.0f, hash %.1f%%, barrier wait %.1f%%, rest %.1f%%\n", cnt,
-                   a[0] / cnt, 100 * a[1] / a[0], 100 * a[2] / a[0], 100 * a[3] / a[0]);
+      std::fprintf(stderr,
+                   "  hash0 waves %d: avg cycles %.0f (%.1f us, shader clock %.0f MHz), hash %.1f%%, barrier wait "
+                   "%.1f%%, rest %.1f%%\n",
+                   cnt, a[0] / cnt, a[4] / cnt / 100.0, a[4] ? 100.0 * a[0] / a[4] : 0.0, 100 * a[1] / a[0],
+                   100 * a[2] / a[0], 100 * a[3] / a[0]);
   }
   static const char* names[7] = {"mark", "final", "lookbk", "rank", "output", "redoN", "redoW"};
   {

@@ -13,6 +13,16 @@ constexpr uint64_t kP = 0x100000001b3ull;
 
 template <int kMode>
 __global__ __launch_bounds__(256) void k_fnv(uint64_t* out, int iters, uint64_t seed) {
+  const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  struct Clk {  // shader clock vs the 100 MHz real-time counter over block 0's life
+    uint64_t *o, c0, r0;
+    __device__ ~Clk() {
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        o[2] = __builtin_amdgcn_s_memtime() - c0;
+        o[3] = __builtin_amdgcn_s_memrealtime() - r0;
+      }
+    }
+  } clk{out, c0, r0};
   uint64_t a = seed ^ (threadIdx.x + 977ull * blockIdx.x), b = a * 3;
   uint64_t v = a * 0x9e3779b97f4a7c15ull;
   if (kMode == 4) {  // variant: hi * 435 by v_mul_lo_u32, (lo << 8) folded, mad64 with addend
@@ -92,12 +102,16 @@ int main(int argc, char** argv) {
       hipEventSynchronize(e1);
       float ms;
       hipEventElapsedTime(&ms, e0, e1);
+      uint64_t hc[4];
+      hipMemcpy(hc, d, sizeof(hc), hipMemcpyDeviceToHost);
+      const double mhz = hc[3] ? 100.0 * (double)hc[2] / (double)hc[3] : 0.0;
       const double steps = (double)blocks * 256 * iters * 8;  // byte-steps over all lanes
       const double lane_steps_per_s = steps / (ms * 1e-3);
       // 256 CUs x 4 SIMDs; a full-rate wave64 VALU op = 64 lane-ops per SIMD per (1 or 2) cycles
-      printf("mode %d rep %d: %.3f ms, %.2f T byte-steps/s, %.3f SIMD-cycles per wave byte-step (clk %d kHz)\n",
+      printf("mode %d rep %d: %.3f ms, %.2f T byte-steps/s, %.3f SIMD-cycles per wave byte-step (clk %d kHz), measured shader clock %.0f MHz -> %.2f cycles\n",
              mode, rep, ms, lane_steps_per_s * 1e-12,
-             (ms * 1e-3) * (clk * 1e3) * 1024.0 / (steps / 64.0), clk);
+             (ms * 1e-3) * (clk * 1e3) * 1024.0 / (steps / 64.0), clk, mhz,
+             (ms * 1e-3) * (mhz * 1e6) * 1024.0 / (steps / 64.0));
     }
   }
   return 0;
