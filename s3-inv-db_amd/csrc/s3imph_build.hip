@@ -354,7 +354,8 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   const bool res0 = !conservative && c->res0 && T0 <= kScatterTiles && (res_fits(c, n, 64 * level_words(n), T0) || c->res0 == 2);
   launch_binned_count(0, blob, offsets, n, b, g0, gr.gc, s, !res0);  // no histogram for the reservation path
   ev_mark(c, s, "hash_count0");
-  static const bool hash_only = std::getenv("S3IMPH_HASH_ONLY") != nullptr;  // TEMPORARY probe knob
+  // profiling aid (tools/hash_only.py): stop after the level-0 hash so it can be timed alone
+  static const bool hash_only = std::getenv("S3IMPH_HASH_ONLY") != nullptr;
   if (hash_only) return;
   if (res0) {
     launch_binned_scatter_res(0, b, g0, 256, s);
@@ -965,11 +966,14 @@ void stager_init(s3imph_ctx* c) {
 // Chunked copy between pageable host memory and the device through the pinned
 // buffers.  h2d: device dst <- host src; with `bias`, src holds u64 words and each is
 // stored minus bias (offsets rebased to a blob that starts at offsets[0]).
-void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias) {
+// conv 1 (h2d): host u64 words, minus bias, stored as device u32 (`bytes` = device
+// bytes); conv 2 (d2h): device u32 words widened to host u64.  Both halve the PCIe bytes
+// of an array whose values fit 32 bits.
+void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias, int conv) {
   if (!bytes) return;
   // Pageable H2D through the runtime already runs at the PCIe rate (C2: 400 MB in
   // 7.4 ms, 54 GB/s); pageable D2H does not (17 GB/s), and neither does rebasing.
-  if (!bias && h2d) {
+  if (!bias && !conv && h2d) {
     HIPCHECK(hipMemcpy(dst, src, bytes, h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost));
     return;
   }
@@ -987,7 +991,11 @@ void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t b
         for (uint64_t ch = w; ch < nch; ch += nw, b ^= 1) {
           const uint64_t off = ch * kStageChunk, len = clen(ch);
           HIPCHECK(hipEventSynchronize(g.ev[w][b]));  // this buffer's previous DMA is done
-          if (bias) {
+          if (conv == 1) {
+            const uint64_t* s64 = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(src) + 2 * off);
+            uint32_t* d32 = static_cast<uint32_t*>(g.pin[w][b]);
+            for (uint64_t i = 0; i < len / 4; ++i) d32[i] = (uint32_t)(s64[i] - bias);
+          } else if (bias) {
             const uint64_t* s64 = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(src) + off);
             uint64_t* d64 = static_cast<uint64_t*>(g.pin[w][b]);
             for (uint64_t i = 0; i < len / 8; ++i) d64[i] = s64[i] - bias;
@@ -1009,7 +1017,13 @@ void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t b
         for (uint64_t ch = w; ch < nch; ch += nw, b ^= 1) {
           if (ch + nw < nch) issue(ch + nw, b ^ 1);
           HIPCHECK(hipEventSynchronize(g.ev[w][b]));
-          std::memcpy(static_cast<uint8_t*>(dst) + ch * kStageChunk, g.pin[w][b], clen(ch));
+          if (conv == 2) {
+            const uint32_t* s32 = static_cast<const uint32_t*>(g.pin[w][b]);
+            uint64_t* d64 = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(dst) + 2 * ch * kStageChunk);
+            for (uint64_t i = 0; i < clen(ch) / 4; ++i) d64[i] = s32[i];
+          } else {
+            std::memcpy(static_cast<uint8_t*>(dst) + ch * kStageChunk, g.pin[w][b], clen(ch));
+          }
         }
       }
       HIPCHECK(hipStreamSynchronize(g.st[w]));
@@ -1055,7 +1069,15 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
     HIPCHECK(hipStreamSynchronize(s));  // staging buffers may be in use by the last build
     const auto t0 = clk::now();
     staged_copy(c, true, c->s_blob, blob + b0, nbytes);
-    staged_copy(c, true, c->s_offsets, offsets, (n + 1) * 8, b0);
+    // offsets cross PCIe as u32 when the blob is under 4 GiB (widened on the device, in
+    // s_fp's space: the build writes s_fp only later on the same stream)
+    if (nbytes < (1ull << 32)) {
+      uint32_t* tmp32 = reinterpret_cast<uint32_t*>(c->s_fp);
+      staged_copy(c, true, tmp32, offsets, (n + 1) * 4, b0, 1);
+      launch_widen32(tmp32, c->s_offsets, n + 1, s);
+    } else {
+      staged_copy(c, true, c->s_offsets, offsets, (n + 1) * 8, b0);
+    }
     if (pos) staged_copy(c, true, c->s_pos, pos, n * 8);
     const auto t1 = clk::now();
     s3imph_build_info info;
@@ -1064,7 +1086,14 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
     if (rc != S3IMPH_OK) return rc;
     const auto t2 = clk::now();
     staged_copy(c, false, fp_out, c->s_fp, n * 8);
-    staged_copy(c, false, pos_out, c->s_posout, n * 8);
+    if (!pos) {  // identity positions are < n < 2^32: u32 over PCIe (offsets' space is free now)
+      uint32_t* tmp32 = reinterpret_cast<uint32_t*>(c->s_offsets);
+      launch_narrow32(c->s_posout, tmp32, n, s);
+      HIPCHECK(hipStreamSynchronize(s));
+      staged_copy(c, false, pos_out, tmp32, n * 4, 0, 2);
+    } else {
+      staged_copy(c, false, pos_out, c->s_posout, n * 8);
+    }
     const auto t3 = clk::now();
     mph->resize(info.mph_bin_len);
     uint64_t len = 0;

@@ -199,7 +199,11 @@ int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
 uint64_t dist_out_cap(const s3imph_ctx* c, uint64_t n_global);
 // Chunked host <-> device copy through the ctx's pinned stager (h2d: device dst <- host src;
 // with `bias`, src holds u64 words stored minus bias).
-void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias = 0);
+// conv 1: host u64 -> device u32 (h2d), conv 2: device u32 -> host u64 (d2h); `bytes` are device bytes.
+void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias = 0,
+                 int conv = 0);
+void launch_widen32(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);
+void launch_narrow32(const uint64_t* in, uint32_t* out, uint64_t n, hipStream_t s);
 int marshal_locked(s3imph_ctx* c, uint8_t* out, uint64_t cap, uint64_t* len, std::string* msg);
 // A context (s3imph_ctx_create) whose multi-GPU collectives go through `comm` (owned).
 s3imph_ctx* make_dist_ctx(int device, Comm* comm, int rank, int nranks, std::string* msg);

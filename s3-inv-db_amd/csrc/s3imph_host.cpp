@@ -4,6 +4,7 @@
 // Reference: pkg/format/mphf_streaming.go (builder, :29-232), pkg/format/writer.go
 // (ArrayWriter :11-145, BlobWriter :148-246), pkg/format/format.go (header :6-45).
 #include <errno.h>
+#include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -45,68 +46,100 @@ void s3id_header(uint8_t out[kS3idHeaderSize], uint64_t count, uint32_t width) {
   put_le32(out + 16, width);
 }
 
-struct File {
-  FILE* f = nullptr;
-  ~File() {
-    if (f) std::fclose(f);
-  }
-};
-
 bool write_all(FILE* f, const void* p, size_t n) { return n == 0 || std::fwrite(p, 1, n, f) == n; }
 
+// Large files are written by several threads, each pwrite()-ing its own byte range
+// (the reference writes its two arrays in parallel goroutines, mphf_streaming.go:546-596;
+// here every big file is split as well).
+constexpr uint64_t kParMin = 32ull << 20;  // files from this size on are split
+constexpr int kWriters = 8;
+
+int writers_for(uint64_t bytes) { return bytes < kParMin ? 1 : (int)std::min<uint64_t>(kWriters, bytes / (16ull << 20)); }
+
+bool pwrite_all(int fd, const void* p, uint64_t n, uint64_t off) {
+  const uint8_t* q = static_cast<const uint8_t*>(p);
+  while (n) {
+    const ssize_t w = ::pwrite(fd, q, std::min<uint64_t>(n, 1ull << 30), (off_t)off);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    q += w;
+    n -= (uint64_t)w;
+    off += (uint64_t)w;
+  }
+  return true;
+}
+
+// Runs part(k, lo, hi) for k-th of T contiguous shares of [0, n) (T threads; part 0 here).
+template <class F>
+bool split_run(uint64_t n, int T, const F& part) {
+  std::vector<char> ok(T, 1);
+  std::vector<std::thread> th;
+  for (int k = 1; k < T; ++k) th.emplace_back([&, k] { ok[k] = part(n * k / T, n * (k + 1) / T); });
+  ok[0] = part(0, n / T);
+  for (auto& t : th) t.join();
+  for (char c : ok)
+    if (!c) return false;
+  return true;
+}
+
 // ArrayWriter of width 8 holding `n` values (+ an optional trailing sentinel), each
-// value = src[i] - bias.  Writes in 1 MiB chunks.
+// value = src[i] - bias, little endian.
 bool write_u64_array(const std::string& path, const uint64_t* src, uint64_t n, uint64_t bias,
                      std::string* msg) {
-  File fh;
-  fh.f = std::fopen(path.c_str(), "wb");
-  if (!fh.f) {
+  const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+  if (fd < 0) {
     *msg = "create array file: open " + path + ": " + std::strerror(errno);
     return false;
   }
   uint8_t hdr[kS3idHeaderSize];
   s3id_header(hdr, n, 8);
-  if (!write_all(fh.f, hdr, sizeof hdr)) {
+  if (!pwrite_all(fd, hdr, sizeof hdr, 0)) {
+    ::close(fd);
     *msg = "write header: " + path;
     return false;
   }
-  std::vector<uint8_t> buf(1 << 20);
-  uint64_t i = 0;
-  while (i < n) {
-    const uint64_t k = std::min<uint64_t>(n - i, buf.size() / 8);
-    for (uint64_t t = 0; t < k; ++t) put_le64(buf.data() + 8 * t, src[i + t] - bias);
-    if (!write_all(fh.f, buf.data(), 8 * k)) {
-      *msg = "write u64 batch: " + path;
-      return false;
+  const bool ok = split_run(n, writers_for(8 * n), [&](uint64_t lo, uint64_t hi) {
+    std::vector<uint8_t> buf(1 << 20);
+    for (uint64_t i = lo; i < hi;) {
+      const uint64_t k = std::min<uint64_t>(hi - i, buf.size() / 8);
+      for (uint64_t t = 0; t < k; ++t) put_le64(buf.data() + 8 * t, src[i + t] - bias);
+      if (!pwrite_all(fd, buf.data(), 8 * k, kS3idHeaderSize + 8 * i)) return false;
+      i += k;
     }
-    i += k;
+    return true;
+  });
+  if (!ok) {
+    ::close(fd);
+    *msg = "write u64 batch: " + path;
+    return false;
   }
-  if (std::fclose(fh.f) != 0) {
-    fh.f = nullptr;
+  if (::close(fd) != 0) {
     *msg = "close file: " + path;
     return false;
   }
-  fh.f = nullptr;
   return true;
 }
 
 bool write_raw(const std::string& path, const uint8_t* p, uint64_t n, std::string* msg) {
-  File fh;
-  fh.f = std::fopen(path.c_str(), "wb");
-  if (!fh.f) {
+  const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+  if (fd < 0) {
     *msg = "create " + path + ": " + std::strerror(errno);
     return false;
   }
-  if (!write_all(fh.f, p, n)) {
+  const bool ok = split_run(n, writers_for(n), [&](uint64_t lo, uint64_t hi) {
+    return pwrite_all(fd, p + lo, hi - lo, lo);
+  });
+  if (!ok) {
+    ::close(fd);
     *msg = "write " + path;
     return false;
   }
-  if (std::fclose(fh.f) != 0) {
-    fh.f = nullptr;
+  if (::close(fd) != 0) {
     *msg = "close " + path;
     return false;
   }
-  fh.f = nullptr;
   return true;
 }
 
@@ -117,28 +150,22 @@ bool is_dir(const std::string& p) {
 
 }  // namespace
 
-int write_index_files(const std::string& dir, const uint8_t* mph_bin, uint64_t mph_len, const uint64_t* fp,
-                      const uint64_t* pos, uint64_t n, const uint8_t* blob, const uint64_t* offsets,
-                      std::string* msg) {
+// mph.bin (mphf_streaming.go:152-169; 0 bytes for the empty set, :509).  On a
+// marshal/write failure the reference removes the partial file (:159-168).
+int write_mph_file(const std::string& dir, const uint8_t* mph_bin, uint64_t mph_len, std::string* msg) {
   const std::string mph_path = dir + "/mph.bin";
-  // mph.bin (mphf_streaming.go:152-169; 0 bytes for the empty set, :509).  On a
-  // marshal/write failure the reference removes the partial file (:159-168).
   if (!write_raw(mph_path, mph_bin, mph_len, msg)) {
     ::unlink(mph_path.c_str());
     *msg = "write MPHF: " + *msg;
     return S3IMPH_ERR_IO;
   }
-  // mph_fp.u64 / mph_pos.u64 (writeArraysParallel :546-596).
-  if (!write_u64_array(dir + "/mph_fp.u64", fp, n, 0, msg)) {
-    *msg = "write fingerprints: " + *msg;
-    return S3IMPH_ERR_IO;
-  }
-  if (!write_u64_array(dir + "/mph_pos.u64", pos, n, 0, msg)) {
-    *msg = "write positions: " + *msg;
-    return S3IMPH_ERR_IO;
-  }
-  // prefix_blob.bin + prefix_offsets.u64 (writePrefixBlobPreorder :453-504, BlobWriter
-  // writer.go:148-237): N offsets plus the sentinel, counted N+1 in the header.
+  return S3IMPH_OK;
+}
+
+// prefix_blob.bin + prefix_offsets.u64 (writePrefixBlobPreorder :453-504, BlobWriter
+// writer.go:148-237): N offsets plus the sentinel, counted N+1 in the header.
+int write_prefix_files(const std::string& dir, const uint8_t* blob, const uint64_t* offsets, uint64_t n,
+                       std::string* msg) {
   static const uint64_t kZero = 0;
   const uint64_t base = (n && offsets) ? offsets[0] : 0;
   const uint64_t nbytes = (n && offsets) ? offsets[n] - base : 0;
@@ -153,11 +180,88 @@ int write_index_files(const std::string& dir, const uint8_t* mph_bin, uint64_t m
   return S3IMPH_OK;
 }
 
+int write_index_files(const std::string& dir, const uint8_t* mph_bin, uint64_t mph_len, const uint64_t* fp,
+                      const uint64_t* pos, uint64_t n, const uint8_t* blob, const uint64_t* offsets,
+                      std::string* msg) {
+  int rc = write_mph_file(dir, mph_bin, mph_len, msg);
+  if (rc != S3IMPH_OK) return rc;
+  // mph_fp.u64 / mph_pos.u64 (writeArraysParallel :546-596), the two in parallel
+  std::string pmsg;
+  bool pos_ok = true;
+  std::thread tp([&] { pos_ok = write_u64_array(dir + "/mph_pos.u64", pos, n, 0, &pmsg); });
+  const bool fp_ok = write_u64_array(dir + "/mph_fp.u64", fp, n, 0, msg);
+  tp.join();
+  if (!fp_ok) {
+    *msg = "write fingerprints: " + *msg;
+    return S3IMPH_ERR_IO;
+  }
+  if (!pos_ok) {
+    *msg = "write positions: " + pmsg;
+    return S3IMPH_ERR_IO;
+  }
+  return write_prefix_files(dir, blob, offsets, n, msg);
+}
+
+namespace {
+
+static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "array files are written from memory as little endian");
+
+// mph_fp.u64 / mph_pos.u64 written as Build's chunks arrive (feed_build): the header
+// first, then each chunk straight from the pinned buffer it landed in.
+struct ArrayFileSink : FeedSink {
+  FILE* f[2] = {nullptr, nullptr};
+  std::string path[2], err[2];
+  ArrayFileSink(const std::string& dir, uint64_t n) {
+    path[0] = dir + "/mph_fp.u64";
+    path[1] = dir + "/mph_pos.u64";
+    for (int a = 0; a < 2; ++a) {
+      f[a] = std::fopen(path[a].c_str(), "wb");
+      if (!f[a]) {
+        err[a] = "create array file: open " + path[a] + ": " + std::strerror(errno);
+        continue;
+      }
+      uint8_t hdr[kS3idHeaderSize];
+      s3id_header(hdr, n, 8);
+      if (!write_all(f[a], hdr, sizeof hdr)) err[a] = "write header: " + path[a];
+    }
+  }
+  ~ArrayFileSink() override {
+    for (int a = 0; a < 2; ++a)
+      if (f[a]) std::fclose(f[a]);
+  }
+  bool put(int a, const uint64_t* v, uint64_t cnt) override {
+    if (!err[a].empty()) return false;
+    if (!write_all(f[a], v, 8 * cnt)) {
+      err[a] = "write u64 batch: " + path[a];
+      return false;
+    }
+    return true;
+  }
+  // close both; the first failure in the reference's order (fingerprints, positions)
+  std::string finish() {
+    for (int a = 0; a < 2; ++a) {
+      if (f[a] && std::fclose(f[a]) != 0 && err[a].empty()) err[a] = "close file: " + path[a];
+      f[a] = nullptr;
+    }
+    if (!err[0].empty()) return "write fingerprints: " + err[0];
+    if (!err[1].empty()) return "write positions: " + err[1];
+    return "";
+  }
+  std::string error() const override {
+    return !err[0].empty() ? "write fingerprints: " + err[0] : "write positions: " + err[1];
+  }
+};
+
+}  // namespace
+
 }  // namespace s3imph
 
 using namespace s3imph;
 
 // --------------------------------------------------------------- builder mirror ----
+// Add keeps the keys in host vectors (for prefix_blob.bin / prefix_offsets.u64 and the
+// multi-GPU path) and, on a single GPU, also feeds them to the device as they arrive
+// (s3imph_feed.hip), so Build starts with the key set already in HBM.
 struct s3imph_builder {
   int device = 0;
   std::vector<int> devices;  // s3imph_builder_set_gpus (empty: `device` alone)
@@ -168,6 +272,25 @@ struct s3imph_builder {
   std::vector<uint64_t> pos;
   uint64_t count = 0;
   bool built = false;
+  Feed* feed = nullptr;
+  bool feed_off = false;  // multi-GPU, or the feed failed once: Build copies from the host vectors
+  ~s3imph_builder() { feed_free(feed); }
+  // the keys [i0, count) just appended to the host vectors, into the device feed
+  void feed_keys(uint64_t i0) {
+    if (feed_off) return;
+    std::string m;
+    if (!feed && !(feed = feed_new(device, &m))) {
+      feed_off = true;
+      return;
+    }
+    const uint64_t b0 = offsets[i0], b1 = offsets[count];
+    if (feed_append(feed, blob.data() + b0, b1 - b0, offsets.data() + i0 + 1, pos.data() + i0, count - i0, &m) !=
+        S3IMPH_OK) {
+      feed_off = true;
+      feed_free(feed);
+      feed = nullptr;
+    }
+  }
 };
 
 extern "C" {
@@ -204,6 +327,7 @@ int s3imph_builder_add(s3imph_builder* b, const uint8_t* prefix, uint64_t len, u
     b->offsets.push_back(b->blob.size());
     b->pos.push_back(pos);
     ++b->count;
+    b->feed_keys(b->count - 1);
     return S3IMPH_OK;
   } catch (const std::bad_alloc&) {
     set_err(err, errlen, "write prefix: out of host memory");
@@ -223,13 +347,19 @@ int s3imph_builder_add_batch(s3imph_builder* b, const uint8_t* blob, const uint6
   try {
     const uint64_t base = offsets[0], nbytes = offsets[n] - base, shift = b->blob.size();
     b->blob.insert(b->blob.end(), blob + base, blob + base + nbytes);
-    b->offsets.reserve(b->offsets.size() + n);
-    b->pos.reserve(b->pos.size() + n);
-    for (uint64_t i = 0; i < n; ++i) {
-      b->offsets.push_back(offsets[i + 1] - base + shift);
-      b->pos.push_back(pos ? pos[i] : b->count + i);
+    const size_t o0 = b->offsets.size(), p0 = b->pos.size();
+    b->offsets.resize(o0 + n);
+    b->pos.resize(p0 + n);
+    uint64_t* od = b->offsets.data() + o0;
+    uint64_t* pd = b->pos.data() + p0;
+    for (uint64_t i = 0; i < n; ++i) od[i] = offsets[i + 1] - base + shift;
+    if (pos) {
+      std::memcpy(pd, pos, n * 8);
+    } else {
+      for (uint64_t i = 0; i < n; ++i) pd[i] = b->count + i;
     }
     b->count += n;
+    b->feed_keys(b->count - n);
     return S3IMPH_OK;
   } catch (const std::bad_alloc&) {
     set_err(err, errlen, "write prefix: out of host memory");
@@ -253,6 +383,41 @@ int s3imph_builder_build(s3imph_builder* b, const char* out_dir, char* err, size
   std::string msg;
   try {
     const uint64_t n = b->count;
+    if (n && b->feed && !b->feed_off && b->devices.empty() && feed_count(b->feed) == n) {
+      // the keys are on the device already: the prefix files are written meanwhile (they
+      // do not depend on the build), the arrays as their chunks come back
+      std::string pmsg;
+      int prc = S3IMPH_OK;
+      std::thread tp([&] { prc = write_prefix_files(dir, b->blob.data(), b->offsets.data(), n, &pmsg); });
+      std::vector<uint8_t> mph;
+      int rc;
+      std::string amsg;
+      {
+        ArrayFileSink sink(dir, n);
+        rc = feed_build(b->feed, &mph, &sink, &msg);
+        amsg = sink.finish();
+      }
+      if (rc == S3IMPH_OK) {
+        rc = write_mph_file(dir, mph.data(), mph.size(), &msg);
+        if (rc == S3IMPH_OK && !amsg.empty()) {
+          rc = S3IMPH_ERR_IO;
+          msg = amsg;
+        }
+      }
+      tp.join();
+      if (rc == S3IMPH_OK && prc != S3IMPH_OK) {
+        rc = prc;
+        msg = pmsg;
+      }
+      if (rc != S3IMPH_OK) {
+        set_err(err, errlen, msg);
+        return rc;
+      }
+      b->built = true;
+      feed_free(b->feed);  // the device copy is no longer needed
+      b->feed = nullptr;
+      return S3IMPH_OK;
+    }
     std::vector<uint64_t> fp(n), pos_out(n);
     std::vector<uint8_t> mph;
     if (n) {
@@ -286,6 +451,9 @@ int s3imph_builder_set_gpus(s3imph_builder* b, int num_gpus, const int* devices,
   b->devices.resize(num_gpus);
   for (int r = 0; r < num_gpus; ++r) b->devices[r] = devices ? devices[r] : r;
   b->multi_flags = flags;
+  b->feed_off = true;  // the multi-GPU build shards from the host vectors
+  feed_free(b->feed);
+  b->feed = nullptr;
   return S3IMPH_OK;
 }
 

@@ -211,6 +211,24 @@ int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const ui
                           const uint64_t* pos, uint64_t n, uint64_t* fp_out, uint64_t* pos_out,
                           std::vector<uint8_t>* mph, std::string* msg);
 
+// ---- the builder mirror's feed (s3imph_feed.hip) ------------------------------------
+// Keys appended by Add go through pinned chunks to device arrays as they arrive; Build
+// runs on those and streams mph_fp (array 0) / mph_pos (array 1) to a sink chunk by
+// chunk, one thread per array.
+struct FeedSink {
+  virtual ~FeedSink() = default;
+  virtual bool put(int arr, const uint64_t* v, uint64_t cnt) = 0;  // false: stop taking data
+  virtual std::string error() const = 0;
+};
+struct Feed;
+Feed* feed_new(int device, std::string* msg);
+void feed_free(Feed* f);
+// n keys: their bytes, their end offsets in the builder's blob, their positions
+int feed_append(Feed* f, const uint8_t* bytes, uint64_t nbytes, const uint64_t* ends, const uint64_t* pos, uint64_t n,
+                std::string* msg);
+uint64_t feed_count(const Feed* f);
+int feed_build(Feed* f, std::vector<uint8_t>* mph, FeedSink* sink, std::string* msg);
+
 // ---- host helpers (s3imph_host.cpp) -------------------------------------------
 void set_err(char* err, size_t errlen, const std::string& msg);
 int write_index_files(const std::string& dir, const uint8_t* mph_bin, uint64_t mph_len,

@@ -237,6 +237,18 @@ __global__ __launch_bounds__(kBlock) void k_lookup(const uint8_t* __restrict__ b
   }
 }
 
+// u32 <-> u64 conversion of a staged host array (offsets in, identity positions out):
+// one element per thread per grid stride (HBM-bound; a few µs per 10M elements).
+__global__ __launch_bounds__(256) void k_widen32(const uint32_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                 uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) out[i] = in[i];
+}
+__global__ __launch_bounds__(256) void k_narrow32(const uint64_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                  uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    out[i] = (uint32_t)in[i];
+}
+
 }  // namespace
 
 // ================================ launchers =======================================
@@ -266,6 +278,13 @@ void launch_lookup(const uint8_t* blob, const uint64_t* offsets, uint64_t n, con
                    const uint64_t* rank_base, const LevelState* st, const uint64_t* fp,
                    const uint64_t* pos, uint64_t count, uint64_t* result, int grid, hipStream_t s) {
   k_lookup<<<grid, kBlock, 0, s>>>(blob, offsets, n, bits, rank_base, st, fp, pos, count, result);
+}
+
+void launch_widen32(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s) {
+  if (n) k_widen32<<<(unsigned)std::min<uint64_t>(8192, (n + 255) / 256), 256, 0, s>>>(in, out, n);
+}
+void launch_narrow32(const uint64_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
+  if (n) k_narrow32<<<(unsigned)std::min<uint64_t>(8192, (n + 255) / 256), 256, 0, s>>>(in, out, n);
 }
 
 }  // namespace s3imph

@@ -48,6 +48,24 @@ def test_write_index_files_matches_reference_framing(tmp_path, oracle_lib):
         assert (tmp_path / name).read_bytes() == data, name
 
 
+def test_write_files_split_over_writer_threads(tmp_path):
+    """Files of 32 MiB and more are written by several threads, each pwrite()-ing its
+    own range: large arrays (6M values, 48 MB) and a large blob (70 MB, not a multiple of
+    the split) still come out byte-identical to the reference framing."""
+    rng = np.random.default_rng(3)
+    n = 6_000_000
+    fp = rng.integers(0, 2**63, n, dtype=np.uint64)
+    pos = rng.permutation(n).astype(np.uint64)
+    blob = rng.integers(0, 256, 70_000_003, dtype=np.uint8)
+    offs = np.linspace(0, len(blob), n + 1).astype(np.uint64)
+    offs[-1] = len(blob)
+    s3imph.write_index_files(str(tmp_path), b"xyz", fp, pos, blob, offs)
+    assert (tmp_path / "mph_fp.u64").read_bytes() == O.s3id_u64_array(fp)
+    assert (tmp_path / "mph_pos.u64").read_bytes() == O.s3id_u64_array(pos)
+    assert (tmp_path / "prefix_blob.bin").read_bytes() == blob.tobytes()
+    assert (tmp_path / "prefix_offsets.u64").read_bytes() == O.s3id_u64_array(offs)
+
+
 def test_write_empty_matches_writeEmpty(tmp_path):
     """mphf_streaming.go:506-541: 0-byte mph.bin, count-0 arrays, offsets = [0] (count 1), empty blob."""
     s3imph.write_index_files(str(tmp_path), b"", np.zeros(0, np.uint64), np.zeros(0, np.uint64),

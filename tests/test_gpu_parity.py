@@ -101,6 +101,52 @@ def test_builder_writes_identical_files(s3, oracle_lib, tmp_path):
         assert (out / name).read_bytes() == data, name
 
 
+def test_builder_feed_many_chunks(s3, oracle_lib, tmp_path):
+    """f3 + f2: Add streams the keys to the GPU through 8 MiB pinned chunks while the caller
+    is still adding (2.5M keys, ~80 MB of blob: past the feed's first 64 MiB device
+    buffer, so it grows), in batches of 100k with custom positions, then single Adds;
+    Build writes mph_fp / mph_pos as their chunks come back and the prefix files beside
+    the build.  The 5 files equal the oracle's."""
+    n = 2_500_000
+    blob, offs = s3.gen_keys(0, 21, 32, 0, n)
+    blob = blob[: int(offs[-1])]
+    pos = np.random.default_rng(5).permutation(n).astype(np.uint64) + np.uint64(7)
+    b = s3.StreamingMPHFBuilder(str(tmp_path))
+    tail = n - 10
+    for lo in range(0, tail, 100_000):
+        hi = min(lo + 100_000, tail)
+        b.add_batch(blob, offs[lo:hi + 1], pos[lo:hi])
+    for i in range(tail, n):
+        b.add(bytes(blob[offs[i]:offs[i + 1]]), int(pos[i]))
+    assert b.count() == n
+    out = tmp_path / "idx"
+    out.mkdir()
+    b.build(str(out))
+    b.close()
+    st, fp, po, mph = oracle_lib.build_mt(blob, offs, pos, threads=16)
+    assert st == 0
+    want = {"mph.bin": mph, "mph_fp.u64": O.s3id_u64_array(fp), "mph_pos.u64": O.s3id_u64_array(po),
+            "prefix_blob.bin": blob.tobytes(), "prefix_offsets.u64": O.s3id_u64_array(offs)}
+    for name, data in want.items():
+        assert (out / name).read_bytes() == data, name
+
+
+def test_builder_feed_duplicate_keys_error(s3, tmp_path):
+    """A duplicate key fed through the device feed fails Build with the duplicate-hash
+    status; no half-written success is reported."""
+    keys = [b"p/%06d/" % i for i in range(50_000)]
+    keys[40_000] = keys[123]
+    b = s3.StreamingMPHFBuilder(str(tmp_path))
+    for i, k in enumerate(keys):
+        b.add(k, i)
+    out = tmp_path / "idx"
+    out.mkdir()
+    with pytest.raises(s3.MPHFError) as e:
+        b.build(str(out))
+    assert e.value.status == s3.ERR_DUP_KEY_HASH
+    b.close()
+
+
 def test_build_host_roundtrip_lookup(s3, oracle_lib):
     """build_host + the oracle's Lookup restatement: every member -> its pos (VerifyMPHF)."""
     keys = [k.encode() for k in keysets.mphf_test_sets()["mphf_no_false_pos"]]
