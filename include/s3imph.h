@@ -235,6 +235,35 @@ int s3imph_lookup_device(s3imph_ctx *ctx, const uint8_t *d_blob, const uint64_t 
                          uint64_t *d_result, void *stream);
 
 /* ------------------------------------------------------------------------
+ * 5b. The rest of IndexBuilder.Finalize (pkg/extsort/indexbuild.go:393-415,
+ *     474-503; pkg/format/depthindex.go:32-96), from the same sorted prefix blob:
+ *       depth.u32                 per prefix: row.Depth (indexbuild.go:185), or when
+ *                                 depths == NULL the aggregator's '/' count
+ *                                 (aggregator.go:44-60);
+ *       subtree_end.u64           last position of the prefix's subtree (the ancestor
+ *                                 stack, indexbuild.go:154-248);
+ *       max_depth_in_subtree.u32  deepest depth in that subtree;
+ *       depth_offsets.u64         maxDepth + 2 offsets into depth_positions;
+ *       depth_positions.u64       positions grouped by depth, ascending in a depth.
+ *     Positions are the Add order 0..n-1 (indexbuild.go:160).  The prefixes must be
+ *     byte-sorted (the reference's Add order); the blob on the device is readable up to
+ *     round_up(offsets[n], 8) as for the build.
+ * ------------------------------------------------------------------------ */
+/* Replaces DepthIndexBuilder.Build + writeSubtreeArrays + the depth.u32 writer: computes
+ * on `device` and writes the five files into out_dir (S3ID framing, format.go:25-32). */
+int s3imph_finalize_index_host(int device, const uint8_t *blob, const uint64_t *offsets,
+                               const uint32_t *depths, uint64_t n, const char *out_dir, char *err,
+                               size_t errlen);
+/* Device form: all arrays in HBM (depths nullable).  depth_offsets holds offsets_cap
+ * entries; *max_depth receives maxDepth, and S3IMPH_ERR_INVALID comes back (outputs other
+ * than depth undefined) when offsets_cap < maxDepth + 2.  Synchronous on `stream`. */
+int s3imph_finalize_index_device(s3imph_ctx *ctx, const uint8_t *d_blob, const uint64_t *d_offsets,
+                                 const uint32_t *d_depths, uint64_t n, uint32_t *d_depth,
+                                 uint64_t *d_subtree_end, uint32_t *d_max_depth_in_subtree,
+                                 uint64_t *d_depth_positions, uint64_t *d_depth_offsets,
+                                 uint64_t offsets_cap, uint32_t *max_depth, void *stream);
+
+/* ------------------------------------------------------------------------
  * 6. Deterministic synthetic prefix sets (bench/test support, not on the path).
  *    kind: 0 = s3-like, lengths uniform in [max(10, avg/2), 3avg/2],
  *              distinct and byte-sorted;

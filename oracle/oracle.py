@@ -123,6 +123,8 @@ class OracleLib:
         lib.orc_key_hash.argtypes = [u64, u64]
         lib.orc_level_words.restype = u64
         lib.orc_level_words.argtypes = [u64]
+        lib.orc_finalize.restype = ctypes.c_int
+        lib.orc_finalize.argtypes = [vp, vp, vp, u64, vp, vp, vp, vp, u64, vp, ctypes.POINTER(ctypes.c_uint32)]
         self.lib = lib
         del u8p
 
@@ -201,6 +203,30 @@ class OracleLib:
         posp = None if pos is None else _ptr(np.ascontiguousarray(pos, np.uint64))
         st = self.lib.orc_build_revmap(_ptr(blob), _ptr(offsets), posp, n, _ptr(fp_out), _ptr(pos_out))
         return st, fp_out, pos_out
+
+    def finalize(self, blob: np.ndarray, offsets: np.ndarray, depths: np.ndarray | None = None) -> dict:
+        """IndexBuilder's finalize arrays (indexbuild.go:154-248,393-415,474-503; depthindex.go:32-96):
+        depth, subtree_end, max_depth_in_subtree, depth_offsets, depth_positions, max_depth."""
+        n = len(offsets) - 1
+        blob = np.ascontiguousarray(blob, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        dp = None if depths is None else _ptr(np.ascontiguousarray(depths, np.uint32))
+        depth = np.zeros(n, np.uint32)
+        send = np.zeros(n, np.uint64)
+        mds = np.zeros(n, np.uint32)
+        dpos = np.zeros(n, np.uint64)
+        maxd = ctypes.c_uint32()
+        cap = 64
+        while True:
+            doff = np.zeros(cap, np.uint64)
+            rc = self.lib.orc_finalize(_ptr(blob), _ptr(offsets), dp, n, _ptr(depth), _ptr(send), _ptr(mds),
+                                       _ptr(doff), cap, _ptr(dpos), ctypes.byref(maxd))
+            if rc != -1:
+                break
+            cap = maxd.value + 2
+        assert rc == 0
+        return {"depth": depth, "subtree_end": send, "max_depth_in_subtree": mds,
+                "depth_offsets": doff[: maxd.value + 2].copy(), "depth_positions": dpos, "max_depth": maxd.value}
 
     def lookup(self, mph: OracleMPHF | None, fp_arr: np.ndarray, pos_arr: np.ndarray, key: bytes):
         out = ctypes.c_uint64()
@@ -322,6 +348,38 @@ def py_build(keys: list[bytes], pos: list[int] | None = None):
 # ---------------------------------------------------------------------------
 # S3ID framing (format.go:6-45; writer.go:19-46,113-140,212-237)
 # ---------------------------------------------------------------------------
+
+def py_finalize(keys: list[bytes], depths: list[int] | None = None) -> dict:
+    """Pure-Python restatement of the finalize arrays (small inputs): the subtree of prefix
+    i is every later key it is a byte prefix of (keys are sorted, so a run), as the
+    ancestor stack of indexbuild.go:201-248 produces; depth index per depthindex.go:32-96."""
+    n = len(keys)
+    depth = [k.count(b"/") for k in keys] if depths is None else list(depths)
+    send, mds = [0] * n, [0] * n
+    for i in range(n):
+        j = i
+        while j + 1 < n and keys[j + 1].startswith(keys[i]):
+            j += 1
+        # the stack closes node i at the first later key it is not a prefix of ... unless
+        # an entry below it on the stack closes first; every entry below i is a prefix of
+        # keys[i], hence of every key in its run, so the run is exact
+        send[i] = j
+        mds[i] = max(depth[i:j + 1])
+    maxd = max(depth) if n else 0
+    offs, dpos = [], []
+    for d in range(maxd + 1):
+        offs.append(len(dpos))
+        dpos.extend(i for i in range(n) if depth[i] == d)
+    offs.append(len(dpos))
+    return {"depth": depth, "subtree_end": send, "max_depth_in_subtree": mds, "depth_offsets": offs,
+            "depth_positions": dpos, "max_depth": maxd}
+
+
+def s3id_u32_array(vals) -> bytes:
+    """ArrayWriter of width 4 (format.go:25-32, writer.go:113-140)."""
+    vals = list(vals)
+    return s3id_header(len(vals), 4) + b"".join(struct.pack("<I", int(v)) for v in vals)
+
 
 def s3id_header(count: int, width: int = 8) -> bytes:
     return struct.pack("<IIQI", S3ID_MAGIC, S3ID_VERSION, count, width)

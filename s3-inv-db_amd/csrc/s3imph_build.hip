@@ -1197,6 +1197,7 @@ int s3imph_ctx_destroy(s3imph_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   free_workspace(c);
+  fin_scratch_free(c);
   delete c->d.comm;
   c->d.comm = nullptr;
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

@@ -133,8 +133,13 @@ using s3imph::LevelState;
 using s3imph::Rec;
 using s3imph::Stager;
 
+namespace s3imph {
+struct FinScratch;  // s3imph_finalize.hip
+}
+
 struct s3imph_ctx {
   int device = 0;
+  s3imph::FinScratch* fin = nullptr;  // finalize-pass scratch (s3imph_finalize.hip), lazily made
   hipStream_t own_stream = nullptr;
   std::mutex mu;
 
@@ -205,6 +210,14 @@ void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t b
 void launch_widen32(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);
 void launch_narrow32(const uint64_t* in, uint32_t* out, uint64_t n, hipStream_t s);
 int marshal_locked(s3imph_ctx* c, uint8_t* out, uint64_t cap, uint64_t* len, std::string* msg);
+// Index finalize arrays (s3imph_finalize.hip): device pass over keys in HBM, and the
+// host-memory form that writes the five files.
+int finalize_device(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint32_t* depths, uint64_t n,
+                    uint32_t* depth, uint64_t* subtree_end, uint32_t* max_depth_sub, uint64_t* depth_positions,
+                    uint64_t* depth_offsets, uint64_t doff_cap, uint32_t* max_depth, hipStream_t s, std::string* msg);
+int finalize_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint32_t* depths, uint64_t n,
+                       const std::string& dir, std::string* msg);
+void fin_scratch_free(s3imph_ctx* c);
 // A context (s3imph_ctx_create) whose multi-GPU collectives go through `comm` (owned).
 s3imph_ctx* make_dist_ctx(int device, Comm* comm, int rank, int nranks, std::string* msg);
 

@@ -122,6 +122,39 @@ bool write_u64_array(const std::string& path, const uint64_t* src, uint64_t n, u
   return true;
 }
 
+// ArrayWriter of width 4 (depth.u32, max_depth_in_subtree.u32; writer.go:113-140).
+bool write_u32_array(const std::string& path, const uint32_t* src, uint64_t n, std::string* msg) {
+  const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+  if (fd < 0) {
+    *msg = "create array file: open " + path + ": " + std::strerror(errno);
+    return false;
+  }
+  uint8_t hdr[kS3idHeaderSize];
+  s3id_header(hdr, n, 4);
+  bool ok = pwrite_all(fd, hdr, sizeof hdr, 0);
+  if (ok)
+    ok = split_run(n, writers_for(4 * n), [&](uint64_t lo, uint64_t hi) {
+      std::vector<uint8_t> buf(1 << 20);
+      for (uint64_t i = lo; i < hi;) {
+        const uint64_t k = std::min<uint64_t>(hi - i, buf.size() / 4);
+        for (uint64_t t = 0; t < k; ++t) put_le32(buf.data() + 4 * t, src[i + t]);
+        if (!pwrite_all(fd, buf.data(), 4 * k, kS3idHeaderSize + 4 * i)) return false;
+        i += k;
+      }
+      return true;
+    });
+  if (!ok) {
+    ::close(fd);
+    *msg = "write u32 batch: " + path;
+    return false;
+  }
+  if (::close(fd) != 0) {
+    *msg = "close file: " + path;
+    return false;
+  }
+  return true;
+}
+
 bool write_raw(const std::string& path, const uint8_t* p, uint64_t n, std::string* msg) {
   const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
   if (fd < 0) {
@@ -175,6 +208,40 @@ int write_prefix_files(const std::string& dir, const uint8_t* blob, const uint64
   }
   if (!write_u64_array(dir + "/prefix_offsets.u64", n ? offsets : &kZero, n + 1, base, msg)) {
     *msg = "write prefix blob: " + *msg;
+    return S3IMPH_ERR_IO;
+  }
+  return S3IMPH_OK;
+}
+
+// The finalize arrays, in the reference's order and with its messages: depth.u32 (closed
+// with the streaming writers, indexbuild.go:449-457), subtree_end.u64 and
+// max_depth_in_subtree.u32 (:474-503), then the depth index (depthindex.go:32-96).
+int write_finalize_files(const std::string& dir, const uint32_t* depth, const uint64_t* subtree_end,
+                         const uint32_t* max_depth_sub, const uint64_t* depth_offsets, uint64_t n_offsets,
+                         const uint64_t* depth_positions, uint64_t n, std::string* msg) {
+  if (!is_dir(dir)) {
+    *msg = "create depth writer: open " + dir + "/depth.u32: no such directory";
+    return S3IMPH_ERR_IO;
+  }
+  std::string m;
+  if (!write_u32_array(dir + "/depth.u32", depth, n, &m)) {
+    *msg = "write depth: " + m;
+    return S3IMPH_ERR_IO;
+  }
+  if (!write_u64_array(dir + "/subtree_end.u64", subtree_end, n, 0, &m)) {
+    *msg = "write subtree_end: " + m;
+    return S3IMPH_ERR_IO;
+  }
+  if (!write_u32_array(dir + "/max_depth_in_subtree.u32", max_depth_sub, n, &m)) {
+    *msg = "write max_depth_in_subtree: " + m;
+    return S3IMPH_ERR_IO;
+  }
+  if (!write_u64_array(dir + "/depth_offsets.u64", depth_offsets, n_offsets, 0, &m)) {
+    *msg = "build depth index: write offset: " + m;
+    return S3IMPH_ERR_IO;
+  }
+  if (!write_u64_array(dir + "/depth_positions.u64", depth_positions, n, 0, &m)) {
+    *msg = "build depth index: write position: " + m;
     return S3IMPH_ERR_IO;
   }
   return S3IMPH_OK;

@@ -60,6 +60,7 @@ EXPORTS = (
     "s3imph_dist_unique_id", "s3imph_ctx_create_dist", "s3imph_ctx_create_dist_host", "s3imph_build_device_dist",
     "s3imph_dist_segments", "s3imph_dist_out_cap", "s3imph_ctx_last_error",
     "s3imph_ctx_load_mph_bin", "s3imph_lookup_device", "s3imph_gen_keys",
+    "s3imph_finalize_index_host", "s3imph_finalize_index_device",
 )
 
 
@@ -133,6 +134,9 @@ def _load():
         "s3imph_ctx_last_error": (cp, [vp]),
         "s3imph_ctx_load_mph_bin": (i32, [vp, vp, u64]),
         "s3imph_lookup_device": (i32, [vp, vp, vp, u64, vp, vp, u64, vp, vp]),
+        "s3imph_finalize_index_host": (i32, [i32, vp, vp, vp, u64, cp, cp, sz]),
+        "s3imph_finalize_index_device": (i32, [vp, vp, vp, vp, u64, vp, vp, vp, vp, vp, u64,
+                                               P(ctypes.c_uint32), vp]),
         "s3imph_gen_keys": (i32, [i32, u64, ctypes.c_uint32, u64, u64, vp, vp, P(u64)]),
     }
     for name, (res, args) in sig.items():
@@ -356,6 +360,31 @@ class DeviceBuilder:
                                         _dev_ptr(d_pos), count, _dev_ptr(d_result), _stream_ptr(stream)),
                None, "lookup")
 
+    def finalize_index(self, d_blob, d_offsets, n: int, d_depths=None, stream=None) -> dict:
+        """IndexBuilder.Finalize's arrays on the device (indexbuild.go:393-415,474-503,
+        depthindex.go:32-96): torch tensors depth (int32), subtree_end (int64),
+        max_depth_in_subtree (int32), depth_positions (int64), depth_offsets (int64), max_depth."""
+        import torch
+        dev = d_offsets.device
+        depth = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        send = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        mds = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        dpos = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        md = ctypes.c_uint32()
+        cap = 64
+        for _ in range(2):
+            doff = torch.empty(cap, dtype=torch.int64, device=dev)
+            rc = LIB.s3imph_finalize_index_device(self._h, _dev_ptr(d_blob), _dev_ptr(d_offsets), _dev_ptr(d_depths),
+                                                  n, _dev_ptr(depth), _dev_ptr(send), _dev_ptr(mds), _dev_ptr(dpos),
+                                                  _dev_ptr(doff), cap, ctypes.byref(md), _stream_ptr(stream))
+            if rc == OK:
+                break
+            if rc != ERR_INVALID or cap >= md.value + 2:
+                raise MPHFError(rc, f"finalize index: {self.last_error() or status_string(rc)}")
+            cap = md.value + 2
+        return {"depth": depth[:n], "subtree_end": send[:n], "max_depth_in_subtree": mds[:n],
+                "depth_positions": dpos[:n], "depth_offsets": doff[: md.value + 2], "max_depth": md.value}
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             LIB.s3imph_ctx_destroy(self._h)
@@ -368,23 +397,42 @@ class DeviceBuilder:
             pass
 
 
+def finalize_index_host(blob: np.ndarray, offsets: np.ndarray, out_dir: str, depths: np.ndarray | None = None,
+                        device: int = 0) -> None:
+    """IndexBuilder.Finalize's depth / subtree / depth-index files (indexbuild.go:393-415,
+    474-503; depthindex.go:32-96), computed on the GPU, written into out_dir."""
+    blob = np.ascontiguousarray(blob, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    dp = None if depths is None else np.ascontiguousarray(depths, np.uint32)
+    err = ctypes.create_string_buffer(1024)
+    rc = LIB.s3imph_finalize_index_host(device, _np_ptr(blob), _np_ptr(offsets), _np_ptr(dp) if dp is not None else None,
+                                        len(offsets) - 1, out_dir.encode(), err, 1024)
+    _check(rc, err)
+
+
 S3ID_MAGIC = 0x53334944  # pkg/format/format.go:6-45
 S3ID_VERSION = 1
 S3ID_HEADER = 20
 
 
-def read_u64_array(path: str) -> np.ndarray:
-    """OpenArray (pkg/format/reader.go:81-119) for width-8 arrays: S3ID header checked,
-    payload returned as little-endian u64 (memory-mapped)."""
+def read_array(path: str, width: int = 8) -> np.ndarray:
+    """OpenArray (pkg/format/reader.go:81-119): S3ID header checked (magic, version, the
+    expected width, payload size), payload returned as little-endian u64 / u32
+    (memory-mapped)."""
     raw = np.memmap(path, dtype=np.uint8, mode="r")
     if len(raw) < S3ID_HEADER:
         raise MPHFError(ERR_FORMAT, f"open array {path}: file too small")
     hdr = bytes(raw[:S3ID_HEADER])
     magic, version = int.from_bytes(hdr[0:4], "little"), int.from_bytes(hdr[4:8], "little")
-    count, width = int.from_bytes(hdr[8:16], "little"), int.from_bytes(hdr[16:20], "little")
-    if magic != S3ID_MAGIC or version != S3ID_VERSION or width != 8 or len(raw) != S3ID_HEADER + 8 * count:
+    count, w = int.from_bytes(hdr[8:16], "little"), int.from_bytes(hdr[16:20], "little")
+    if magic != S3ID_MAGIC or version != S3ID_VERSION or w != width or len(raw) != S3ID_HEADER + width * count:
         raise MPHFError(ERR_FORMAT, f"open array {path}: bad header")
-    return raw[S3ID_HEADER:].view("<u8")
+    return raw[S3ID_HEADER:].view("<u8" if width == 8 else "<u4")
+
+
+def read_u64_array(path: str) -> np.ndarray:
+    """OpenArray for width-8 arrays (mph_fp.u64, mph_pos.u64, prefix_offsets.u64, ...)."""
+    return read_array(path, 8)
 
 
 class MPHF:
