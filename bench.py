@@ -29,7 +29,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "s3-inv-db_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-FNV_STEP_PEAK_T = 3.49  # FNV-1a + FNV-1 byte steps per second (x1e12), tools/ubench_fnv.hip on MI355X
+# FNV-1a + FNV-1 byte steps per second (x1e12): tools/ubench_fnv.hip mode 3 (the product's
+# byte step, s3imph_device.h) from registers at 4 waves/SIMD — the level-0 hash kernel's
+# occupancy — on MI355X (profiles/r02_b/ubench_fnv.txt: 4.20 at a measured 2.37 GHz shader
+# clock; the hash kernel itself runs at ~2.0 GHz under HBM load).
+FNV_STEP_PEAK_T = 4.20
 
 CONFIGS = {
     "c2": dict(kind=0, avg=32, keys_per_gpu=10_000_000,
@@ -234,6 +238,7 @@ def main() -> None:
         result["dominant_stage"] = max(stages, key=stages.get)
     if world == 1 and not use_dist:
         result["lookup"] = lookup_rate(ctx, d_blob, d_offs, n, d_fp, d_po)
+        result["finalize"] = finalize_rate(ctx, d_blob, d_offs, n)
     if world == 1:
         result["host_e2e"] = host_e2e(s3imph, blob, offs, local_rank)
     if world == 1 and not args.no_cpu_baseline:
@@ -265,6 +270,22 @@ def lookup_rate(ctx, d_blob, d_offs, n: int, d_fp, d_po, reps: int = 5) -> dict:
     dt = (time.perf_counter() - t0) / reps
     return {"keys_per_s": n / dt, "ms": dt * 1e3, "all_members_found": ok,
             "note": "every member looked up against the last build (device-resident)"}
+
+
+def finalize_rate(ctx, d_blob, d_offs, n: int, reps: int = 5) -> dict:
+    """IndexBuilder.Finalize's other arrays (depth, subtree_end, max_depth_in_subtree, depth
+    index; indexbuild.go:393-415,474-503, depthindex.go:32-96) over the same keys in HBM.
+    Reported beside `value`, never as it."""
+    import torch
+    r = ctx.finalize_index(d_blob, d_offs, n)  # scratch + warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = ctx.finalize_index(d_blob, d_offs, n)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    return {"keys_per_s": n / dt, "ms": dt * 1e3, "max_depth": r["max_depth"],
+            "note": "depth ('/' count), subtree_end, max_depth_in_subtree, depth_offsets/positions; device-resident"}
 
 
 def host_e2e(s3imph, blob, offs, device: int, reps: int = 3) -> dict:
@@ -312,11 +333,12 @@ def secondary_line(s3imph, device: int, seed: int, steps: int, warmup: int) -> d
     ctx.set_profiling(1)
     ctx.build(d_blob, d_offs, n, d_fp, d_po)
     stages = {k: round(v, 4) for k, v in ctx.stage_times().items()}
+    fin = finalize_rate(ctx, d_blob, d_offs, n)
     ctx.close()
     del d_blob, d_offs, d_fp, d_po
     torch.cuda.empty_cache()
     return {"workload": cfg["workload"], "keys": n, "ms_per_step": dt * 1e3, "keys_per_s": n / dt,
-            "key_bytes_GBps": int(offs[-1]) / dt / 1e9, "stages_ms": stages,
+            "key_bytes_GBps": int(offs[-1]) / dt / 1e9, "stages_ms": stages, "finalize": fin,
             "host_e2e": host_e2e(s3imph, blob, offs, device), "builder_e2e": builder_e2e(s3imph, blob, offs, device)}
 
 

@@ -1560,6 +1560,255 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
   if (bad) atomicOr(&st->status, kStRank);
 }
 
+// ------------------------------------------------------------ mid-size levels --------
+// Levels between the single-workgroup tail (<= kTailKeys keys) and the binned pipeline's
+// scatter + tile kernels, where the latter pay mostly fixed latency (two launches, a
+// reservation round trip, a look-back chain: ~20-40 us per level of 10^4-10^5 keys).
+// kMidG workgroups of kMidT threads, all resident, run every such level in one launch:
+//   mark      each workgroup takes a contiguous share of the level's input list (records
+//             stay in registers, kMidR per thread) and counts keys per position in a global
+//             8-bit counter array with no-return device-scope atomic adds (nothing waits
+//             on a returned value; a count wraps only past 255 keys on one position, which
+//             only duplicate keys reach, and those end the build with DUP_KEY_HASH);
+//   finalize  each workgroup turns a slice of the level's words into its bits (count ==
+//             1), the per-word rank prefix inside the slice and the slice's total, and
+//             clears its slice of the other count buffer for the next level;
+//   settle    rank = level base + prefix of the slice totals + word prefix + popcount
+//             below the bit -> fp_out / pos_out; collided records -> the next list with one
+//             reservation per workgroup;
+// with a grid barrier (device-scope counter, release / acquire fences) after each phase.
+// Every decision derives from the same level state, so all workgroups take the same
+// branches.  Level bookkeeping mirrors k_scatter_res + k_tile_reg (words, woff, nlevels,
+// lvl_base, n[L+1]); a level of <= kTailKeys keys is left to the tail as they leave it.
+// Grid barrier (MI355X_MICROARCH.md, inter-workgroup visibility): every wave waits for its
+// own stores and atomics, the workgroup meets, then ONE release (one L2 write-back per
+// workgroup, not per wave) and the arrival; after the count is reached, one agent-scope
+// acquire for the CU before anyone loads.
+__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, LevelState* st, int* s_ok) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    unsigned spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++spins > (1u << 22)) {  // bounded: a missing workgroup must not hang the GPU
+        atomicOr(&st->status, kStLookback);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this CU's L1 invalidated for the loads after
+    *s_ok = ok;
+  }
+  __syncthreads();
+  return *s_ok != 0;
+}
+
+__global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0, Rec* list1, uint64_t* bits,
+                                                      uint64_t cap_words, uint64_t* __restrict__ fp_out,
+                                                      uint64_t* __restrict__ pos_out, LevelState* st,
+                                                      uint32_t* mid, unsigned long long* __restrict__ prof) {
+  // debug (prof != null): phase stamps of the first and last workgroup, 8 per level
+  unsigned long long* tp =
+      prof && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)
+          ? prof + (uint64_t)(kMaxLevels - 4) * kMaxTiles * 8 + (blockIdx.x ? 512 : 0)
+          : nullptr;
+#define MPROF(li, i)                                         \
+  do {                                                       \
+    if (tp && threadIdx.x == 0 && (li) < 64) tp[(li) * 8 + (i)] = wall_clock64(); \
+  } while (0)
+  __shared__ unsigned long long s_pre[kMidG + 1];
+  __shared__ unsigned s_wc[kMidT / 64];
+  __shared__ unsigned long long s_wbase[kMidT / 64];
+  __shared__ int s_go, s_ok;
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const unsigned g = blockIdx.x, G = gridDim.x;
+  uint32_t* R = mid + kMidR32;
+  unsigned long long* tot = reinterpret_cast<unsigned long long*>(mid + kMidTot);
+  unsigned* bar = mid;
+  const uint64_t N = st->out_cap;
+  const uint64_t lt = lanemask_lt();
+  unsigned target = 0;
+  int buf = 0;
+  bool bad = false;
+  for (int L = L0; L <= L1; ++L) {
+    // ---- level setup: the same reads in every workgroup, workgroup 0 publishes
+    if (tid == 0) {
+      const int p = L - 1;
+      int go = !(st->status & kStStop) && !(p > 0 && !st->preset[p] && st->n[p] <= kGate);
+      if (go) {
+        const uint64_t n = st->n[L];
+        const uint64_t words = n ? level_words(n) : 0;
+        const uint64_t woff = st->woff[p] + st->words[p];
+        if (g == 0) {
+          st->words[L] = words;
+          st->magic[L] = level_magic(words);
+          st->woff[L] = woff;
+          st->woff[L + 1] = woff + words;
+          st->nlevels = L;
+          if (woff + words > cap_words) atomicOr(&st->status, kStOverflow);
+        }
+        if (n <= kGate || woff + words > cap_words) {
+          go = 0;  // the tail takes this level (or the workspace is too small: rerun)
+        } else if (n > kMidMaxKeys) {
+          if (g == 0) atomicOr(&st->status, kStTailOverflow);  // bigger than predicted: rerun
+          go = 0;
+        } else if (!st->preset[L] && !st->preset[p] && n == st->n[p]) {
+          if (g == 0) {  // no key placed at the previous level: duplicates (no_progress)
+            st->stop_level = L;
+            atomicOr(&st->status, kStTooManyLevels);
+          }
+          go = 0;
+        }
+      }
+      s_go = go;
+    }
+    __syncthreads();
+    if (!s_go) break;
+    const uint64_t n = st->n[L];
+    const uint64_t words = level_words(n), magic = level_magic(words);
+    const uint64_t woff = st->woff[L - 1] + st->words[L - 1];
+    const uint64_t seed = level_seed(L);
+    const Rec* in = (L & 1) ? list0 : list1;  // list[(L - 1) & 1]
+    Rec* next = (L & 1) ? list1 : list0;      // list[L & 1]
+    uint32_t* cnt = mid + kMidCnt + (uint64_t)buf * kMidCntU32;  // 4 positions per u32
+    const unsigned W32 = (unsigned)(2 * words);
+    const int li = L - L0;
+    MPROF(li, 0);
+    // ---- mark
+    const uint64_t per = (n + G - 1) / G, r0 = (uint64_t)g * per, r1 = min(n, r0 + per);
+    uint64_t k[kMidR], f[kMidR], pp[kMidR];
+    unsigned x[kMidR];
+#pragma unroll
+    for (int r = 0; r < kMidR; ++r) {
+      const uint64_t j = r0 + (uint64_t)r * kMidT + tid;
+      k[r] = f[r] = pp[r] = 0;
+      x[r] = 0xffffffffu;
+      if (j < r1) {
+        const Rec* q = in + j;
+        k[r] = q->k;
+        f[r] = q->f;
+        pp[r] = q->p;
+      }
+    }
+    MPROF(li, 1);
+#pragma unroll
+    for (int r = 0; r < kMidR; ++r) {
+      const uint64_t j = r0 + (uint64_t)r * kMidT + tid;
+      if (j < r1) {
+        x[r] = (unsigned)bb_index(seed, k[r], words, magic);
+        __hip_atomic_fetch_add(&cnt[x[r] >> 2], 1u << (8 * (x[r] & 3)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    MPROF(li, 2);
+    target += G;
+    if (!grid_sync(bar, target, st, &s_ok)) break;
+    MPROF(li, 3);
+    // ---- finalize: this workgroup's slice of the level's u32 words (<= kMidT of them)
+    const unsigned sl = (W32 + G - 1) / G, w0 = min(W32, g * sl), w1 = min(W32, w0 + sl);
+    uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + woff);
+    {
+      uint4* cnt2 = reinterpret_cast<uint4*>(mid + kMidCnt + (uint64_t)(buf ^ 1) * kMidCntU32);
+      const unsigned w = w0 + tid;
+      uint32_t v = 0;
+      if (w < w1) {
+        const uint4* c4 = reinterpret_cast<const uint4*>(cnt) + 2 * (uint64_t)w;  // 32 counts
+        const uint4 c0 = c4[0], c1 = c4[1];
+        const uint32_t cw[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) v |= (uint32_t)(((cw[q] >> (8 * b)) & 0xffu) == 1u) << (4 * q + b);
+        g32[w] = v;
+        cnt2[2 * (uint64_t)w] = make_uint4(0, 0, 0, 0);  // the next level's counts (fewer words)
+        cnt2[2 * (uint64_t)w + 1] = make_uint4(0, 0, 0, 0);
+      }
+      uint64_t total;
+      const uint64_t ex = block_exscan<kMidT>((uint64_t)__popc(v), &total);
+      if (w < w1) R[w] = (uint32_t)ex;
+      if (tid == 0) tot[g] = total;
+    }
+    MPROF(li, 4);
+    target += G;
+    if (!grid_sync(bar, target, st, &s_ok)) break;
+    MPROF(li, 5);
+    // ---- settle / redo
+    if (wave == 0) {
+      const unsigned long long v = lane < G ? tot[lane] : 0ull;
+      unsigned long long xs = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long y = __shfl_up(xs, d);
+        if (lane >= (unsigned)d) xs += y;
+      }
+      if (lane < G) s_pre[lane] = xs - v;
+      if (lane == G - 1) s_pre[G] = xs;
+    }
+    __syncthreads();
+    const uint64_t lvl_base = st->lvl_base[L];
+    const uint64_t settled = s_pre[G];
+    if (g == 0 && tid == 0) st->lvl_base[L + 1] = lvl_base + settled;
+    const bool out_on = level_out_on(st, L);
+    const bool ok = lvl_base + settled <= N;
+    if (!ok && out_on) bad = true;
+    unsigned wc = 0;
+    unsigned redo_m = 0;
+#pragma unroll
+    for (int r = 0; r < kMidR; ++r) {
+      bool redo = false;
+      if (x[r] != 0xffffffffu) {
+        const unsigned w = x[r] >> 5;
+        const uint32_t vb = g32[w];
+        const uint32_t bit = 1u << (x[r] & 31);
+        if (vb & bit) {
+          if (ok && out_on) {
+            const uint64_t rank = lvl_base + s_pre[w / sl] + R[w] + __popc(vb & (bit - 1));
+            fp_out[rank] = f[r];
+            pos_out[rank] = pp[r];
+          }
+        } else {
+          redo = true;
+          redo_m |= 1u << r;
+        }
+      }
+      wc += __popcll(__ballot(redo));
+    }
+    if (lane == 0) s_wc[wave] = wc;
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long c = 0;
+      for (int w = 0; w < kMidT / 64; ++w) c += s_wc[w];
+      unsigned long long b0 = c ? atomicAdd(&st->n[L + 1], c) : 0ull;
+      for (int w = 0; w < kMidT / 64; ++w) {
+        s_wbase[w] = b0;
+        b0 += s_wc[w];
+      }
+    }
+    __syncthreads();
+    if (wc) {
+      uint64_t o = s_wbase[wave];
+#pragma unroll
+      for (int r = 0; r < kMidR; ++r) {
+        const bool redo = (redo_m >> r) & 1u;
+        const uint64_t m = __ballot(redo);
+        if (redo) next[o + __popcll(m & lt)] = Rec{k[r], f[r], pp[r]};
+        o += __popcll(m);
+      }
+    }
+    MPROF(li, 6);
+    target += G;
+    if (!grid_sync(bar, target, st, &s_ok)) break;  // n[L + 1] and lvl_base[L + 1] final
+    MPROF(li, 7);
+    buf ^= 1;
+  }
+  if (bad) atomicOr(&st->status, kStRank);
+#undef MPROF
+}
+
 // --------------------------------------------------------------------- tail --------
 constexpr unsigned kWaveKeys = 64;  // tail levels this small run in one wave
 // The wave tail holds key i in lane i, compacts with 64-bit ballots and reads the level's
@@ -2002,6 +2251,13 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
   k_scatter_res<kSubRound, kLdsTiles><<<grid, kSB, 0, s>>>(level, il, b.kh, b.fp, b.pos, b.pos_base, tc, b.bucket,
                                                            b.bucket_cap, b.flags, b.st, g.tb, b.cap_words,
                                                            b.tile_prof, i_lo, i_hi);
+}
+
+void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s) {
+  // the barrier counter and the first level's counts start at zero
+  (void)hipMemsetAsync(b.mid, 0, (kMidCnt + kMidCntU32) * sizeof(uint32_t), s);  // barrier + counts[0]
+  k_mid_levels<<<kMidG, kMidT, 0, s>>>(L0, L1, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out, b.pos_out, b.st,
+                                       b.mid, b.tile_prof);
 }
 
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s) {

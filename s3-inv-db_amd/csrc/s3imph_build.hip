@@ -97,6 +97,7 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
 }
 
 void free_workspace(s3imph_ctx* c) {
+  dfree(c->mid);
   dfree(c->kh); dfree(c->fp); dfree(c->bits); dfree(c->rank_base);
   dfree(c->block_sums); dfree(c->d_st);
   dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
@@ -241,6 +242,8 @@ BinBuffers make_bufs(s3imph_ctx* c, const uint64_t* pos, uint64_t* fp_out, uint6
     HIPCHECK(hipMemsetAsync(c->tile_prof, 0, nprof * sizeof(unsigned long long), s));
     b.tile_prof = c->tile_prof;
   }
+  if (!c->mid) dalloc(c->mid, kMidScratchU32);
+  b.mid = c->mid;
   b.bits = c->bits;
   b.cap_words = c->cap_words;
   b.fp_out = fp_out;
@@ -319,6 +322,15 @@ int enqueue_levels_from(s3imph_ctx* c, const BinBuffers& b, int L0, uint64_t n0,
     // kStTailOverflow and rerun conservatively).
     const double pred = (double)n0 * std::pow(q, L - L0);
     if (!conservative && pred * kTailMargin < (double)kTailKeys) break;
+    if (!conservative && pred * kMidMargin <= (double)kMidMaxKeys) {
+      // this level and the rest above the tail: one persistent launch
+      int L1 = L;
+      while (L1 + 1 <= big && L1 + 1 < kMaxLevels - 1 && pred * std::pow(q, L1 + 1 - L) * kTailMargin >= (double)kTailKeys)
+        ++L1;
+      launch_binned_mid(L, L1, b, s);
+      launched = L1;
+      break;
+    }
     launched = L;
     const uint64_t nb = conservative ? n0 : (uint64_t)(pred * 1.1) + 4096;
     enqueue_list_level(c, b, L, nb, 64 * level_words(nb), conservative, conservative ? &gcons : nullptr, s);
@@ -434,6 +446,18 @@ void print_tile_profile(s3imph_ctx* c) {
                    "%.1f%%, rest %.1f%%\n",
                    cnt, a[0] / cnt, a[4] / cnt / 100.0, a[4] ? 100.0 * a[0] / a[4] : 0.0, 100 * a[1] / a[0],
                    100 * a[2] / a[0], 100 * a[3] / a[0]);
+  }
+  {  // k_mid_levels phase stamps: workgroup 0 and the last one, 8 per level
+    const unsigned long long* m = &h[(size_t)(kMaxLevels - 4) * kMaxTiles * 8];
+    static const char* mn[7] = {"load", "mark", "bar1", "final", "bar2", "settle", "bar3"};
+    for (int wg = 0; wg < 2; ++wg)
+      for (int li = 0; li < 64; ++li) {
+        const unsigned long long* q = m + wg * 512 + li * 8;
+        if (!q[0]) break;
+        std::fprintf(stderr, "  mid wg%s level+%d:", wg ? "last" : "0", li);
+        for (int k = 0; k < 7; ++k) std::fprintf(stderr, " %s %.2f", mn[k], q[k + 1] ? (q[k + 1] - q[k]) / 100.0 : -1.0);
+        std::fprintf(stderr, " us\n");
+      }
   }
   static const char* names[7] = {"mark", "final", "lookbk", "rank", "output", "redoN", "redoW"};
   {

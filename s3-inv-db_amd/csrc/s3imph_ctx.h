@@ -140,6 +140,7 @@ struct FinScratch;  // s3imph_finalize.hip
 struct s3imph_ctx {
   int device = 0;
   s3imph::FinScratch* fin = nullptr;  // finalize-pass scratch (s3imph_finalize.hip), lazily made
+  uint32_t* mid = nullptr;            // k_mid_levels scratch (kMidScratchU32), lazily made
   hipStream_t own_stream = nullptr;
   std::mutex mu;
 

@@ -130,6 +130,23 @@ constexpr unsigned kStStop = kStGeometry | kStOverflow | kStLookback | kStTooMan
 // Levels whose active-key count is at most this run inside one workgroup with
 // LDS-resident bit vectors (k_tail); larger levels run as full-grid kernels.
 constexpr unsigned long long kTailKeys = 12288;
+// Mid-size levels (above the tail, at most kMidMaxKeys keys) run inside one persistent
+// kernel of kMidG cooperating workgroups (s3imph_binned.hip, k_mid_levels): global A/C
+// bit vectors, grid barriers between phases, records in registers.
+constexpr int kMidG = 48;
+constexpr int kMidT = 1024;
+constexpr int kMidR = 8;  // records per thread
+constexpr unsigned long long kMidMaxKeys = (unsigned long long)kMidG * kMidT * kMidR;
+constexpr uint64_t kMidW32 = 2 * ((2 * kMidMaxKeys + 63) / 64);  // u32 words of the largest mid level
+// scratch (u32 units): barrier counter [64], per-position 8-bit key counts ping-pong
+// [2][8 kMidW32] (32 positions per level word), per-word rank prefix [kMidW32], per-block
+// totals [kMidG] u64
+constexpr uint64_t kMidCnt = 64;                       // first count buffer
+constexpr uint64_t kMidCntU32 = 8 * kMidW32;           // u32 words per count buffer
+constexpr uint64_t kMidR32 = kMidCnt + 2 * kMidCntU32;  // rank prefix
+constexpr uint64_t kMidTot = kMidR32 + kMidW32;         // totals (8-byte aligned: all terms even)
+constexpr uint64_t kMidScratchU32 = kMidTot + 2 * kMidG;
+constexpr double kMidMargin = 1.15;  // a level predicted above kMidMaxKeys / kMidMargin stays binned
 constexpr int kTailThreads = 1024;
 constexpr int kTailLdsWords32 = 2 * 2 * ((kGammaNum * kTailKeys + 63) / 64);  // A and C, u32 words
 
@@ -174,6 +191,7 @@ struct BinBuffers {
   uint64_t* pos_out;
   LevelState* st;
   bool dist;                            // multi-GPU owner levels: level 0 reads list[1] too
+  uint32_t* mid;                        // k_mid_levels scratch (kMidScratchU32)
 };
 void binned_set_lds_limits();
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
@@ -185,6 +203,8 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s,
                                uint64_t i_lo = 0, uint64_t i_hi = 0);
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s);
+// levels L0..L1 (each predicted above the tail and at most kMidMaxKeys keys) in one launch
+void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s);
 
 // ---- multi-GPU launchers (s3imph_dist.hip) ------------------------------------------
 constexpr int kMaxRanks = 64;
