@@ -1564,22 +1564,23 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
 // Levels between the single-workgroup tail (<= kTailKeys keys) and the binned pipeline's
 // scatter + tile kernels, where the latter pay mostly fixed latency (two launches, a
 // reservation round trip, a look-back chain: ~20-40 us per level of 10^4-10^5 keys).
-// kMidG workgroups of kMidT threads, all resident, run every such level in one launch:
-//   mark      each workgroup takes a contiguous share of the level's input list (records
-//             stay in registers, kMidR per thread) and counts keys per position in a global
-//             8-bit counter array with no-return device-scope atomic adds (nothing waits
-//             on a returned value; a count wraps only past 255 keys on one position, which
-//             only duplicate keys reach, and those end the build with DUP_KEY_HASH);
-//   finalize  each workgroup turns a slice of the level's words into its bits (count ==
-//             1), the per-word rank prefix inside the slice and the slice's total, and
-//             clears its slice of the other count buffer for the next level;
-//   settle    rank = level base + prefix of the slice totals + word prefix + popcount
-//             below the bit -> fp_out / pos_out; collided records -> the next list with one
-//             reservation per workgroup;
-// with a grid barrier (device-scope counter, release / acquire fences) after each phase.
-// Every decision derives from the same level state, so all workgroups take the same
-// branches.  Level bookkeeping mirrors k_scatter_res + k_tile_reg (words, woff, nlevels,
-// lvl_base, n[L+1]); a level of <= kTailKeys keys is left to the tail as they leave it.
+// kMidG workgroups of kMidT threads, all resident, run every such level in one launch.
+// Workgroup g owns the level words [g sl, (g+1) sl) (sl = ceil(words32 / kMidG)), and the
+// records a workgroup holds stay in its registers (kMidR per thread) from level to level:
+//   route     each record goes to the owner of its position: counted per owner in LDS and
+//             written to the (owner, sender) segment of an exchange area (kMidSeg records);
+//   own       the owner gathers its segments into its registers, marks A / C for its
+//             words in LDS, writes the level's bits A & ~C and its words' rank prefix,
+//             publishes its settled total;
+//   settle    rank = level base + totals of the owners before it + in-slice rank: settled
+//             (f, p) are staged by rank in LDS and written as one contiguous run; collided
+//             records stay in registers for the next level and are also appended to the
+//             next list (one reservation per workgroup), where the tail finds them;
+// with a grid barrier after each phase.  Every decision derives from the same level
+// state, so all workgroups take the same branches; an overflow (a segment or an owner
+// past its capacity, predicted not to happen) is flagged and the build reruns on the
+// conservative path.  Level bookkeeping mirrors k_scatter_res + k_tile_reg (words, woff,
+// nlevels, lvl_base, n[L+1]); a level of <= kTailKeys keys is left to the tail.
 // Grid barrier (MI355X_MICROARCH.md, inter-workgroup visibility): every wave waits for its
 // own stores and atomics, the workgroup meets, then ONE release (one L2 write-back per
 // workgroup, not per wave) and the arrival; after the count is reached, one agent-scope
@@ -1610,30 +1611,36 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, LevelS
 __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0, Rec* list1, uint64_t* bits,
                                                       uint64_t cap_words, uint64_t* __restrict__ fp_out,
                                                       uint64_t* __restrict__ pos_out, LevelState* st,
-                                                      uint32_t* mid, unsigned long long* __restrict__ prof) {
+                                                      uint32_t* mid, Rec* __restrict__ xb,
+                                                      unsigned long long* __restrict__ prof) {
   // debug (prof != null): phase stamps of the first and last workgroup, 8 per level
   unsigned long long* tp =
       prof && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)
           ? prof + (uint64_t)(kMaxLevels - 4) * kMaxTiles * 8 + (blockIdx.x ? 512 : 0)
           : nullptr;
-#define MPROF(li, i)                                         \
-  do {                                                       \
+#define MPROF(li, i)                                                              \
+  do {                                                                            \
     if (tp && threadIdx.x == 0 && (li) < 64) tp[(li) * 8 + (i)] = wall_clock64(); \
   } while (0)
+  constexpr unsigned kSlW = (unsigned)((kMidW32 + kMidG - 1) / kMidG);  // owner slice, u32 words
+  __shared__ uint32_t sA[kSlW], sC[kSlW], sP[kSlW];
+  __shared__ uint64_t sf[kMidStage], sp[kMidStage];
+  __shared__ unsigned s_cnt[kMidG], s_spre[kMidG + 1];
   __shared__ unsigned long long s_pre[kMidG + 1];
   __shared__ unsigned s_wc[kMidT / 64];
   __shared__ unsigned long long s_wbase[kMidT / 64];
   __shared__ int s_go, s_ok;
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const unsigned g = blockIdx.x, G = gridDim.x;
-  uint32_t* R = mid + kMidR32;
-  unsigned long long* tot = reinterpret_cast<unsigned long long*>(mid + kMidTot);
   unsigned* bar = mid;
+  unsigned* xc = mid + kMidXc;  // [owner][sender] segment counts
+  unsigned long long* tot = reinterpret_cast<unsigned long long*>(mid + kMidTot);
   const uint64_t N = st->out_cap;
   const uint64_t lt = lanemask_lt();
   unsigned target = 0;
-  int buf = 0;
   bool bad = false;
+  uint64_t k[kMidR], f[kMidR], pp[kMidR];
+  unsigned valid = 0;  // bit r: k/f/pp[r] hold a record of the current level
   for (int L = L0; L <= L1; ++L) {
     // ---- level setup: the same reads in every workgroup, workgroup 0 publishes
     if (tid == 0) {
@@ -1672,71 +1679,119 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
     const uint64_t words = level_words(n), magic = level_magic(words);
     const uint64_t woff = st->woff[L - 1] + st->words[L - 1];
     const uint64_t seed = level_seed(L);
-    const Rec* in = (L & 1) ? list0 : list1;  // list[(L - 1) & 1]
-    Rec* next = (L & 1) ? list1 : list0;      // list[L & 1]
-    uint32_t* cnt = mid + kMidCnt + (uint64_t)buf * kMidCntU32;  // 4 positions per u32
     const unsigned W32 = (unsigned)(2 * words);
+    const unsigned sl = (W32 + G - 1) / G, w0 = min(W32, g * sl), w1 = min(W32, w0 + sl);
     const int li = L - L0;
     MPROF(li, 0);
-    // ---- mark
-    const uint64_t per = (n + G - 1) / G, r0 = (uint64_t)g * per, r1 = min(n, r0 + per);
-    uint64_t k[kMidR], f[kMidR], pp[kMidR];
-    unsigned x[kMidR];
+    if (L == L0) {  // the first level's records: this workgroup's share of the input list
+      const Rec* in = (L & 1) ? list0 : list1;  // list[(L - 1) & 1]
+      const uint64_t per = (n + G - 1) / G, r0 = (uint64_t)g * per, r1 = min(n, r0 + per);
+      valid = 0;
+#pragma unroll
+      for (int r = 0; r < kMidR; ++r) {
+        const uint64_t j = r0 + (uint64_t)r * kMidT + tid;
+        if (j < r1) {
+          const Rec* q = in + j;
+          k[r] = q->k;
+          f[r] = q->f;
+          pp[r] = q->p;
+          valid |= 1u << r;
+        }
+      }
+    }
+    // ---- route: records -> (owner, sender) segments
+    if (tid < kMidG) s_cnt[tid] = 0;
+    __syncthreads();
+    {
+      bool over = false;
+#pragma unroll
+      for (int r = 0; r < kMidR; ++r) {
+        if ((valid >> r) & 1u) {
+          const unsigned x = (unsigned)bb_index(seed, k[r], words, magic);
+          const unsigned o = (x >> 5) / sl;
+          const unsigned slot = atomicAdd(&s_cnt[o], 1u);
+          if (slot < kMidSeg)
+            xb[((uint64_t)o * kMidG + g) * kMidSeg + slot] = Rec{k[r], f[r], pp[r]};
+          else
+            over = true;
+        }
+      }
+      if (over) atomicOr(&st->status, kStTailOverflow);
+    }
+    __syncthreads();
+    if (tid < G) xc[tid * kMidG + g] = min(s_cnt[tid], (unsigned)kMidSeg);
+    MPROF(li, 1);
+    target += G;
+    if (!grid_sync(bar, target, st, &s_ok)) break;
+    MPROF(li, 2);
+    // ---- own: gather this slice's records, mark A / C, bits, word rank prefix, total
+    if (wave == 0) {  // segment prefix over the senders
+      const unsigned v = lane < G ? xc[g * kMidG + lane] : 0u;
+      unsigned xs = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned y = __shfl_up(xs, d);
+        if (lane >= (unsigned)d) xs += y;
+      }
+      if (lane < G) s_spre[lane] = xs - v;
+      if (lane == G - 1) s_spre[G] = xs;
+    }
+    for (unsigned w = tid; w < sl; w += kMidT) {
+      sA[w] = 0;
+      sC[w] = 0;
+    }
+    __syncthreads();
+    const unsigned m = s_spre[G];
+    if (m > (unsigned)kMidR * kMidT && tid == 0) atomicOr(&st->status, kStTailOverflow);
+    unsigned lx[kMidR];
+    valid = 0;
 #pragma unroll
     for (int r = 0; r < kMidR; ++r) {
-      const uint64_t j = r0 + (uint64_t)r * kMidT + tid;
-      k[r] = f[r] = pp[r] = 0;
-      x[r] = 0xffffffffu;
-      if (j < r1) {
-        const Rec* q = in + j;
+      const unsigned j = r * kMidT + tid;
+      lx[r] = 0;
+      if (j < m) {
+        unsigned lo = 0, hi = G;  // last sender b with s_spre[b] <= j
+        while (hi - lo > 1) {
+          const unsigned mid2 = (lo + hi) >> 1;
+          if (s_spre[mid2] <= j) lo = mid2;
+          else hi = mid2;
+        }
+        const Rec* q = xb + ((uint64_t)g * kMidG + lo) * kMidSeg + (j - s_spre[lo]);
         k[r] = q->k;
         f[r] = q->f;
         pp[r] = q->p;
+        valid |= 1u << r;
       }
     }
-    MPROF(li, 1);
 #pragma unroll
     for (int r = 0; r < kMidR; ++r) {
-      const uint64_t j = r0 + (uint64_t)r * kMidT + tid;
-      if (j < r1) {
-        x[r] = (unsigned)bb_index(seed, k[r], words, magic);
-        __hip_atomic_fetch_add(&cnt[x[r] >> 2], 1u << (8 * (x[r] & 3)), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+      if ((valid >> r) & 1u) {
+        lx[r] = (unsigned)bb_index(seed, k[r], words, magic) - 32u * w0;
+        const uint32_t bit = 1u << (lx[r] & 31);
+        const uint32_t old = atomicOr(&sA[lx[r] >> 5], bit);
+        if (old & bit) atomicOr(&sC[lx[r] >> 5], bit);
       }
     }
-    MPROF(li, 2);
-    target += G;
-    if (!grid_sync(bar, target, st, &s_ok)) break;
-    MPROF(li, 3);
-    // ---- finalize: this workgroup's slice of the level's u32 words (<= kMidT of them)
-    const unsigned sl = (W32 + G - 1) / G, w0 = min(W32, g * sl), w1 = min(W32, w0 + sl);
-    uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + woff);
+    __syncthreads();
     {
-      uint4* cnt2 = reinterpret_cast<uint4*>(mid + kMidCnt + (uint64_t)(buf ^ 1) * kMidCntU32);
-      const unsigned w = w0 + tid;
+      uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + woff);
+      const unsigned w = tid;  // sl <= kSlW <= kMidT words
       uint32_t v = 0;
-      if (w < w1) {
-        const uint4* c4 = reinterpret_cast<const uint4*>(cnt) + 2 * (uint64_t)w;  // 32 counts
-        const uint4 c0 = c4[0], c1 = c4[1];
-        const uint32_t cw[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-#pragma unroll
-          for (int b = 0; b < 4; ++b) v |= (uint32_t)(((cw[q] >> (8 * b)) & 0xffu) == 1u) << (4 * q + b);
-        g32[w] = v;
-        cnt2[2 * (uint64_t)w] = make_uint4(0, 0, 0, 0);  // the next level's counts (fewer words)
-        cnt2[2 * (uint64_t)w + 1] = make_uint4(0, 0, 0, 0);
+      if (w0 + w < w1) {
+        v = sA[w] & ~sC[w];
+        sA[w] = v;
+        g32[w0 + w] = v;
       }
       uint64_t total;
       const uint64_t ex = block_exscan<kMidT>((uint64_t)__popc(v), &total);
-      if (w < w1) R[w] = (uint32_t)ex;
+      if (w0 + w < w1) sP[w] = (uint32_t)ex;
       if (tid == 0) tot[g] = total;
     }
-    MPROF(li, 4);
+    MPROF(li, 3);
     target += G;
     if (!grid_sync(bar, target, st, &s_ok)) break;
-    MPROF(li, 5);
-    // ---- settle / redo
+    MPROF(li, 4);
+    // ---- settle: staged outputs, collided records kept and appended to the next list
     if (wave == 0) {
       const unsigned long long v = lane < G ? tot[lane] : 0ull;
       unsigned long long xs = v;
@@ -1750,29 +1805,31 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
     }
     __syncthreads();
     const uint64_t lvl_base = st->lvl_base[L];
-    const uint64_t settled = s_pre[G];
-    if (g == 0 && tid == 0) st->lvl_base[L + 1] = lvl_base + settled;
+    if (g == 0 && tid == 0) st->lvl_base[L + 1] = lvl_base + s_pre[G];
     const bool out_on = level_out_on(st, L);
-    const bool ok = lvl_base + settled <= N;
+    const uint64_t base = lvl_base + s_pre[g];
+    const uint64_t mine = s_pre[g + 1] - s_pre[g];
+    const bool ok = lvl_base + s_pre[G] <= N;
     if (!ok && out_on) bad = true;
-    unsigned wc = 0;
-    unsigned redo_m = 0;
+    unsigned wc = 0, keep = 0;
 #pragma unroll
     for (int r = 0; r < kMidR; ++r) {
       bool redo = false;
-      if (x[r] != 0xffffffffu) {
-        const unsigned w = x[r] >> 5;
-        const uint32_t vb = g32[w];
-        const uint32_t bit = 1u << (x[r] & 31);
-        if (vb & bit) {
-          if (ok && out_on) {
-            const uint64_t rank = lvl_base + s_pre[w / sl] + R[w] + __popc(vb & (bit - 1));
-            fp_out[rank] = f[r];
-            pos_out[rank] = pp[r];
+      if ((valid >> r) & 1u) {
+        const uint32_t wv = sA[lx[r] >> 5];
+        const uint32_t bit = 1u << (lx[r] & 31);
+        if (wv & bit) {
+          const unsigned rank = sP[lx[r] >> 5] + __popc(wv & (bit - 1));
+          if (rank < kMidStage) {
+            sf[rank] = f[r];
+            sp[rank] = pp[r];
+          } else if (ok && out_on) {
+            fp_out[base + rank] = f[r];
+            pos_out[base + rank] = pp[r];
           }
         } else {
           redo = true;
-          redo_m |= 1u << r;
+          keep |= 1u << r;
         }
       }
       wc += __popcll(__ballot(redo));
@@ -1789,21 +1846,30 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
       }
     }
     __syncthreads();
+    if (ok && out_on) {
+      const uint64_t ns = min<uint64_t>(mine, kMidStage);
+      for (uint64_t i = tid; i < ns; i += kMidT) {
+        fp_out[base + i] = sf[i];
+        pos_out[base + i] = sp[i];
+      }
+    }
     if (wc) {
+      Rec* next = (L & 1) ? list1 : list0;  // list[L & 1]
       uint64_t o = s_wbase[wave];
 #pragma unroll
       for (int r = 0; r < kMidR; ++r) {
-        const bool redo = (redo_m >> r) & 1u;
-        const uint64_t m = __ballot(redo);
-        if (redo) next[o + __popcll(m & lt)] = Rec{k[r], f[r], pp[r]};
-        o += __popcll(m);
+        const bool redo = (keep >> r) & 1u;
+        const uint64_t mm = __ballot(redo);
+        if (redo) next[o + __popcll(mm & lt)] = Rec{k[r], f[r], pp[r]};
+        o += __popcll(mm);
       }
     }
-    MPROF(li, 6);
+    valid = keep;
+    MPROF(li, 5);
     target += G;
-    if (!grid_sync(bar, target, st, &s_ok)) break;  // n[L + 1] and lvl_base[L + 1] final
-    MPROF(li, 7);
-    buf ^= 1;
+    if (!grid_sync(bar, target, st, &s_ok)) break;  // n[L + 1], lvl_base[L + 1], overflow flags final
+    MPROF(li, 6);
+    if (st->status & kStTailOverflow) break;
   }
   if (bad) atomicOr(&st->status, kStRank);
 #undef MPROF
@@ -2254,10 +2320,9 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
 }
 
 void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s) {
-  // the barrier counter and the first level's counts start at zero
-  (void)hipMemsetAsync(b.mid, 0, (kMidCnt + kMidCntU32) * sizeof(uint32_t), s);  // barrier + counts[0]
+  (void)hipMemsetAsync(b.mid, 0, 64 * sizeof(uint32_t), s);  // the barrier counter
   k_mid_levels<<<kMidG, kMidT, 0, s>>>(L0, L1, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out, b.pos_out, b.st,
-                                       b.mid, b.tile_prof);
+                                       b.mid, reinterpret_cast<Rec*>(b.mid + kMidXb), b.tile_prof);
 }
 
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s) {

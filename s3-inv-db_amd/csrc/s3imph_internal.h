@@ -131,21 +131,21 @@ constexpr unsigned kStStop = kStGeometry | kStOverflow | kStLookback | kStTooMan
 // LDS-resident bit vectors (k_tail); larger levels run as full-grid kernels.
 constexpr unsigned long long kTailKeys = 12288;
 // Mid-size levels (above the tail, at most kMidMaxKeys keys) run inside one persistent
-// kernel of kMidG cooperating workgroups (s3imph_binned.hip, k_mid_levels): global A/C
-// bit vectors, grid barriers between phases, records in registers.
+// kernel of kMidG cooperating workgroups (s3imph_binned.hip, k_mid_levels): records in
+// registers, routed to the workgroup owning their position's words, grid barriers.
 constexpr int kMidG = 48;
 constexpr int kMidT = 1024;
-constexpr int kMidR = 8;  // records per thread
-constexpr unsigned long long kMidMaxKeys = (unsigned long long)kMidG * kMidT * kMidR;
+constexpr int kMidR = 8;                   // records per thread (registers)
+constexpr unsigned kMidSeg = 512;          // exchange records per (owner, sender)
+constexpr unsigned kMidStage = 6144;       // settled records staged per owner (LDS)
+constexpr unsigned long long kMidMaxKeys = 320ull << 10;  // owners average <= 6.8k of 8k slots
 constexpr uint64_t kMidW32 = 2 * ((2 * kMidMaxKeys + 63) / 64);  // u32 words of the largest mid level
-// scratch (u32 units): barrier counter [64], per-position 8-bit key counts ping-pong
-// [2][8 kMidW32] (32 positions per level word), per-word rank prefix [kMidW32], per-block
-// totals [kMidG] u64
-constexpr uint64_t kMidCnt = 64;                       // first count buffer
-constexpr uint64_t kMidCntU32 = 8 * kMidW32;           // u32 words per count buffer
-constexpr uint64_t kMidR32 = kMidCnt + 2 * kMidCntU32;  // rank prefix
-constexpr uint64_t kMidTot = kMidR32 + kMidW32;         // totals (8-byte aligned: all terms even)
-constexpr uint64_t kMidScratchU32 = kMidTot + 2 * kMidG;
+// scratch (u32 units): barrier counter [64], segment counts [kMidG][kMidG], per-owner
+// totals [kMidG] u64, then the exchange area [kMidG][kMidG][kMidSeg] Rec
+constexpr uint64_t kMidXc = 64;
+constexpr uint64_t kMidTot = kMidXc + (uint64_t)kMidG * kMidG;  // even: u64-aligned
+constexpr uint64_t kMidXb = kMidTot + 2 * kMidG + 16;          // 16-byte aligned
+constexpr uint64_t kMidScratchU32 = kMidXb + (uint64_t)kMidG * kMidG * kMidSeg * 6;
 constexpr double kMidMargin = 1.15;  // a level predicted above kMidMaxKeys / kMidMargin stays binned
 constexpr int kTailThreads = 1024;
 constexpr int kTailLdsWords32 = 2 * 2 * ((kGammaNum * kTailKeys + 63) / 64);  // A and C, u32 words
