@@ -1275,6 +1275,308 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
   if (bad) atomicOr(&st->status, kStRank);
 }
 
+// ------------------------------------------------------------- split big tile -----
+// Tiles of 2^15 / 2^16 positions (C3/C4's first levels, where a tile holds ~16k / ~33k
+// records and the rank permutation of its settled keys does not fit a CU's LDS).  One
+// persistent 1024-thread workgroup per CU takes tiles by ticket:
+//   split     the tile's records are read once (coalesced), A / C marked in LDS, and each
+//             record appended to the scratch segment of its 2^14-position sub-tile (an
+//             LDS cursor per sub-tile: a wave's lanes with one sub-tile land on one run);
+//   finalize  A & ~C -> LDS + global bits, per-word rank prefix; wave look-back for the
+//             tile's rank base; the tile's next-list slots (nk - pop) reserved at once;
+//   per sub-tile: its records come back into registers (kSplitR per thread, coalesced),
+//             settled (f, p) are staged by rank in LDS and written as one run, collided
+//             records go to the next list.
+// Every record is read twice and written once more than in a register tile, all in
+// runs, instead of k_tile's rank-order gathers of (f, p) (16-byte random reads) and its
+// second pass for the collided records.
+constexpr unsigned kSplitSubBits = 14;
+constexpr int kSplitR = 9;                  // sub-tile records per thread in registers (9216 >= 8192 + 11 sigma)
+constexpr unsigned kSplitStage = 6144;      // settled records staged per sub-tile (~0.6 x 8192)
+constexpr unsigned kSplitSeg = 20480;       // scratch records per sub-tile (2.5 x the mean)
+constexpr int kSplitT = 1024;
+constexpr int kSplitGrid = 256;             // one workgroup per CU (its LDS takes ~115 KiB)
+__host__ __device__ constexpr uint64_t split_scratch_recs() { return (uint64_t)kSplitGrid * 4 * kSplitSeg; }
+
+__global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __restrict__ bucket,
+                                                        const unsigned* __restrict__ tile_start,
+                                                        const unsigned* __restrict__ tcnt, uint64_t bucket_cap,
+                                                        unsigned long long* flags, uint64_t* __restrict__ bits,
+                                                        Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
+                                                        uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
+                                                        Rec* __restrict__ scratch, unsigned long long* __restrict__ prof) {
+  __shared__ uint32_t sA[1u << (16 - 5)], sC[1u << (16 - 5)];
+  __shared__ uint64_t sf[kSplitStage], sp[kSplitStage];
+  __shared__ unsigned s_q[4];
+  __shared__ unsigned s_wc[kSplitT / 64];
+  __shared__ unsigned long long s_t, s_prefix, s_b0, s_run;
+  if (!level_active(level, st)) return;
+  const uint64_t N = st->out_cap;
+  const bool out_on = level_out_on(st, level);
+  const uint64_t words = st->words[level], magic = st->magic[level];
+  const uint64_t T = st->ntiles[level];
+  const LevelRange rg = level_range(st, level, words);
+  const uint64_t w32_level = 2 * rg.rw;
+  const unsigned tpw = 1u << (tb - 5);
+  const unsigned nsub = 1u << (tb - kSplitSubBits);
+  uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[level] + rg.plo / 64);
+  const uint64_t seed = level_seed(level);
+  const uint64_t lvl_base = st->lvl_base[level];
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint64_t lt = lanemask_lt();
+  Rec* seg = scratch + (uint64_t)blockIdx.x * 4 * kSplitSeg;  // this workgroup's sub-tile segments
+  bool bad = false;
+  for (;;) {
+    if (tid == 0) s_t = atomicAdd(&st->ticket[level], 1ull);
+    for (unsigned w = tid; w < tpw; w += kSplitT) {
+      sA[w] = 0;
+      sC[w] = 0;
+    }
+    if (tid < 4) s_q[tid] = 0;
+    __syncthreads();
+    const uint64_t t = s_t;
+    if (t >= T) break;
+    // debug: phase stamps (split, finalize, look-back, then one per sub-tile)
+    unsigned long long* tp = prof ? prof + ((uint64_t)level * kMaxTiles + (t < kMaxTiles ? t : 0)) * 8 : nullptr;
+#define SPROF2(i)                                \
+  do {                                           \
+    if (tp && tid == 0) tp[i] = wall_clock64(); \
+  } while (0)
+    SPROF2(0);
+    // bucket range: histogram scan, or the kResShards shard ranges of the tile's slot
+    uint64_t lo, nk, shcap = 0;
+    unsigned pre[kResShards];
+    if (tcnt) {
+      const uint64_t cap = bucket_cap / T;
+      shcap = cap / kResShards;
+      lo = t * cap;
+      unsigned acc = 0;
+#pragma unroll
+      for (int x = 0; x < kResShards; ++x) {
+        pre[x] = acc;
+        acc += tcnt[t * kResShards + x];
+      }
+      nk = acc;
+    } else {
+      lo = tile_start[t];
+      nk = tile_start[t + 1] - lo;
+#pragma unroll
+      for (int x = 0; x < kResShards; ++x) pre[x] = x ? 0xffffffffu : 0u;
+    }
+    const Rec* rb = bucket + lo;
+    auto shard_off = [&](uint64_t j) -> uint64_t {
+      uint64_t o = j;
+#pragma unroll
+      for (int x = 1; x < kResShards; ++x)
+        if (j >= pre[x]) o = (uint64_t)x * shcap + (j - pre[x]);
+      return o;
+    };
+    const uint64_t tbase = rg.plo + (t << tb);
+    // ---- split: mark A / C, append each record to its sub-tile's scratch segment
+    bool over = false;
+    for (uint64_t j0 = tid; j0 < nk; j0 += (uint64_t)kSplitT * kTU) {
+      uint64_t k[kTU], f[kTU], p[kTU];
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        const uint64_t j = j0 + (uint64_t)u * kSplitT;
+        k[u] = f[u] = p[u] = 0;
+        if (j < nk) {
+          const Rec* q = rb + shard_off(j);
+          k[u] = q->k;
+          f[u] = q->f;
+          p[u] = q->p;
+        }
+      }
+      unsigned locs[kTU];
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        const uint64_t j = j0 + (uint64_t)u * kSplitT;
+        locs[u] = 0xffffffffu;
+        if (j < nk) {
+          const unsigned loc = (unsigned)(bb_index(seed, k[u], words, magic) - tbase);
+          locs[u] = loc;
+          const uint32_t bit = 1u << (loc & 31);
+          const uint32_t old = atomicOr(&sA[loc >> 5], bit);
+          if (old & bit) atomicOr(&sC[loc >> 5], bit);
+        }
+      }
+      // sub-tile slots: one LDS reservation per (wave, sub-tile), lanes of a sub-tile in lane order
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        const unsigned q = locs[u] != 0xffffffffu ? locs[u] >> kSplitSubBits : 4u;
+        unsigned slot = 0;
+#pragma unroll
+        for (unsigned qq = 0; qq < 4; ++qq) {
+          const uint64_t mq = __ballot(q == qq);
+          if (!mq) continue;
+          unsigned b = 0;
+          if (lane == (unsigned)__builtin_ctzll(mq)) b = atomicAdd(&s_q[qq], (unsigned)__popcll(mq));
+          b = __shfl(b, __builtin_ctzll(mq));
+          if (q == qq) slot = b + (unsigned)__popcll(mq & lt);
+        }
+        if (q < 4) {
+          if (slot < kSplitSeg) seg[(uint64_t)q * kSplitSeg + slot] = Rec{k[u], f[u], p[u]};
+          else over = true;
+        }
+      }
+    }
+    if (over) atomicOr(&st->status, kStOverflow);
+    __syncthreads();
+    SPROF2(1);
+    // ---- finalize: A & ~C -> LDS + global bits; per-word rank prefix into C
+    const unsigned per = (tpw + kSplitT - 1) / kSplitT, w0 = tid * per;
+    uint64_t cntw = 0;
+    for (unsigned q = 0; q < per; ++q) {
+      const unsigned w = w0 + q;
+      if (w < tpw) {
+        const uint32_t v = sA[w] & ~sC[w];
+        sA[w] = v;
+        const uint64_t gw = (uint64_t)t * tpw + w;
+        if (gw < w32_level) g32[gw] = v;
+        cntw += __popc(v);
+      }
+    }
+    uint64_t pop;
+    uint64_t run = block_exscan<kSplitT>(cntw, &pop);
+    for (unsigned q = 0; q < per; ++q) {
+      const unsigned w = w0 + q;
+      if (w < tpw) {
+        sC[w] = (uint32_t)run;
+        run += __popc(sA[w]);
+      }
+    }
+    SPROF2(2);
+    if (tid == 64) {
+      s_b0 = nk > pop ? atomicAdd(&st->n[level + 1], (unsigned long long)(nk - pop)) : 0ull;
+      s_run = 0;
+    }
+    if (wave == 0) {
+      const uint64_t excl = look_back_wave(flags, t, pop, st);
+      if (lane == 0) {
+        if (t == T - 1) st->lvl_base[level + 1] = lvl_base + excl + pop;
+        s_prefix = excl;
+      }
+    }
+    __syncthreads();
+    SPROF2(3);
+    const uint64_t base = lvl_base + s_prefix;
+    const bool ok = base + pop <= N;
+    if (!ok && out_on) bad = true;
+    // ---- per sub-tile: records back into registers, staged outputs, collided -> next
+    for (unsigned sq = 0; sq < nsub; ++sq) {
+      const unsigned m = min(s_q[sq], kSplitSeg);
+      const Rec* sr = seg + (uint64_t)sq * kSplitSeg;
+      const unsigned qw = sq << (kSplitSubBits - 5);              // first word of the sub-tile
+      const unsigned qrank = sC[qw];                               // its first rank in the tile
+      const unsigned qend = sq + 1 < nsub ? sC[qw + (1u << (kSplitSubBits - 5))] : (unsigned)pop;
+      const bool fits = m <= (unsigned)kSplitR * kSplitT;
+      unsigned wc = 0;
+      if (fits) {
+        uint64_t k[kSplitR], f[kSplitR], p[kSplitR];
+#pragma unroll
+        for (int r = 0; r < kSplitR; ++r) {
+          const unsigned j = r * kSplitT + tid;
+          k[r] = f[r] = p[r] = 0;
+          if (j < m) {
+            k[r] = sr[j].k;
+            f[r] = sr[j].f;
+            p[r] = sr[j].p;
+          }
+        }
+        unsigned redo = 0;
+#pragma unroll
+        for (int r = 0; r < kSplitR; ++r) {
+          const unsigned j = r * kSplitT + tid;
+          bool rd = false;
+          if (j < m) {
+            const unsigned loc = (unsigned)(bb_index(seed, k[r], words, magic) - tbase);
+            const uint32_t wv = sA[loc >> 5];
+            const uint32_t bit = 1u << (loc & 31);
+            if (wv & bit) {
+              const unsigned local = sC[loc >> 5] + __popc(wv & (bit - 1)) - qrank;
+              if (local < kSplitStage) {
+                sf[local] = f[r];
+                sp[local] = p[r];
+              } else if (ok && out_on) {
+                fp_out[base + qrank + local] = f[r];
+                pos_out[base + qrank + local] = p[r];
+              }
+            } else {
+              rd = true;
+              redo |= 1u << r;
+            }
+          }
+          wc += __popcll(__ballot(rd));
+        }
+        if (lane == 0) s_wc[wave] = wc;
+        __syncthreads();
+        uint64_t o = s_b0 + s_run;
+        for (unsigned w = 0; w < wave; ++w) o += s_wc[w];
+#pragma unroll
+        for (int r = 0; r < kSplitR; ++r) {
+          const bool rd = (redo >> r) & 1u;
+          const uint64_t mm = __ballot(rd);
+          if (rd) next[o + __popcll(mm & lt)] = Rec{k[r], f[r], p[r]};
+          o += __popcll(mm);
+        }
+      } else {
+        // more records than registers hold (never at load 1/2): straight from scratch
+        for (unsigned jb = wave * 64; jb < m; jb += kSplitT) {
+          const unsigned j = jb + lane;
+          bool rd = false;
+          if (j < m) {
+            const unsigned loc = (unsigned)(bb_index(seed, sr[j].k, words, magic) - tbase);
+            const uint32_t wv = sA[loc >> 5];
+            const uint32_t bit = 1u << (loc & 31);
+            if (wv & bit) {
+              if (ok && out_on) {
+                const uint64_t q = base + sC[loc >> 5] + __popc(wv & (bit - 1));
+                fp_out[q] = sr[j].f;
+                pos_out[q] = sr[j].p;
+              }
+            } else {
+              rd = true;
+            }
+          }
+          wc += __popcll(__ballot(rd));
+        }
+        if (lane == 0) s_wc[wave] = wc;
+        __syncthreads();
+        uint64_t o = s_b0 + s_run;
+        for (unsigned w = 0; w < wave; ++w) o += s_wc[w];
+        for (unsigned jb = wave * 64; jb < m; jb += kSplitT) {
+          const unsigned j = jb + lane;
+          bool rd = false;
+          if (j < m) {
+            const unsigned loc = (unsigned)(bb_index(seed, sr[j].k, words, magic) - tbase);
+            rd = !((sA[loc >> 5] >> (loc & 31)) & 1u);
+          }
+          const uint64_t mm = __ballot(rd);
+          if (rd) next[o + __popcll(mm & lt)] = sr[j];
+          o += __popcll(mm);
+        }
+      }
+      if (ok && out_on && fits) {
+        const unsigned ns = min(qend - qrank, kSplitStage);
+        for (unsigned i = tid; i < ns; i += kSplitT) {
+          fp_out[base + qrank + i] = sf[i];
+          pos_out[base + qrank + i] = sp[i];
+        }
+      }
+      __syncthreads();  // stage / s_wc reused by the next sub-tile
+      if (tid == 0) {
+        unsigned long long c = 0;
+        for (int w = 0; w < kSplitT / 64; ++w) c += s_wc[w];
+        s_run += c;
+      }
+      __syncthreads();
+      if (sq < 4) SPROF2(4 + sq);
+    }
+#undef SPROF2
+  }
+  if (bad) atomicOr(&st->status, kStRank);
+}
+
 // ------------------------------------------------------- register-resident tile -----
 // Tiles of at most 2^kRegMaxBits positions hold ~2^(tb-1) records, at most kRegR per
 // thread (record r NT + i belongs to thread i, so every load instruction is coalesced):
@@ -2232,6 +2534,8 @@ size_t tile_lds_bytes(unsigned tb) {
 
 }  // namespace
 
+uint64_t split_scratch_records() { return split_scratch_recs(); }
+
 void binned_set_lds_limits() {
   (void)hipFuncSetAttribute((const void*)k_tile<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)std::max(tile_lds_bytes(kTileMaxBits), tile_lds_bytes(kCacheBits)));
@@ -2304,6 +2608,14 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
     return;
   }
   const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kScatterTiles * kResShards : nullptr;
+  // 2^15 / 2^16 tiles: the split kernel (k_tile stays for contexts without its scratch
+  // and for the 2^17+ tiles of oversized conservative reruns)
+  if (b.split && (g.tb == 15 || g.tb == 16)) {
+    k_tile_split<<<kSplitGrid, kSplitT, 0, s>>>(level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags, b.bits,
+                                                b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.split,
+                                                b.tile_prof);
+    return;
+  }
   k_tile<1024><<<grid_tiles, 1024, tile_lds_bytes(g.tb), s>>>(level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags,
                                                           b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb,
                                                           b.tile_prof);

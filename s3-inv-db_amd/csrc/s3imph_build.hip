@@ -98,6 +98,7 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
 
 void free_workspace(s3imph_ctx* c) {
   dfree(c->mid);
+  dfree(c->split);
   dfree(c->kh); dfree(c->fp); dfree(c->bits); dfree(c->rank_base);
   dfree(c->block_sums); dfree(c->d_st);
   dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
@@ -244,6 +245,9 @@ BinBuffers make_bufs(s3imph_ctx* c, const uint64_t* pos, uint64_t* fp_out, uint6
   }
   if (!c->mid) dalloc(c->mid, kMidScratchU32);
   b.mid = c->mid;
+  // 2^15 / 2^16-position tiles appear once a level has more than 2^14 x 4096 positions
+  if (!c->split && c->cap_keys > (kMaxTiles << kRegTileMaxBits) / 2) dalloc(c->split, split_scratch_records());
+  b.split = c->split;
   b.bits = c->bits;
   b.cap_words = c->cap_words;
   b.fp_out = fp_out;

@@ -141,6 +141,7 @@ struct s3imph_ctx {
   int device = 0;
   s3imph::FinScratch* fin = nullptr;  // finalize-pass scratch (s3imph_finalize.hip), lazily made
   uint32_t* mid = nullptr;            // k_mid_levels scratch (kMidScratchU32), lazily made
+  Rec* split = nullptr;               // k_tile_split scratch, made for sets big enough for 2^15+ tiles
   hipStream_t own_stream = nullptr;
   std::mutex mu;
 

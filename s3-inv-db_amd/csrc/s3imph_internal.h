@@ -192,7 +192,9 @@ struct BinBuffers {
   LevelState* st;
   bool dist;                            // multi-GPU owner levels: level 0 reads list[1] too
   uint32_t* mid;                        // k_mid_levels scratch (kMidScratchU32)
+  Rec* split;                           // k_tile_split scratch (split_scratch_records()), or null
 };
+uint64_t split_scratch_records();  // sub-tile segments of the split big-tile kernel
 void binned_set_lds_limits();
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s, bool histogram = true);

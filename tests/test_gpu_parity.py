@@ -408,6 +408,12 @@ def test_big_tiles_bit_exact(s3, oracle_lib):
         c.close()
 
 
+def test_big_tiles_counted_path(s3, oracle_lib):
+    """2^16-position tiles fed by the counted scatter (histogram-scan ranges instead of
+    reservation shards), 40M keys: the split big-tile kernel reads contiguous buckets."""
+    _parity_subprocess({"S3IMPH_RES_MAX": "0", "S3IMPH_RES0": "0"}, [(40_000_000, 0, 12)])
+
+
 @pytest.mark.parametrize("kind,avg", [(0, 32), (1, 0)])
 def test_repeated_builds_identical(s3, oracle_lib, ctx, kind, avg):
     """Schedule-dependent races show up as a build that differs from the others: 12
