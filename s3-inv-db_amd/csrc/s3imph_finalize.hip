@@ -126,10 +126,185 @@ __global__ __launch_bounds__(kFB) void k_fin_keys(const uint8_t* __restrict__ bl
   }
 }
 
+// Pass 1, LDS-staged (byte-aligned blobs, the default): a workgroup walks its contiguous
+// key range in rounds of up to 2 kFinT keys whose bytes (<= kFinBB) come in with coalesced
+// 16-byte loads and are staged in LDS, as the level-0 hash does; each lane then counts its
+// keys' '/' bytes and compares each key with its successor from LDS words.  The round's
+// last key meets its successor (the next round's first key) through global loads.
+constexpr int kFinT = 256;
+constexpr int kFinBB = 32 << 10;
+constexpr int kFinGrid = 4096;
+
+// 8 bytes at byte offset o of the LDS window (16 readable bytes past its end)
+__device__ __forceinline__ uint64_t lds8(const uint64_t* sw, unsigned o) {
+  const unsigned s8 = o & 7u;
+  const uint64_t lo = sw[o >> 3];
+  return s8 ? funnel_bytes(lo, sw[(o >> 3) + 1], s8) : lo;
+}
+
+__global__ __launch_bounds__(kFinT) void k_fin_keys_lds(const uint8_t* __restrict__ blob,
+                                                        const uint64_t* __restrict__ offsets,
+                                                        const uint32_t* __restrict__ depths_in, uint64_t n,
+                                                        uint32_t* __restrict__ depth, int32_t* __restrict__ lcp) {
+  constexpr int G = 2 * kFinT;
+  constexpr int KW = (kFinBB / 16 + kFinT - 1) / kFinT;
+  __shared__ uint64_t sw[kFinBB / 8 + 4];
+  __shared__ unsigned s_cnt[kFinT / 64];
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+  uint64_t g = (uint64_t)blockIdx.x * per;
+  const uint64_t gend = min(n, g + per);
+  const uint64_t end8 = (offsets[n] + 7) & ~7ull;
+  // the round at r0: key bounds and its window chunks in registers (issued one round ahead)
+  uint64_t kb0[2], kb1[2], wlo = 0, wend = 0;
+  bool kin[2];
+  uint4 wr[KW];
+  auto prefetch = [&](uint64_t r0) {
+    const uint64_t last = min(gend, r0 + G);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t i = r0 + tid + (unsigned)h * kFinT;
+      kin[h] = i < last;
+      kb0[h] = kin[h] ? offsets[i] : 0;
+      kb1[h] = kin[h] ? offsets[i + 1] : 0;
+    }
+    wlo = uniform64(offsets[r0] & ~15ull);
+    wend = uniform64(min((offsets[last] + 15) & ~15ull, wlo + (uint64_t)kFinBB));
+#pragma unroll
+    for (int kk = 0; kk < KW; ++kk) {
+      const uint64_t a = wlo + 16ull * (tid + (unsigned)kk * kFinT);
+      wr[kk] = make_uint4(0, 0, 0, 0);
+      if (a < wend) {
+        if (a + 16 <= end8) {
+          wr[kk] = *reinterpret_cast<const uint4*>(blob + a);
+        } else {
+          const uint2 hh = *reinterpret_cast<const uint2*>(blob + a);
+          wr[kk].x = hh.x;
+          wr[kk].y = hh.y;
+        }
+      }
+    }
+  };
+  if (g < gend) prefetch(g);
+  while (g < gend) {
+#pragma unroll
+    for (int kk = 0; kk < KW; ++kk) {
+      const unsigned c = tid + (unsigned)kk * kFinT;
+      if (wlo + 16ull * c < wend) {
+        sw[2 * c] = (uint64_t)wr[kk].x | ((uint64_t)wr[kk].y << 32);
+        sw[2 * c + 1] = (uint64_t)wr[kk].z | ((uint64_t)wr[kk].w << 32);
+      }
+    }
+    if (tid < 4) sw[(wend - wlo) / 8 + tid] = 0;  // read slack past the window
+    // keys whose bytes all lie in the window: a prefix of the round (offsets ascend)
+    bool fits[2];
+    unsigned mine = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      fits[h] = kin[h] && kb1[h] - wlo <= (uint64_t)(wend - wlo);
+      mine += (unsigned)__popcll(__ballot(fits[h]));
+    }
+    if (lane == 0) s_cnt[wave] = mine;
+    __syncthreads();
+    unsigned m = 0;
+#pragma unroll
+    for (int w = 0; w < kFinT / 64; ++w) m += s_cnt[w];
+    if (m == 0) m = 1;  // a first key longer than the window: taken from global memory
+    const uint64_t r0 = g, rwlo = wlo, rwend = wend;
+    const uint64_t t0[2] = {kb0[0], kb0[1]}, t1[2] = {kb1[0], kb1[1]};
+    g += m;
+    if (g < gend) prefetch(g);  // the next round's loads land while this one is compared
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const unsigned idx = tid + (unsigned)h * kFinT;
+      const uint64_t i = r0 + idx;
+      if (idx < m && i < n) {
+        const uint64_t b0 = t0[h], b1 = t1[h], len = b1 - b0;
+        const bool in_w = fits[h];
+        auto key8 = [&](uint64_t k8) -> uint64_t {  // 8 bytes of key i from byte k8
+          return in_w ? lds8(sw, (unsigned)(b0 - rwlo + k8)) : load8(blob, b0 + k8, end8);
+        };
+        uint32_t d = 0;
+        if (depths_in) {
+          d = depths_in[i];
+        } else {
+          for (uint64_t k8 = 0; k8 < len; k8 += 8) {
+            uint64_t z = zero_bytes(key8(k8) ^ 0x2f2f2f2f2f2f2f2full);
+            if (len - k8 < 8) z &= (1ull << (8 * (len - k8))) - 1;
+            d += (uint32_t)__popcll(z & 0x8080808080808080ull);
+          }
+        }
+        depth[i] = d;
+        int32_t l = -1;
+        if (i + 1 < n) {
+          // the successor: in the window when it is one of this round's keys that fit
+          const uint64_t c0 = b1, c1 = offsets[i + 2], mm = min(len, c1 - c0);
+          const bool nin = in_w && idx + 1 < m && c1 - rwlo <= (uint64_t)(rwend - rwlo);
+          uint64_t k8 = 0;
+          for (; k8 < mm; k8 += 8) {
+            const uint64_t y = nin ? lds8(sw, (unsigned)(c0 - rwlo + k8)) : load8(blob, c0 + k8, end8);
+            const uint64_t x = key8(k8) ^ y;
+            if (x) {
+              k8 += (uint64_t)(__builtin_ctzll(x) >> 3);
+              break;
+            }
+          }
+          l = (int32_t)min(k8, mm);
+        }
+        lcp[i] = l;
+      }
+    }
+    __syncthreads();  // the window is reused by the next round
+  }
+}
+
+// Block minima of lcp / maxima of depth from the arrays pass 1 wrote: one 1024-key block
+// per 256-thread workgroup, four keys per lane in 16-byte loads (a 1024-thread workgroup per
+// block was latency-bound: 1.13 ms on C3).  The global maxDepth is taken per superblock.
+constexpr int kFBT = kFB / 4;
+__global__ __launch_bounds__(kFBT) void k_fin_blocks(const uint32_t* __restrict__ depth,
+                                                     const int32_t* __restrict__ lcp, uint64_t n,
+                                                     int32_t* __restrict__ bmin, uint32_t* __restrict__ bmax) {
+  __shared__ int32_t s_min[kFBT / 64];
+  __shared__ uint32_t s_max[kFBT / 64];
+  const uint64_t i = (uint64_t)blockIdx.x * kFB + 4ull * threadIdx.x;
+  int32_t mn = 0x7fffffff;
+  uint32_t mx = 0;
+  if (i + 4 <= n && ((uintptr_t)depth & 15) == 0) {  // lcp is our scratch (aligned); depth the caller's
+    const int4 l4 = *reinterpret_cast<const int4*>(lcp + i);
+    const uint4 d4 = *reinterpret_cast<const uint4*>(depth + i);
+    mn = min(min(l4.x, l4.y), min(l4.z, l4.w));
+    mx = max(max(d4.x, d4.y), max(d4.z, d4.w));
+  } else {
+    for (uint64_t q = i; q < n; ++q) {
+      mn = min(mn, lcp[q]);
+      mx = max(mx, depth[q]);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    mn = min(mn, __shfl_xor(mn, o));
+    mx = max(mx, __shfl_xor(mx, o));
+  }
+  if (lane_id() == 0) {
+    s_min[threadIdx.x >> 6] = mn;
+    s_max[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 0; w < kFBT / 64; ++w) {
+      mn = min(mn, s_min[w]);
+      mx = max(mx, s_max[w]);
+    }
+    bmin[blockIdx.x] = mn;
+    bmax[blockIdx.x] = mx;
+  }
+}
+
 // Pass 1b: superblock minima / maxima over the block arrays (one block per superblock).
 __global__ __launch_bounds__(kFS) void k_fin_super(const int32_t* __restrict__ bmin, const uint32_t* __restrict__ bmax,
                                                    uint64_t nb, int32_t* __restrict__ smin,
-                                                   uint32_t* __restrict__ smax) {
+                                                   uint32_t* __restrict__ smax, unsigned* __restrict__ maxd) {
   __shared__ int32_t s_min[kFS / 64];
   __shared__ uint32_t s_max[kFS / 64];
   const uint64_t b = (uint64_t)blockIdx.x * kFS + threadIdx.x;
@@ -152,6 +327,7 @@ __global__ __launch_bounds__(kFS) void k_fin_super(const int32_t* __restrict__ b
     }
     smin[blockIdx.x] = mn;
     smax[blockIdx.x] = mx;
+    if (maxd) atomicMax(maxd, mx);  // one atomic per superblock
   }
 }
 
@@ -296,8 +472,15 @@ int finalize_device(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
     f.cap = n;
   }
   HIPCHECK(hipMemsetAsync(f.maxd, 0, sizeof(unsigned), s));
-  k_fin_keys<<<(unsigned)nb, kFB, 0, s>>>(blob, offsets, depths, n, depth, f.lcp, f.bmin, f.bmax, f.maxd);
-  k_fin_super<<<(unsigned)nsb, kFS, 0, s>>>(f.bmin, f.bmax, nb, f.smin, f.smax);
+  const bool staged = ((uintptr_t)blob & 15) == 0;
+  if (staged) {
+    k_fin_keys_lds<<<(unsigned)std::min<uint64_t>(kFinGrid, (n + 2 * kFinT - 1) / (2 * kFinT)), kFinT, 0, s>>>(
+        blob, offsets, depths, n, depth, f.lcp);
+    k_fin_blocks<<<(unsigned)nb, kFBT, 0, s>>>(depth, f.lcp, n, f.bmin, f.bmax);
+  } else {  // a caller's unaligned blob: per-lane unaligned loads
+    k_fin_keys<<<(unsigned)nb, kFB, 0, s>>>(blob, offsets, depths, n, depth, f.lcp, f.bmin, f.bmax, f.maxd);
+  }
+  k_fin_super<<<(unsigned)nsb, kFS, 0, s>>>(f.bmin, f.bmax, nb, f.smin, f.smax, staged ? f.maxd : nullptr);
   k_fin_subtree<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(offsets, n, depth, f.lcp, f.bmin, f.bmax, f.smin, f.smax,
                                                            nb, nsb, subtree_end, max_depth_sub);
   HIPCHECK(hipGetLastError());
