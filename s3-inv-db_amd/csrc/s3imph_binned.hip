@@ -697,7 +697,11 @@ __global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __re
 // kR records per round, at most kT tiles (<4096, 4096>: one block per CU, 152 KiB of LDS).
 // <2048, 2048> (two blocks per CU, so one block's atomics and barriers overlap the other's
 // memory phases) measured slower on C2: level-0 scatter 0.156 -> 0.214 ms.
-template <int kR, int kT>
+// kSrc: 0 records from ilist; 1 level-0 arrays ik / ifp with caller positions ipos;
+// 2 level-0 arrays with identity positions.  A compile-time source keeps the loads
+// straight-line: with run-time selects the compiler waited out every record's loads
+// before issuing the next record's (four round trips per round).
+template <int kR, int kT, int kSrc>
 __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __restrict__ ilist,
                                                      const uint64_t* __restrict__ ik, const uint64_t* __restrict__ ifp,
                                                      const uint64_t* __restrict__ ipos, uint64_t pos_base,
@@ -759,27 +763,33 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   const uint64_t stride = (uint64_t)gridDim.x * kR;
   uint64_t r0 = i_lo + (uint64_t)blockIdx.x * kR;
   if (r0 >= n) return;
-  // debug: round-0 phase timestamps of this block in prof row 32 + level
+  // debug: this block's time per phase summed over all its rounds, in prof row 32 + level
+  // (stored as cumulative stamps: p[0] start, p[i] = p[i-1] + time of phase i)
   unsigned long long* tp =
       prof && blockIdx.x < kMaxTiles ? prof + ((uint64_t)(32 + level) * kMaxTiles + blockIdx.x) * 8 : nullptr;
-  int round = 0;
-#define SPROF(i)                                                \
-  do {                                                          \
-    if (tp && tid == 0 && round == 0) tp[i] = wall_clock64(); \
+  unsigned long long t_last = 0, t_first = 0, acc[4] = {0, 0, 0, 0};
+#define SPROF(i)                                                       \
+  do {                                                                 \
+    if (tp && tid == 0) {                                              \
+      const unsigned long long now_ = wall_clock64();                  \
+      if ((i) == 0) t_first = now_;                                    \
+      else if ((i) <= 4) acc[(i) > 0 ? (i) - 1 : 0] += now_ - t_last;    \
+      t_last = now_;                                                   \
+    }                                                                  \
   } while (0)
   SPROF(0);
   // records as three scalar arrays: a conditionally loaded Rec[] would live in scratch.
   // Level 0 reads the hash kernel's key-order arrays instead of a record list.
   uint64_t rk_[kKPT], rf_[kKPT], rp_[kKPT];
   auto load = [&](uint64_t i, int q) {
-    if (ilist) {
+    if constexpr (kSrc == 0) {
       rk_[q] = ilist[i].k;
       rf_[q] = ilist[i].f;
       rp_[q] = ilist[i].p;
     } else {
       rk_[q] = ik[i];
       rf_[q] = ifp[i];
-      rp_[q] = ipos ? ipos[i] : pos_base + i;
+      rp_[q] = kSrc == 1 ? ipos[i] : pos_base + i;
     }
   };
 #pragma unroll
@@ -819,16 +829,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
       if (t0 + q < T) start[t0 + q] = (unsigned)ex;
       ex += a[q];
     }
-    // one tile per thread, so the returning atomics of a round are all in flight at once
-    for (uint64_t t = tid; t < T; t += kSB) {
-      const unsigned c = cnt[t];
-      if (c) {
-        const uint64_t at = atomicAdd(&tcnt[t * kResShards + shard], c);
-        if (at + c > scap) s_over = 1;
-        cur[t] = (unsigned)(t * cap + shard * scap + at);
-      }
-    }
-    __syncthreads();
+    __syncthreads();  // start[] complete
     SPROF(2);
 #pragma unroll
     for (int q = 0; q < kKPT; ++q) {
@@ -839,6 +840,18 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
         stile[slot] = (unsigned short)tt[q];
       }
     }
+    // The round's returning atomics (up to kTPT tiles per thread) and the next round's
+    // loads are all issued before any atomic result is used, so the two latencies
+    // overlap; one tile at a time waited out each round trip in turn (C3 level 0: ~10 of
+    // ~20 us per round).
+    unsigned ac[kTPT], at[kTPT];
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      const uint64_t t = (uint64_t)q * kSB + tid;
+      ac[q] = t < T ? cnt[t] : 0u;
+      at[q] = 0;
+      if (ac[q]) at[q] = atomicAdd(&tcnt[t * kResShards + shard], ac[q]);
+    }
     const unsigned m = (unsigned)min<uint64_t>(kR, n - r0);
     r0 += stride;
     const bool more = r0 < n;
@@ -846,6 +859,14 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     for (int q = 0; q < kKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < n) load(i, q);
+    }
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      if (ac[q]) {
+        const uint64_t t = (uint64_t)q * kSB + tid;
+        if (at[q] + ac[q] > scap) s_over = 1;
+        cur[t] = (unsigned)(t * cap + shard * scap + at[q]);
+      }
     }
     __syncthreads();
     SPROF(3);
@@ -856,13 +877,17 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     }
     __syncthreads();
     SPROF(4);
-    SPROF(7);
-    ++round;
     if (!more) break;
     for (uint64_t t = tid; t < T; t += kSB) cnt[t] = 0;
     __syncthreads();
   }
   if (s_over && tid == 0) atomicOr(&st->status, kStOverflow | kStResOverflow);
+  if (tp && tid == 0) {
+    unsigned long long c = t_first;
+    tp[0] = c;
+    for (int i = 0; i < 4; ++i) tp[i + 1] = (c += acc[i]);
+    tp[7] = c;
+  }
 #undef SPROF
 }
 
@@ -1291,12 +1316,13 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
 // runs, instead of k_tile's rank-order gathers of (f, p) (16-byte random reads) and its
 // second pass for the collided records.
 constexpr unsigned kSplitSubBits = 14;
+constexpr unsigned kSplitMaxSub = 1u << (kSplitMaxBits - kSplitSubBits);  // 16 sub-tiles of a 2^18 tile
 constexpr int kSplitR = 9;                  // sub-tile records per thread in registers (9216 >= 8192 + 11 sigma)
-constexpr unsigned kSplitStage = 6144;      // settled records staged per sub-tile (~0.6 x 8192)
-constexpr unsigned kSplitSeg = 20480;       // scratch records per sub-tile (2.5 x the mean)
+constexpr unsigned kSplitStage = 5120;      // settled records staged per sub-tile (mean ~4970, sigma ~44)
+constexpr unsigned kSplitSeg = 10240;       // scratch records per sub-tile (mean 8192, sigma ~90)
 constexpr int kSplitT = 1024;
-constexpr int kSplitGrid = 256;             // one workgroup per CU (its LDS takes ~115 KiB)
-__host__ __device__ constexpr uint64_t split_scratch_recs() { return (uint64_t)kSplitGrid * 4 * kSplitSeg; }
+constexpr int kSplitGrid = 256;             // one workgroup per CU (its LDS takes ~144 KiB)
+__host__ __device__ constexpr uint64_t split_scratch_recs() { return (uint64_t)kSplitGrid * kSplitMaxSub * kSplitSeg; }
 
 __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __restrict__ bucket,
                                                         const unsigned* __restrict__ tile_start,
@@ -1305,9 +1331,9 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
                                                         Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
                                                         uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
                                                         Rec* __restrict__ scratch, unsigned long long* __restrict__ prof) {
-  __shared__ uint32_t sA[1u << (16 - 5)], sC[1u << (16 - 5)];
+  __shared__ uint32_t sA[1u << (kSplitMaxBits - 5)], sC[1u << (kSplitMaxBits - 5)];
   __shared__ uint64_t sf[kSplitStage], sp[kSplitStage];
-  __shared__ unsigned s_q[4];
+  __shared__ unsigned s_q[kSplitMaxSub];
   __shared__ unsigned s_wc[kSplitT / 64];
   __shared__ unsigned long long s_t, s_prefix, s_b0, s_run;
   if (!level_active(level, st)) return;
@@ -1324,7 +1350,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
   const uint64_t lvl_base = st->lvl_base[level];
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint64_t lt = lanemask_lt();
-  Rec* seg = scratch + (uint64_t)blockIdx.x * 4 * kSplitSeg;  // this workgroup's sub-tile segments
+  Rec* seg = scratch + (uint64_t)blockIdx.x * kSplitMaxSub * kSplitSeg;  // this workgroup's sub-tile segments
   bool bad = false;
   for (;;) {
     if (tid == 0) s_t = atomicAdd(&st->ticket[level], 1ull);
@@ -1332,7 +1358,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
       sA[w] = 0;
       sC[w] = 0;
     }
-    if (tid < 4) s_q[tid] = 0;
+    if (tid < kSplitMaxSub) s_q[tid] = 0;
     __syncthreads();
     const uint64_t t = s_t;
     if (t >= T) break;
@@ -1372,25 +1398,27 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
       return o;
     };
     const uint64_t tbase = rg.plo + (t << tb);
-    // ---- split: mark A / C, append each record to its sub-tile's scratch segment
+    // ---- split: mark A / C, append each record to its sub-tile's scratch segment.
+    // Batches of kTU records per thread, the next batch's loads in flight while one is
+    // processed (double-buffered registers); workgroup-uniform trip count and clamped
+    // indices keep the loads unconditional, so the compiler waits for one batch only.
     bool over = false;
-    for (uint64_t j0 = tid; j0 < nk; j0 += (uint64_t)kSplitT * kTU) {
-      uint64_t k[kTU], f[kTU], p[kTU];
+    auto load_batch = [&](uint64_t jb, uint64_t (&k)[kTU], uint64_t (&f)[kTU], uint64_t (&p)[kTU]) {
 #pragma unroll
       for (int u = 0; u < kTU; ++u) {
-        const uint64_t j = j0 + (uint64_t)u * kSplitT;
-        k[u] = f[u] = p[u] = 0;
-        if (j < nk) {
-          const Rec* q = rb + shard_off(j);
-          k[u] = q->k;
-          f[u] = q->f;
-          p[u] = q->p;
-        }
+        const uint64_t j = min(jb + (uint64_t)u * kSplitT + tid, nk - 1);
+        const Rec* q = rb + shard_off(j);
+        k[u] = q->k;
+        f[u] = q->f;
+        p[u] = q->p;
       }
+    };
+    auto split_batch = [&](uint64_t jb, const uint64_t (&k)[kTU], const uint64_t (&f)[kTU],
+                           const uint64_t (&p)[kTU]) {
       unsigned locs[kTU];
 #pragma unroll
       for (int u = 0; u < kTU; ++u) {
-        const uint64_t j = j0 + (uint64_t)u * kSplitT;
+        const uint64_t j = jb + (uint64_t)u * kSplitT + tid;
         locs[u] = 0xffffffffu;
         if (j < nk) {
           const unsigned loc = (unsigned)(bb_index(seed, k[u], words, magic) - tbase);
@@ -1400,24 +1428,39 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
           if (old & bit) atomicOr(&sC[loc >> 5], bit);
         }
       }
-      // sub-tile slots: one LDS reservation per (wave, sub-tile), lanes of a sub-tile in lane order
+      // sub-tile slots: one LDS reservation per (wave, sub-tile), lanes of a sub-tile in
+      // lane order.  A lane's peers (lanes of its sub-tile) come from one ballot per bit of
+      // the sub-tile index; the lowest peer reserves for all of them.
 #pragma unroll
       for (int u = 0; u < kTU; ++u) {
-        const unsigned q = locs[u] != 0xffffffffu ? locs[u] >> kSplitSubBits : 4u;
-        unsigned slot = 0;
+        const unsigned q = locs[u] != 0xffffffffu ? locs[u] >> kSplitSubBits : kSplitMaxSub;
+        uint64_t peers = __ballot(true);
 #pragma unroll
-        for (unsigned qq = 0; qq < 4; ++qq) {
-          const uint64_t mq = __ballot(q == qq);
-          if (!mq) continue;
-          unsigned b = 0;
-          if (lane == (unsigned)__builtin_ctzll(mq)) b = atomicAdd(&s_q[qq], (unsigned)__popcll(mq));
-          b = __shfl(b, __builtin_ctzll(mq));
-          if (q == qq) slot = b + (unsigned)__popcll(mq & lt);
+        for (unsigned bq = 1; bq <= kSplitMaxSub; bq <<= 1) {
+          const uint64_t m1 = __ballot((q & bq) != 0);
+          peers &= (q & bq) ? m1 : ~m1;
         }
-        if (q < 4) {
+        const unsigned lead = (unsigned)__builtin_ctzll(peers);
+        unsigned b = 0;
+        if (lane == lead && q < kSplitMaxSub) b = atomicAdd(&s_q[q], (unsigned)__popcll(peers));
+        b = __shfl(b, lead);
+        if (q < kSplitMaxSub) {
+          const unsigned slot = b + (unsigned)__popcll(peers & lt);
           if (slot < kSplitSeg) seg[(uint64_t)q * kSplitSeg + slot] = Rec{k[u], f[u], p[u]};
           else over = true;
         }
+      }
+    };
+    constexpr uint64_t kBatch = (uint64_t)kSplitT * kTU;
+    if (nk) {
+      uint64_t kA[kTU], fA[kTU], pA[kTU], kB[kTU], fB[kTU], pB[kTU];
+      load_batch(0, kA, fA, pA);
+      for (uint64_t jb = 0; jb < nk; jb += 2 * kBatch) {
+        load_batch(jb + kBatch, kB, fB, pB);
+        split_batch(jb, kA, fA, pA);
+        if (jb + kBatch >= nk) break;
+        load_batch(jb + 2 * kBatch, kA, fA, pA);
+        split_batch(jb + kBatch, kB, fB, pB);
       }
     }
     if (over) atomicOr(&st->status, kStOverflow);
@@ -2610,7 +2653,7 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
   const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kScatterTiles * kResShards : nullptr;
   // 2^15 / 2^16 tiles: the split kernel (k_tile stays for contexts without its scratch
   // and for the 2^17+ tiles of oversized conservative reruns)
-  if (b.split && (g.tb == 15 || g.tb == 16)) {
+  if (b.split && g.tb > kRegMaxBits && g.tb <= kSplitMaxBits) {
     k_tile_split<<<kSplitGrid, kSplitT, 0, s>>>(level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags, b.bits,
                                                 b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.split,
                                                 b.tile_prof);
@@ -2626,9 +2669,10 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
   const bool l0 = level == 0 && !b.dist;
   const Rec* il = l0 ? nullptr : b.list[(level - 1) & 1];
   unsigned* tc = b.tcnt + (uint64_t)level * kScatterTiles * kResShards;
-  k_scatter_res<kSubRound, kLdsTiles><<<grid, kSB, 0, s>>>(level, il, b.kh, b.fp, b.pos, b.pos_base, tc, b.bucket,
-                                                           b.bucket_cap, b.flags, b.st, g.tb, b.cap_words,
-                                                           b.tile_prof, i_lo, i_hi);
+  auto kern = !l0 ? k_scatter_res<kSubRound, kLdsTiles, 0>
+             : b.pos ? k_scatter_res<kSubRound, kLdsTiles, 1> : k_scatter_res<kSubRound, kLdsTiles, 2>;
+  kern<<<grid, kSB, 0, s>>>(level, il, b.kh, b.fp, b.pos, b.pos_base, tc, b.bucket, b.bucket_cap, b.flags, b.st, g.tb,
+                            b.cap_words, b.tile_prof, i_lo, i_hi);
 }
 
 void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s) {

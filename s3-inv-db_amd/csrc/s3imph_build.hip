@@ -360,7 +360,8 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
   const BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
   const double q = 1.0 - std::exp(-0.5);
-  const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
+  LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
+  if (const char* e = std::getenv("S3IMPH_L0TB")) g0.tb = (unsigned)std::atoi(e);  // TEMP experiment
   launch_init_state(c->d_st, n, n, s, offsets);
   ev_mark(c, s, "init");
   const Grids gr = level_grids(n, 64 * level_words(n), g0);
@@ -496,7 +497,7 @@ void print_tile_profile(s3imph_ctx* c) {
     static const char* snames[7] = {"count", "resv", "stage", "write", "-", "-", "-"};
     const bool sc = L >= 32;
     std::fprintf(stderr, "  %s L%d: %d %s, span %.1f us, avg us:", sc ? "scatter_res" : "tile", sc ? L - 32 : L, cnt,
-                 sc ? "blocks (round 0)" : "tiles", (hi - lo) / 100.0);
+                 sc ? "blocks (all rounds)" : "tiles", (hi - lo) / 100.0);
     for (int i = 0; i < (sc ? 4 : 7); ++i) std::fprintf(stderr, " %s %.2f", (sc ? snames : names)[i], sum[i] / cnt / 100.0);
     std::fprintf(stderr, "\n");
   }

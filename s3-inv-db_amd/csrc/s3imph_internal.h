@@ -74,6 +74,12 @@ constexpr uint64_t kTargetTiles0 = 2048;              // level 0: 2^14-position 
 constexpr uint64_t kTargetTiles = 1024;               // levels >= 1 on the counted path
 constexpr uint64_t kTargetTilesRes = 256;             // reservation-path levels: ~1 tile per CU
 constexpr unsigned kRegTileMaxBits = 14;              // largest tile of the register-resident kernel
+// Levels too big for 2^14-position tiles (C3/C4's first levels) take the split kernel's
+// 2^15..2^18 tiles, the smallest with at most kSplitTargetTiles tiles: fewer, bigger tiles give
+// the reservation scatter longer runs and fewer slot atomics per round (C3 level 0:
+// 2^16 / 2^17 / 2^18 tiles, scatter 1.73 / 1.45 / 1.19 ms).
+constexpr unsigned kSplitMaxBits = 18;
+constexpr uint64_t kSplitTargetTiles = 1024;
 constexpr uint64_t kHistCap = 8ull << 20;             // tiles x chunks entries
 constexpr unsigned kStTailOverflow = 16u;             // tail reached with a level too big for LDS
 constexpr unsigned kStGeometry = 32u;                 // tiles/chunks outside the workspace
@@ -107,6 +113,8 @@ inline LevelGeom choose_geom_sz(uint64_t n, uint64_t size, uint64_t target_tiles
   unsigned tb = kTileMinBits;
   while (tb < max_tb && (size >> tb) > target_tiles) ++tb;
   while (tb < kTileMaxBits && ((size + (1ull << tb) - 1) >> tb) > kMaxTiles) ++tb;  // workspace bound
+  if (tb > kRegTileMaxBits)
+    while (tb < kSplitMaxBits && ((size + (1ull << tb) - 1) >> tb) > kSplitTargetTiles) ++tb;
   const uint64_t T = (size + (1ull << tb) - 1) >> tb;
   uint64_t chunk = ((n + target_chunks - 1) / target_chunks + kChunkGran - 1) / kChunkGran * kChunkGran;
   if (chunk < kSubRound) chunk = kSubRound;
