@@ -360,8 +360,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
   const BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
   const double q = 1.0 - std::exp(-0.5);
-  LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
-  if (const char* e = std::getenv("S3IMPH_L0TB")) g0.tb = (unsigned)std::atoi(e);  // TEMP experiment
+  const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
   launch_init_state(c->d_st, n, n, s, offsets);
   ev_mark(c, s, "init");
   const Grids gr = level_grids(n, 64 * level_words(n), g0);
