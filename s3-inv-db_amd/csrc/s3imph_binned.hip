@@ -2613,6 +2613,13 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
 
 void launch_hash0_only(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                        int grid, hipStream_t s) {
+  if (((uintptr_t)blob & 15) == 0) {  // as the single-GPU level 0: pair rounds unless st->skew
+    k_hash0_pair<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
+                                                           g.tb, g.chunk, b.tcnt, nullptr);
+    k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
+                                             g.chunk, b.tcnt, 5);
+    return;
+  }
   k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
                                            g.chunk, b.tcnt, 3);
 }

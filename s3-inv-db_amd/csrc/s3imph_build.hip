@@ -709,8 +709,17 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   const int P = d.nranks, R = d.rank;
   LevelState* st = c->d_st;
   const BinBuffers b = make_bufs(c, nullptr, fp_out, pos_out, s);
+  // Distributed levels keep their input in list[1] and their collided records in list[0]:
+  // the route of level L reads list[0] and writes this rank's own records straight into
+  // list[1] (no exchange copy), the received ones after them.  The tile pipeline reads
+  // level L from list[(L-1)&1] and writes redo to list[L&1], so odd levels see the two
+  // buffers swapped.
+  BinBuffers bsw = b;
+  std::swap(bsw.list[0], bsw.list[1]);
+  Rec* const lin = c->list[1];
+  Rec* const lredo = c->list[0];
   const double q = 1.0 - std::exp(-0.5);
-  launch_init_state(st, 0, out_cap, s);
+  launch_init_state(st, n_local, out_cap, s, n_local ? offsets : nullptr);  // samples key lengths (st->skew)
   HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kScatterTiles * kResShards * sizeof(unsigned), s));
   launch_dist_setup(st, 0, nullptr, N, R, P, s);
   ev_mark(c, s, "init");
@@ -736,9 +745,9 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
       }
       HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
       if (L == 0)
-        launch_route0_arrays(c->kh, c->fp, pos, key_base, n_local, d.send, C, d.scnt, st, P, s);
+        launch_route0_arrays(c->kh, c->fp, pos, key_base, n_local, d.send, C, d.scnt, st, P, R, lin, d.cap_list, s);
       else
-        launch_route(L, c->list[(L - 1) & 1], (uint64_t)src_pred, d.send, C, d.scnt, st, P, s);
+        launch_route(L, lredo, (uint64_t)src_pred, d.send, C, d.scnt, st, P, R, lin, d.cap_list, s);
       launch_route_flag(st, d.scnt, P, s);
       cm.allgather(d.scnt, d.mat, 8ull * (P + 1), s);
       HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, s));
@@ -767,20 +776,20 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
              std::to_string(d.cap_list) + ")";
       return S3IMPH_ERR_NOMEM;
     }
-    // ---- exchange: the received records become this level's list, list[(L-1)&1]
-    uint64_t acc = 0;
+    // ---- exchange: the received records follow this rank's own ones in list[1]
+    uint64_t acc = M[(uint64_t)R * (P + 1) + R] * sizeof(Rec);
     for (int t = 0; t < P; ++t) {
       soff[t] = (uint64_t)t * C * sizeof(Rec);
-      sbytes[t] = M[(uint64_t)R * (P + 1) + t] * sizeof(Rec);
-      roff[t] = acc;
-      rbytes[t] = M[(uint64_t)t * (P + 1) + R] * sizeof(Rec);
+      sbytes[t] = t == R ? 0 : M[(uint64_t)R * (P + 1) + t] * sizeof(Rec);
+      roff[t] = t == R ? 0 : acc;
+      rbytes[t] = t == R ? 0 : M[(uint64_t)t * (P + 1) + R] * sizeof(Rec);
       acc += rbytes[t];
     }
-    cm.alltoallv(d.send, soff.data(), sbytes.data(), c->list[(L - 1) & 1], roff.data(), rbytes.data(), s);
+    cm.alltoallv(d.send, soff.data(), sbytes.data(), lin, roff.data(), rbytes.data(), s);
     launch_set_u64(&st->n[L], m, s);
     ev_mark(c, s, L == 0 ? "route0" : "route");
     // ---- the owner's tile pipeline over positions [64 lo, 64 (lo + rw))
-    enqueue_list_level(c, b, L, m, 64 * rw, conservative, nullptr, s);
+    enqueue_list_level(c, (L & 1) ? bsw : b, L, m, 64 * rw, conservative, nullptr, s);
     ev_mark(c, s, L == 0 ? "level0" : "levels");
     // ---- size the next level from the global redo count (device side, no host sync)
     cm.allreduce_u64(&st->n[L + 1], d.gslot + L + 1, 1, s);
@@ -811,7 +820,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
       dalloc(d.send, (uint64_t)P * maxc);
       d.cap_send = (uint64_t)P * maxc;
     }
-    cm.allgather(rl, d.send, maxc * sizeof(Rec), s);
+    cm.allgather(lredo, d.send, maxc * sizeof(Rec), s);
     uint64_t o = 0;
     for (int r = 0; r < P; ++r) {
       if (cnt[r])

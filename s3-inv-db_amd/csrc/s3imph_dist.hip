@@ -42,7 +42,9 @@ __device__ __forceinline__ unsigned owner_of(uint64_t w, uint64_t S, uint64_t mS
 // over the bytes, as StreamingMPHFBuilder.Add does); 2: level 0 from the hash kernel's
 // key-order kh / fp arrays; 1: the collided records list[0..n[level]).  Each round of kRRound records is counting-sorted by owner
 // in LDS; one atomic per (round, owner) reserves its run in the owner's send region
-// [d*cap, (d+1)*cap), and the runs are written out coalesced.  A region overflow sets
+// [d*cap, (d+1)*cap), and the runs are written out coalesced.  Records this rank owns
+// itself skip the exchange: they go straight to `self_dst` (the level's input list,
+// capacity self_cap), counted in scnt[rank] like any owner's.  A region overflow sets
 // kStRouteOverflow (the host re-routes with larger regions; bytes are unaffected).
 template <int kSrc>
 __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restrict__ blob,
@@ -51,11 +53,12 @@ __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restr
                                                const uint64_t* __restrict__ ipos, uint64_t pos_base,
                                                uint64_t n_keys, const Rec* __restrict__ ilist,
                                                Rec* __restrict__ send, uint64_t cap,
-                                               unsigned long long* __restrict__ scnt, LevelState* st, int P) {
+                                               unsigned long long* __restrict__ scnt, LevelState* st, int P,
+                                               int rank, Rec* __restrict__ self_dst, uint64_t self_cap) {
   __shared__ Rec stage[kRRound];
   __shared__ unsigned char sdst[kRRound];
   __shared__ unsigned cnt[kMaxRanks], start[kMaxRanks];
-  __shared__ unsigned long long base[kMaxRanks];
+  __shared__ Rec* base[kMaxRanks];
   __shared__ unsigned s_over;
   const unsigned tid = threadIdx.x;
   if (tid == 0) s_over = 0;
@@ -102,8 +105,9 @@ __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restr
       start[tid] = x - c;
       if (c) {
         const unsigned long long at = atomicAdd(&scnt[tid], (unsigned long long)c);
-        if (at + c > cap) s_over = 1;
-        base[tid] = (unsigned long long)tid * cap + at;
+        const bool self = (int)tid == rank;
+        if (at + c > (self ? self_cap : cap)) s_over = 1;
+        base[tid] = (self ? self_dst : send + (uint64_t)tid * cap) + at;
       }
     }
     __syncthreads();
@@ -121,7 +125,7 @@ __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restr
     if (!s_over) {
       for (unsigned j = tid; j < m; j += kRT) {
         const unsigned o = sdst[j];
-        send[base[o] + (j - start[o])] = stage[j];
+        base[o][j - start[o]] = stage[j];
       }
     }
     __syncthreads();
@@ -181,22 +185,26 @@ void launch_route_flag(LevelState* st, unsigned long long* scnt, int P, hipStrea
 }
 
 void launch_route0(const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t pos_base, uint64_t n,
-                   Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, hipStream_t s) {
+                   Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, int rank, Rec* self_dst,
+                   uint64_t self_cap, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + kRRound - 1) / kRRound, 2048));
-  k_route<0><<<grid, kRT, 0, s>>>(0, blob, offsets, nullptr, nullptr, pos, pos_base, n, nullptr, send, cap, scnt, st, P);
+  k_route<0><<<grid, kRT, 0, s>>>(0, blob, offsets, nullptr, nullptr, pos, pos_base, n, nullptr, send, cap, scnt, st, P,
+                                   rank, self_dst, self_cap);
 }
 
 void launch_route0_arrays(const uint64_t* kh, const uint64_t* fp, const uint64_t* pos, uint64_t pos_base, uint64_t n,
-                          Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, hipStream_t s) {
+                          Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, int rank,
+                          Rec* self_dst, uint64_t self_cap, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + kRRound - 1) / kRRound, 2048));
-  k_route<2><<<grid, kRT, 0, s>>>(0, nullptr, nullptr, kh, fp, pos, pos_base, n, nullptr, send, cap, scnt, st, P);
+  k_route<2><<<grid, kRT, 0, s>>>(0, nullptr, nullptr, kh, fp, pos, pos_base, n, nullptr, send, cap, scnt, st, P, rank,
+                                   self_dst, self_cap);
 }
 
 void launch_route(int level, const Rec* list, uint64_t n_pred, Rec* send, uint64_t cap, unsigned long long* scnt,
-                  LevelState* st, int P, hipStream_t s) {
+                  LevelState* st, int P, int rank, Rec* self_dst, uint64_t self_cap, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n_pred + kRRound - 1) / kRRound + 8, 2048));
   k_route<1><<<grid, kRT, 0, s>>>(level, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, list, send, cap, scnt, st,
-                                   P);
+                                   P, rank, self_dst, self_cap);
 }
 
 void launch_dist_setup(LevelState* st, int L, const unsigned long long* gcount, uint64_t n_value, int rank, int P,

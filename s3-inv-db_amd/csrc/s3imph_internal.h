@@ -218,16 +218,19 @@ void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s);
 
 // ---- multi-GPU launchers (s3imph_dist.hip) ------------------------------------------
 constexpr int kMaxRanks = 64;
+// Records owned by `rank` itself go straight to self_dst (capacity self_cap), not to a send region.
 void launch_route0(const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t pos_base, uint64_t n,
-                   Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, hipStream_t s);
+                   Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, int rank, Rec* self_dst,
+                   uint64_t self_cap, hipStream_t s);
 // level-0 records from the hash kernel's kh / fp arrays (multi-GPU build)
 void launch_route0_arrays(const uint64_t* kh, const uint64_t* fp, const uint64_t* pos, uint64_t pos_base, uint64_t n,
-                          Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, hipStream_t s);
+                          Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, int rank,
+                          Rec* self_dst, uint64_t self_cap, hipStream_t s);
 // the level-0 hash kernel alone (kh, fp in key order; no histogram)
 void launch_hash0_only(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                        int grid, hipStream_t s);
 void launch_route(int level, const Rec* list, uint64_t n_pred, Rec* send, uint64_t cap, unsigned long long* scnt,
-                  LevelState* st, int P, hipStream_t s);
+                  LevelState* st, int P, int rank, Rec* self_dst, uint64_t self_cap, hipStream_t s);
 void launch_dist_setup(LevelState* st, int L, const unsigned long long* gcount, uint64_t n_value, int rank, int P,
                        hipStream_t s);
 void launch_set_u64(unsigned long long* p, uint64_t v, hipStream_t s);
