@@ -73,6 +73,8 @@ def main() -> None:
                     help="N>1 collectives: RCCL over xGMI (default), or host copies over gloo — a rehearsal "
                          "mode that lets several ranks share one GPU (not a measurement)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 line beside the C3 headline")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="skip the lookup / finalize / host_e2e lines (profiling runs)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC summary (HBM bytes per launch) to attach as roofline.traffic")
     args = ap.parse_args()
@@ -236,10 +238,10 @@ def main() -> None:
                                        "unit": "T byte-steps/s", "frac": steps_per_s / 1e12 / FNV_STEP_PEAK_T,
                                        "hbm": hbm})
         result["dominant_stage"] = max(stages, key=stages.get)
-    if world == 1 and not use_dist:
+    if world == 1 and not use_dist and not args.headline_only:
         result["lookup"] = lookup_rate(ctx, d_blob, d_offs, n, d_fp, d_po)
         result["finalize"] = finalize_rate(ctx, d_blob, d_offs, n)
-    if world == 1:
+    if world == 1 and not args.headline_only:
         result["host_e2e"] = host_e2e(s3imph, blob, offs, local_rank)
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(s3imph, cfg, args.seed)
