@@ -264,6 +264,24 @@ int s3imph_finalize_index_device(s3imph_ctx *ctx, const uint8_t *d_blob, const u
                                  uint64_t offsets_cap, uint32_t *max_depth, void *stream);
 
 /* ------------------------------------------------------------------------
+ * 5b. manifest.json (optional part): size + SHA-256 of every index file.
+ *     Replaces format.WriteManifest / VerifyManifest (pkg/format/manifest.go:33-138), which
+ *     IndexBuilder.Finalize calls after the other files (indexbuild.go:429-432).  The JSON
+ *     text is Go's json.MarshalIndent output (map keys sorted; created_at RFC 3339 UTC).
+ *     Host-only; files are hashed in parallel, with the x86 SHA extensions when present.
+ * ------------------------------------------------------------------------ */
+/* WriteManifest(dir, nodeCount, maxDepth): absent index files are skipped; error text
+ * "write manifest: ..." as IndexBuilder wraps it. */
+int s3imph_write_manifest(const char *out_dir, uint64_t node_count, uint32_t max_depth, char *err,
+                          size_t errlen);
+/* ReadManifest + VerifyManifest: S3IMPH_ERR_FORMAT on a size or checksum mismatch
+ * ("file %s: checksum mismatch"), S3IMPH_ERR_IO when a listed file is missing. */
+int s3imph_verify_manifest(const char *dir, char *err, size_t errlen);
+/* checksumFile (manifest.go:140-155): lowercase hex SHA-256 of a file into hex_out (65 B,
+ * NUL-terminated); portable != 0 forces the portable compression loop (tests). */
+int s3imph_sha256_file(const char *path, int portable, char hex_out[65], char *err, size_t errlen);
+
+/* ------------------------------------------------------------------------
  * 6. Deterministic synthetic prefix sets (bench/test support, not on the path).
  *    kind: 0 = s3-like, lengths uniform in [max(10, avg/2), 3avg/2],
  *              distinct and byte-sorted;

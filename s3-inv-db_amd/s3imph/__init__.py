@@ -61,6 +61,7 @@ EXPORTS = (
     "s3imph_dist_segments", "s3imph_dist_out_cap", "s3imph_ctx_last_error",
     "s3imph_ctx_load_mph_bin", "s3imph_lookup_device", "s3imph_gen_keys",
     "s3imph_finalize_index_host", "s3imph_finalize_index_device",
+    "s3imph_write_manifest", "s3imph_verify_manifest", "s3imph_sha256_file",
 )
 
 
@@ -138,6 +139,9 @@ def _load():
         "s3imph_finalize_index_device": (i32, [vp, vp, vp, vp, u64, vp, vp, vp, vp, vp, u64,
                                                P(ctypes.c_uint32), vp]),
         "s3imph_gen_keys": (i32, [i32, u64, ctypes.c_uint32, u64, u64, vp, vp, P(u64)]),
+        "s3imph_write_manifest": (i32, [cp, u64, ctypes.c_uint32, cp, sz]),
+        "s3imph_verify_manifest": (i32, [cp, cp, sz]),
+        "s3imph_sha256_file": (i32, [cp, i32, cp, cp, sz]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -408,6 +412,35 @@ def finalize_index_host(blob: np.ndarray, offsets: np.ndarray, out_dir: str, dep
     rc = LIB.s3imph_finalize_index_host(device, _np_ptr(blob), _np_ptr(offsets), _np_ptr(dp) if dp is not None else None,
                                         len(offsets) - 1, out_dir.encode(), err, 1024)
     _check(rc, err)
+
+
+def write_manifest(out_dir: str, node_count: int, max_depth: int) -> None:
+    """format.WriteManifest (pkg/format/manifest.go:33-95): manifest.json with the size and
+    SHA-256 of every index file present in out_dir."""
+    err = ctypes.create_string_buffer(1024)
+    _check(LIB.s3imph_write_manifest(out_dir.encode(), node_count, max_depth, err, 1024), err)
+
+
+def read_manifest(dir_: str) -> dict:
+    """format.ReadManifest (manifest.go:97-111)."""
+    import json
+    with open(os.path.join(dir_, "manifest.json"), "rb") as f:
+        return json.loads(f.read())
+
+
+def verify_manifest(dir_: str) -> None:
+    """format.VerifyManifest (manifest.go:113-138): every listed file's size and checksum;
+    raises MPHFError (ERR_FORMAT on a mismatch, ERR_IO on a missing file)."""
+    err = ctypes.create_string_buffer(1024)
+    _check(LIB.s3imph_verify_manifest(dir_.encode(), err, 1024), err)
+
+
+def sha256_file(path: str, portable: bool = False) -> str:
+    """checksumFile (manifest.go:140-155): hex SHA-256 of a file."""
+    err = ctypes.create_string_buffer(1024)
+    out = ctypes.create_string_buffer(65)
+    _check(LIB.s3imph_sha256_file(path.encode(), int(portable), out, err, 1024), err)
+    return out.value.decode()
 
 
 S3ID_MAGIC = 0x53334944  # pkg/format/format.go:6-45

@@ -16,7 +16,7 @@ from conftest import ROOT
 
 def _declared():
     src = open(os.path.join(ROOT, "include", "s3imph.h")).read()
-    return set(re.findall(r"^(?:int|void|uint64_t|const char)\s*\*?\s*(s3imph_[a-z_]+)\(", src, re.M))
+    return set(re.findall(r"^(?:int|void|uint64_t|const char)\s*\*?\s*(s3imph_[a-z0-9_]+)\(", src, re.M))
 
 
 def test_header_and_binding_agree():
