@@ -433,25 +433,9 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
       for (int h = 0; h < 2; ++h) {
         const unsigned slot = h == 0 ? tid : m - 1 - tid;
         if (h == 0 ? tid < (m + 1) / 2 : tid < m / 2) {
-          uint64_t a = kFnvOffset, b = kFnvOffset;
+          uint64_t a, b;
           const unsigned j = sidx[slot];
-          const unsigned o = soff[slot], len = slen[slot];
-          const uint64_t* w = sw + (o >> 3);
-          const unsigned s = o & 7u;
-          const unsigned nfull = len >> 3;
-          uint64_t cur = w[0];
-          for (unsigned q = 0; q < nfull; ++q) {
-            const uint64_t nxt = w[q + 1];
-            fnv_8(a, b, funnel_bytes(cur, nxt, s));
-            cur = nxt;
-          }
-          const unsigned rem = len & 7u;
-          if (rem) {
-            const uint64_t v = funnel_bytes(cur, w[nfull + 1], s);
-#pragma unroll
-            for (unsigned t = 0; t < 7; ++t)
-              if (t < rem) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
-          }
+          fnv_window(reinterpret_cast<const uint32_t*>(sw), soff[slot], slen[slot], a, b);
           kh[r0 + j] = a;
           fp[r0 + j] = b;
           zero |= (a == 0);

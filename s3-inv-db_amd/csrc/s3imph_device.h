@@ -81,6 +81,84 @@ static __device__ __forceinline__ void fnv_step(uint64_t& a, uint64_t& b, uint32
   b = (uint64_t)blo | ((uint64_t)bhi << 32);
 }
 
+// x ^ (byte B of w): one v_xor_b32 with an SDWA byte select (the compiler's own lowering
+// spends a shift on bytes 1 and 2).
+template <int B>
+static __device__ __forceinline__ uint32_t xor_byte(uint32_t x, uint32_t w) {
+  uint32_t r;
+  if constexpr (B == 0)
+    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD"
+        : "=v"(r) : "v"(w), "v"(x));
+  else if constexpr (B == 1)
+    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+        : "=v"(r) : "v"(w), "v"(x));
+  else if constexpr (B == 2)
+    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+        : "=v"(r) : "v"(w), "v"(x));
+  else
+    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+        : "=v"(r) : "v"(w), "v"(x));
+  return r;
+}
+
+// FNV-1a + FNV-1 steps on byte B of w: 8 VALU ops (xor, 3 for the multiply, per hash).
+template <int B>
+static __device__ __forceinline__ void fnv_step_b(uint32_t& alo, uint32_t& ahi, uint32_t& blo, uint32_t& bhi,
+                                                  uint32_t w) {
+  alo = xor_byte<B>(alo, w);
+  fnv_mulP(alo, ahi);
+  fnv_mulP(blo, bhi);
+  blo = xor_byte<B>(blo, w);
+}
+
+// The four bytes of w in stream order.
+static __device__ __forceinline__ void fnv_4b(uint32_t& alo, uint32_t& ahi, uint32_t& blo, uint32_t& bhi,
+                                              uint32_t w) {
+  fnv_step_b<0>(alo, ahi, blo, bhi, w);
+  fnv_step_b<1>(alo, ahi, blo, bhi, w);
+  fnv_step_b<2>(alo, ahi, blo, bhi, w);
+  fnv_step_b<3>(alo, ahi, blo, bhi, w);
+}
+
+// The first `rem` (< 8) bytes of the stream words r0, r1.
+static __device__ __forceinline__ void fnv_tail_b(uint32_t& alo, uint32_t& ahi, uint32_t& blo, uint32_t& bhi,
+                                                  uint32_t r0, uint32_t r1, unsigned rem) {
+  if (rem > 0) fnv_step_b<0>(alo, ahi, blo, bhi, r0);
+  if (rem > 1) fnv_step_b<1>(alo, ahi, blo, bhi, r0);
+  if (rem > 2) fnv_step_b<2>(alo, ahi, blo, bhi, r0);
+  if (rem > 3) fnv_step_b<3>(alo, ahi, blo, bhi, r0);
+  if (rem > 4) fnv_step_b<0>(alo, ahi, blo, bhi, r1);
+  if (rem > 5) fnv_step_b<1>(alo, ahi, blo, bhi, r1);
+  if (rem > 6) fnv_step_b<2>(alo, ahi, blo, bhi, r1);
+}
+
+// FNV-1a + FNV-1 of a key of `len` bytes starting `o` bytes into a dword-addressed window
+// (LDS): each 8-byte stream word is two v_alignbyte funnels of consecutive dwords, so the
+// key's start needs no select between the word's halves.  Reads up to 12 bytes past the
+// key's end.
+static __device__ __forceinline__ void fnv_window(const uint32_t* win, unsigned o, unsigned len, uint64_t& ha,
+                                                  uint64_t& hb) {
+  uint32_t alo = (uint32_t)kFnvOffset, ahi = (uint32_t)(kFnvOffset >> 32), blo = alo, bhi = ahi;
+  const uint32_t* w = win + (o >> 2);
+  const unsigned sb = o & 3u;
+  const unsigned nfull = len >> 3;
+  uint32_t cur = w[0];
+  for (unsigned q = 0; q < nfull; ++q) {
+    const uint32_t n1 = w[2 * q + 1], n2 = w[2 * q + 2];
+    fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n1, cur, sb));
+    fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n2, n1, sb));
+    cur = n2;
+  }
+  const unsigned rem = len & 7u;
+  if (rem) {
+    const uint32_t n1 = w[2 * nfull + 1], n2 = w[2 * nfull + 2];
+    fnv_tail_b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n1, cur, sb), __builtin_amdgcn_alignbyte(n2, n1, sb),
+               rem);
+  }
+  ha = (uint64_t)alo | ((uint64_t)ahi << 32);
+  hb = (uint64_t)blo | ((uint64_t)bhi << 32);
+}
+
 // FNV-1a and FNV-1 over the 8 bytes of v, little-endian order.
 static __device__ __forceinline__ void fnv_8(uint64_t& a, uint64_t& b, uint64_t v) {
   uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
