@@ -162,9 +162,16 @@ static __device__ __forceinline__ void fnv_window(const uint32_t* win, unsigned 
 // FNV-1a and FNV-1 over the 8 bytes of v, little-endian order.
 static __device__ __forceinline__ void fnv_8(uint64_t& a, uint64_t& b, uint64_t v) {
   uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
-  const uint32_t w0 = (uint32_t)v, w1 = (uint32_t)(v >> 32);
-#pragma unroll
-  for (int t = 0; t < 8; ++t) fnv_step_w(alo, ahi, blo, bhi, ((t < 4 ? w0 : w1) >> (8 * (t & 3))) & 0xffu);
+  fnv_4b(alo, ahi, blo, bhi, (uint32_t)v);
+  fnv_4b(alo, ahi, blo, bhi, (uint32_t)(v >> 32));
+  a = (uint64_t)alo | ((uint64_t)ahi << 32);
+  b = (uint64_t)blo | ((uint64_t)bhi << 32);
+}
+
+// FNV-1a and FNV-1 over the first rem (< 8) bytes of v.
+static __device__ __forceinline__ void fnv_tail8(uint64_t& a, uint64_t& b, uint64_t v, unsigned rem) {
+  uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
+  fnv_tail_b(alo, ahi, blo, bhi, (uint32_t)v, (uint32_t)(v >> 32), rem);
   a = (uint64_t)alo | ((uint64_t)ahi << 32);
   b = (uint64_t)blo | ((uint64_t)bhi << 32);
 }
@@ -188,9 +195,7 @@ static __device__ __forceinline__ void fnv_words(const uint64_t* w, uint64_t nw,
     if (rem) {
       const uint64_t nxt = (nfull + 1 < nw) ? w[nfull + 1] : 0;
       const uint64_t v = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
-#pragma unroll
-      for (unsigned t = 0; t < 7; ++t)
-        if (t < rem) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
+      fnv_tail8(a, b, v, rem);
     }
   }
   ha = a;
@@ -243,9 +248,7 @@ static __device__ __forceinline__ void fnv_both_pf(const uint8_t* __restrict__ b
     const unsigned rem = (unsigned)(len & 7);
     if (rem) {
       const uint64_t v = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
-#pragma unroll
-      for (unsigned t = 0; t < 7; ++t)
-        if (t < rem) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
+      fnv_tail8(a, b, v, rem);
     }
   }
   ha = a;
@@ -319,10 +322,7 @@ static __device__ __forceinline__ void fnv_both_16(const uint8_t* __restrict__ b
         fnv_8(a, b, lo);
         v = hi;
       }
-      const unsigned r8 = rem & 7;
-#pragma unroll
-      for (unsigned t = 0; t < 7; ++t)
-        if (t < r8) fnv_step(a, b, (uint32_t)(v >> (8 * t)) & 0xffu);
+      fnv_tail8(a, b, v, rem & 7);
     }
   }
   ha = a;
@@ -356,7 +356,7 @@ static __device__ __forceinline__ void fnv_both(const uint8_t* __restrict__ blob
         cur = W[q];
       }
     }
-    for (unsigned t = 0; t < rem; ++t) fnv_step(a, b, (uint32_t)(vrem >> (8 * t)) & 0xffu);
+    fnv_tail8(a, b, vrem, rem);
   }
   ha = a;
   hb = b;
