@@ -1315,9 +1315,16 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
                                                         Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
                                                         uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
                                                         Rec* __restrict__ scratch, unsigned long long* __restrict__ prof) {
+  constexpr int kSU = 3;  // split-phase records per thread per batch (the batch is staged in sfp)
+  static_assert((size_t)kSU * kSplitT * sizeof(Rec) <= 2 * kSplitStage * sizeof(uint64_t), "split stage fits sf/sp");
   __shared__ uint32_t sA[1u << (kSplitMaxBits - 5)], sC[1u << (kSplitMaxBits - 5)];
-  __shared__ uint64_t sf[kSplitStage], sp[kSplitStage];
-  __shared__ unsigned s_q[kSplitMaxSub];
+  __shared__ uint64_t sfp[2 * kSplitStage];  // phase 2: settled (f, p) by rank; split phase: the batch by sub-tile
+  __shared__ unsigned char stq[kSU * kSplitT];
+  __shared__ unsigned s_q[kSplitMaxSub], s_cnt[kSplitMaxSub], s_start[kSplitMaxSub], s_base[kSplitMaxSub];
+  __shared__ unsigned s_m;
+  uint64_t* const sf = sfp;
+  uint64_t* const sp = sfp + kSplitStage;
+  Rec* const stg = reinterpret_cast<Rec*>(sfp);
   __shared__ unsigned s_wc[kSplitT / 64];
   __shared__ unsigned long long s_t, s_prefix, s_b0, s_run;
   if (!level_active(level, st)) return;
@@ -1342,7 +1349,10 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
       sA[w] = 0;
       sC[w] = 0;
     }
-    if (tid < kSplitMaxSub) s_q[tid] = 0;
+    if (tid < kSplitMaxSub) {
+      s_q[tid] = 0;
+      s_cnt[tid] = 0;
+    }
     __syncthreads();
     const uint64_t t = s_t;
     if (t >= T) break;
@@ -1383,13 +1393,15 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
     };
     const uint64_t tbase = rg.plo + (t << tb);
     // ---- split: mark A / C, append each record to its sub-tile's scratch segment.
-    // Batches of kTU records per thread, the next batch's loads in flight while one is
-    // processed (double-buffered registers); workgroup-uniform trip count and clamped
-    // indices keep the loads unconditional, so the compiler waits for one batch only.
+    // Batches of kSU records per thread, the next batch's loads in flight while one is
+    // processed (double-buffered registers; workgroup-uniform trip count and clamped
+    // indices keep the loads unconditional).  A batch is counting-sorted by sub-tile in
+    // LDS and written to the segments as runs of ~kSU kSplitT / nsub records, so the
+    // scratch stores are whole lines (lane-order appends gave runs of ~4 records).
     bool over = false;
-    auto load_batch = [&](uint64_t jb, uint64_t (&k)[kTU], uint64_t (&f)[kTU], uint64_t (&p)[kTU]) {
+    auto load_batch = [&](uint64_t jb, uint64_t (&k)[kSU], uint64_t (&f)[kSU], uint64_t (&p)[kSU]) {
 #pragma unroll
-      for (int u = 0; u < kTU; ++u) {
+      for (int u = 0; u < kSU; ++u) {
         const uint64_t j = min(jb + (uint64_t)u * kSplitT + tid, nk - 1);
         const Rec* q = rb + shard_off(j);
         k[u] = q->k;
@@ -1397,27 +1409,26 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
         p[u] = q->p;
       }
     };
-    auto split_batch = [&](uint64_t jb, const uint64_t (&k)[kTU], const uint64_t (&f)[kTU],
-                           const uint64_t (&p)[kTU]) {
-      unsigned locs[kTU];
+    auto split_batch = [&](uint64_t jb, const uint64_t (&k)[kSU], const uint64_t (&f)[kSU],
+                           const uint64_t (&p)[kSU]) {
+      unsigned qs[kSU], rk[kSU];
 #pragma unroll
-      for (int u = 0; u < kTU; ++u) {
+      for (int u = 0; u < kSU; ++u) {
         const uint64_t j = jb + (uint64_t)u * kSplitT + tid;
-        locs[u] = 0xffffffffu;
+        qs[u] = kSplitMaxSub;
         if (j < nk) {
           const unsigned loc = (unsigned)(bb_index(seed, k[u], words, magic) - tbase);
-          locs[u] = loc;
+          qs[u] = loc >> kSplitSubBits;
           const uint32_t bit = 1u << (loc & 31);
           const uint32_t old = atomicOr(&sA[loc >> 5], bit);
           if (old & bit) atomicOr(&sC[loc >> 5], bit);
         }
       }
-      // sub-tile slots: one LDS reservation per (wave, sub-tile), lanes of a sub-tile in
-      // lane order.  A lane's peers (lanes of its sub-tile) come from one ballot per bit of
-      // the sub-tile index; the lowest peer reserves for all of them.
+      // rank inside the batch's sub-tile run: one LDS count per (wave, sub-tile) present; a
+      // lane's peers (lanes of its sub-tile) come from one ballot per bit of the index
 #pragma unroll
-      for (int u = 0; u < kTU; ++u) {
-        const unsigned q = locs[u] != 0xffffffffu ? locs[u] >> kSplitSubBits : kSplitMaxSub;
+      for (int u = 0; u < kSU; ++u) {
+        const unsigned q = qs[u];
         uint64_t peers = __ballot(true);
 #pragma unroll
         for (unsigned bq = 1; bq <= kSplitMaxSub; bq <<= 1) {
@@ -1426,18 +1437,47 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
         }
         const unsigned lead = (unsigned)__builtin_ctzll(peers);
         unsigned b = 0;
-        if (lane == lead && q < kSplitMaxSub) b = atomicAdd(&s_q[q], (unsigned)__popcll(peers));
-        b = __shfl(b, lead);
-        if (q < kSplitMaxSub) {
-          const unsigned slot = b + (unsigned)__popcll(peers & lt);
-          if (slot < kSplitSeg) seg[(uint64_t)q * kSplitSeg + slot] = Rec{k[u], f[u], p[u]};
-          else over = true;
+        if (lane == lead && q < kSplitMaxSub) b = atomicAdd(&s_cnt[q], (unsigned)__popcll(peers));
+        rk[u] = __shfl(b, lead) + (unsigned)__popcll(peers & lt);
+      }
+      __syncthreads();
+      if (wave == 0) {  // run starts in the stage, segment reservations
+        const unsigned c = lane < kSplitMaxSub ? s_cnt[lane] : 0u;
+        unsigned x = c;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+          const unsigned y = __shfl_up(x, d);
+          if (lane >= (unsigned)d) x += y;
+        }
+        if (lane < kSplitMaxSub) {
+          s_start[lane] = x - c;
+          s_base[lane] = s_q[lane];
+          s_q[lane] += c;
+          s_cnt[lane] = 0;
+        }
+        if (lane == kSplitMaxSub - 1) s_m = x;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) {
+        if (qs[u] < kSplitMaxSub) {
+          const unsigned slot = s_start[qs[u]] + rk[u];
+          stg[slot] = Rec{k[u], f[u], p[u]};
+          stq[slot] = (unsigned char)qs[u];
         }
       }
+      __syncthreads();
+      const unsigned m = s_m;
+      for (unsigned jj = tid; jj < m; jj += kSplitT) {
+        const unsigned q = stq[jj];
+        const unsigned d = s_base[q] + (jj - s_start[q]);
+        if (d < kSplitSeg) seg[(uint64_t)q * kSplitSeg + d] = stg[jj];
+        else over = true;
+      }
     };
-    constexpr uint64_t kBatch = (uint64_t)kSplitT * kTU;
+    constexpr uint64_t kBatch = (uint64_t)kSplitT * kSU;
     if (nk) {
-      uint64_t kA[kTU], fA[kTU], pA[kTU], kB[kTU], fB[kTU], pB[kTU];
+      uint64_t kA[kSU], fA[kSU], pA[kSU], kB[kSU], fB[kSU], pB[kSU];
       load_batch(0, kA, fA, pA);
       for (uint64_t jb = 0; jb < nk; jb += 2 * kBatch) {
         load_batch(jb + kBatch, kB, fB, pB);
