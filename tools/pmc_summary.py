@@ -51,7 +51,7 @@ def main():
             first.setdefault(o["kernel"], o)
         ent = tr.setdefault(cfg, {})
         scatter0 = "k_scatter_res" if "k_scatter_res" in first and "k_hscan" not in first else "k_scatter"
-        tile0 = next((o["kernel"] for o in out if o["kernel"] in ("k_tile_reg", "k_tile")), "k_tile_reg")
+        tile0 = next((o["kernel"] for o in out if o["kernel"] in ("k_tile_reg", "k_tile_split", "k_tile")), "k_tile_reg")
         hash0 = "k_hash0_pair" if "k_hash0_pair" in first else "k_hash_count0"  # skewed sets: k_hash_count0
         for stage, kern in (("hash_count0", hash0), ("scatter0", scatter0), ("tile0", tile0)):
             if kern in first:
