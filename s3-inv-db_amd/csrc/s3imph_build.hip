@@ -697,6 +697,100 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
 
 
 constexpr int kDistRetry = -1;
+constexpr uint64_t kChunkedRoute0Keys = 8ull << 20;  // sharded level 0 of this many keys per rank: 4 chunks
+constexpr int kRoute0Chunks = 4;
+
+// Level 0 of the sharded build in K key chunks: chunk c is hashed and routed on the build
+// stream s while chunk c-1's records cross xGMI on the exchange stream d.xs, so the
+// level-0 all-to-all hides behind the hash instead of following it.  Records for a peer
+// go to its send region in chunk order (scnt keeps counting across chunks); this rank's
+// own records of chunk c land in list[1] right after everything received for chunks < c
+// (self_dst = lin + received so far), and chunk c's received records follow them.  On
+// return, M holds the cumulative gathered counts, the exchanges are complete on s, and
+// *recv_total is the level's record count on this rank.  Per-chunk counts need one host
+// round trip each, taken while the next chunk is hashed.  Returns kDistRetry when a send
+// region overflowed (the caller reruns on the conservative, unchunked path).
+int route0_chunked(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
+                   uint64_t n_local, uint64_t key_base, uint64_t N, const BinBuffers& b, uint64_t C, Rec* lin,
+                   hipStream_t s, unsigned long long* M, uint64_t* recv_total) {
+  DistState& d = c->d;
+  Comm& cm = *d.comm;
+  const int P = d.nranks, R = d.rank;
+  LevelState* st = c->d_st;
+  if (!d.xs) {
+    HIPCHECK(hipStreamCreateWithFlags(&d.xs, hipStreamNonBlocking));
+    HIPCHECK(hipEventCreateWithFlags(&d.ev_route, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&d.ev_counts, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&d.ev_x, hipEventDisableTiming));
+  }
+  const int K = kRoute0Chunks;
+  const uint64_t per = (n_local + K - 1) / K;
+  const LevelGeom gh = choose_geom_sz(n_local, 64 * level_words(N), kTargetTiles0, chunks0(n_local), kTileMaxBits);
+  auto hash_chunk = [&](int k) {
+    const uint64_t k0 = std::min(n_local, (uint64_t)k * per), k1 = std::min(n_local, k0 + per);
+    if (k1 <= k0) return;
+    BinBuffers bc = b;
+    bc.kh = c->kh + k0;
+    bc.fp = c->fp + k0;
+    launch_hash0_only(blob, offsets + k0, k1 - k0, bc, gh, level_grids(k1 - k0, 64 * level_words(N), gh).gc, s);
+  };
+  HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
+  std::vector<unsigned long long> prev((size_t)(P + 1) * P, 0);
+  std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
+  uint64_t received = 0;  // records received from peers in chunks < k
+  hash_chunk(0);
+  for (int k = 0; k < K; ++k) {
+    const uint64_t k0 = std::min(n_local, (uint64_t)k * per), k1 = std::min(n_local, k0 + per);
+    launch_route0_arrays(c->kh + k0, c->fp + k0, pos ? pos + k0 : nullptr, key_base + k0, k1 - k0, d.send, C, d.scnt,
+                         st, P, R, lin + received, d.cap_list - received, s);
+    launch_route_flag(st, d.scnt, P, s);
+    HIPCHECK(hipEventRecord(d.ev_route, s));
+    if (k + 1 < K) hash_chunk(k + 1);  // the build stream keeps hashing while the counts travel
+    HIPCHECK(hipStreamWaitEvent(d.xs, d.ev_route, 0));
+    cm.allgather(d.scnt, d.mat, 8ull * (P + 1), d.xs);
+    HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, d.xs));
+    HIPCHECK(hipEventRecord(d.ev_counts, d.xs));
+    HIPCHECK(hipEventSynchronize(d.ev_counts));
+    bool over = false;
+    for (int r = 0; r < P; ++r) over |= M[(uint64_t)r * (P + 1) + P] != 0;
+    if (over) {  // every rank sees the same flags: all return, after draining the exchange stream
+      HIPCHECK(hipStreamSynchronize(d.xs));
+      HIPCHECK(hipStreamSynchronize(s));
+      return kDistRetry;
+    }
+    // chunk k: this rank's own records sit at [self_before + received, self_now + received);
+    // the peers' records of chunk k follow them
+    auto at = [&](const unsigned long long* m, int r, int t) { return m[(uint64_t)r * (P + 1) + t]; };
+    uint64_t acc = (at(M, R, R) + received) * sizeof(Rec);
+    uint64_t got = 0;
+    for (int t = 0; t < P; ++t) {
+      const uint64_t sn = at(M, R, t) - at(prev.data(), R, t), rn = at(M, t, R) - at(prev.data(), t, R);
+      soff[t] = ((uint64_t)t * C + at(prev.data(), R, t)) * sizeof(Rec);
+      sbytes[t] = t == R ? 0 : sn * sizeof(Rec);
+      roff[t] = t == R ? 0 : acc;
+      rbytes[t] = t == R ? 0 : rn * sizeof(Rec);
+      if (t != R) {
+        acc += rbytes[t];
+        got += rn;
+      }
+    }
+    if (at(M, R, R) + received + got > d.cap_list) {
+      HIPCHECK(hipStreamSynchronize(d.xs));
+      HIPCHECK(hipStreamSynchronize(s));
+      return S3IMPH_ERR_NOMEM;
+    }
+    cm.alltoallv(d.send, soff.data(), sbytes.data(), lin, roff.data(), rbytes.data(), d.xs);
+    received += got;
+    std::copy(M, M + (size_t)(P + 1) * P, prev.begin());
+  }
+  HIPCHECK(hipEventRecord(d.ev_x, d.xs));
+  HIPCHECK(hipStreamWaitEvent(s, d.ev_x, 0));  // level 0's pipeline reads the received records
+  *recv_total = M[(uint64_t)R * (P + 1) + R] + received;
+  if (c->debug)
+    std::fprintf(stderr, "[s3imph] rank %d: level 0 exchanged in %d chunks (%llu records)\n", R, K,
+                 (unsigned long long)*recv_total);
+  return S3IMPH_OK;
+}
 
 // One attempt of the multi-GPU build (see s3imph_dist.hip for the decomposition).
 // `conservative` runs every level on the counted path and the replicated levels with
@@ -723,8 +817,10 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kScatterTiles * kResShards * sizeof(unsigned), s));
   launch_dist_setup(st, 0, nullptr, N, R, P, s);
   ev_mark(c, s, "init");
-  // level 0's key hashes and fingerprints, once (the routing below may be retried)
-  if (n_local) {
+  // level 0's key hashes and fingerprints, once (the routing below may be retried); a big
+  // sharded level 0 hashes chunk by chunk inside route0_chunked instead
+  const bool chunked = !conservative && P > 1 && n_local >= kChunkedRoute0Keys;
+  if (n_local && !chunked) {
     const LevelGeom gh = choose_geom_sz(n_local, 64 * level_words(N), kTargetTiles0, chunks0(n_local), kTileMaxBits);
     launch_hash0_only(blob, offsets, n_local, b, gh, level_grids(n_local, 64 * level_words(N), gh).gc, s);
   }
@@ -737,7 +833,20 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   for (;;) {
     // ---- route level L's records to their owners
     uint64_t C = (uint64_t)(src_pred / P * 1.15) + 4096;
-    for (int tries = 0;; ++tries) {
+    uint64_t m_chunked = 0;
+    if (L == 0 && chunked) {
+      if ((uint64_t)P * C > d.cap_send) {
+        HIPCHECK(hipStreamSynchronize(s));
+        dalloc(d.send, (uint64_t)P * C);
+        d.cap_send = (uint64_t)P * C;
+      }
+      const int rc = route0_chunked(c, blob, offsets, pos, n_local, key_base, N, b, C, lin, s, M, &m_chunked);
+      if (rc != S3IMPH_OK) {
+        if (rc == S3IMPH_ERR_NOMEM) *msg = "build MPHF: rank " + std::to_string(R) + " received too many records";
+        return rc;
+      }
+    }
+    for (int tries = 0; !(L == 0 && chunked); ++tries) {
       if ((uint64_t)P * C > d.cap_send) {
         HIPCHECK(hipStreamSynchronize(s));
         dalloc(d.send, (uint64_t)P * C);
@@ -777,15 +886,23 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
       return S3IMPH_ERR_NOMEM;
     }
     // ---- exchange: the received records follow this rank's own ones in list[1]
-    uint64_t acc = M[(uint64_t)R * (P + 1) + R] * sizeof(Rec);
-    for (int t = 0; t < P; ++t) {
-      soff[t] = (uint64_t)t * C * sizeof(Rec);
-      sbytes[t] = t == R ? 0 : M[(uint64_t)R * (P + 1) + t] * sizeof(Rec);
-      roff[t] = t == R ? 0 : acc;
-      rbytes[t] = t == R ? 0 : M[(uint64_t)t * (P + 1) + R] * sizeof(Rec);
-      acc += rbytes[t];
+    if (L == 0 && chunked) {
+      if (m_chunked != m) {
+        *msg = "build MPHF: internal error: chunked level-0 exchange received " + std::to_string(m_chunked) +
+               " of " + std::to_string(m) + " records";
+        return S3IMPH_ERR_INTERNAL;
+      }
+    } else {
+      uint64_t acc = M[(uint64_t)R * (P + 1) + R] * sizeof(Rec);
+      for (int t = 0; t < P; ++t) {
+        soff[t] = (uint64_t)t * C * sizeof(Rec);
+        sbytes[t] = t == R ? 0 : M[(uint64_t)R * (P + 1) + t] * sizeof(Rec);
+        roff[t] = t == R ? 0 : acc;
+        rbytes[t] = t == R ? 0 : M[(uint64_t)t * (P + 1) + R] * sizeof(Rec);
+        acc += rbytes[t];
+      }
+      cm.alltoallv(d.send, soff.data(), sbytes.data(), lin, roff.data(), rbytes.data(), s);
     }
-    cm.alltoallv(d.send, soff.data(), sbytes.data(), lin, roff.data(), rbytes.data(), s);
     launch_set_u64(&st->n[L], m, s);
     ev_mark(c, s, L == 0 ? "route0" : "route");
     // ---- the owner's tile pipeline over positions [64 lo, 64 (lo + rw))
@@ -1237,6 +1354,9 @@ int s3imph_ctx_destroy(s3imph_ctx* c) {
   fin_scratch_free(c);
   delete c->d.comm;
   c->d.comm = nullptr;
+  if (c->d.xs) (void)hipStreamDestroy(c->d.xs);
+  for (hipEvent_t e : {c->d.ev_route, c->d.ev_counts, c->d.ev_x})
+    if (e) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return S3IMPH_OK;

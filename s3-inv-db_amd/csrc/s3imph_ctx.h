@@ -79,6 +79,9 @@ struct DistState {
   unsigned long long* h_pinned = nullptr;    // host staging (64 x 64 + 256 u64)
   std::vector<uint64_t> seg;                 // last build: (p_lo, count, local_off) triples
   uint64_t out_n = 0;
+  // level 0's exchange runs on its own stream, chunk by chunk, beside the next chunk's hash
+  hipStream_t xs = nullptr;
+  hipEvent_t ev_route = nullptr, ev_counts = nullptr, ev_x = nullptr;
 };
 
 // RCCL over xGMI: all-to-all as grouped point-to-point send/recv (xGMI is a full mesh

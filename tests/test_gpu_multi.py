@@ -58,6 +58,24 @@ def test_thread_per_rank_shared_gpu(s3, oracle_lib, monkeypatch, ranks, kind, av
     assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
 
 
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_thread_per_rank_chunked_level0_exchange(s3, oracle_lib, monkeypatch, capfd, ranks):
+    """Shards of >= 8M keys take the chunked level 0 (s3imph_build.hip route0_chunked):
+    four key chunks, each hashed and routed on the build stream while the previous one's
+    records cross on the exchange stream; own records land between chunks' received
+    ones.  Bit-exact with the oracle (10-12M keys per rank, host-copy transport), and
+    every rank reports the chunked exchange on its first attempt (S3IMPH_DEBUG)."""
+    monkeypatch.setenv("S3IMPH_DEBUG", "1")
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", str(3_000_000 + ranks))  # fresh contexts read S3IMPH_DEBUG
+    n = 10_000_000 * ranks + 2_000_000
+    blob, offs = s3.gen_keys(0, 21, 24, 0, n)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    g = s3.build_host(blob, offs, devices=[0] * ranks)
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+    err = capfd.readouterr().err
+    assert err.count("level 0 exchanged in 4 chunks") == ranks, err[-2000:]
+
+
 def test_thread_per_rank_custom_positions_offset_blob(s3, oracle_lib, monkeypatch):
     """A blob starting at a non-zero offsets[0] with custom positions, 3 ranks."""
     monkeypatch.setenv("S3IMPH_DIST_SWITCH", "15000")
