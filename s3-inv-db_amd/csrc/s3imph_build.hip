@@ -697,7 +697,7 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
 
 
 constexpr int kDistRetry = -1;
-constexpr uint64_t kChunkedRoute0Keys = 8ull << 20;  // sharded level 0 of this many keys per rank: 4 chunks
+constexpr uint64_t kChunkedRoute0Keys = 8ull << 20;  // sharded level 0 of this many keys per rank (N / P): 4 chunks
 constexpr int kRoute0Chunks = 4;
 
 // Level 0 of the sharded build in K key chunks: chunk c is hashed and routed on the build
@@ -819,7 +819,8 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   ev_mark(c, s, "init");
   // level 0's key hashes and fingerprints, once (the routing below may be retried); a big
   // sharded level 0 hashes chunk by chunk inside route0_chunked instead
-  const bool chunked = !conservative && P > 1 && n_local >= kChunkedRoute0Keys;
+  // (decided from global values only: every rank must issue the same collectives)
+  const bool chunked = !conservative && P > 1 && N / (uint64_t)P >= kChunkedRoute0Keys;
   if (n_local && !chunked) {
     const LevelGeom gh = choose_geom_sz(n_local, 64 * level_words(N), kTargetTiles0, chunks0(n_local), kTileMaxBits);
     launch_hash0_only(blob, offsets, n_local, b, gh, level_grids(n_local, 64 * level_words(N), gh).gc, s);
