@@ -92,6 +92,21 @@ def test_dist_unbalanced_shards_custom_pos(oracle_lib):
     _check(res, n, fp, po, mph)
 
 
+def test_dist_chunked_level0_unbalanced(oracle_lib):
+    """N / P >= 8M keys: level 0 runs chunked on every rank (the decision is global), here
+    with one rank holding 16M keys and the other 1M (chunks of 4M and 250k), custom
+    positions, two processes over gloo on the one GPU: bit-exact."""
+    import s3imph
+    n, world = 17_000_000, 2
+    blob, offs = s3imph.gen_keys(0, 13, 16, 0, n)
+    blob = blob[: int(offs[-1])]
+    pos = (np.random.default_rng(3).permutation(n).astype(np.uint64) + np.uint64(11))
+    st, fp, po, mph = oracle_lib.build_mt(blob, offs, pos, threads=16)
+    assert st == 0
+    res = _run(world, _shards(blob, offs, [0, 16_000_000, n], pos), n, 1 << 21)
+    _check(res, n, fp, po, mph)
+
+
 def test_dist_tiny_set_and_empty_rank(oracle_lib):
     """5 keys on 3 ranks (one rank holds none; most ranks own no level positions)."""
     keys = [b"", b"a/", b"data/", b"data/2024/", b"root/"]
