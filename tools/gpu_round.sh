@@ -15,9 +15,9 @@ if [ "$PYT" = pytest ]; then
 fi
 timeout -k 10 400 python bench.py --config $CFG > $OUT/bench.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
-  python3 bench.py --config $CFG --steps 10 --warmup 2 --no-cpu-baseline --no-secondary > $OUT/bench_prof.log 2>&1
+  python3 bench.py --config $CFG --steps 10 --warmup 2 --no-cpu-baseline --no-secondary --headline-only > $OUT/bench_prof.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \
-  python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-secondary > $OUT/pmc_fetch.log 2>&1
+  python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-secondary --headline-only > $OUT/pmc_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- \
-  python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-secondary > $OUT/pmc_write.log 2>&1
+  python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-secondary --headline-only > $OUT/pmc_write.log 2>&1
 echo done > $OUT/DONE
