@@ -276,14 +276,24 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
 // the last blocks' load / sort phases exposed.
 // prof (S3IMPH_DEBUG): per wave, shader cycles total / hashing / barrier wait / rest, and
 // the real-time clock span, for the phase report of print_tile_profile.
-template <int NT, int BB, bool PF>
+//
+// RT (multi-GPU build): the level-0 route is fused in.  A round's (kh, fp, pos) records
+// never reach kh / fp: they are counting-sorted by owner rank in LDS (staged in the
+// round's byte window, free once every lane has hashed), one atomic per (round, owner)
+// reserves the owner's run, and the runs are written out whole — k_route's work without
+// its 16-byte-per-key read and the hash's 16-byte-per-key write.  The reservations are
+// the kernel's limit: same-address device atomics serialise at ~12 ns each
+// (tools/ubench_atomics.hip); 1024-key rounds (512 threads, 64 KiB windows) halve them
+// but measured slower (C3 3.02 -> 3.51 ms: register spills, the larger rounds' tail).
+template <int NT, int BB, bool PF, bool RT = false>
 __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(const uint8_t* __restrict__ blob,
                                                   const uint64_t* __restrict__ offsets, uint64_t n,
                                                   uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
                                                   unsigned long long* __restrict__ flags,
                                                   unsigned long long* __restrict__ sflags, LevelState* st,
                                                   unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt,
-                                                  unsigned long long* __restrict__ prof = nullptr) {
+                                                  unsigned long long* __restrict__ prof = nullptr,
+                                                  Route0 rt = Route0{}) {
   unsigned long long pt0 = __builtin_amdgcn_s_memtime(), ph = 0, pw = 0;  // debug phase clock
   const unsigned long long prt0 = __builtin_amdgcn_s_memrealtime();
   constexpr int G = 2 * NT;                    // keys per round
@@ -295,8 +305,29 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   __shared__ unsigned short sidx[G];           // sorted slot -> key index in the round
   __shared__ unsigned lcnt[kLB];
   __shared__ unsigned s_cnt[NW];
+  // RT: per-owner counts / run starts of the round, the owners' reserved run bases (record
+  // offsets into self_dst or send), the block's sticky overflow flag
+  __shared__ unsigned r_cnt[RT ? kMaxRanks : 1], r_start[RT ? kMaxRanks : 1];
+  __shared__ uint64_t r_base[RT ? kMaxRanks : 1];
+  __shared__ unsigned r_over;
   if (st->skew) return;  // k_hash_count0 hashes skewed sets (and clears the tile state)
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  static_assert(!RT || G * sizeof(Rec) + G <= sizeof(sw), "the route stage aliases the byte window");
+  // RT: level 0's geometry and owner ranges; this rank's own-record shift (records received
+  // for earlier key chunks sit before its own ones)
+  uint64_t r_words = 0, r_magic = 0, r_S = 1, r_mS = 0, r_rb = 0;
+  if (RT) {
+    if (tid == 0) r_over = 0;
+    r_words = st->words[0];
+    r_magic = st->magic[0];
+    r_S = st->dS[0];
+    r_mS = st->dmagic[0];
+    uint64_t v = rt.mat_prev && lane < (unsigned)rt.P && (int)lane != rt.rank
+                     ? rt.mat_prev[(uint64_t)lane * (rt.P + 1) + rt.rank] : 0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    r_rb = uniform64(v);
+  }
   {
     const uint64_t T = ntiles_of(st->words[0], tb), B = (n + chunk - 1) / chunk;
     const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
@@ -357,6 +388,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
       }
     }
     for (unsigned b = tid; b < kLB; b += NT) lcnt[b] = 0;
+    if (RT && tid < kMaxRanks) r_cnt[tid] = 0;
     const uint64_t rw = wlo;
     const uint64_t t_b0[2] = {kb0[0], kb0[1]}, t_b1[2] = {kb1[0], kb1[1]};
     // keys whose bytes all lie in the window: a prefix of the round (offsets ascend)
@@ -420,12 +452,21 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
     if (PF && more) prefetch(g);  // the next round's loads land while this one is hashed
     unsigned long long pta = prof ? __builtin_amdgcn_s_memtime() : 0;
     // ---- hash: slot tid (shorter half), then slot m - 1 - tid (longer half)
+    uint64_t ra[2] = {0, 0}, rb[2] = {0, 0};
+    unsigned rj[2] = {0, 0};
+    bool rv[2] = {false, false};
     if (alone) {
       if (tid == 0) {
         uint64_t a, b;
         fnv_both_pf(blob, t_b0[0], t_b1[0], a, b);
-        kh[r0] = a;
-        fp[r0] = b;
+        if (RT) {
+          ra[0] = a;
+          rb[0] = b;
+          rv[0] = true;
+        } else {
+          kh[r0] = a;
+          fp[r0] = b;
+        }
         zero |= (a == 0);
       }
     } else {
@@ -436,9 +477,63 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
           uint64_t a, b;
           const unsigned j = sidx[slot];
           fnv_window(reinterpret_cast<const uint32_t*>(sw), soff[slot], slen[slot], a, b);
-          kh[r0 + j] = a;
-          fp[r0 + j] = b;
+          if (RT) {
+            ra[h] = a;
+            rb[h] = b;
+            rj[h] = j;
+            rv[h] = true;
+          } else {
+            kh[r0 + j] = a;
+            fp[r0 + j] = b;
+          }
           zero |= (a == 0);
+        }
+      }
+    }
+    if (RT) {  // ---- route the round's records to their owners (k_route's scheme)
+      unsigned od[2] = {0, 0}, ork[2] = {0, 0};
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (rv[h]) {
+          const uint64_t x = bb_index(level_seed(0), ra[h], r_words, r_magic);
+          od[h] = owner_of(x >> 6, r_S, r_mS);
+          if (od[h] >= (unsigned)rt.P) od[h] = rt.P - 1;  // unreachable: x < 64 words <= 64 P S
+          ork[h] = atomicAdd(&r_cnt[od[h]], 1u);
+        }
+      __syncthreads();  // every lane has hashed (the window is free) and counted
+      if (tid < 64) {
+        const unsigned c = tid < (unsigned)rt.P ? r_cnt[tid] : 0u;
+        unsigned x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const unsigned y = __shfl_up(x, o);
+          if (tid >= (unsigned)o) x += y;
+        }
+        r_start[tid] = x - c;
+        if (c) {
+          const unsigned long long at = atomicAdd(&rt.scnt[tid], (unsigned long long)c);
+          const bool self = (int)tid == rt.rank;
+          if (self ? r_rb + at + c > rt.self_cap : at + c > rt.cap) r_over = 1;
+          r_base[tid] = self ? r_rb + at : (uint64_t)tid * rt.cap + at;
+        }
+      }
+      __syncthreads();
+      Rec* stg = reinterpret_cast<Rec*>(sw);
+      unsigned char* sdst = reinterpret_cast<unsigned char*>(stg + G);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (rv[h]) {
+          const unsigned slot = r_start[od[h]] + ork[h];
+          const uint64_t i = r0 + rj[h];
+          stg[slot] = Rec{ra[h], rb[h], rt.pos ? rt.pos[i] : rt.pos_base + i};
+          sdst[slot] = (unsigned char)od[h];
+        }
+      __syncthreads();
+      if (!r_over) {
+        for (unsigned j = tid; j < m; j += NT) {
+          const unsigned o = sdst[j];
+          Rec* dst = ((int)o == rt.rank ? rt.self_dst : rt.send) + r_base[o];
+          dst[j - r_start[o]] = stg[j];
         }
       }
     }
@@ -463,6 +558,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
     q[6] = prt1;
   }
   if (zero) atomicOr(&st->status, kStKeyZero);
+  if (RT && tid == 0 && r_over) atomicOr(&st->status, kStRouteOverflow);
 }
 
 // ------------------------------------------------------------- level L setup ---------
@@ -1945,8 +2041,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
 //             (f, p) are staged by rank in LDS and written as one contiguous run; collided
 //             records stay in registers for the next level and are also appended to the
 //             next list (one reservation per workgroup), where the tail finds them;
-// with a grid barrier after each phase.  Every decision derives from the same level
-// state, so all workgroups take the same branches; an overflow (a segment or an owner
+// with a grid barrier after the route and own phases (the settle needs none: the next
+// level's key count is derived from the totals).  Every decision derives from the same
+// level state, so all workgroups take the same branches; an overflow (a segment or an owner
 // past its capacity, predicted not to happen) is flagged and the build reruns on the
 // conservative path.  Level bookkeeping mirrors k_scatter_res + k_tile_reg (words, woff,
 // nlevels, lvl_base, n[L+1]); a level of <= kTailKeys keys is left to the tail.
@@ -2010,13 +2107,17 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
   bool bad = false;
   uint64_t k[kMidR], f[kMidR], pp[kMidR];
   unsigned valid = 0;  // bit r: k/f/pp[r] hold a record of the current level
+  // key counts of the current and previous level after L0: every workgroup derives them
+  // from the settled totals (n[L+1] = n[L] - settled), so no barrier waits for the
+  // next-list atomics and no decision reads state another workgroup may still be writing
+  uint64_t n_loc = 0, n_prev = 0;
   for (int L = L0; L <= L1; ++L) {
-    // ---- level setup: the same reads in every workgroup, workgroup 0 publishes
+    // ---- level setup: the same values in every workgroup, workgroup 0 publishes
     if (tid == 0) {
       const int p = L - 1;
-      int go = !(st->status & kStStop) && !(p > 0 && !st->preset[p] && st->n[p] <= kGate);
+      int go = L > L0 || (!(st->status & kStStop) && !(p > 0 && !st->preset[p] && st->n[p] <= kGate));
       if (go) {
-        const uint64_t n = st->n[L];
+        const uint64_t n = L > L0 ? n_loc : st->n[L];
         const uint64_t words = n ? level_words(n) : 0;
         const uint64_t woff = st->woff[p] + st->words[p];
         if (g == 0) {
@@ -2032,7 +2133,7 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
         } else if (n > kMidMaxKeys) {
           if (g == 0) atomicOr(&st->status, kStTailOverflow);  // bigger than predicted: rerun
           go = 0;
-        } else if (!st->preset[L] && !st->preset[p] && n == st->n[p]) {
+        } else if (!st->preset[L] && !st->preset[p] && n == (L > L0 ? n_prev : st->n[p])) {
           if (g == 0) {  // no key placed at the previous level: duplicates (no_progress)
             st->stop_level = L;
             atomicOr(&st->status, kStTooManyLevels);
@@ -2044,7 +2145,7 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
     }
     __syncthreads();
     if (!s_go) break;
-    const uint64_t n = st->n[L];
+    const uint64_t n = L > L0 ? n_loc : st->n[L];
     const uint64_t words = level_words(n), magic = level_magic(words);
     const uint64_t woff = st->woff[L - 1] + st->words[L - 1];
     const uint64_t seed = level_seed(L);
@@ -2234,11 +2335,14 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
       }
     }
     valid = keep;
+    // No barrier here: the next level's route writes only exchange segments and counts its
+    // owners read after that level's first grid barrier (which this workgroup's settle
+    // precedes), n[L + 1] is derived, and lvl_base[L + 1] / the tot[] totals are read only
+    // after later barriers.  An overflow flagged above leaves garbage the host discards
+    // (the conservative rerun); every access stays within its capacity meanwhile.
+    n_prev = n;
+    n_loc = n - s_pre[G];
     MPROF(li, 5);
-    target += G;
-    if (!grid_sync(bar, target, st, &s_ok)) break;  // n[L + 1], lvl_base[L + 1], overflow flags final
-    MPROF(li, 6);
-    if (st->status & kStTailOverflow) break;
   }
   if (bad) atomicOr(&st->status, kStRank);
 #undef MPROF
@@ -2646,6 +2750,22 @@ void launch_hash0_only(const uint8_t* blob, const uint64_t* offsets, uint64_t n,
   }
   k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
                                            g.chunk, b.tcnt, 3);
+}
+
+void launch_hash0_route(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
+                        int grid, const Route0& rt, hipStream_t s) {
+  if (((uintptr_t)blob & 15) == 0) {  // near-uniform lengths: hash + route in one pass
+    k_hash0_pair<kH0T, kH0B, true, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags,
+                                                                 b.st, g.tb, g.chunk, b.tcnt, nullptr, rt);
+    // a skewed set (st->skew): k_hash_count0's length-sorted groups, then k_route
+    k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
+                                             g.chunk, b.tcnt, 5);
+    launch_route0_arrays(b.kh, b.fp, n, rt, b.st, true, s);
+    return;
+  }
+  k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
+                                           g.chunk, b.tcnt, 3);
+  launch_route0_arrays(b.kh, b.fp, n, rt, b.st, false, s);
 }
 
 void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s) {

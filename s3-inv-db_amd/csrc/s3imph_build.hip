@@ -137,7 +137,7 @@ void ev_begin(s3imph_ctx* c) {
 void ev_mark(s3imph_ctx* c, hipStream_t s, const char* name) {
   if (!c->profiling) return;
   if (c->profiling == 2 && std::strcmp(name, "init") != 0 && std::strcmp(name, "hash_count0") != 0 &&
-      std::strcmp(name, "route0") != 0)
+      std::strcmp(name, "hash_route0") != 0 && std::strcmp(name, "route0") != 0)
     return;  // light mode: two events per build, around the dominant kernel
   if (c->ev_used >= (int)c->events.size()) {
     hipEvent_t e;
@@ -453,13 +453,13 @@ void print_tile_profile(s3imph_ctx* c) {
   }
   {  // k_mid_levels phase stamps: workgroup 0 and the last one, 8 per level
     const unsigned long long* m = &h[(size_t)(kMaxLevels - 4) * kMaxTiles * 8];
-    static const char* mn[7] = {"load", "mark", "bar1", "final", "bar2", "settle", "bar3"};
+    static const char* mn[5] = {"route", "bar1", "own", "bar2", "settle"};
     for (int wg = 0; wg < 2; ++wg)
       for (int li = 0; li < 64; ++li) {
         const unsigned long long* q = m + wg * 512 + li * 8;
         if (!q[0]) break;
         std::fprintf(stderr, "  mid wg%s level+%d:", wg ? "last" : "0", li);
-        for (int k = 0; k < 7; ++k) std::fprintf(stderr, " %s %.2f", mn[k], q[k + 1] ? (q[k + 1] - q[k]) / 100.0 : -1.0);
+        for (int k = 0; k < 5; ++k) std::fprintf(stderr, " %s %.2f", mn[k], q[k + 1] ? (q[k + 1] - q[k]) / 100.0 : -1.0);
         std::fprintf(stderr, " us\n");
       }
   }
@@ -726,30 +726,40 @@ int route0_chunked(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, 
   const int K = kRoute0Chunks;
   const uint64_t per = (n_local + K - 1) / K;
   const LevelGeom gh = choose_geom_sz(n_local, 64 * level_words(N), kTargetTiles0, chunks0(n_local), kTileMaxBits);
-  auto hash_chunk = [&](int k) {
-    const uint64_t k0 = std::min(n_local, (uint64_t)k * per), k1 = std::min(n_local, k0 + per);
-    if (k1 <= k0) return;
-    BinBuffers bc = b;
-    bc.kh = c->kh + k0;
-    bc.fp = c->fp + k0;
-    launch_hash0_only(blob, offsets + k0, k1 - k0, bc, gh, level_grids(k1 - k0, 64 * level_words(N), gh).gc, s);
-  };
   HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
   std::vector<unsigned long long> prev((size_t)(P + 1) * P, 0);
   std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
   uint64_t received = 0;  // records received from peers in chunks < k
-  hash_chunk(0);
-  for (int k = 0; k < K; ++k) {
+  // Build stream: chunk k hashed and routed in one pass; its own records land past
+  // everything received for chunks < k, which the kernel reads from the previous gather
+  // (d.mat), so it waits for that gather (a few us), not for the exchange it feeds, and is
+  // enqueued before the host blocks on the previous chunk's counts.
+  auto enqueue_build = [&](int k) {
     const uint64_t k0 = std::min(n_local, (uint64_t)k * per), k1 = std::min(n_local, k0 + per);
-    launch_route0_arrays(c->kh + k0, c->fp + k0, pos ? pos + k0 : nullptr, key_base + k0, k1 - k0, d.send, C, d.scnt,
-                         st, P, R, lin + received, d.cap_list - received, s);
+    if (k) HIPCHECK(hipStreamWaitEvent(s, d.ev_x, 0));  // chunk k-1's counts gathered: d.mat, scnt free
+    if (k1 > k0) {
+      BinBuffers bc = b;
+      bc.kh = c->kh + k0;
+      bc.fp = c->fp + k0;
+      const Route0 rt{pos ? pos + k0 : nullptr, key_base + k0, d.send, C, d.scnt, lin, d.cap_list,
+                      k ? d.mat : nullptr, P, R};
+      launch_hash0_route(blob, offsets + k0, k1 - k0, bc, gh, level_grids(k1 - k0, 64 * level_words(N), gh).gc, rt, s);
+    }
     launch_route_flag(st, d.scnt, P, s);
     HIPCHECK(hipEventRecord(d.ev_route, s));
-    if (k + 1 < K) hash_chunk(k + 1);  // the build stream keeps hashing while the counts travel
+  };
+  // Exchange stream: gather chunk k's cumulative counts, then to the host.
+  auto enqueue_gather = [&]() {
     HIPCHECK(hipStreamWaitEvent(d.xs, d.ev_route, 0));
     cm.allgather(d.scnt, d.mat, 8ull * (P + 1), d.xs);
+    HIPCHECK(hipEventRecord(d.ev_x, d.xs));
     HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, d.xs));
     HIPCHECK(hipEventRecord(d.ev_counts, d.xs));
+  };
+  enqueue_build(0);
+  enqueue_gather();
+  for (int k = 0; k < K; ++k) {
+    if (k + 1 < K) enqueue_build(k + 1);  // the build stream keeps hashing while the counts travel
     HIPCHECK(hipEventSynchronize(d.ev_counts));
     bool over = false;
     for (int r = 0; r < P; ++r) over |= M[(uint64_t)r * (P + 1) + P] != 0;
@@ -782,7 +792,9 @@ int route0_chunked(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, 
     cm.alltoallv(d.send, soff.data(), sbytes.data(), lin, roff.data(), rbytes.data(), d.xs);
     received += got;
     std::copy(M, M + (size_t)(P + 1) * P, prev.begin());
+    if (k + 1 < K) enqueue_gather();
   }
+  ev_mark(c, s, "hash_route0");
   HIPCHECK(hipEventRecord(d.ev_x, d.xs));
   HIPCHECK(hipStreamWaitEvent(s, d.ev_x, 0));  // level 0's pipeline reads the received records
   *recv_total = M[(uint64_t)R * (P + 1) + R] + received;
@@ -821,11 +833,10 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   // sharded level 0 hashes chunk by chunk inside route0_chunked instead
   // (decided from global values only: every rank must issue the same collectives)
   const bool chunked = !conservative && P > 1 && N / (uint64_t)P >= kChunkedRoute0Keys;
-  if (n_local && !chunked) {
-    const LevelGeom gh = choose_geom_sz(n_local, 64 * level_words(N), kTargetTiles0, chunks0(n_local), kTileMaxBits);
-    launch_hash0_only(blob, offsets, n_local, b, gh, level_grids(n_local, 64 * level_words(N), gh).gc, s);
-  }
-  ev_mark(c, s, "hash_count0");
+  const LevelGeom gh0 = choose_geom_sz(std::max<uint64_t>(n_local, 1), 64 * level_words(N), kTargetTiles0,
+                                       chunks0(std::max<uint64_t>(n_local, 1)), kTileMaxBits);
+  const int gc0 = level_grids(std::max<uint64_t>(n_local, 1), 64 * level_words(N), gh0).gc;
+  bool have_kh = false;  // kh / fp written (a retried level-0 route reads them)
   std::vector<uint64_t> hw, hS;  // words and per-rank range of each distributed level
   std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
   double src_pred = (double)n_local;  // records this rank routes at the current level
@@ -854,9 +865,17 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
         d.cap_send = (uint64_t)P * C;
       }
       HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
-      if (L == 0)
+      if (L == 0 && tries == 0) {  // hash + route in one pass
+        if (n_local) {
+          const Route0 rt{pos, key_base, d.send, C, d.scnt, lin, d.cap_list, nullptr, P, R};
+          launch_hash0_route(blob, offsets, n_local, b, gh0, gc0, rt, s);
+        }
+        ev_mark(c, s, "hash_route0");
+      } else if (L == 0) {  // a retry routes from kh / fp (hashed once)
+        if (n_local && !have_kh) launch_hash0_only(blob, offsets, n_local, b, gh0, gc0, s);
+        have_kh = true;
         launch_route0_arrays(c->kh, c->fp, pos, key_base, n_local, d.send, C, d.scnt, st, P, R, lin, d.cap_list, s);
-      else
+      } else
         launch_route(L, lredo, (uint64_t)src_pred, d.send, C, d.scnt, st, P, R, lin, d.cap_list, s);
       launch_route_flag(st, d.scnt, P, s);
       cm.allgather(d.scnt, d.mat, 8ull * (P + 1), s);

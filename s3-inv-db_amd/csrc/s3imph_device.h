@@ -47,6 +47,14 @@ static __device__ __forceinline__ uint64_t bb_index_mk(uint64_t seed, uint64_t m
   return (r << 6) | (h & 63);
 }
 
+// Owner rank of level word w in the multi-GPU build: w / S by a Barrett step (w < 2^32,
+// one correction; mS = level_magic(S)).
+static __device__ __forceinline__ unsigned owner_of(uint64_t w, uint64_t S, uint64_t mS) {
+  uint64_t d = __umul64hi(w, mS);
+  if (w - d * S >= S) ++d;
+  return (unsigned)d;
+}
+
 // ---- FNV-64 multiply by the prime P = 2^40 + 435, on 32-bit halves -----------------
 // x * P mod 2^64 with x = lo + 2^32 hi:
 //   lo' = lo * 435 (low word),  hi' = mulhi(lo, 435) + hi * 435 + (lo << 8)   (mod 2^32).

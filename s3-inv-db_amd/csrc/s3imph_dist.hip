@@ -30,13 +30,6 @@ constexpr int kRT = 1024;               // route block
 constexpr int kRK = 2;                  // records per thread per round
 constexpr int kRRound = kRT * kRK;
 
-// Owner rank of word w: w / S by a Barrett step (w < 2^32, one correction).
-__device__ __forceinline__ unsigned owner_of(uint64_t w, uint64_t S, uint64_t mS) {
-  uint64_t d = __umul64hi(w, mS);
-  if (w - d * S >= S) ++d;
-  return (unsigned)d;
-}
-
 // Route this rank's records of level `level` to their owners.  kSrc 0: level 0, the
 // records are made here from the keys (FNV-1a key hash + FNV-1 fingerprint, one pass
 // over the bytes, as StreamingMPHFBuilder.Add does); 2: level 0 from the hash kernel's
@@ -54,14 +47,30 @@ __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restr
                                                uint64_t n_keys, const Rec* __restrict__ ilist,
                                                Rec* __restrict__ send, uint64_t cap,
                                                unsigned long long* __restrict__ scnt, LevelState* st, int P,
-                                               int rank, Rec* __restrict__ self_dst, uint64_t self_cap) {
+                                               int rank, Rec* __restrict__ self_dst, uint64_t self_cap,
+                                               const unsigned long long* __restrict__ mat_prev, int only_skew) {
   __shared__ Rec stage[kRRound];
   __shared__ unsigned char sdst[kRRound];
   __shared__ unsigned cnt[kMaxRanks], start[kMaxRanks];
   __shared__ Rec* base[kMaxRanks];
   __shared__ unsigned s_over;
+  __shared__ uint64_t s_rb;
+  if (only_skew && !st->skew) return;  // the fused hash kernel routed this set
   const unsigned tid = threadIdx.x;
   if (tid == 0) s_over = 0;
+  if (tid < 64) {  // records received for earlier key chunks sit before this rank's own ones
+    uint64_t v = mat_prev && tid < (unsigned)P && (int)tid != rank ? mat_prev[(uint64_t)tid * (P + 1) + rank] : 0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if (tid == 0) s_rb = v;
+  }
+  __syncthreads();
+  if (s_rb > self_cap) {
+    if (tid == 0) atomicOr(&st->status, kStRouteOverflow);
+    return;
+  }
+  self_dst += s_rb;
+  self_cap -= s_rb;
   const uint64_t n = kSrc != 1 ? n_keys : st->n[level];
   const uint64_t words = st->words[level], magic = st->magic[level];
   const uint64_t S = st->dS[level], mS = st->dmagic[level];
@@ -189,7 +198,7 @@ void launch_route0(const uint8_t* blob, const uint64_t* offsets, const uint64_t*
                    uint64_t self_cap, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + kRRound - 1) / kRRound, 2048));
   k_route<0><<<grid, kRT, 0, s>>>(0, blob, offsets, nullptr, nullptr, pos, pos_base, n, nullptr, send, cap, scnt, st, P,
-                                   rank, self_dst, self_cap);
+                                   rank, self_dst, self_cap, nullptr, 0);
 }
 
 void launch_route0_arrays(const uint64_t* kh, const uint64_t* fp, const uint64_t* pos, uint64_t pos_base, uint64_t n,
@@ -197,14 +206,21 @@ void launch_route0_arrays(const uint64_t* kh, const uint64_t* fp, const uint64_t
                           Rec* self_dst, uint64_t self_cap, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + kRRound - 1) / kRRound, 2048));
   k_route<2><<<grid, kRT, 0, s>>>(0, nullptr, nullptr, kh, fp, pos, pos_base, n, nullptr, send, cap, scnt, st, P, rank,
-                                   self_dst, self_cap);
+                                   self_dst, self_cap, nullptr, 0);
+}
+
+void launch_route0_arrays(const uint64_t* kh, const uint64_t* fp, uint64_t n, const Route0& rt, LevelState* st,
+                          bool only_skew, hipStream_t s) {
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + kRRound - 1) / kRRound, 2048));
+  k_route<2><<<grid, kRT, 0, s>>>(0, nullptr, nullptr, kh, fp, rt.pos, rt.pos_base, n, nullptr, rt.send, rt.cap, rt.scnt,
+                                   st, rt.P, rt.rank, rt.self_dst, rt.self_cap, rt.mat_prev, only_skew ? 1 : 0);
 }
 
 void launch_route(int level, const Rec* list, uint64_t n_pred, Rec* send, uint64_t cap, unsigned long long* scnt,
                   LevelState* st, int P, int rank, Rec* self_dst, uint64_t self_cap, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n_pred + kRRound - 1) / kRRound + 8, 2048));
   k_route<1><<<grid, kRT, 0, s>>>(level, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, list, send, cap, scnt, st,
-                                   P, rank, self_dst, self_cap);
+                                   P, rank, self_dst, self_cap, nullptr, 0);
 }
 
 void launch_dist_setup(LevelState* st, int L, const unsigned long long* gcount, uint64_t n_value, int rank, int P,

@@ -221,6 +221,27 @@ void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s);
 
 // ---- multi-GPU launchers (s3imph_dist.hip) ------------------------------------------
 constexpr int kMaxRanks = 64;
+// Level-0 routing of the multi-GPU build (k_route, or fused into the level-0 hash kernel):
+// record (kh, fp, pos) of key i goes to its owner's send region [o*cap, (o+1)*cap), this
+// rank's own records to self_dst (capacity self_cap), counted in scnt like any owner's.
+// mat_prev (nullable) holds the gathered (P + 1) x P counts of the key chunks routed
+// before: self_dst then starts past the records received for them (chunked level 0).
+struct Route0 {
+  const uint64_t* pos;  // caller positions of these keys, or null: pos_base + i
+  uint64_t pos_base;
+  Rec* send;
+  uint64_t cap;
+  unsigned long long* scnt;
+  Rec* self_dst;
+  uint64_t self_cap;
+  const unsigned long long* mat_prev;
+  int P, rank;
+};
+// The level-0 hash with the route fused in (no kh / fp arrays; a skewed set, decided on
+// the device, goes through k_hash_count0 + k_route instead).  b.kh / b.fp are scratch
+// for that fallback.
+void launch_hash0_route(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
+                        int grid, const Route0& rt, hipStream_t s);
 // Records owned by `rank` itself go straight to self_dst (capacity self_cap), not to a send region.
 void launch_route0(const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t pos_base, uint64_t n,
                    Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, int rank, Rec* self_dst,
@@ -229,6 +250,10 @@ void launch_route0(const uint8_t* blob, const uint64_t* offsets, const uint64_t*
 void launch_route0_arrays(const uint64_t* kh, const uint64_t* fp, const uint64_t* pos, uint64_t pos_base, uint64_t n,
                           Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, int rank,
                           Rec* self_dst, uint64_t self_cap, hipStream_t s);
+// the same from a Route0 (only_skew: nothing to do unless st->skew, i.e. unless the fused
+// hash kernel left this set to k_hash_count0)
+void launch_route0_arrays(const uint64_t* kh, const uint64_t* fp, uint64_t n, const Route0& rt, LevelState* st,
+                          bool only_skew, hipStream_t s);
 // the level-0 hash kernel alone (kh, fp in key order; no histogram)
 void launch_hash0_only(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                        int grid, hipStream_t s);
