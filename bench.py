@@ -53,6 +53,8 @@ def stage_alg_bytes(stage: str, n: int, key_bytes: int, info: dict) -> int | Non
     settled = math.exp(-0.5)
     if stage == "hash_count0":  # key bytes + offsets read once; kh + fp written once
         return key_bytes + 8 * (n + 1) + 16 * n
+    if stage == "hash_route0":  # sharded build: key bytes + offsets read; (kh, fp, pos) records written once
+        return key_bytes + 8 * (n + 1) + 24 * n
     if stage == "scatter0":     # kh + fp read, (kh, fp, pos) record written to its tile bucket
         return 16 * n + 24 * n
     if stage == "tile0":        # bucket records read once; fp_out/pos_out or the next-level
@@ -228,7 +230,7 @@ def main() -> None:
         hbm = {"achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS}
         result["roofline"] = {"kernel": dom, "bound": "hbm", **hbm, "traffic": traffic, "alg_bytes": alg,
                               "avg_ms": dom_ms, "timed_region_events": dom in timed_stages}
-        if dom == "hash_count0":
+        if dom in ("hash_count0", "hash_route0"):
             # The hash is bounded by VALU before HBM: every key byte is one FNV-1a + FNV-1 step
             # (two 64-bit multiplies by the FNV prime); tools/ubench_fnv.hip measured the chip's
             # ceiling for that step from registers.  Its HBM rate rides
