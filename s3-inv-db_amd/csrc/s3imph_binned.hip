@@ -767,6 +767,24 @@ __global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __re
   }
 }
 
+// ------------------------------------------------------ 20-byte level-0 records ------
+// Level 0 with identity positions (pos_out = pos_base + key index, the builder's case):
+// a bucket / scratch record is (k, f, i) in 20 bytes — five dwords, i the key's index —
+// instead of Rec's 24, so the level-0 scatter writes and the split kernel's bucket reads,
+// scratch writes and scratch reads move 4 bytes less per key (1.6 GB less at C3).  Only
+// the reservation scatter and the split big-tile kernel use it; the next list stays Rec.
+struct R20 {
+  uint32_t w[5];
+};
+__device__ __forceinline__ R20 r20_make(uint64_t k, uint64_t f, uint32_t i) {
+  return R20{{(uint32_t)k, (uint32_t)(k >> 32), (uint32_t)f, (uint32_t)(f >> 32), i}};
+}
+__device__ __forceinline__ void r20_split(const R20& r, uint64_t pos_base, uint64_t& k, uint64_t& f, uint64_t& p) {
+  k = (uint64_t)r.w[0] | ((uint64_t)r.w[1] << 32);
+  f = (uint64_t)r.w[2] | ((uint64_t)r.w[3] << 32);
+  p = pos_base + r.w[4];
+}
+
 // ---------------------------------------------------------- reservation scatter ------
 // Small levels (a few 10^5 .. 10^6 keys) skip the count and histogram-scan kernels:
 // tile t owns the fixed bucket slot [t * cap, (t + 1) * cap), cap = bucket_cap / T
@@ -781,7 +799,8 @@ __global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __re
 // 2 level-0 arrays with identity positions.  A compile-time source keeps the loads
 // straight-line: with run-time selects the compiler waited out every record's loads
 // before issuing the next record's (four round trips per round).
-template <int kR, int kT, int kSrc>
+// kP20 (kSrc 2 only): bucket records are R20 (the split kernel reads them).
+template <int kR, int kT, int kSrc, bool kP20 = false>
 __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __restrict__ ilist,
                                                      const uint64_t* __restrict__ ik, const uint64_t* __restrict__ ifp,
                                                      const uint64_t* __restrict__ ipos, uint64_t pos_base,
@@ -791,7 +810,11 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
                                                      unsigned long long* __restrict__ prof, uint64_t i_lo,
                                                      uint64_t i_hi) {
   constexpr int kKPT = kR / kSB;
-  __shared__ Rec stage[kR];
+  static_assert(!kP20 || kSrc == 2, "20-byte records carry identity positions");
+  __shared__ uint64_t stage_raw[kR * 3];  // kR Rec, or kR R20
+  Rec* const stage = reinterpret_cast<Rec*>(stage_raw);
+  R20* const stage20 = reinterpret_cast<R20*>(stage_raw);
+  R20* const bucket20 = reinterpret_cast<R20*>(bucket);
   __shared__ unsigned short stile[kR];
   __shared__ unsigned cnt[kT];
   __shared__ unsigned start[kT];
@@ -916,7 +939,8 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < n) {
         const unsigned slot = start[tt[q]] + rk[q];
-        stage[slot] = Rec{rk_[q], rf_[q], rp_[q]};
+        if constexpr (kP20) stage20[slot] = r20_make(rk_[q], rf_[q], (uint32_t)(rp_[q] - pos_base));
+        else stage[slot] = Rec{rk_[q], rf_[q], rp_[q]};
         stile[slot] = (unsigned short)tt[q];
       }
     }
@@ -953,7 +977,8 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     if (s_over) break;
     for (unsigned j = tid; j < m; j += kSB) {
       const unsigned t = stile[j];
-      bucket[cur[t] + (j - start[t])] = stage[j];
+      if constexpr (kP20) bucket20[cur[t] + (j - start[t])] = stage20[j];
+      else bucket[cur[t] + (j - start[t])] = stage[j];
     }
     __syncthreads();
     SPROF(4);
@@ -1404,13 +1429,17 @@ constexpr int kSplitT = 1024;
 constexpr int kSplitGrid = 256;             // one workgroup per CU (its LDS takes ~144 KiB)
 __host__ __device__ constexpr uint64_t split_scratch_recs() { return (uint64_t)kSplitGrid * kSplitMaxSub * kSplitSeg; }
 
+// kP20: the bucket holds level 0's R20 records (p = pos_base + i); the scratch segments
+// then hold R20 too.
+template <bool kP20>
 __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __restrict__ bucket,
                                                         const unsigned* __restrict__ tile_start,
                                                         const unsigned* __restrict__ tcnt, uint64_t bucket_cap,
                                                         unsigned long long* flags, uint64_t* __restrict__ bits,
                                                         Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
                                                         uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
-                                                        Rec* __restrict__ scratch, unsigned long long* __restrict__ prof) {
+                                                        Rec* __restrict__ scratch, unsigned long long* __restrict__ prof,
+                                                        uint64_t pos_base) {
   constexpr int kSU = 3;  // split-phase records per thread per batch (the batch is staged in sfp)
   static_assert((size_t)kSU * kSplitT * sizeof(Rec) <= 2 * kSplitStage * sizeof(uint64_t), "split stage fits sf/sp");
   __shared__ uint32_t sA[1u << (kSplitMaxBits - 5)], sC[1u << (kSplitMaxBits - 5)];
@@ -1421,6 +1450,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
   uint64_t* const sf = sfp;
   uint64_t* const sp = sfp + kSplitStage;
   Rec* const stg = reinterpret_cast<Rec*>(sfp);
+  R20* const stg20 = reinterpret_cast<R20*>(sfp);
   __shared__ unsigned s_wc[kSplitT / 64];
   __shared__ unsigned long long s_t, s_prefix, s_b0, s_run;
   if (!level_active(level, st)) return;
@@ -1438,6 +1468,18 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint64_t lt = lanemask_lt();
   Rec* seg = scratch + (uint64_t)blockIdx.x * kSplitMaxSub * kSplitSeg;  // this workgroup's sub-tile segments
+  R20* seg20 = reinterpret_cast<R20*>(scratch) + (uint64_t)blockIdx.x * kSplitMaxSub * kSplitSeg;
+  // record j of a bucket / scratch array as (k, f, p)
+  auto rec_get = [&](const Rec* a, const R20* a20, uint64_t j, uint64_t& k, uint64_t& f, uint64_t& p) {
+    if constexpr (kP20) {
+      r20_split(a20[j], pos_base, k, f, p);
+    } else {
+      const Rec* q = a + j;
+      k = q->k;
+      f = q->f;
+      p = q->p;
+    }
+  };
   bool bad = false;
   for (;;) {
     if (tid == 0) s_t = atomicAdd(&st->ticket[level], 1ull);
@@ -1480,6 +1522,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
       for (int x = 0; x < kResShards; ++x) pre[x] = x ? 0xffffffffu : 0u;
     }
     const Rec* rb = bucket + lo;
+    const R20* rb20 = reinterpret_cast<const R20*>(bucket) + lo;
     auto shard_off = [&](uint64_t j) -> uint64_t {
       uint64_t o = j;
 #pragma unroll
@@ -1499,10 +1542,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
 #pragma unroll
       for (int u = 0; u < kSU; ++u) {
         const uint64_t j = min(jb + (uint64_t)u * kSplitT + tid, nk - 1);
-        const Rec* q = rb + shard_off(j);
-        k[u] = q->k;
-        f[u] = q->f;
-        p[u] = q->p;
+        rec_get(rb, rb20, shard_off(j), k[u], f[u], p[u]);
       }
     };
     auto split_batch = [&](uint64_t jb, const uint64_t (&k)[kSU], const uint64_t (&f)[kSU],
@@ -1558,7 +1598,8 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
       for (int u = 0; u < kSU; ++u) {
         if (qs[u] < kSplitMaxSub) {
           const unsigned slot = s_start[qs[u]] + rk[u];
-          stg[slot] = Rec{k[u], f[u], p[u]};
+          if constexpr (kP20) stg20[slot] = r20_make(k[u], f[u], (uint32_t)(p[u] - pos_base));
+          else stg[slot] = Rec{k[u], f[u], p[u]};
           stq[slot] = (unsigned char)qs[u];
         }
       }
@@ -1567,8 +1608,9 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
       for (unsigned jj = tid; jj < m; jj += kSplitT) {
         const unsigned q = stq[jj];
         const unsigned d = s_base[q] + (jj - s_start[q]);
-        if (d < kSplitSeg) seg[(uint64_t)q * kSplitSeg + d] = stg[jj];
-        else over = true;
+        if (d >= kSplitSeg) over = true;
+        else if constexpr (kP20) seg20[(uint64_t)q * kSplitSeg + d] = stg20[jj];
+        else seg[(uint64_t)q * kSplitSeg + d] = stg[jj];
       }
     };
     constexpr uint64_t kBatch = (uint64_t)kSplitT * kSU;
@@ -1629,6 +1671,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
     for (unsigned sq = 0; sq < nsub; ++sq) {
       const unsigned m = min(s_q[sq], kSplitSeg);
       const Rec* sr = seg + (uint64_t)sq * kSplitSeg;
+      const R20* sr20 = seg20 + (uint64_t)sq * kSplitSeg;
       const unsigned qw = sq << (kSplitSubBits - 5);              // first word of the sub-tile
       const unsigned qrank = sC[qw];                               // its first rank in the tile
       const unsigned qend = sq + 1 < nsub ? sC[qw + (1u << (kSplitSubBits - 5))] : (unsigned)pop;
@@ -1640,11 +1683,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
         for (int r = 0; r < kSplitR; ++r) {
           const unsigned j = r * kSplitT + tid;
           k[r] = f[r] = p[r] = 0;
-          if (j < m) {
-            k[r] = sr[j].k;
-            f[r] = sr[j].f;
-            p[r] = sr[j].p;
-          }
+          if (j < m) rec_get(sr, sr20, j, k[r], f[r], p[r]);
         }
         unsigned redo = 0;
 #pragma unroll
@@ -1688,14 +1727,16 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
           const unsigned j = jb + lane;
           bool rd = false;
           if (j < m) {
-            const unsigned loc = (unsigned)(bb_index(seed, sr[j].k, words, magic) - tbase);
+            uint64_t jk, jf, jp;
+            rec_get(sr, sr20, j, jk, jf, jp);
+            const unsigned loc = (unsigned)(bb_index(seed, jk, words, magic) - tbase);
             const uint32_t wv = sA[loc >> 5];
             const uint32_t bit = 1u << (loc & 31);
             if (wv & bit) {
               if (ok && out_on) {
                 const uint64_t q = base + sC[loc >> 5] + __popc(wv & (bit - 1));
-                fp_out[q] = sr[j].f;
-                pos_out[q] = sr[j].p;
+                fp_out[q] = jf;
+                pos_out[q] = jp;
               }
             } else {
               rd = true;
@@ -1710,12 +1751,14 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
         for (unsigned jb = wave * 64; jb < m; jb += kSplitT) {
           const unsigned j = jb + lane;
           bool rd = false;
+          uint64_t jk = 0, jf = 0, jp = 0;
           if (j < m) {
-            const unsigned loc = (unsigned)(bb_index(seed, sr[j].k, words, magic) - tbase);
+            rec_get(sr, sr20, j, jk, jf, jp);
+            const unsigned loc = (unsigned)(bb_index(seed, jk, words, magic) - tbase);
             rd = !((sA[loc >> 5] >> (loc & 31)) & 1u);
           }
           const uint64_t mm = __ballot(rd);
-          if (rd) next[o + __popcll(mm & lt)] = sr[j];
+          if (rd) next[o + __popcll(mm & lt)] = Rec{jk, jf, jp};
           o += __popcll(mm);
         }
       }
@@ -2805,9 +2848,11 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
   // 2^15 / 2^16 tiles: the split kernel (k_tile stays for contexts without its scratch
   // and for the 2^17+ tiles of oversized conservative reruns)
   if (b.split && g.tb > kRegMaxBits && g.tb <= kSplitMaxBits) {
-    k_tile_split<<<kSplitGrid, kSplitT, 0, s>>>(level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags, b.bits,
-                                                b.list[level & 1], b.fp_out, b.pos_out, b.st, g.tb, b.split,
-                                                b.tile_prof);
+    // level 0 through the reservation scatter with identity positions: R20 records
+    const bool p20 = level == 0 && !b.dist && !b.pos && reserved;
+    (p20 ? k_tile_split<true> : k_tile_split<false>)<<<kSplitGrid, kSplitT, 0, s>>>(
+        level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st,
+        g.tb, b.split, b.tile_prof, b.pos_base);
     return;
   }
   k_tile<1024><<<grid_tiles, 1024, tile_lds_bytes(g.tb), s>>>(level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags,
@@ -2820,8 +2865,13 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
   const bool l0 = level == 0 && !b.dist;
   const Rec* il = l0 ? nullptr : b.list[(level - 1) & 1];
   unsigned* tc = b.tcnt + (uint64_t)level * kScatterTiles * kResShards;
-  auto kern = !l0 ? k_scatter_res<kSubRound, kLdsTiles, 0>
-             : b.pos ? k_scatter_res<kSubRound, kLdsTiles, 1> : k_scatter_res<kSubRound, kLdsTiles, 2>;
+  // level 0 whose tiles go to the split kernel, identity positions: R20 records (the
+  // split launch makes the same choice)
+  const bool p20 = l0 && !b.pos && b.split && g.tb > kRegMaxBits && g.tb <= kSplitMaxBits;
+  auto kern = !l0    ? k_scatter_res<kSubRound, kLdsTiles, 0>
+              : b.pos ? k_scatter_res<kSubRound, kLdsTiles, 1>
+              : p20   ? k_scatter_res<kSubRound, kLdsTiles, 2, true>
+                      : k_scatter_res<kSubRound, kLdsTiles, 2>;
   kern<<<grid, kSB, 0, s>>>(level, il, b.kh, b.fp, b.pos, b.pos_base, tc, b.bucket, b.bucket_cap, b.flags, b.st, g.tb,
                             b.cap_words, b.tile_prof, i_lo, i_hi);
 }
