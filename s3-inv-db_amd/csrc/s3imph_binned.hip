@@ -917,6 +917,17 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     __syncthreads();
     SPROF(1);
     constexpr int kTPT = (int)(kT / kSB);
+    // The round's returning reservation atomics (one per tile present; thread tid takes
+    // tiles q kSB + tid) go out as soon as the counts are final, so their round trip
+    // overlaps the count scan, the stage writes and the next round's loads.
+    unsigned ac[kTPT], at[kTPT];
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      const uint64_t t = (uint64_t)q * kSB + tid;
+      ac[q] = t < T ? cnt[t] : 0u;
+      at[q] = 0;
+      if (ac[q]) at[q] = atomicAdd(&tcnt[t * kResShards + shard], ac[q]);
+    }
     const uint64_t t0 = (uint64_t)kTPT * tid;
     unsigned a[kTPT];
     uint64_t sum = 0;
@@ -944,18 +955,9 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
         stile[slot] = (unsigned short)tt[q];
       }
     }
-    // The round's returning atomics (up to kTPT tiles per thread) and the next round's
-    // loads are all issued before any atomic result is used, so the two latencies
-    // overlap; one tile at a time waited out each round trip in turn (C3 level 0: ~10 of
-    // ~20 us per round).
-    unsigned ac[kTPT], at[kTPT];
-#pragma unroll
-    for (int q = 0; q < kTPT; ++q) {
-      const uint64_t t = (uint64_t)q * kSB + tid;
-      ac[q] = t < T ? cnt[t] : 0u;
-      at[q] = 0;
-      if (ac[q]) at[q] = atomicAdd(&tcnt[t * kResShards + shard], ac[q]);
-    }
+    // The next round's loads are issued before any atomic result is used, so the two
+    // latencies overlap; one tile at a time waited out each round trip in turn (C3 level
+    // 0: ~10 of ~20 us per round).
     const unsigned m = (unsigned)min<uint64_t>(kR, n - r0);
     r0 += stride;
     const bool more = r0 < n;
