@@ -119,21 +119,11 @@ __device__ __forceinline__ bool no_progress(LevelState* st, int level, uint64_t 
 
 // ---------------------------------------------------------------- level 0 count ----
 // Hash every key (FNV-1a key hash + FNV-1 fingerprint, one pass over the bytes),
-// store both in key order, and histogram the level-0 tiles per chunk.
-// kVar: 0 one load per word (fnv_both_loop), 1 batched 8-word loads (fnv_both),
-// 2 loads pipelined two words ahead (fnv_both_pf), 3 16-byte loads (fnv_both_16).
-template <int kVar>
-__device__ __forceinline__ void hash_key(const uint8_t* blob, uint64_t b0, uint64_t b1, uint64_t& h1, uint64_t& h2) {
-  if (kVar == 1) fnv_both(blob, b0, b1, h1, h2);
-  else if (kVar == 2) fnv_both_pf(blob, b0, b1, h1, h2);
-  else if (kVar == 3) fnv_both_16(blob, b0, b1, h1, h2);
-  else fnv_both_loop(blob, b0, b1, h1, h2);
-}
-
-// smode: 0 direct (hash_key<kVD>); 1 length-sorted groups (hash_key<kVS>), a group that is
-// not skewed hashed directly; 2 sort every group; 3 pick 1 or 0 from st->skew (k_init_state
-// sampled the key lengths) — one launch whatever the set.
-template <int kVD, int kVS>
+// store both in key order, and (counted path) histogram the level-0 tiles per chunk.
+// A key is read with aligned 8-byte loads pipelined two words ahead (fnv_both_pf), or
+// with 16-byte loads (fnv_both_16) inside length-sorted groups.
+// smode 3: sort a group when the set is skewed (st->skew, sampled by k_init_state);
+// smode 5: the same, and a no-op launch unless skewed (k_hash0_pair hashed the set).
 __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restrict__ blob,
                                                      const uint64_t* __restrict__ offsets, uint64_t n,
                                                      uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
@@ -148,7 +138,7 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
   __shared__ uint64_t sb0[kCB], sb1[kCB], sh1[kCB], sh2[kCB];
   __shared__ uint64_t s_lmax[kCB / 64], s_lsum[kCB / 64];
   if (smode == 5 && !st->skew) return;  // k_hash0_pair hashed this near-uniform set
-  const bool sort = smode == 1 || smode == 2 || ((smode == 3 || smode == 5) && st->skew);
+  const bool sort = st->skew != 0;
   const uint64_t words = st->words[0], magic = st->magic[0];
   const uint64_t T = ntiles_of(words, tb), B = (n + chunk - 1) / chunk;
   if (!geom_ok(st, T, B)) return;
@@ -170,7 +160,7 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
       __syncthreads();
       for (uint64_t i = lo + tid; i < hi; i += kCB) {
         uint64_t h1, h2;
-        hash_key<kVD>(blob, offsets[i], offsets[i + 1], h1, h2);
+        fnv_both_pf(blob, offsets[i], offsets[i + 1], h1, h2);
         kh[i] = h1;
         fp[i] = h2;
         zero |= (h1 == 0);
@@ -210,10 +200,10 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
         gsum += s_lsum[w];
       }
       const uint64_t gcnt = min<uint64_t>(kCB, hi - g);
-      if (smode != 2 && gmax * gcnt <= 2 * gsum + 16 * gcnt) {
+      if (gmax * gcnt <= 2 * gsum + 16 * gcnt) {
         if (i < hi) {
           uint64_t h1, h2;
-          hash_key<kVS>(blob, b0, b1, h1, h2);
+          fnv_both_16(blob, b0, b1, h1, h2);
           kh[i] = h1;
           fp[i] = h2;
           zero |= (h1 == 0);
@@ -237,7 +227,7 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
       const unsigned j = sidx[tid];
       if (g + j < hi) {
         uint64_t h1, h2;
-        hash_key<kVS>(blob, sb0[tid], sb1[tid], h1, h2);
+        fnv_both_16(blob, sb0[tid], sb1[tid], h1, h2);
         sh1[j] = h1;
         sh2[j] = h2;
         zero |= (h1 == 0);
@@ -2772,11 +2762,11 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       unsigned long long* prof = b.tile_prof ? b.tile_prof + (uint64_t)(kMaxLevels - 3) * kMaxTiles * 8 : nullptr;
       k_hash0_pair<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
                                                              g.tb, g.chunk, b.tcnt, prof);
-      k_hash_count0<2, 3><<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st,
+      k_hash_count0<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st,
                                                       g.tb, g.chunk, b.tcnt, 5);
       return;
     }
-    k_hash_count0<2, 3><<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, histogram ? b.hist : nullptr,
+    k_hash_count0<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, histogram ? b.hist : nullptr,
                                                   b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, 3);
   } else {
     k_count<<<grid_chunks, kCB, 0, s>>>(level, b.list[(level - 1) & 1], b.hist, b.flags, b.sflags, b.st, g.tb,
@@ -2789,11 +2779,11 @@ void launch_hash0_only(const uint8_t* blob, const uint64_t* offsets, uint64_t n,
   if (((uintptr_t)blob & 15) == 0) {  // as the single-GPU level 0: pair rounds unless st->skew
     k_hash0_pair<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
                                                            g.tb, g.chunk, b.tcnt, nullptr);
-    k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
+    k_hash_count0<<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
                                              g.chunk, b.tcnt, 5);
     return;
   }
-  k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
+  k_hash_count0<<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
                                            g.chunk, b.tcnt, 3);
 }
 
@@ -2803,12 +2793,12 @@ void launch_hash0_route(const uint8_t* blob, const uint64_t* offsets, uint64_t n
     k_hash0_pair<kH0T, kH0B, true, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags,
                                                                  b.st, g.tb, g.chunk, b.tcnt, nullptr, rt);
     // a skewed set (st->skew): k_hash_count0's length-sorted groups, then k_route
-    k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
+    k_hash_count0<<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
                                              g.chunk, b.tcnt, 5);
     launch_route0_arrays(b.kh, b.fp, n, rt, b.st, true, s);
     return;
   }
-  k_hash_count0<2, 3><<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
+  k_hash_count0<<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
                                            g.chunk, b.tcnt, 3);
   launch_route0_arrays(b.kh, b.fp, n, rt, b.st, false, s);
 }

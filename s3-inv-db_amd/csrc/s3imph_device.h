@@ -82,13 +82,6 @@ static __device__ __forceinline__ void fnv_step_w(uint32_t& alo, uint32_t& ahi, 
   blo ^= c;
 }
 
-static __device__ __forceinline__ void fnv_step(uint64_t& a, uint64_t& b, uint32_t byte) {
-  uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
-  fnv_step_w(alo, ahi, blo, bhi, byte);
-  a = (uint64_t)alo | ((uint64_t)ahi << 32);
-  b = (uint64_t)blo | ((uint64_t)bhi << 32);
-}
-
 // x ^ (byte B of w): one v_xor_b32 with an SDWA byte select (the compiler's own lowering
 // spends a shift on bytes 1 and 2).
 template <int B>
@@ -184,32 +177,6 @@ static __device__ __forceinline__ void fnv_tail8(uint64_t& a, uint64_t& b, uint6
   b = (uint64_t)blo | ((uint64_t)bhi << 32);
 }
 
-// FNV-1a + FNV-1 over a key whose bytes start `sh` bits into aligned word w[0] and
-// span nw aligned words: stream word q = funnel(w[q], w[q+1]).  w may point into
-// global memory or LDS (the caller's pointer decides the address space once inlined).
-static __device__ __forceinline__ void fnv_words(const uint64_t* w, uint64_t nw, unsigned sh, uint64_t len,
-                                                 uint64_t& ha, uint64_t& hb) {
-  uint64_t a = kFnvOffset, b = kFnvOffset;
-  if (len) {
-    const uint64_t nfull = len >> 3;
-    uint64_t cur = w[0];
-    for (uint64_t q = 0; q < nfull; ++q) {
-      const uint64_t nxt = (q + 1 < nw) ? w[q + 1] : 0;
-      const uint64_t v = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
-      fnv_8(a, b, v);
-      cur = nxt;
-    }
-    const unsigned rem = (unsigned)(len & 7);
-    if (rem) {
-      const uint64_t nxt = (nfull + 1 < nw) ? w[nfull + 1] : 0;
-      const uint64_t v = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
-      fnv_tail8(a, b, v, rem);
-    }
-  }
-  ha = a;
-  hb = b;
-}
-
 // Bytes [s, s + 8) of the 16-byte little-endian concatenation lo:hi (s in 0..7), from
 // 32-bit byte funnels (v_alignbyte_b32): the key stream word of a key that starts s bytes
 // into aligned word `lo`.
@@ -221,14 +188,6 @@ static __device__ __forceinline__ uint64_t funnel_bytes(uint64_t lo, uint64_t hi
   const uint32_t r0 = __builtin_amdgcn_alignbyte(x1, x0, sb);
   const uint32_t r1 = __builtin_amdgcn_alignbyte(x2, x1, sb);
   return (uint64_t)r0 | ((uint64_t)r1 << 32);
-}
-
-// FNV-1a + FNV-1 of blob[b0, b1), one dependent load per aligned word (funnel shifts).
-static __device__ __forceinline__ void fnv_both_loop(const uint8_t* __restrict__ blob, uint64_t b0, uint64_t b1,
-                                                     uint64_t& ha, uint64_t& hb) {
-  const uint64_t* w = reinterpret_cast<const uint64_t*>(blob + (b0 & ~7ull));
-  const uint64_t nw = b1 > b0 ? ((b1 - 1) >> 3) - (b0 >> 3) + 1 : 0;  // aligned words overlapping the key
-  fnv_words(w, nw, (unsigned)(b0 & 7) * 8, b1 - b0, ha, hb);
 }
 
 // FNV-1a + FNV-1 of blob[b0, b1) with the aligned-word loads software-pipelined two
@@ -337,38 +296,6 @@ static __device__ __forceinline__ void fnv_both_16(const uint8_t* __restrict__ b
   hb = b;
 }
 
-// FNV-1a (key hash) and FNV-1 (fingerprint) of blob[b0, b1) in one pass.  The key's
-// aligned words are loaded 8 at a time (all 8 loads in flight before the first use);
-// stream word q = bytes [8q, 8q+8) of the key = funnel(w[q], w[q+1]) by the key's
-// misalignment.  Never reads past the key's last aligned word.
-static __device__ __forceinline__ void fnv_both(const uint8_t* __restrict__ blob, uint64_t b0, uint64_t b1,
-                                                uint64_t& ha, uint64_t& hb) {
-  uint64_t a = kFnvOffset, b = kFnvOffset;
-  if (b1 > b0) {
-    const uint64_t* w = reinterpret_cast<const uint64_t*>(blob + (b0 & ~7ull));
-    const uint64_t nw = ((b1 - 1) >> 3) - (b0 >> 3) + 1;  // aligned words overlapping the key
-    const unsigned sh = (unsigned)(b0 & 7) * 8;
-    const uint64_t len = b1 - b0;
-    const uint64_t nfull = len >> 3;
-    const unsigned rem = (unsigned)(len & 7);
-    uint64_t cur = w[0], vrem = 0;
-    for (uint64_t base = 0; base <= nfull; base += 8) {
-      uint64_t W[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) W[q] = (base + q + 1 < nw) ? w[base + q + 1] : 0;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint64_t v = sh ? (cur >> sh) | (W[q] << (64 - sh)) : cur;
-        if (base + q < nfull) fnv_8(a, b, v);
-        if (base + q == nfull) vrem = v;
-        cur = W[q];
-      }
-    }
-    fnv_tail8(a, b, vrem, rem);
-  }
-  ha = a;
-  hb = b;
-}
 
 
 }  // namespace s3imph

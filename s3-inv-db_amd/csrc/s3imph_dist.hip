@@ -30,19 +30,16 @@ constexpr int kRT = 1024;               // route block
 constexpr int kRK = 2;                  // records per thread per round
 constexpr int kRRound = kRT * kRK;
 
-// Route this rank's records of level `level` to their owners.  kSrc 0: level 0, the
-// records are made here from the keys (FNV-1a key hash + FNV-1 fingerprint, one pass
-// over the bytes, as StreamingMPHFBuilder.Add does); 2: level 0 from the hash kernel's
-// key-order kh / fp arrays; 1: the collided records list[0..n[level]).  Each round of kRRound records is counting-sorted by owner
-// in LDS; one atomic per (round, owner) reserves its run in the owner's send region
+// Route this rank's records of level `level` to their owners.  kSrc 2: level 0 from the
+// hash kernel's key-order kh / fp arrays (a skewed set, or a retried route; the pair-round
+// hash routes level 0 itself otherwise); 1: the collided records list[0..n[level]).  Each
+// round of kRRound records is counting-sorted by owner in LDS; one atomic per (round, owner) reserves its run in the owner's send region
 // [d*cap, (d+1)*cap), and the runs are written out coalesced.  Records this rank owns
 // itself skip the exchange: they go straight to `self_dst` (the level's input list,
 // capacity self_cap), counted in scnt[rank] like any owner's.  A region overflow sets
 // kStRouteOverflow (the host re-routes with larger regions; bytes are unaffected).
 template <int kSrc>
-__global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restrict__ blob,
-                                               const uint64_t* __restrict__ offsets,
-                                               const uint64_t* __restrict__ ikh, const uint64_t* __restrict__ ifp,
+__global__ __launch_bounds__(kRT) void k_route(int level, const uint64_t* __restrict__ ikh, const uint64_t* __restrict__ ifp,
                                                const uint64_t* __restrict__ ipos, uint64_t pos_base,
                                                uint64_t n_keys, const Rec* __restrict__ ilist,
                                                Rec* __restrict__ send, uint64_t cap,
@@ -75,7 +72,6 @@ __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restr
   const uint64_t words = st->words[level], magic = st->magic[level];
   const uint64_t S = st->dS[level], mS = st->dmagic[level];
   const uint64_t seed = level_seed(level);
-  bool zero = false;
   for (uint64_t r0 = (uint64_t)blockIdx.x * kRRound; r0 < n; r0 += (uint64_t)gridDim.x * kRRound) {
     if (tid < kMaxRanks) cnt[tid] = 0;
     __syncthreads();
@@ -86,12 +82,7 @@ __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restr
       const uint64_t i = r0 + (uint64_t)q * kRT + tid;
       d[q] = rk[q] = 0;
       if (i < n) {
-        if (kSrc == 0) {
-          uint64_t h1, h2;
-          fnv_both_pf(blob, offsets[i], offsets[i + 1], h1, h2);
-          zero |= (h1 == 0);
-          rec[q] = Rec{h1, h2, ipos ? ipos[i] : pos_base + i};
-        } else if (kSrc == 2) {
+        if (kSrc == 2) {
           rec[q] = Rec{ikh[i], ifp[i], ipos ? ipos[i] : pos_base + i};
         } else {
           rec[q] = ilist[i];
@@ -139,7 +130,6 @@ __global__ __launch_bounds__(kRT) void k_route(int level, const uint8_t* __restr
     }
     __syncthreads();
   }
-  if (zero) atomicOr(&st->status, kStKeyZero);
   if (tid == 0 && s_over) atomicOr(&st->status, kStRouteOverflow);
 }
 
@@ -193,33 +183,25 @@ void launch_route_flag(LevelState* st, unsigned long long* scnt, int P, hipStrea
   k_route_flag<<<1, 64, 0, s>>>(st, scnt, P);
 }
 
-void launch_route0(const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t pos_base, uint64_t n,
-                   Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, int rank, Rec* self_dst,
-                   uint64_t self_cap, hipStream_t s) {
-  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + kRRound - 1) / kRRound, 2048));
-  k_route<0><<<grid, kRT, 0, s>>>(0, blob, offsets, nullptr, nullptr, pos, pos_base, n, nullptr, send, cap, scnt, st, P,
-                                   rank, self_dst, self_cap, nullptr, 0);
-}
-
 void launch_route0_arrays(const uint64_t* kh, const uint64_t* fp, const uint64_t* pos, uint64_t pos_base, uint64_t n,
                           Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, int rank,
                           Rec* self_dst, uint64_t self_cap, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + kRRound - 1) / kRRound, 2048));
-  k_route<2><<<grid, kRT, 0, s>>>(0, nullptr, nullptr, kh, fp, pos, pos_base, n, nullptr, send, cap, scnt, st, P, rank,
+  k_route<2><<<grid, kRT, 0, s>>>(0, kh, fp, pos, pos_base, n, nullptr, send, cap, scnt, st, P, rank,
                                    self_dst, self_cap, nullptr, 0);
 }
 
 void launch_route0_arrays(const uint64_t* kh, const uint64_t* fp, uint64_t n, const Route0& rt, LevelState* st,
                           bool only_skew, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + kRRound - 1) / kRRound, 2048));
-  k_route<2><<<grid, kRT, 0, s>>>(0, nullptr, nullptr, kh, fp, rt.pos, rt.pos_base, n, nullptr, rt.send, rt.cap, rt.scnt,
+  k_route<2><<<grid, kRT, 0, s>>>(0, kh, fp, rt.pos, rt.pos_base, n, nullptr, rt.send, rt.cap, rt.scnt,
                                    st, rt.P, rt.rank, rt.self_dst, rt.self_cap, rt.mat_prev, only_skew ? 1 : 0);
 }
 
 void launch_route(int level, const Rec* list, uint64_t n_pred, Rec* send, uint64_t cap, unsigned long long* scnt,
                   LevelState* st, int P, int rank, Rec* self_dst, uint64_t self_cap, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n_pred + kRRound - 1) / kRRound + 8, 2048));
-  k_route<1><<<grid, kRT, 0, s>>>(level, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, list, send, cap, scnt, st,
+  k_route<1><<<grid, kRT, 0, s>>>(level, nullptr, nullptr, nullptr, 0, 0, list, send, cap, scnt, st,
                                    P, rank, self_dst, self_cap, nullptr, 0);
 }
 

@@ -243,9 +243,6 @@ struct Route0 {
 void launch_hash0_route(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                         int grid, const Route0& rt, hipStream_t s);
 // Records owned by `rank` itself go straight to self_dst (capacity self_cap), not to a send region.
-void launch_route0(const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t pos_base, uint64_t n,
-                   Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, int rank, Rec* self_dst,
-                   uint64_t self_cap, hipStream_t s);
 // level-0 records from the hash kernel's kh / fp arrays (multi-GPU build)
 void launch_route0_arrays(const uint64_t* kh, const uint64_t* fp, const uint64_t* pos, uint64_t pos_base, uint64_t n,
                           Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, int P, int rank,
