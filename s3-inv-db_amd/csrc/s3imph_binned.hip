@@ -757,6 +757,8 @@ __global__ __launch_bounds__(kSB) void k_scatter(int level, const uint64_t* __re
   }
 }
 
+constexpr unsigned kSplitSubBitsDev = 14;  // = kSplitSubBits (sub-tile of the split kernel)
+
 // ------------------------------------------------------ 20-byte level-0 records ------
 // Level 0 with identity positions (pos_out = pos_base + key index, the builder's case):
 // a bucket / scratch record is (k, f, i) in 20 bytes — five dwords, i the key's index —
@@ -798,7 +800,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
                                                      uint64_t bucket_cap, unsigned long long* __restrict__ flags,
                                                      LevelState* st, unsigned tb, uint64_t cap_words,
                                                      unsigned long long* __restrict__ prof, uint64_t i_lo,
-                                                     uint64_t i_hi) {
+                                                     uint64_t i_hi, unsigned ts) {
   constexpr int kKPT = kR / kSB;
   static_assert(!kP20 || kSrc == 2, "20-byte records carry identity positions");
   __shared__ uint64_t stage_raw[kR * 3];  // kR Rec, or kR R20
@@ -837,7 +839,10 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     if (no_progress(st, level, n)) return;
   }
   const LevelRange rg = level_range(st, level, words);
-  const uint64_t T = ntiles_of(rg.rw, tb);
+  const uint64_t T = tiles_of(rg.rw, tb, ts);
+  // ts tiles: tile = (position offset >> 14) / ts by a 32-bit reciprocal (exact: the
+  // quotient's operand is < 2^18 and ts <= 16)
+  const uint32_t ts_mul = ts ? 0xffffffffu / ts + 1 : 0;
   if (T > kT) {
     if (tid == 0) atomicOr(&st->status, kStGeometry);
     return;
@@ -900,7 +905,8 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     for (int q = 0; q < kKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < n) {
-        tt[q] = (unsigned)((bb_index(seed, rk_[q], words, magic) - rg.plo) >> tb);
+        const uint64_t lp = bb_index(seed, rk_[q], words, magic) - rg.plo;
+        tt[q] = ts ? __umulhi((uint32_t)(lp >> kSplitSubBitsDev), ts_mul) : (unsigned)(lp >> tb);
         rk[q] = atomicAdd(&cnt[tt[q]], 1u);
       }
     }
@@ -1412,13 +1418,13 @@ __global__ __launch_bounds__(NT) void k_tile(int level, const Rec* __restrict__ 
 // Every record is read twice and written once more than in a register tile, all in
 // runs, instead of k_tile's rank-order gathers of (f, p) (16-byte random reads) and its
 // second pass for the collided records.
-constexpr unsigned kSplitSubBits = 14;
+constexpr unsigned kSplitSubBits = kSplitSubBitsDev;
 constexpr unsigned kSplitMaxSub = 1u << (kSplitMaxBits - kSplitSubBits);  // 16 sub-tiles of a 2^18 tile
 constexpr int kSplitR = 9;                  // sub-tile records per thread in registers (9216 >= 8192 + 11 sigma)
 constexpr unsigned kSplitStage = 5120;      // settled records staged per sub-tile (mean ~4970, sigma ~44)
 constexpr unsigned kSplitSeg = 10240;       // scratch records per sub-tile (mean 8192, sigma ~90)
 constexpr int kSplitT = 1024;
-constexpr int kSplitGrid = 256;             // one workgroup per CU (its LDS takes ~144 KiB)
+constexpr int kSplitGrid = kSplitGridHost;  // one workgroup per CU (its LDS takes ~144 KiB)
 __host__ __device__ constexpr uint64_t split_scratch_recs() { return (uint64_t)kSplitGrid * kSplitMaxSub * kSplitSeg; }
 
 // kP20: the bucket holds level 0's R20 records (p = pos_base + i); the scratch segments
@@ -1431,7 +1437,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
                                                         Rec* __restrict__ next, uint64_t* __restrict__ fp_out,
                                                         uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
                                                         Rec* __restrict__ scratch, unsigned long long* __restrict__ prof,
-                                                        uint64_t pos_base) {
+                                                        uint64_t pos_base, unsigned ts) {
   constexpr int kSU = 3;  // split-phase records per thread per batch (the batch is staged in sfp)
   static_assert((size_t)kSU * kSplitT * sizeof(Rec) <= 2 * kSplitStage * sizeof(uint64_t), "split stage fits sf/sp");
   __shared__ uint32_t sA[1u << (kSplitMaxBits - 5)], sC[1u << (kSplitMaxBits - 5)];
@@ -1452,8 +1458,8 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
   const uint64_t T = st->ntiles[level];
   const LevelRange rg = level_range(st, level, words);
   const uint64_t w32_level = 2 * rg.rw;
-  const unsigned tpw = 1u << (tb - 5);
-  const unsigned nsub = 1u << (tb - kSplitSubBits);
+  const unsigned nsub = ts ? ts : 1u << (tb - kSplitSubBits);  // 2^14-position sub-tiles per tile
+  const unsigned tpw = nsub << (kSplitSubBits - 5);
   uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[level] + rg.plo / 64);
   const uint64_t seed = level_seed(level);
   const uint64_t lvl_base = st->lvl_base[level];
@@ -1522,7 +1528,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
         if (j >= pre[x]) o = (uint64_t)x * shcap + (j - pre[x]);
       return o;
     };
-    const uint64_t tbase = rg.plo + (t << tb);
+    const uint64_t tbase = rg.plo + t * ((uint64_t)nsub << kSplitSubBits);
     // ---- split: mark A / C, append each record to its sub-tile's scratch segment.
     // Batches of kSU records per thread, the next batch's loads in flight while one is
     // processed (double-buffered registers; workgroup-uniform trip count and clamped
@@ -2844,7 +2850,7 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
     const bool p20 = level == 0 && !b.dist && !b.pos && reserved;
     (p20 ? k_tile_split<true> : k_tile_split<false>)<<<kSplitGrid, kSplitT, 0, s>>>(
         level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st,
-        g.tb, b.split, b.tile_prof, b.pos_base);
+        g.tb, b.split, b.tile_prof, b.pos_base, reserved ? g.ts : 0u);
     return;
   }
   k_tile<1024><<<grid_tiles, 1024, tile_lds_bytes(g.tb), s>>>(level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags,
@@ -2865,7 +2871,7 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
               : p20   ? k_scatter_res<kSubRound, kLdsTiles, 2, true>
                       : k_scatter_res<kSubRound, kLdsTiles, 2>;
   kern<<<grid, kSB, 0, s>>>(level, il, b.kh, b.fp, b.pos, b.pos_base, tc, b.bucket, b.bucket_cap, b.flags, b.st, g.tb,
-                            b.cap_words, b.tile_prof, i_lo, i_hi);
+                            b.cap_words, b.tile_prof, i_lo, i_hi, b.split ? g.ts : 0u);
 }
 
 void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s) {

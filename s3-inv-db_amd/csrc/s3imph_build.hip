@@ -290,15 +290,39 @@ bool res_fits(const s3imph_ctx* c, uint64_t nb, uint64_t size, uint64_t T = 0) {
   return m >= 768.0 && (double)c->bucket_cap >= (double)nb * (1.02 + 7.0 / std::sqrt(m));
 }
 
+// Split-kernel tile size for a reservation-path level of `size` (predicted, ~10 % high)
+// positions: the split kernel runs one persistent workgroup per CU taking tiles by ticket,
+// so a level of T tiles takes ceil(T / 256) rounds of a tile's time, and a tile's time is
+// proportional to its ts sub-tiles.  Pick ts (2..16) minimising ceil(T / 256) x ts with a
+// 5 % margin under each round boundary, the larger ts on ties (fewer tiles: longer
+// scatter runs).  C3 level 1: 601 tiles of 8 sub-tiles (3 rounds) -> 481 of 10 (2 rounds).
+unsigned choose_split_ts(uint64_t size) {
+  const double est = (double)size / 1.1;
+  unsigned best = 0;
+  double best_cost = 0;
+  for (unsigned ts = 2; ts <= (1u << (kSplitMaxBits - 14)); ++ts) {
+    const double T = est / (double)((uint64_t)ts << 14);
+    if (T > (double)kSplitTargetTiles) continue;
+    const double rounds = std::ceil(T / (0.95 * kSplitGridHost));
+    const double cost = rounds * ts;
+    if (best == 0 || cost <= best_cost) {
+      best = ts;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
 // One list-input level L (records in list[(L-1)&1]): about nb records over `size`
 // positions.  Small levels take the reservation scatter (no count / histogram scan).
 void enqueue_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, uint64_t size, bool conservative,
                         const LevelGeom* force, hipStream_t s) {
   // reservation slots are bucket_cap / T records per tile: keep them >= 4x the mean fill
   const bool res = !conservative && nb <= c->res_max_keys && res_fits(c, nb, size) && L < kResLevels;
-  const LevelGeom g = force ? *force
-                      : res ? choose_geom_sz(nb, size, kTargetTilesRes, kTargetChunks, kRegTileMaxBits)
-                            : choose_geom_sz(nb, size, kTargetTiles, kTargetChunks, kRegTileMaxBits);
+  LevelGeom g = force ? *force
+                : res ? choose_geom_sz(nb, size, kTargetTilesRes, kTargetChunks, kRegTileMaxBits)
+                      : choose_geom_sz(nb, size, kTargetTiles, kTargetChunks, kRegTileMaxBits);
+  if (res && !force && b.split && g.tb > kRegTileMaxBits && g.tb <= kSplitMaxBits) g.ts = choose_split_ts(size);
   const Grids gr = level_grids(nb, size, g);
   if (res) {
     const int gsr = (int)std::min<uint64_t>((nb + kSubRound - 1) / kSubRound, 256);

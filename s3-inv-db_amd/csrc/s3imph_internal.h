@@ -79,6 +79,7 @@ constexpr unsigned kRegTileMaxBits = 14;              // largest tile of the reg
 // the reservation scatter longer runs and fewer slot atomics per round (C3 level 0:
 // 2^16 / 2^17 / 2^18 tiles, scatter 1.73 / 1.45 / 1.19 ms).
 constexpr unsigned kSplitMaxBits = 18;
+constexpr int kSplitGridHost = 256;                   // k_tile_split's persistent workgroups (one per CU)
 constexpr uint64_t kSplitTargetTiles = 1024;
 constexpr uint64_t kHistCap = 8ull << 20;             // tiles x chunks entries
 constexpr unsigned kStTailOverflow = 16u;             // tail reached with a level too big for LDS
@@ -91,7 +92,14 @@ constexpr uint64_t kScanSeg = 8192;                   // histogram entries per s
 struct LevelGeom {
   unsigned tb;        // tile bits
   uint64_t chunk;     // keys per count/scatter chunk
+  unsigned ts = 0;    // split tiles of ts x 2^14 positions (2..16; 0: 2^tb)
 };
+// Tiles of a level of 64 * rw positions: 2^tb positions each, or ts 2^14-position
+// sub-tiles each (split-kernel levels sized for a whole number of rounds over the CUs).
+__host__ __device__ inline uint64_t tiles_of(uint64_t rw, unsigned tb, unsigned ts) {
+  const uint64_t tp = ts ? (uint64_t)ts << 14 : 1ull << tb;
+  return (64 * rw + tp - 1) / tp;
+}
 
 // Host-side choice for a level of about n keys: the smallest tile (>= 2^kTileMinBits
 // positions) that leaves at most target_tiles tiles, and about target_chunks chunks of
