@@ -290,20 +290,20 @@ bool res_fits(const s3imph_ctx* c, uint64_t nb, uint64_t size, uint64_t T = 0) {
   return m >= 768.0 && (double)c->bucket_cap >= (double)nb * (1.02 + 7.0 / std::sqrt(m));
 }
 
-// Split-kernel tile size for a reservation-path level of `size` (predicted, ~10 % high)
-// positions: the split kernel runs one persistent workgroup per CU taking tiles by ticket,
+// Split-kernel tile size for a reservation-path level of `size` positions (predicted,
+// ~10 % high, unless `exact`: the sharded build's levels): the split kernel runs one persistent workgroup per CU taking tiles by ticket,
 // so a level of T tiles takes ceil(T / 256) rounds of a tile's time, and a tile's time is
 // proportional to its ts sub-tiles.  Pick ts (2..16) minimising ceil(T / 256) x ts with a
 // 5 % margin under each round boundary, the larger ts on ties (fewer tiles: longer
 // scatter runs).  C3 level 1: 601 tiles of 8 sub-tiles (3 rounds) -> 481 of 10 (2 rounds).
-unsigned choose_split_ts(uint64_t size) {
-  const double est = (double)size / 1.1;
+unsigned choose_split_ts(uint64_t size, bool exact) {
+  const double est = exact ? (double)size : (double)size / 1.1;
   unsigned best = 0;
   double best_cost = 0;
   for (unsigned ts = 2; ts <= (1u << (kSplitMaxBits - 14)); ++ts) {
     const double T = est / (double)((uint64_t)ts << 14);
     if (T > (double)kSplitTargetTiles) continue;
-    const double rounds = std::ceil(T / (0.95 * kSplitGridHost));
+    const double rounds = std::ceil(T / ((exact ? 1.0 : 0.95) * kSplitGridHost));
     const double cost = rounds * ts;
     if (best == 0 || cost <= best_cost) {
       best = ts;
@@ -316,13 +316,13 @@ unsigned choose_split_ts(uint64_t size) {
 // One list-input level L (records in list[(L-1)&1]): about nb records over `size`
 // positions.  Small levels take the reservation scatter (no count / histogram scan).
 void enqueue_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, uint64_t size, bool conservative,
-                        const LevelGeom* force, hipStream_t s) {
+                        const LevelGeom* force, hipStream_t s, bool exact_size = false) {
   // reservation slots are bucket_cap / T records per tile: keep them >= 4x the mean fill
   const bool res = !conservative && nb <= c->res_max_keys && res_fits(c, nb, size) && L < kResLevels;
   LevelGeom g = force ? *force
                 : res ? choose_geom_sz(nb, size, kTargetTilesRes, kTargetChunks, kRegTileMaxBits)
                       : choose_geom_sz(nb, size, kTargetTiles, kTargetChunks, kRegTileMaxBits);
-  if (res && !force && b.split && g.tb > kRegTileMaxBits && g.tb <= kSplitMaxBits) g.ts = choose_split_ts(size);
+  if (res && !force && b.split && g.tb > kRegTileMaxBits && g.tb <= kSplitMaxBits) g.ts = choose_split_ts(size, exact_size);
   const Grids gr = level_grids(nb, size, g);
   if (res) {
     const int gsr = (int)std::min<uint64_t>((nb + kSubRound - 1) / kSubRound, 256);
@@ -950,7 +950,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
     launch_set_u64(&st->n[L], m, s);
     ev_mark(c, s, L == 0 ? "route0" : "route");
     // ---- the owner's tile pipeline over positions [64 lo, 64 (lo + rw))
-    enqueue_list_level(c, (L & 1) ? bsw : b, L, m, 64 * rw, conservative, nullptr, s);
+    enqueue_list_level(c, (L & 1) ? bsw : b, L, m, 64 * rw, conservative, nullptr, s, true);
     ev_mark(c, s, L == 0 ? "level0" : "levels");
     // ---- size the next level from the global redo count (device side, no host sync)
     cm.allreduce_u64(&st->n[L + 1], d.gslot + L + 1, 1, s);
