@@ -398,9 +398,11 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   static const bool hash_only = std::getenv("S3IMPH_HASH_ONLY") != nullptr;
   if (hash_only) return;
   if (res0) {
-    launch_binned_scatter_res(0, b, g0, 256, s);
+    LevelGeom gr0 = g0;  // split-kernel level 0: tiles in whole rounds over the CUs (exact size)
+    if (b.split && g0.tb > kRegTileMaxBits && g0.tb <= kSplitMaxBits) gr0.ts = choose_split_ts(64 * level_words(n), true);
+    launch_binned_scatter_res(0, b, gr0, 256, s);
     ev_mark(c, s, "scatter0");
-    launch_binned_tile(0, b, g0, gr.gt, s, true);
+    launch_binned_tile(0, b, gr0, gr.gt, s, true);
     ev_mark(c, s, "tile0");
     enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
     return;
