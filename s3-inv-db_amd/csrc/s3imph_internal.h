@@ -152,12 +152,12 @@ constexpr unsigned long long kTailKeys = 12288;
 // Mid-size levels (above the tail, at most kMidMaxKeys keys) run inside one persistent
 // kernel of kMidG cooperating workgroups (s3imph_binned.hip, k_mid_levels): records in
 // registers, routed to the workgroup owning their position's words, grid barriers.
-constexpr int kMidG = 48;
+constexpr int kMidG = 64;
 constexpr int kMidT = 1024;
 constexpr int kMidR = 8;                   // records per thread (registers)
 constexpr unsigned kMidSeg = 512;          // exchange records per (owner, sender)
 constexpr unsigned kMidStage = 6144;       // settled records staged per owner (LDS)
-constexpr unsigned long long kMidMaxKeys = 320ull << 10;  // owners average <= 6.8k of 8k slots
+constexpr unsigned long long kMidMaxKeys = 440ull << 10;  // owners average <= 6.9k of 8k slots
 constexpr uint64_t kMidW32 = 2 * ((2 * kMidMaxKeys + 63) / 64);  // u32 words of the largest mid level
 // scratch (u32 units): barrier counter [64], segment counts [kMidG][kMidG], per-owner
 // totals [kMidG] u64, then the exchange area [kMidG][kMidG][kMidSeg] Rec
