@@ -70,6 +70,13 @@ int s3imph_builder_add(s3imph_builder *b, const uint8_t *prefix, uint64_t len, u
 int s3imph_builder_add_batch(s3imph_builder *b, const uint8_t *blob, const uint64_t *offsets,
                              const uint64_t *pos, uint64_t n, char *err, size_t errlen);
 
+/* Capacity hint (no reference counterpart; the reference's IndexBuilder sizes its own
+ * arrays from NewIndexBuilderWithCapacity, indexbuild.go:72-127): the device copy of the keys
+ * is allocated once for n_keys keys of n_bytes key bytes, so Add never grows it.  Optional;
+ * exceeding it is allowed (the buffers then grow).  A device allocation failure is not an
+ * error: the build then runs from the host copy. */
+int s3imph_builder_reserve(s3imph_builder *b, uint64_t n_keys, uint64_t n_bytes, char *err, size_t errlen);
+
 /* Count() — mphf_streaming.go:100-102. */
 uint64_t s3imph_builder_count(const s3imph_builder *b);
 

@@ -380,6 +380,14 @@ uint64_t chunks0(uint64_t n) {
 // Enqueue one attempt of the binned pipeline.  `conservative` sizes every level with
 // the level-0 geometry (always inside the workspace bounds) and runs every level that
 // is still big as a full-grid level; the default predicts each level's size.
+// Profiling aid (tools/hash_only.py): with S3IMPH_HASH_ONLY set the build stops after the
+// level-0 hash so that kernel can be timed alone, and FAILS with S3IMPH_ERR_INTERNAL — the
+// outputs are not an index, and no caller may mistake the run for a build.
+bool hash_only_knob() {
+  static const bool on = std::getenv("S3IMPH_HASH_ONLY") != nullptr;
+  return on;
+}
+
 void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
   const BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
@@ -394,9 +402,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   const bool res0 = !conservative && c->res0 && T0 <= kScatterTiles && (res_fits(c, n, 64 * level_words(n), T0) || c->res0 == 2);
   launch_binned_count(0, blob, offsets, n, b, g0, gr.gc, s, !res0);  // no histogram for the reservation path
   ev_mark(c, s, "hash_count0");
-  // profiling aid (tools/hash_only.py): stop after the level-0 hash so it can be timed alone
-  static const bool hash_only = std::getenv("S3IMPH_HASH_ONLY") != nullptr;
-  if (hash_only) return;
+  if (hash_only_knob()) return;
   if (res0) {
     LevelGeom gr0 = g0;  // split-kernel level 0: tiles in whole rounds over the CUs (exact size)
     if (b.split && g0.tb > kRegTileMaxBits && g0.tb <= kSplitMaxBits) gr0.ts = choose_split_ts(64 * level_words(n), true);
@@ -555,6 +561,10 @@ int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
     HIPCHECK(hipMemcpyAsync(c->h_st, c->d_st, sizeof(LevelState), hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
     ev_collect(c);
+    if (hash_only_knob()) {
+      *msg = "build MPHF: S3IMPH_HASH_ONLY is set (profiling run: level-0 hash only, no index built)";
+      return S3IMPH_ERR_INTERNAL;
+    }
     if (c->debug) {
       const LevelState& d = *c->h_st;
       std::fprintf(stderr, "[s3imph] attempt %d: status 0x%x nlevels %u tail_first %u rank_total %llu\n  n:", attempt,
@@ -1610,6 +1620,10 @@ int s3imph_ctx_load_mph_bin(s3imph_ctx* c, const uint8_t* mph_bin, uint64_t len)
         uint64_t w = 0;
         if (!get(&w) || w > (len - at) / 8) {
           c->last_msg = "open MPHF: unmarshal: truncated level " + std::to_string(L);
+          return S3IMPH_ERR_FORMAT;
+        }
+        if (w == 0) {  // a level holds >= 1 key, so >= 1 word; 0 would make every probe index garbage
+          c->last_msg = "open MPHF: unmarshal: empty level " + std::to_string(L);
           return S3IMPH_ERR_FORMAT;
         }
         h.words[L] = w;

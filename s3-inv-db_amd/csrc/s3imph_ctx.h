@@ -62,6 +62,9 @@ struct Comm {
   // d_send + soff[q] (sbytes[q] bytes) -> rank q; rank q's bytes -> d_recv + roff[q] (rbytes[q]); host arrays
   virtual void alltoallv(const void* d_send, const uint64_t* soff, const uint64_t* sbytes, void* d_recv,
                          const uint64_t* roff, const uint64_t* rbytes, hipStream_t s) = 0;
+  // a peer failed: make every pending and future collective of this rank return (RCCL:
+  // ncclCommAbort, whose kernels then exit); the communicator is unusable afterwards
+  virtual void abort() {}
 };
 
 constexpr uint64_t kDistSwitchKeysDefault = 2ull << 20;  // levels below this run replicated
@@ -91,6 +94,10 @@ struct RcclComm final : Comm {
   ncclComm_t comm = nullptr;
   ~RcclComm() override {
     if (comm) (void)ncclCommDestroy(comm);
+  }
+  void abort() override {
+    if (comm) (void)ncclCommAbort(comm);
+    comm = nullptr;
   }
   void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
     NCCLCHECK(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, s));

@@ -276,7 +276,8 @@ __global__ __launch_bounds__(kFBT) void k_fin_blocks(const uint32_t* __restrict_
     mn = min(min(l4.x, l4.y), min(l4.z, l4.w));
     mx = max(max(d4.x, d4.y), max(d4.z, d4.w));
   } else {
-    for (uint64_t q = i; q < n; ++q) {
+    const uint64_t qe = i + 4 < n ? i + 4 : n;  // this lane's four keys only
+    for (uint64_t q = i; q < qe; ++q) {
       mn = min(mn, lcp[q]);
       mx = max(mx, depth[q]);
     }

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <string>
 #include <thread>
@@ -36,14 +37,6 @@ void put_le64(uint8_t* p, uint64_t v) {
 }
 void put_le32(uint8_t* p, uint32_t v) {
   for (int b = 0; b < 4; ++b) p[b] = (uint8_t)(v >> (8 * b));
-}
-
-// EncodeHeader (format.go:25-32): magic, version, count, width — little endian, 20 bytes.
-void s3id_header(uint8_t out[kS3idHeaderSize], uint64_t count, uint32_t width) {
-  put_le32(out, kS3idMagic);
-  put_le32(out + 4, kS3idVersion);
-  put_le64(out + 8, count);
-  put_le32(out + 16, width);
 }
 
 bool write_all(FILE* f, const void* p, size_t n) { return n == 0 || std::fwrite(p, 1, n, f) == n; }
@@ -182,6 +175,50 @@ bool is_dir(const std::string& p) {
 }
 
 }  // namespace
+
+// EncodeHeader (format.go:25-32): magic, version, count, width — little endian, 20 bytes.
+void s3id_header(uint8_t out[kS3idHeaderSize], uint64_t count, uint32_t width) {
+  put_le32(out, kS3idMagic);
+  put_le32(out + 4, kS3idVersion);
+  put_le64(out + 8, count);
+  put_le32(out + 16, width);
+}
+
+bool write_pieces(const std::string& path, size_t count,
+                  const std::function<void(size_t, const uint8_t**, uint64_t*, uint64_t*)>& piece, std::string* msg) {
+  const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+  if (fd < 0) {
+    *msg = "create " + path + ": " + std::strerror(errno);
+    return false;
+  }
+  uint64_t bytes = 0;
+  for (size_t i = 0; i < count; ++i) {
+    const uint8_t* p;
+    uint64_t n, off;
+    piece(i, &p, &n, &off);
+    bytes += n;
+  }
+  const int T = std::max(1, std::min<int>(writers_for(bytes), (int)count));
+  const bool ok = split_run(count, T, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; ++i) {
+      const uint8_t* p;
+      uint64_t n, off;
+      piece(i, &p, &n, &off);
+      if (!pwrite_all(fd, p, n, off)) return false;
+    }
+    return true;
+  });
+  if (!ok) {
+    ::close(fd);
+    *msg = "write " + path;
+    return false;
+  }
+  if (::close(fd) != 0) {
+    *msg = "close " + path;
+    return false;
+  }
+  return true;
+}
 
 // mph.bin (mphf_streaming.go:152-169; 0 bytes for the empty set, :509).  On a
 // marshal/write failure the reference removes the partial file (:159-168).
@@ -326,37 +363,21 @@ struct ArrayFileSink : FeedSink {
 using namespace s3imph;
 
 // --------------------------------------------------------------- builder mirror ----
-// Add keeps the keys in host vectors (for prefix_blob.bin / prefix_offsets.u64 and the
-// multi-GPU path) and, on a single GPU, also feeds them to the device as they arrive
-// (s3imph_feed.hip), so Build starts with the key set already in HBM.
+// Add copies each key once into the feed's pooled pinned chunks (s3imph_feed.hip): they are
+// the builder's host copy (prefix_blob.bin / prefix_offsets.u64 come straight from them) and,
+// on a single GPU, DMA to HBM as they fill, so Build starts with the key set on the device.
 struct s3imph_builder {
   int device = 0;
   std::vector<int> devices;  // s3imph_builder_set_gpus (empty: `device` alone)
   unsigned multi_flags = 0;
   std::string temp_dir;
-  std::vector<uint8_t> blob;
-  std::vector<uint64_t> offsets{0};
-  std::vector<uint64_t> pos;
+  Feed* feed = nullptr;
   uint64_t count = 0;
   bool built = false;
-  Feed* feed = nullptr;
-  bool feed_off = false;  // multi-GPU, or the feed failed once: Build copies from the host vectors
   ~s3imph_builder() { feed_free(feed); }
-  // the keys [i0, count) just appended to the host vectors, into the device feed
-  void feed_keys(uint64_t i0) {
-    if (feed_off) return;
-    std::string m;
-    if (!feed && !(feed = feed_new(device, &m))) {
-      feed_off = true;
-      return;
-    }
-    const uint64_t b0 = offsets[i0], b1 = offsets[count];
-    if (feed_append(feed, blob.data() + b0, b1 - b0, offsets.data() + i0 + 1, pos.data() + i0, count - i0, &m) !=
-        S3IMPH_OK) {
-      feed_off = true;
-      feed_free(feed);
-      feed = nullptr;
-    }
+  Feed* store() {
+    if (!feed) feed = feed_new(device, devices.empty());
+    return feed;
   }
 };
 
@@ -389,17 +410,12 @@ int s3imph_builder_add(s3imph_builder* b, const uint8_t* prefix, uint64_t len, u
     set_err(err, errlen, "add to MPHF builder: builder already built");
     return S3IMPH_ERR_STATE;
   }
-  try {
-    b->blob.insert(b->blob.end(), prefix, prefix + len);
-    b->offsets.push_back(b->blob.size());
-    b->pos.push_back(pos);
-    ++b->count;
-    b->feed_keys(b->count - 1);
-    return S3IMPH_OK;
-  } catch (const std::bad_alloc&) {
+  if (!feed_add(b->store(), prefix, len, pos)) {
     set_err(err, errlen, "write prefix: out of host memory");
     return S3IMPH_ERR_NOMEM;
   }
+  ++b->count;
+  return S3IMPH_OK;
 }
 
 int s3imph_builder_add_batch(s3imph_builder* b, const uint8_t* blob, const uint64_t* offsets,
@@ -411,27 +427,24 @@ int s3imph_builder_add_batch(s3imph_builder* b, const uint8_t* blob, const uint6
   }
   if (n == 0) return S3IMPH_OK;  // an empty batch may pass NULL blob / offsets
   if (!blob || !offsets) return S3IMPH_ERR_INVALID;
-  try {
-    const uint64_t base = offsets[0], nbytes = offsets[n] - base, shift = b->blob.size();
-    b->blob.insert(b->blob.end(), blob + base, blob + base + nbytes);
-    const size_t o0 = b->offsets.size(), p0 = b->pos.size();
-    b->offsets.resize(o0 + n);
-    b->pos.resize(p0 + n);
-    uint64_t* od = b->offsets.data() + o0;
-    uint64_t* pd = b->pos.data() + p0;
-    for (uint64_t i = 0; i < n; ++i) od[i] = offsets[i + 1] - base + shift;
-    if (pos) {
-      std::memcpy(pd, pos, n * 8);
-    } else {
-      for (uint64_t i = 0; i < n; ++i) pd[i] = b->count + i;
-    }
-    b->count += n;
-    b->feed_keys(b->count - n);
-    return S3IMPH_OK;
-  } catch (const std::bad_alloc&) {
+  if (!feed_add_batch(b->store(), blob, offsets, pos, n)) {
     set_err(err, errlen, "write prefix: out of host memory");
     return S3IMPH_ERR_NOMEM;
   }
+  b->count += n;
+  return S3IMPH_OK;
+}
+
+int s3imph_builder_reserve(s3imph_builder* b, uint64_t n_keys, uint64_t n_bytes, char* err, size_t errlen) {
+  if (!b) return S3IMPH_ERR_INVALID;
+  if (b->built) {
+    set_err(err, errlen, "reserve MPHF builder: builder already built");
+    return S3IMPH_ERR_STATE;
+  }
+  std::string msg;
+  const int rc = feed_reserve(b->store(), n_keys, n_bytes, &msg);
+  if (rc != S3IMPH_OK) set_err(err, errlen, msg);  // not fatal: Build falls back to the host path
+  return S3IMPH_OK;
 }
 
 uint64_t s3imph_builder_count(const s3imph_builder* b) { return b ? b->count : 0; }
@@ -450,20 +463,24 @@ int s3imph_builder_build(s3imph_builder* b, const char* out_dir, char* err, size
   std::string msg;
   try {
     const uint64_t n = b->count;
-    if (n && b->feed && !b->feed_off && b->devices.empty() && feed_count(b->feed) == n) {
-      // the keys are on the device already: the prefix files are written meanwhile (they
-      // do not depend on the build), the arrays as their chunks come back
-      std::string pmsg;
+    Feed* f = b->store();
+    if (n) feed_flush(f);
+    if (n && b->devices.empty() && feed_on_device(f)) {
+      // the keys are on the device already.  Once the build has succeeded (a failed
+      // bbhash.New writes nothing, mphf_streaming.go:141-144) the prefix files are written
+      // from the host chunks on one thread while the arrays are written as their chunks
+      // come back on two others
+      std::string pmsg, amsg;
       int prc = S3IMPH_OK;
-      std::thread tp([&] { prc = write_prefix_files(dir, b->blob.data(), b->offsets.data(), n, &pmsg); });
+      std::thread tp;
+      std::unique_ptr<ArrayFileSink> sink;
       std::vector<uint8_t> mph;
-      int rc;
-      std::string amsg;
-      {
-        ArrayFileSink sink(dir, n);
-        rc = feed_build(b->feed, &mph, &sink, &msg);
-        amsg = sink.finish();
-      }
+      int rc = feed_build(f, &mph, [&]() -> FeedSink* {
+        tp = std::thread([&] { prc = feed_write_prefix_files(f, dir, &pmsg); });
+        sink.reset(new ArrayFileSink(dir, n));
+        return sink.get();
+      }, &msg);
+      if (sink) amsg = sink->finish();
       if (rc == S3IMPH_OK) {
         rc = write_mph_file(dir, mph.data(), mph.size(), &msg);
         if (rc == S3IMPH_OK && !amsg.empty()) {
@@ -471,7 +488,7 @@ int s3imph_builder_build(s3imph_builder* b, const char* out_dir, char* err, size
           msg = amsg;
         }
       }
-      tp.join();
+      if (tp.joinable()) tp.join();
       if (rc == S3IMPH_OK && prc != S3IMPH_OK) {
         rc = prc;
         msg = pmsg;
@@ -481,25 +498,28 @@ int s3imph_builder_build(s3imph_builder* b, const char* out_dir, char* err, size
         return rc;
       }
       b->built = true;
-      feed_free(b->feed);  // the device copy is no longer needed
-      b->feed = nullptr;
+      feed_drop_device(f);  // the device copy is no longer needed
       return S3IMPH_OK;
     }
+    // host path: several GPUs, or the device feed is off (it failed, or there is no GPU)
+    std::vector<uint8_t> blob;
+    std::vector<uint64_t> offsets, pos;
+    feed_materialize(f, &blob, &offsets, &pos);
     std::vector<uint64_t> fp(n), pos_out(n);
     std::vector<uint8_t> mph;
     if (n) {
       int rc = b->devices.empty()
-                   ? build_from_host(b->device, b->blob.data(), b->offsets.data(), b->pos.data(), n, fp.data(),
-                                     pos_out.data(), &mph, &msg)
-                   : build_from_host_multi(b->devices, b->multi_flags, b->blob.data(), b->offsets.data(),
-                                           b->pos.data(), n, fp.data(), pos_out.data(), &mph, &msg);
+                   ? build_from_host(b->device, blob.data(), offsets.data(), pos.data(), n, fp.data(), pos_out.data(),
+                                     &mph, &msg)
+                   : build_from_host_multi(b->devices, b->multi_flags, blob.data(), offsets.data(), pos.data(), n,
+                                           fp.data(), pos_out.data(), &mph, &msg);
       if (rc != S3IMPH_OK) {
         set_err(err, errlen, msg);
         return rc;
       }
     }
-    int rc = write_index_files(dir, mph.data(), mph.size(), fp.data(), pos_out.data(), n, b->blob.data(),
-                               b->offsets.data(), &msg);
+    int rc = write_index_files(dir, mph.data(), mph.size(), fp.data(), pos_out.data(), n, blob.data(),
+                               offsets.data(), &msg);
     if (rc != S3IMPH_OK) {
       set_err(err, errlen, msg);
       return rc;
@@ -518,9 +538,7 @@ int s3imph_builder_set_gpus(s3imph_builder* b, int num_gpus, const int* devices,
   b->devices.resize(num_gpus);
   for (int r = 0; r < num_gpus; ++r) b->devices[r] = devices ? devices[r] : r;
   b->multi_flags = flags;
-  b->feed_off = true;  // the multi-GPU build shards from the host vectors
-  feed_free(b->feed);
-  b->feed = nullptr;
+  if (b->feed) feed_drop_device(b->feed);  // the multi-GPU build shards from the host chunks
   return S3IMPH_OK;
 }
 
@@ -549,12 +567,13 @@ int s3imph_write_index_files(const char* out_dir, const uint8_t* mph_bin, uint64
 // aggregator.go:48); g >= 1 -> 9 lowercase hex digits of g-1, '/', then pseudo-random
 // [a-z0-5] segments separated by '/' every 12 bytes, ending in '/'.  The fixed-width hex
 // head makes the sequence byte-sorted and distinct by construction.
-// kind 1 (C5): g == 0 -> ""; g >= 1 -> a length L drawn log-uniform on [1, 1024], raised
-// to the base-64 digit count of g-1 where that is longer (so short keys stay distinct:
-// 64^4 = 16.7M keys fit in 4 bytes, 64^5 in 5).  Keys of <= 11 bytes are g-1 in exactly
-// L base-64 digits; longer keys start with g-1 in 11 digits and continue as kind 0's
-// segments.  Equal lengths therefore mean distinct digit strings: distinct by
-// construction, not byte-sorted.
+// kind 1 (C5): g == 0 -> ""; g >= 1 -> an order-preserving head of j = g-1 over the
+// ASCII-sorted 64-symbol alphabet kSorted64 — 5 digits while j < 63·64^4 (1.06e9; the top
+// digit stays below the last symbol), beyond that the last symbol and 6 more digits — then
+// kind 0's segments up to a length L drawn log-uniform on [1, 1024] (raised to the head's
+// width where it is shorter: 200M distinct keys cannot be 23 % of <= 4 bytes).  The heads are
+// prefix-free and ordered like j, so the sequence is byte-sorted (types.go:160-164) and
+// distinct by construction, and key g does not depend on the shard that generates it.
 static inline uint64_t splitmix64(uint64_t x) {
   x += 0x9e3779b97f4a7c15ull;
   x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -562,14 +581,10 @@ static inline uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-static const char kB64[] = "0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ-_";
-constexpr uint32_t kHeadDigits = 11;  // 64^11 = 2^66 > any index
+static const char kSorted64[] = "-0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ_abcdefghijklmnopqrstuvwxyz";
+constexpr uint64_t kShortHeads = 63ull << 24;  // j below this: 5-digit head (top digit <= 62)
 
-static uint32_t b64_digits(uint64_t j) {
-  uint32_t d = 1;
-  while (d < kHeadDigits && (j >> (6 * d)) != 0) ++d;
-  return d;
-}
+static uint32_t head_len(uint64_t j) { return j < kShortHeads ? 5 : 7; }
 
 static uint32_t gen_len(int kind, uint64_t seed, uint32_t avg, uint64_t g) {
   if (g == 0) return 0;
@@ -578,7 +593,7 @@ static uint32_t gen_len(int kind, uint64_t seed, uint32_t avg, uint64_t g) {
     const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);  // [0, 1)
     uint32_t L = (uint32_t)std::floor(std::exp(u * std::log(1025.0)));
     L = std::min<uint32_t>(std::max<uint32_t>(L, 1), 1024);
-    return std::max(L, b64_digits(g - 1));
+    return std::max(L, head_len(g - 1));
   }
   uint32_t lo = std::max<uint32_t>(10, avg / 2), hi = std::max<uint32_t>(lo, avg + avg / 2);
   return lo + (uint32_t)(r % (uint64_t)(hi - lo + 1));
@@ -611,12 +626,14 @@ static void gen_fill(int kind, uint64_t seed, uint64_t g, uint32_t L, uint8_t* o
   if (L == 0) return;
   const uint64_t j = g - 1;
   if (kind == 1) {
-    const uint32_t d = std::min(L, kHeadDigits);
-    for (uint32_t i = 0; i < d; ++i) {
-      const uint32_t sh = 6 * (d - 1 - i);
-      out[i] = (uint8_t)kB64[sh < 64 ? (j >> sh) & 63 : 0];
+    const uint32_t h = head_len(j);
+    const uint64_t v = j < kShortHeads ? j : j - kShortHeads;
+    if (h == 7) out[0] = (uint8_t)kSorted64[63];
+    for (uint32_t i = 0; i < 5 + (h == 7); ++i) {  // the digits, most significant first
+      const uint32_t sh = 6 * (4 + (h == 7) - i);
+      out[h - 5 - (h == 7) + i] = (uint8_t)kSorted64[(v >> sh) & 63];
     }
-    if (L > kHeadDigits) gen_segments(seed, g, kHeadDigits, L, out);
+    if (L > h) gen_segments(seed, g, h, L, out);
     return;
   }
   for (int d = 0; d < 9; ++d) out[d] = (uint8_t)kHex[(j >> (4 * (8 - d))) & 0xf];

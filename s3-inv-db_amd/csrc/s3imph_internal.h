@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -277,26 +278,40 @@ int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const ui
                           const uint64_t* pos, uint64_t n, uint64_t* fp_out, uint64_t* pos_out,
                           std::vector<uint8_t>* mph, std::string* msg);
 
-// ---- the builder mirror's feed (s3imph_feed.hip) ------------------------------------
-// Keys appended by Add go through pinned chunks to device arrays as they arrive; Build
-// runs on those and streams mph_fp (array 0) / mph_pos (array 1) to a sink chunk by
-// chunk, one thread per array.
+// ---- the builder mirror's key store and feed (s3imph_feed.hip) ----------------------
+// Keys appended by Add are copied once into pooled pinned chunks (the builder's host copy)
+// and DMA'd to device arrays chunk by chunk; Build runs on those, then streams mph_fp
+// (array 0) / mph_pos (array 1) to a sink chunk by chunk, one thread per array.
 struct FeedSink {
   virtual ~FeedSink() = default;
   virtual bool put(int arr, const uint64_t* v, uint64_t cnt) = 0;  // false: stop taking data
   virtual std::string error() const = 0;
 };
 struct Feed;
-Feed* feed_new(int device, std::string* msg);
+Feed* feed_new(int device, bool use_gpu);  // use_gpu false: host chunks only (multi-GPU, no GPU)
 void feed_free(Feed* f);
-// n keys: their bytes, their end offsets in the builder's blob, their positions
-int feed_append(Feed* f, const uint8_t* bytes, uint64_t nbytes, const uint64_t* ends, const uint64_t* pos, uint64_t n,
-                std::string* msg);
+void feed_drop_device(Feed* f);  // stop feeding the device (the host copy stays)
+int feed_reserve(Feed* f, uint64_t n_keys, uint64_t n_bytes, std::string* msg);
+bool feed_add(Feed* f, const uint8_t* key, uint64_t len, uint64_t pos);  // false: out of host memory
+// n keys of the caller's blob (offsets[0..n], any base); pos NULL -> count, count+1, ...
+bool feed_add_batch(Feed* f, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t n);
 uint64_t feed_count(const Feed* f);
-int feed_build(Feed* f, std::vector<uint8_t>* mph, FeedSink* sink, std::string* msg);
+void feed_flush(Feed* f);              // enqueue the partial chunks (may turn the device path off)
+bool feed_on_device(const Feed* f);
+// contiguous copies (offsets N+1 from 0; blob padded to whole words + 16 B) for the host builds
+void feed_materialize(const Feed* f, std::vector<uint8_t>* blob, std::vector<uint64_t>* offsets,
+                      std::vector<uint64_t>* pos);
+int feed_write_prefix_files(const Feed* f, const std::string& dir, std::string* msg);
+// the single-GPU build on the fed arrays; open_sink() is called only once the build succeeded
+int feed_build(Feed* f, std::vector<uint8_t>* mph, const std::function<FeedSink*()>& open_sink, std::string* msg);
 
 // ---- host helpers (s3imph_host.cpp) -------------------------------------------
 void set_err(char* err, size_t errlen, const std::string& msg);
+void s3id_header(uint8_t out[kS3idHeaderSize], uint64_t count, uint32_t width);  // format.go:25-32
+// a file made of `count` pieces, piece(i, &p, &n, &off) giving bytes p[0..n) at file offset
+// off; the pieces are pwrite()-n by up to 8 threads
+bool write_pieces(const std::string& path, size_t count,
+                  const std::function<void(size_t, const uint8_t**, uint64_t*, uint64_t*)>& piece, std::string* msg);
 int write_index_files(const std::string& dir, const uint8_t* mph_bin, uint64_t mph_len,
                       const uint64_t* fp, const uint64_t* pos, uint64_t n, const uint8_t* blob,
                       const uint64_t* offsets, std::string* msg);

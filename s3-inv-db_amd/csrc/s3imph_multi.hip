@@ -141,10 +141,24 @@ struct MultiCtx {
   std::vector<s3imph_ctx*> ctx;
   std::unique_ptr<ThreadHub> hub;
   std::mutex mu;
+  std::mutex abort_mu;
+  bool aborted = false;  // a rank failed alone: the transport was torn down, the set is dropped
+  // Unblock every rank: the host hub wakes its barrier waiters with an error; RCCL
+  // communicators are aborted (their pending kernels exit, so peers blocked in a stream
+  // sync return) and cannot be reused.
+  void abort_all() {
+    std::lock_guard<std::mutex> lk(abort_mu);
+    if (aborted) return;
+    aborted = true;
+    if (hub) hub->abort();
+    for (s3imph_ctx* c : ctx)
+      if (c->d.comm) c->d.comm->abort();
+  }
 };
 
 std::mutex g_multi_mu;
 std::map<std::tuple<std::vector<int>, bool, uint64_t>, std::unique_ptr<MultiCtx>> g_multi;
+std::vector<std::unique_ptr<MultiCtx>> g_retired;  // aborted sets (see build_from_host_multi)
 
 MultiCtx* multi_ctx(const std::vector<int>& devs, bool host_transport, std::string* msg) {
   uint64_t sw = kDistSwitchKeysDefault;  // contexts read S3IMPH_DIST_SWITCH when made
@@ -292,8 +306,18 @@ int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const ui
     MultiCtx* mc = multi_ctx(devs, repeated || (flags & S3IMPH_MULTI_HOST_TRANSPORT), msg);
     if (!mc) return S3IMPH_ERR_RCCL;
     std::lock_guard<std::mutex> lk(mc->mu);
+    if (mc->aborted) {
+      *msg = "build MPHF: the multi-GPU set was torn down by a failed build; call again";
+      return S3IMPH_ERR_RCCL;
+    }
     if (mc->hub) mc->hub->reset();
     const std::vector<uint64_t> cuts = byte_cuts(offsets, n, P);
+    // argument checks every rank would make alone, made here so that all ranks fail together
+    for (int r = 0; r < P; ++r)
+      if (cuts[r + 1] - cuts[r] > 0xffffffffull) {
+        *msg = "build MPHF: more than 2^32-1 keys on one rank";
+        return S3IMPH_ERR_INVALID;
+      }
     std::vector<int> rcs(P, S3IMPH_OK);
     std::vector<std::string> msgs(P);
     auto work = [&](int r) {
@@ -302,17 +326,40 @@ int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const ui
       } catch (const Fail& f) {
         rcs[r] = f.code;
         msgs[r] = f.msg;
-        if (mc->hub) mc->hub->abort();
       } catch (const std::bad_alloc&) {
         rcs[r] = S3IMPH_ERR_NOMEM;
         msgs[r] = "out of host memory";
-        if (mc->hub) mc->hub->abort();
       }
+      // Key-set failures (duplicate or zero key hashes, too many levels) are decided from
+      // all-reduced counts, so every rank returns them at the same point.  Anything else
+      // (HIP / RCCL errors, allocation failures, internal checks) may leave the peers inside
+      // a collective: tear the transport down so that they return too.
+      const int rc = rcs[r];
+      if (rc != S3IMPH_OK && rc != S3IMPH_ERR_DUP_KEY_HASH && rc != S3IMPH_ERR_KEY_HASH_ZERO &&
+          rc != S3IMPH_ERR_TOO_MANY_LEVELS)
+        mc->abort_all();
     };
     std::vector<std::thread> th;
     for (int r = 1; r < P; ++r) th.emplace_back(work, r);
     work(0);
     for (auto& t : th) t.join();
+    if (mc->aborted) {
+      // the communicators are gone: retire this set (the next build makes a fresh one).  It
+      // stays allocated, empty and marked aborted, for any caller already waiting on its mutex.
+      for (s3imph_ctx* c : mc->ctx) {
+        (void)hipSetDevice(c->device);
+        (void)hipDeviceSynchronize();
+      }
+      for (s3imph_ctx* c : mc->ctx) s3imph_ctx_destroy(c);
+      mc->ctx.clear();
+      std::lock_guard<std::mutex> glk(g_multi_mu);
+      for (auto it = g_multi.begin(); it != g_multi.end(); ++it)
+        if (it->second.get() == mc) {
+          g_retired.push_back(std::move(it->second));
+          g_multi.erase(it);
+          break;
+        }
+    }
     // every rank takes the same branches (decisions use global counts), so a build error
     // shows on every rank; report the first rank's, or the first transport failure
     for (int r = 0; r < P; ++r)

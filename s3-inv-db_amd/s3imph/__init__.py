@@ -52,7 +52,7 @@ MULTI_HOST_TRANSPORT = 2  # in-process host-copy collectives instead of RCCL
 EXPORTS = (
     "s3imph_abi_version", "s3imph_status_string",
     "s3imph_builder_new", "s3imph_builder_add", "s3imph_builder_add_batch", "s3imph_builder_count",
-    "s3imph_builder_build", "s3imph_builder_close",
+    "s3imph_builder_build", "s3imph_builder_close", "s3imph_builder_reserve",
     "s3imph_build_host", "s3imph_build_host_multi", "s3imph_builder_set_gpus", "s3imph_free",
     "s3imph_write_index_files",
     "s3imph_ctx_create", "s3imph_ctx_destroy", "s3imph_ctx_reserve", "s3imph_build_device",
@@ -112,6 +112,7 @@ def _load():
         "s3imph_builder_add": (i32, [vp, cp, u64, u64, cp, sz]),
         "s3imph_builder_add_batch": (i32, [vp, vp, vp, vp, u64, cp, sz]),
         "s3imph_builder_count": (u64, [vp]),
+        "s3imph_builder_reserve": (i32, [vp, u64, u64, cp, sz]),
         "s3imph_builder_build": (i32, [vp, cp, cp, sz]),
         "s3imph_builder_close": (i32, [vp]),
         "s3imph_build_host": (i32, [i32, vp, vp, vp, u64, vp, vp, P(vp), P(u64), cp, sz]),
@@ -215,6 +216,11 @@ class StreamingMPHFBuilder:
 
     def count(self) -> int:
         return LIB.s3imph_builder_count(self._h)
+
+    def reserve(self, n_keys: int, n_bytes: int) -> None:
+        """Capacity hint: the device copy of the keys is allocated once (s3imph_builder_reserve)."""
+        err = ctypes.create_string_buffer(256)
+        _check(LIB.s3imph_builder_reserve(self._h, n_keys, n_bytes, err, 256), err)
 
     def set_gpus(self, num_gpus: int, devices=None, flags: int = 0) -> None:
         """Build on `num_gpus` GPUs (s3imph_builder_set_gpus; see build_host)."""
@@ -486,8 +492,9 @@ class MPHF:
             if len(fp) != len(pos):
                 raise MPHFError(ERR_FORMAT, "open MPHF: fingerprint and position arrays differ in length")
             self.count = len(fp)
-            self.d_fp = torch.from_numpy(np.ascontiguousarray(fp).view(np.int64)).to(self.dev)
-            self.d_pos = torch.from_numpy(np.ascontiguousarray(pos).view(np.int64)).to(self.dev)
+            # read_u64_array may hand back a read-only view of the file: copy before torch takes it
+            self.d_fp = torch.from_numpy(np.array(fp, dtype=np.uint64).view(np.int64)).to(self.dev)
+            self.d_pos = torch.from_numpy(np.array(pos, dtype=np.uint64).view(np.int64)).to(self.dev)
         else:
             self.d_fp = self.d_pos = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.ctx.load_mph_bin(mph)

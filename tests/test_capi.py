@@ -131,15 +131,21 @@ def test_generator_sorted_distinct_and_shardable():
     b2, o2 = s3imph.gen_keys(0, 42, 32, 12345, 100)
     for i in range(100):
         assert bytes(b2[o2[i]:o2[i + 1]]) == keys[12345 + i]
-    # C5's kind 1: lengths log-uniform on [1, 1024] (raised to the digits a distinct key
-    # needs), distinct, reproducible by shard
+    # C5's kind 1: lengths log-uniform on [1, 1024] (raised to the 5-byte head a distinct
+    # sorted key needs), byte-sorted, distinct, reproducible by shard
     b3, o3 = s3imph.gen_keys(1, 42, 0, 0, 20000)
     l3 = np.diff(o3.astype(np.int64))[1:]
-    assert l3.min() == 1 and l3.max() == 1024 and 130 < l3.mean() < 170
+    assert l3.min() == 5 and l3.max() == 1024 and 130 < l3.mean() < 170
+    assert (l3 == 5).mean() > 0.2  # the log-uniform mass below 5 bytes lands on the head width
     k3 = [bytes(b3[o3[i]:o3[i + 1]]) for i in range(20000)]
-    assert len(set(k3)) == 20000
+    assert k3 == sorted(k3) and len(set(k3)) == 20000
     b4, o4 = s3imph.gen_keys(1, 42, 0, 777, 50)
     assert [bytes(b4[o4[i]:o4[i + 1]]) for i in range(50)] == k3[777:827]
+    # around the switch from 5- to 7-byte heads (j = 63 * 64^4) and at 200M (C5's size)
+    for lo in (63 * 64 ** 4 - 40, 200_000_000 - 100):
+        b5, o5 = s3imph.gen_keys(1, 42, 0, lo, 80)
+        k5 = [bytes(b5[o5[i]:o5[i + 1]]) for i in range(80)]
+        assert k5 == sorted(k5) and len(set(k5)) == 80
     assert hashlib.sha256(blob[: offs[-1]].tobytes()).hexdigest() == \
         hashlib.sha256(s3imph.gen_keys(0, 42, 32, 0, 50000)[0][: offs[-1]].tobytes()).hexdigest()
 

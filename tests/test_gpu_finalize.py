@@ -114,6 +114,30 @@ def test_c2_synthetic_and_custom_depths(s3, ctx, oracle_lib):
     _same(_device(ctx, blob, offs, depths), oracle_lib.finalize(blob, offs, depths))
 
 
+@pytest.mark.parametrize("n_obj", [3000, 300_000])
+def test_unaligned_caller_depths(s3, ctx, oracle_lib, n_obj):
+    """Caller depths (row.Depth) handed over as a view at a 4-byte offset: the block pass
+    takes its per-lane fallback for every lane, and each lane must cover its own four keys
+    only (subtrees crossing 1024-key blocks, the maximum depth below each node)."""
+    import torch
+    keys = _prefix_set(7, n_obj, 8, 7, True)
+    blob, offs = O.keys_to_blob(keys)
+    n = len(keys)
+    depths = np.array([k.count(b"/") for k in keys], np.uint32)
+    buf = torch.zeros(n + 4, dtype=torch.int32, device="cuda")
+    buf[1:n + 1] = torch.from_numpy(depths.view(np.int32)).cuda()
+    view = buf[1:n + 1]
+    assert view.data_ptr() % 16 == 4
+    r = ctx.finalize_index(to_dev(blob, pad8=True), to_dev(offs), n, view)
+    torch.cuda.synchronize()
+    got = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in r.items()}
+    for k in ("depth", "max_depth_in_subtree"):
+        got[k] = got[k].view(np.uint32)
+    for k in ("subtree_end", "depth_positions", "depth_offsets"):
+        got[k] = got[k].view(np.uint64)
+    _same(got, oracle_lib.finalize(blob, offs, depths))
+
+
 def test_empty_and_single(s3, ctx, oracle_lib, tmp_path):
     blob, offs = O.keys_to_blob([])
     s3.finalize_index_host(blob, offs, str(tmp_path))

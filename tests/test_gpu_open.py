@@ -76,7 +76,10 @@ def test_empty_and_malformed(s3, tmp_path):
     m.close()
     ctx = s3.DeviceBuilder(0)
     good = O.lib().build(*O.keys_to_blob([b"a/", b"b/", b"c/"]))[3]
-    for bad in (good[:-1], good + b"\0", b"\2" + good[1:], good[:8]):
+    import struct
+    zero_word_level = struct.pack("<QQQQQ", 1, 2, 1, 0b111, 0)  # level 1 claims 0 words
+    zero_first = struct.pack("<QQQQQ", 1, 2, 0, 1, 0b111)       # level 0 claims 0 words
+    for bad in (good[:-1], good + b"\0", b"\2" + good[1:], good[:8], zero_word_level, zero_first):
         with pytest.raises(s3.MPHFError) as e:
             ctx.load_mph_bin(bad)
         assert e.value.status == s3.ERR_FORMAT

@@ -102,11 +102,12 @@ def test_builder_writes_identical_files(s3, oracle_lib, tmp_path):
 
 
 def test_builder_feed_many_chunks(s3, oracle_lib, tmp_path):
-    """f3 + f2: Add streams the keys to the GPU through 8 MiB pinned chunks while the caller
-    is still adding (2.5M keys, ~80 MB of blob: past the feed's first 64 MiB device
-    buffer, so it grows), in batches of 100k with custom positions, then single Adds;
-    Build writes mph_fp / mph_pos as their chunks come back and the prefix files beside
-    the build.  The 5 files equal the oracle's."""
+    """f3 + f2: Add copies the keys once into pooled pinned chunks (256 KiB doubling to
+    64 MiB) that DMA to the GPU while the caller is still adding (2.5M keys, ~80 MB of blob:
+    past the feed's first 16 MiB device buffers, so they grow), in batches of 100k with
+    custom positions, then single Adds; Build writes mph_fp / mph_pos as their chunks come
+    back and the prefix files from the host chunks beside them.  The 5 files equal the
+    oracle's."""
     n = 2_500_000
     blob, offs = s3.gen_keys(0, 21, 32, 0, n)
     blob = blob[: int(offs[-1])]
@@ -131,6 +132,40 @@ def test_builder_feed_many_chunks(s3, oracle_lib, tmp_path):
         assert (out / name).read_bytes() == data, name
 
 
+@pytest.mark.parametrize("hint", ["exact", "short", "none"])
+def test_builder_reserve_hint(s3, oracle_lib, tmp_path, hint):
+    """The capacity hint (s3imph_builder_reserve): exact (device arrays allocated once), too
+    short (they grow past it), none; batches with identity positions (pos NULL ->
+    Count()+i) between single Adds.  The 5 files equal the oracle's."""
+    n = 1_200_000
+    blob, offs = s3.gen_keys(0, 23, 40, 0, n)
+    blob = blob[: int(offs[-1])]
+    b = s3.StreamingMPHFBuilder(str(tmp_path))
+    if hint == "exact":
+        b.reserve(n, int(offs[-1]))
+    elif hint == "short":
+        b.reserve(n // 10, int(offs[-1]) // 10)
+    i = 0
+    for lo, hi in ((0, 3), (3, 500_003), (500_003, 500_010), (500_010, n)):
+        if hi - lo < 10:
+            for k in range(lo, hi):
+                b.add(bytes(blob[offs[k]:offs[k + 1]]), k)
+        else:
+            b.add_batch(blob, offs[lo:hi + 1])
+        i = hi
+    assert b.count() == n == i
+    out = tmp_path / "idx"
+    out.mkdir()
+    b.build(str(out))
+    b.close()
+    st, fp, po, mph = oracle_lib.build_mt(blob, offs, threads=16)
+    assert st == 0
+    want = {"mph.bin": mph, "mph_fp.u64": O.s3id_u64_array(fp), "mph_pos.u64": O.s3id_u64_array(po),
+            "prefix_blob.bin": blob.tobytes(), "prefix_offsets.u64": O.s3id_u64_array(offs)}
+    for name, data in want.items():
+        assert (out / name).read_bytes() == data, name
+
+
 def test_builder_feed_duplicate_keys_error(s3, tmp_path):
     """A duplicate key fed through the device feed fails Build with the duplicate-hash
     status; no half-written success is reported."""
@@ -144,6 +179,9 @@ def test_builder_feed_duplicate_keys_error(s3, tmp_path):
     with pytest.raises(s3.MPHFError) as e:
         b.build(str(out))
     assert e.value.status == s3.ERR_DUP_KEY_HASH
+    # the reference's Build fails in bbhash.New before it writes any file
+    # (mphf_streaming.go:141-144): out_dir stays empty
+    assert list(out.iterdir()) == []
     b.close()
 
 
