@@ -118,6 +118,7 @@ void s3imph_free(void *p);
  * s3imph_build_host.  Outputs equal s3imph_build_host's byte for byte. */
 #define S3IMPH_MULTI_FORCE_SHARDED 1u   /* the sharded (multi-GPU) build even for one GPU */
 #define S3IMPH_MULTI_HOST_TRANSPORT 2u  /* host-copy collectives instead of RCCL */
+#define S3IMPH_MULTI_BITMAP 4u          /* the bitmap decomposition (s3imph_ctx_set_dist_mode) */
 int s3imph_build_host_multi(int num_gpus, const int *devices, unsigned flags, const uint8_t *blob,
                             const uint64_t *offsets, const uint64_t *pos, uint64_t n, uint64_t *fp_out,
                             uint64_t *pos_out, uint8_t **mph_bin, uint64_t *mph_len, char *err, size_t errlen);
@@ -205,6 +206,21 @@ typedef struct s3imph_host_comm {
 
 int s3imph_ctx_create_dist_host(int device, const s3imph_host_comm *comm, int rank, int nranks,
                                 s3imph_ctx **out, char *err, size_t errlen);
+
+/* Decomposition of the sharded levels (every rank of a build must choose the same; the
+ * default comes from S3IMPH_DIST_MODE=route|bitmap, else route):
+ *   S3IMPH_DIST_ROUTE  — position-range ownership: each level's 24-byte records are routed
+ *                        to the rank owning their position range (one all-to-all per level);
+ *   S3IMPH_DIST_BITMAP — the per-level collision bitmap reduced over RCCL: count lanes
+ *                        (min(local count, 2), one byte per position) reduce-scattered, the
+ *                        final bits all-gathered, each rank settles its own keys; one
+ *                        all-to-all of the settled (p, fp, pos) at the end.  A level larger
+ *                        than its host-side bound reruns the build on ROUTE.
+ * Both give byte-identical outputs.  No reference counterpart (bbhash.New runs on one
+ * thread, mphf_streaming.go:141). */
+#define S3IMPH_DIST_ROUTE 0
+#define S3IMPH_DIST_BITMAP 1
+int s3imph_ctx_set_dist_mode(s3imph_ctx *ctx, int mode);
 
 /* This rank holds keys [key_base, key_base + n_local) of the global set (the
  * shard's blob/offsets/pos, offsets relative to d_blob; d_pos NULL => pos_i =

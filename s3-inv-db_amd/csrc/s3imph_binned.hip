@@ -551,6 +551,194 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   if (RT && tid == 0 && r_over) atomicOr(&st->status, kStRouteOverflow);
 }
 
+// ------------------------------------------- level-0 hash, skewed key lengths --------
+// FNV-1a + FNV-1 of every key (mphf.go:349-369) for sets whose sampled lengths are skewed
+// (st->skew: C5's log-uniform 1-1024 B).  FNV is one dependent multiply chain per byte, so
+// one lane hashes one key, and a wave runs as long as its longest lane: the wave's 64 keys
+// must have (nearly) one length.  A block takes its contiguous key range in groups of kSkG
+// keys; each group is counting-sorted by length (4-byte classes) in LDS and cut into
+// batches of 64 consecutive sorted keys, which the block's waves take longest first from
+// an LDS ticket (LPT: the last batches to start are the shortest, so the waves reach the
+// group's barrier together).  A batch's key bytes are staged through a wave-private LDS
+// buffer kSkC bytes per key at a time: lanes 4m..4m+3 of load t fetch the 16-byte units of
+// key 16t+m's next chunk (one contiguous 64-byte run per key, issued while the previous
+// chunk is hashed), so every key's bytes cross HBM / L2 once in whole segments instead of
+// one lane's 16-byte stream per key (k_hash_count0: ~0.30 of the FNV ceiling on C5, its L1
+// thrashed by 1024 interleaved streams).  Each lane then hashes its key's bytes of the
+// chunk from LDS with the funnel step of fnv_window.  Results go to LDS by key and leave
+// in key order with coalesced stores.  (Simulated over C5's lengths: 95 % of lane-steps do
+// work with 4096-key groups, 82 % with 1024.)
+constexpr int kSkT = 1024;             // threads (16 waves, one block per CU)
+constexpr int kSkG = 4096;             // keys per sorted group
+constexpr int kSkC = 64;               // chunk bytes per key per step
+constexpr int kSkS = kSkC + 16;        // LDS stride per key (16-B aligned for ds_write_b128)
+constexpr int kSkU = kSkC / 16;        // 16-byte units per key chunk = loads per step
+constexpr unsigned kSkLB = 256;        // length classes (4 B each)
+constexpr size_t kSkStage = (size_t)(kSkT / 64) * 64 * kSkS;
+constexpr size_t kSkLds = kSkStage + 2 * kSkG * sizeof(uint64_t) + kSkG * sizeof(unsigned short) +
+                          kSkLB * sizeof(unsigned) + 16;
+static_assert(kSkLds <= 160 * 1024, "k_hash_skew's LDS");
+static_assert(kSkU * 16 == 64, "a load instruction covers 16 keys x 64 B");
+
+__global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict__ blob,
+                                                       const uint64_t* __restrict__ offsets, uint64_t n,
+                                                       uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
+                                                       unsigned long long* __restrict__ flags,
+                                                       unsigned long long* __restrict__ sflags, LevelState* st,
+                                                       unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
+  extern __shared__ __align__(16) unsigned char sk_lds[];
+  if (!st->skew) return;  // k_hash0_pair hashed this near-uniform set
+  uint4* stage = reinterpret_cast<uint4*>(sk_lds);
+  uint64_t* res_a = reinterpret_cast<uint64_t*>(sk_lds + kSkStage);
+  uint64_t* res_b = res_a + kSkG;
+  unsigned short* sidx = reinterpret_cast<unsigned short*>(res_b + kSkG);
+  unsigned* cnt = reinterpret_cast<unsigned*>(sidx + kSkG);
+  unsigned* next = cnt + kSkLB;
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  {  // the level-0 tile state the reservation path starts from (as k_hash0_pair)
+    const uint64_t T = ntiles_of(st->words[0], tb), B = (n + chunk - 1) / chunk;
+    const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
+    const uint64_t g0 = (uint64_t)blockIdx.x * kSkT + tid, gs = (uint64_t)gridDim.x * kSkT;
+    if (blockIdx.x == 0 && tid == 0) {
+      st->ntiles[0] = T;
+      st->nchunks[0] = B;
+    }
+    for (uint64_t t = g0; t < T; t += gs) flags[t] = 0;
+    for (uint64_t q = g0; q < nseg; q += gs) sflags[q] = 0;
+    for (uint64_t q = g0; q < kTcntWords; q += gs) tcnt[q] = 0;
+  }
+  const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const uint64_t gbeg = min(n, (uint64_t)blockIdx.x * per), gend = min(n, gbeg + per);
+  const uint64_t end8 = (offsets[n] + 7) & ~7ull;
+  uint4* wst = stage + (size_t)wave * 64 * (kSkS / 16);  // this wave's 64 key regions
+  const uint32_t* wst32 = reinterpret_cast<const uint32_t*>(wst);
+  bool zero = false;
+  constexpr int KPT = kSkG / kSkT;  // keys per thread in the sort
+  for (uint64_t grp = gbeg; grp < gend; grp += kSkG) {
+    const unsigned m = (unsigned)min<uint64_t>(kSkG, gend - grp);
+    // ---- counting sort of the group's keys by length (ascending)
+    for (unsigned c = tid; c < kSkLB; c += kSkT) cnt[c] = 0;
+    if (tid == 0) *next = 0;
+    __syncthreads();
+    unsigned cls[KPT], rk[KPT];
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+      const unsigned k = tid + (unsigned)q * kSkT;
+      if (k < m) {
+        const uint64_t len = offsets[grp + k + 1] - offsets[grp + k];
+        cls[q] = (unsigned)min<uint64_t>(len >> 2, kSkLB - 1);
+        rk[q] = atomicAdd(&cnt[cls[q]], 1u);
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      unsigned v[kSkLB / 64], sum = 0;
+#pragma unroll
+      for (int q = 0; q < (int)(kSkLB / 64); ++q) {
+        v[q] = cnt[tid * (kSkLB / 64) + q];
+        sum += v[q];
+      }
+      unsigned x = sum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned y = __shfl_up(x, d);
+        if (tid >= (unsigned)d) x += y;
+      }
+      unsigned ex = x - sum;
+#pragma unroll
+      for (int q = 0; q < (int)(kSkLB / 64); ++q) {
+        cnt[tid * (kSkLB / 64) + q] = ex;
+        ex += v[q];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+      const unsigned k = tid + (unsigned)q * kSkT;
+      if (k < m) sidx[cnt[cls[q]] + rk[q]] = (unsigned short)k;
+    }
+    __syncthreads();
+    // ---- batches of 64 sorted keys, longest first, one wave each
+    const unsigned nb = (m + 63) / 64;
+    for (;;) {
+      unsigned b = 0;
+      if (lane == 0) b = atomicAdd(next, 1u);
+      b = __shfl(b, 0);
+      if (b >= nb) break;
+      const int hi = (int)m - 64 * (int)b;  // sorted slots [hi - 64, hi)
+      const int slot = hi - 64 + (int)lane;
+      const bool valid = slot >= 0;
+      const unsigned k = valid ? sidx[slot] : 0u;
+      const uint64_t ks = valid ? offsets[grp + k] : 0, ke = valid ? offsets[grp + k + 1] : 0;
+      const uint64_t kbase = ks & ~15ull;
+      const uint64_t span = valid ? ke - kbase : 0;
+      unsigned steps = (unsigned)((span + kSkC - 1) / kSkC);
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) steps = max(steps, (unsigned)__shfl_xor(steps, d));
+      // the keys this lane loads for: key 16t + lane/4, unit lane%4
+      uint64_t lb[kSkU], le[kSkU];
+#pragma unroll
+      for (int t = 0; t < kSkU; ++t) {
+        const int src = 16 * t + (int)(lane >> 2);
+        lb[t] = __shfl(kbase, src);
+        le[t] = __shfl(valid ? ke : 0ull, src);
+      }
+      const unsigned u = lane & 3u;
+      uint4 r[kSkU];
+      auto load = [&](unsigned step) {
+#pragma unroll
+        for (int t = 0; t < kSkU; ++t) {
+          const uint64_t a = lb[t] + (uint64_t)step * kSkC + 16u * u;
+          r[t] = make_uint4(0, 0, 0, 0);
+          if (a < le[t]) {
+            if (a + 16 <= end8) {
+              r[t] = *reinterpret_cast<const uint4*>(blob + a);
+            } else {  // the blob's last 8 readable bytes
+              const uint2 h2 = *reinterpret_cast<const uint2*>(blob + a);
+              r[t].x = h2.x;
+              r[t].y = h2.y;
+            }
+          }
+        }
+      };
+      uint32_t alo = (uint32_t)kFnvOffset, ahi = (uint32_t)(kFnvOffset >> 32), blo = alo, bhi = ahi;
+      load(0);
+      for (unsigned step = 0; step < steps; ++step) {
+#pragma unroll
+        for (int t = 0; t < kSkU; ++t) wst[(16 * t + (lane >> 2)) * (kSkS / 16) + u] = r[t];
+        // LDS operations of one wave complete in order: the lanes' reads below see every
+        // lane's writes above, and the next step's writes follow this step's reads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (step + 1 < steps) load(step + 1);
+        const uint64_t clo = kbase + (uint64_t)step * kSkC;
+        if (ke > clo) {
+          const unsigned o = step == 0 ? (unsigned)(ks - kbase) : 0u;
+          const unsigned top = (unsigned)min<uint64_t>(ke - clo, kSkC);
+          fnv_window_cont(wst32 + lane * (kSkS / 4), o, top - o, alo, ahi, blo, bhi);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      if (valid) {
+        res_a[k] = (uint64_t)alo | ((uint64_t)ahi << 32);
+        res_b[k] = (uint64_t)blo | ((uint64_t)bhi << 32);
+      }
+    }
+    __syncthreads();
+    for (unsigned k = tid; k < m; k += kSkT) {
+      const uint64_t a = res_a[k];
+      kh[grp + k] = a;
+      fp[grp + k] = res_b[k];
+      zero |= a == 0;
+    }
+    __syncthreads();  // the next group reuses cnt / sidx / res
+  }
+  if (zero) atomicOr(&st->status, kStKeyZero);
+}
+
 // ------------------------------------------------------------- level L setup ---------
 // Size level L from the redo count the previous level produced and carry its word
 // offset (the rank base lvl_base[L] was published by the previous level's last tile).
@@ -2749,6 +2937,7 @@ size_t tile_lds_bytes(unsigned tb) {
 uint64_t split_scratch_records() { return split_scratch_recs(); }
 
 void binned_set_lds_limits() {
+  (void)hipFuncSetAttribute((const void*)k_hash_skew, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSkLds);
   (void)hipFuncSetAttribute((const void*)k_tile<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)std::max(tile_lds_bytes(kTileMaxBits), tile_lds_bytes(kCacheBits)));
   (void)hipFuncSetAttribute((const void*)k_tile_reg<512, 20, 2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2768,8 +2957,8 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       unsigned long long* prof = b.tile_prof ? b.tile_prof + (uint64_t)(kMaxLevels - 3) * kMaxTiles * 8 : nullptr;
       k_hash0_pair<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
                                                              g.tb, g.chunk, b.tcnt, prof);
-      k_hash_count0<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st,
-                                                      g.tb, g.chunk, b.tcnt, 5);
+      k_hash_skew<<<256, kSkT, kSkLds, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk,
+                                            b.tcnt);
       return;
     }
     k_hash_count0<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, histogram ? b.hist : nullptr,
@@ -2785,8 +2974,8 @@ void launch_hash0_only(const uint8_t* blob, const uint64_t* offsets, uint64_t n,
   if (((uintptr_t)blob & 15) == 0) {  // as the single-GPU level 0: pair rounds unless st->skew
     k_hash0_pair<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
                                                            g.tb, g.chunk, b.tcnt, nullptr);
-    k_hash_count0<<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
-                                             g.chunk, b.tcnt, 5);
+    k_hash_skew<<<256, kSkT, kSkLds, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk,
+                                          b.tcnt);
     return;
   }
   k_hash_count0<<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
@@ -2798,9 +2987,9 @@ void launch_hash0_route(const uint8_t* blob, const uint64_t* offsets, uint64_t n
   if (((uintptr_t)blob & 15) == 0) {  // near-uniform lengths: hash + route in one pass
     k_hash0_pair<kH0T, kH0B, true, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags,
                                                                  b.st, g.tb, g.chunk, b.tcnt, nullptr, rt);
-    // a skewed set (st->skew): k_hash_count0's length-sorted groups, then k_route
-    k_hash_count0<<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
-                                             g.chunk, b.tcnt, 5);
+    // a skewed set (st->skew): k_hash_skew's length-sorted batches, then k_route
+    k_hash_skew<<<256, kSkT, kSkLds, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk,
+                                          b.tcnt);
     launch_route0_arrays(b.kh, b.fp, n, rt, b.st, true, s);
     return;
   }

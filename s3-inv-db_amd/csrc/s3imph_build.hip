@@ -96,6 +96,8 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   c->bucket_cap = bcap;
 }
 
+void free_bm_workspace(DistState& d);
+
 void free_workspace(s3imph_ctx* c) {
   dfree(c->mid);
   dfree(c->split);
@@ -120,6 +122,7 @@ void free_workspace(s3imph_ctx* c) {
   }
   c->stager.ready = false;
   DistState& d = c->d;
+  free_bm_workspace(d);
   dfree(d.send); dfree(d.stage_bits); dfree(d.scnt); dfree(d.mat); dfree(d.gslot); dfree(d.small);
   if (d.h_pinned) (void)hipHostFree(d.h_pinned);
   d.h_pinned = nullptr;
@@ -622,6 +625,22 @@ struct HostComm final : Comm {
     h2d(d_recv, hr.data(), bytes * nranks, s);
     HIPCHECK(hipStreamSynchronize(s));
   }
+  void reduce_scatter_u8(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
+    // block q of this rank's lanes to rank q (the harness's all-to-all), summed here
+    std::vector<uint64_t> off(nranks), cnt(nranks, bytes);
+    for (int q = 0; q < nranks; ++q) off[q] = (uint64_t)q * bytes;
+    hs.resize(bytes * nranks + 1);
+    hr.resize(bytes * nranks + 1);
+    d2h(hs.data(), d_send, bytes * nranks, s);
+    HIPCHECK(hipStreamSynchronize(s));
+    if (cb.alltoallv(cb.user, hs.data(), off.data(), cnt.data(), hr.data(), off.data(), cnt.data()) != 0)
+      throw Fail{S3IMPH_ERR_RCCL, "host alltoallv failed"};
+    std::vector<uint8_t> sum(bytes + 1, 0);
+    for (int r = 0; r < nranks; ++r)
+      for (uint64_t i = 0; i < bytes; ++i) sum[i] = (uint8_t)(sum[i] + hr[(uint64_t)r * bytes + i]);
+    h2d(d_recv, sum.data(), bytes, s);
+    HIPCHECK(hipStreamSynchronize(s));
+  }
   void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
                      hipStream_t s) override {
     const uint64_t bytes = 8 * count;
@@ -1078,6 +1097,255 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   return S3IMPH_OK;
 }
 
+// ------------------------------------------------------- bitmap decomposition ----
+// The north_star's multi-GPU build (s3imph_bitmap.hip): per distributed level, local
+// count lanes -> reduce-scatter -> final bits of this rank's slice -> all-gather -> every
+// rank settles its own records; then the replicated tail as in the routed build, and one
+// all-to-all of the settled (p, fp, pos) triples to the owners of the output slices.
+
+void ensure_bm_workspace(s3imph_ctx* c, uint64_t N) {
+  DistState& d = c->d;
+  const uint64_t P = (uint64_t)d.nranks;
+  const uint64_t w0 = level_words(N), S = (w0 + P - 1) / P, wpad = S * P;
+  if (wpad <= d.bm_cap_words && d.bm_a) return;
+  if (wpad > bm_max_words()) throw Fail{S3IMPH_ERR_INVALID, "build MPHF: key set too large for the bitmap decomposition"};
+  dalloc(d.bm_a, wpad);
+  dalloc(d.bm_c, wpad);
+  dalloc(d.bm_g, wpad);
+  dalloc(d.bm_dec, S);
+  dalloc(d.bm_lanes, 64 * wpad);
+  dalloc(d.bm_slice, 64 * S);
+  dalloc(d.bm_wpre, wpad);
+  dalloc(d.bm_bsum, bm_scan_blocks(wpad) + 2);
+  d.bm_cap_words = wpad;
+}
+
+void free_bm_workspace(DistState& d) {
+  dfree(d.bm_a); dfree(d.bm_c); dfree(d.bm_g); dfree(d.bm_dec);
+  dfree(d.bm_lanes); dfree(d.bm_slice); dfree(d.bm_wpre); dfree(d.bm_bsum);
+  d.bm_cap_words = 0;
+}
+
+int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
+                        uint64_t n_local, uint64_t key_base, uint64_t N, uint64_t* fp_out, uint64_t* pos_out,
+                        uint64_t out_cap, hipStream_t s, s3imph_build_info* info, std::string* msg) {
+  DistState& d = c->d;
+  Comm& cm = *d.comm;
+  const int P = d.nranks, R = d.rank;
+  LevelState* st = c->d_st;
+  ensure_bm_workspace(c, N);
+  const BinBuffers b = make_bufs(c, nullptr, fp_out, pos_out, s);
+  const double q = 1.0 - std::exp(-0.5);
+  launch_init_state(st, n_local, out_cap, s, n_local ? offsets : nullptr);
+  launch_dist_setup(st, 0, nullptr, N, R, P, s);
+  ev_mark(c, s, "init");
+  if (n_local) {
+    const LevelGeom gh0 = choose_geom_sz(n_local, 64 * level_words(N), kTargetTiles0, chunks0(n_local), kTileMaxBits);
+    launch_hash0_only(blob, offsets, n_local, b, gh0, level_grids(n_local, 64 * level_words(N), gh0).gc, s);
+  }
+  ev_mark(c, s, "hash_count0");
+  Rec* const out = c->bucket;                  // this rank's settled (p, fp, pos) triples
+  unsigned long long* const out_cnt = d.small + 4096;
+  HIPCHECK(hipMemsetAsync(out_cnt, 0, 8, s));
+  // Level sizes: the host bounds n_L from above (mean q n + 6 sigma), so every collective's
+  // size is known without a host round trip; a level outgrowing its bound sets
+  // kStBitmapBound and the build reruns on the routed decomposition.
+  double nb = (double)N, npred = (double)n_local;
+  int L = 0;
+  for (;;) {
+    const uint64_t wmax = level_words((uint64_t)std::ceil(nb)), S = (wmax + P - 1) / P, wpad = S * (uint64_t)P;
+    if (L > 0) launch_dist_setup(st, L, d.gslot + L, 0, R, P, s);
+    launch_bm_check(st, L, wmax, s);
+    HIPCHECK(hipMemsetAsync(d.bm_a, 0, 8 * wpad, s));
+    HIPCHECK(hipMemsetAsync(d.bm_c, 0, 8 * wpad, s));
+    const Rec* lin = L ? c->list[(L - 1) & 1] : nullptr;
+    const uint64_t np = (uint64_t)(npred * 1.1) + 4096;
+    launch_bm_mark(L, c->kh, n_local, lin, np, st, d.bm_a, d.bm_c, s);
+    launch_bm_lanes(d.bm_a, d.bm_c, wpad, d.bm_lanes, st, s);
+    cm.reduce_scatter_u8(d.bm_lanes, d.bm_slice, 64 * S, s);
+    launch_bm_decide(d.bm_slice, S, d.bm_dec, st, s);
+    cm.allgather(d.bm_dec, d.bm_g, 8 * S, s);
+    launch_bm_level_end(L, d.bm_g, wpad, c->bits, d.bm_bsum, d.bm_wpre, st, d.gslot, s);
+    launch_bm_settle(L, c->kh, c->fp, pos, key_base, n_local, lin, np, st, d.bm_g, d.bm_wpre, out, out_cnt,
+                     c->bucket_cap, c->list[L & 1], d.cap_list, s);
+    ev_mark(c, s, L == 0 ? "level0" : "levels");
+    const double nbn = nb * q + 6.0 * std::sqrt(nb) + 64.0;
+    npred *= q;
+    if (L + 1 >= kMaxDistLevels || nbn <= (double)c->dist_switch) break;
+    nb = nbn;
+    ++L;
+  }
+  const int Ls = L + 1;  // first replicated level
+  // ---- gather every rank's remaining records; all ranks finish the build identically,
+  // the tail's outputs (global p in [N - total, N)) into scratch (kh / fp are free now)
+  unsigned long long* M = d.h_pinned;
+  HIPCHECK(hipMemcpyAsync(d.small, &st->n[Ls], 8, hipMemcpyDeviceToDevice, s));
+  HIPCHECK(hipMemcpyAsync(d.small + 1, &st->status, 4, hipMemcpyDeviceToDevice, s));
+  HIPCHECK(hipMemsetAsync(reinterpret_cast<uint8_t*>(d.small + 1) + 4, 0, 4, s));
+  cm.allgather(d.small, d.small + 64, 16, s);
+  HIPCHECK(hipMemcpyAsync(M, d.small + 64, 16ull * P, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  uint64_t total = 0, maxc = 0;
+  unsigned flags = 0;
+  std::vector<uint64_t> cnt(P);
+  for (int r = 0; r < P; ++r) {
+    cnt[r] = M[2 * r];
+    flags |= (unsigned)M[2 * r + 1];
+    total += cnt[r];
+    maxc = std::max(maxc, cnt[r]);
+  }
+  if (flags & kStBitmapBound) return kDistRetry;  // a global fact: every rank returns here
+  if (flags & kStOverflow) {
+    *msg = "build MPHF: bitmap decomposition: list capacity exceeded";
+    return S3IMPH_ERR_INTERNAL;
+  }
+  if (total > d.cap_list || total > c->cap_keys) {
+    *msg = "build MPHF: replicated level of " + std::to_string(total) + " records exceeds the workspace";
+    return S3IMPH_ERR_NOMEM;
+  }
+  Rec* rl = c->list[(Ls - 1) & 1];
+  if (total) {
+    if ((uint64_t)P * maxc > d.cap_send) {
+      dalloc(d.send, (uint64_t)P * maxc);
+      d.cap_send = (uint64_t)P * maxc;
+    }
+    cm.allgather(rl, d.send, maxc * sizeof(Rec), s);
+    uint64_t o = 0;
+    for (int r = 0; r < P; ++r) {
+      if (cnt[r])
+        HIPCHECK(hipMemcpyAsync(rl + o, d.send + (uint64_t)r * maxc, cnt[r] * sizeof(Rec), hipMemcpyDeviceToDevice, s));
+      o += cnt[r];
+    }
+  }
+  launch_dist_replicate(st, Ls, total, 0, s);
+  launch_set_u64(&st->lvl_base[Ls], 0, s);  // tail ranks count from 0: scratch index = p - (N - total)
+  ev_mark(c, s, "gather");
+  BinBuffers bt = b;
+  bt.fp_out = c->kh;
+  bt.pos_out = c->fp;
+  const LevelGeom gcons = choose_geom(std::max<uint64_t>(total, 1), kTargetTiles, kTargetChunks, kRegTileMaxBits);
+  enqueue_levels_from(c, bt, Ls, total, gcons, false, s);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemcpyAsync(c->h_st, st, sizeof(LevelState), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipMemcpyAsync(M, out_cnt, 8, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  const uint64_t n_out = M[0];
+  // ---- every rank's flags, tail result and settled count
+  {
+    const LevelState& hs = *c->h_st;
+    M[0] = hs.status;
+    M[1] = hs.rank_total;
+    M[2] = n_out;
+    HIPCHECK(hipMemcpyAsync(d.small, M, 24, hipMemcpyHostToDevice, s));
+    cm.allgather(d.small, d.small + 64, 24, s);
+    HIPCHECK(hipMemcpyAsync(M, d.small + 64, 24ull * P, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+  }
+  uint64_t settled = 0;
+  flags = 0;
+  for (int r = 0; r < P; ++r) {
+    flags |= (unsigned)M[3 * r];
+    settled += M[3 * r + 2];
+  }
+  const LevelState& hs = *c->h_st;
+  if (flags & (kStGeometry | kStTailOverflow | kStResOverflow)) return kDistRetry;
+  if (flags & kStTooManyLevels) {
+    const unsigned nl = hs.stop_level ? hs.stop_level : hs.nlevels;
+    const uint64_t rem = nl < (unsigned)kMaxLevels + 2 ? hs.n[nl] : 0;
+    if (records_have_duplicates(c->list[(nl - 1) & 1], rem)) {
+      *msg = "build MPHF: duplicate FNV-1a key hashes: bbhash cannot place them";
+      return S3IMPH_ERR_DUP_KEY_HASH;
+    }
+    *msg = "build MPHF: can't find minimal perfect hash after " + std::to_string(kMaxLevels) + " levels";
+    return S3IMPH_ERR_TOO_MANY_LEVELS;
+  }
+  if (flags & kStKeyZero) {
+    *msg = "MPHF Key(...) returned 0, possible hash collision with sentinel";
+    return S3IMPH_ERR_KEY_HASH_ZERO;
+  }
+  if (flags) {
+    *msg = "build MPHF: internal error (device flags " + std::to_string(flags) + ")";
+    return S3IMPH_ERR_INTERNAL;
+  }
+  if (hs.rank_total != total || settled + total != N) {
+    *msg = "build MPHF: internal error: placed " + std::to_string(settled) + " + " + std::to_string(hs.rank_total) +
+           " of " + std::to_string(N) + " keys";
+    return S3IMPH_ERR_INTERNAL;
+  }
+  // ---- settled triples to the owners of their output slices
+  const uint64_t slice = (N + P - 1) / P;
+  const uint64_t lo = std::min<uint64_t>((uint64_t)R * slice, N), mine = std::min<uint64_t>(N, lo + slice) - lo;
+  if (mine > out_cap) {
+    *msg = "build MPHF: output capacity " + std::to_string(out_cap) + " < " + std::to_string(mine);
+    return S3IMPH_ERR_INVALID;
+  }
+  std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
+  uint64_t C = n_out / P + n_out / (4 * (uint64_t)P) + 4096;
+  uint64_t got = 0;
+  for (int tries = 0;; ++tries) {
+    if ((uint64_t)P * C > d.cap_send) {
+      HIPCHECK(hipStreamSynchronize(s));
+      dalloc(d.send, (uint64_t)P * C);
+      d.cap_send = (uint64_t)P * C;
+    }
+    HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
+    launch_bm_route_out(out, out_cnt, n_out, slice, P, d.send, C, d.scnt, st, s);
+    launch_route_flag(st, d.scnt, P, s);
+    cm.allgather(d.scnt, d.mat, 8ull * (P + 1), s);
+    HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    bool over = false;
+    uint64_t need = 0;
+    for (int r = 0; r < P; ++r) over |= M[(uint64_t)r * (P + 1) + P] != 0;
+    for (int t = 0; t < P; ++t) need = std::max<uint64_t>(need, M[(uint64_t)R * (P + 1) + t]);
+    if (!over) break;
+    if (tries >= 3) {
+      *msg = "build MPHF: output route regions keep overflowing";
+      return S3IMPH_ERR_INTERNAL;
+    }
+    // every rank sees the overflow; each grows to its own need (the regions are per rank)
+    C = std::max<uint64_t>(need, C) + C / 2 + 4096;
+  }
+  uint64_t acc = 0;
+  for (int t = 0; t < P; ++t) {
+    soff[t] = (uint64_t)t * C * sizeof(Rec);
+    sbytes[t] = M[(uint64_t)R * (P + 1) + t] * sizeof(Rec);
+    roff[t] = acc;
+    rbytes[t] = M[(uint64_t)t * (P + 1) + R] * sizeof(Rec);
+    acc += rbytes[t];
+    got += M[(uint64_t)t * (P + 1) + R];
+  }
+  const uint64_t g0 = N - total;
+  const uint64_t tail_mine = std::min<uint64_t>(N, lo + mine) > std::max(g0, lo)
+                                 ? std::min<uint64_t>(N, lo + mine) - std::max(g0, lo) : 0;
+  if (got + tail_mine != mine || got > d.cap_list) {
+    *msg = "build MPHF: internal error: output slice of rank " + std::to_string(R) + " receives " +
+           std::to_string(got) + " + " + std::to_string(tail_mine) + " of " + std::to_string(mine) + " entries";
+    return S3IMPH_ERR_INTERNAL;
+  }
+  Rec* recv = c->list[Ls & 1];
+  cm.alltoallv(d.send, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), s);
+  launch_bm_place(recv, got, lo, mine, fp_out, pos_out, st, s);
+  launch_bm_tail_copy(c->kh, c->fp, g0, total, lo, mine, fp_out, pos_out, s);
+  ev_mark(c, s, "exchange_out");
+  HIPCHECK(hipMemcpyAsync(M, &st->status, 4, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  ev_collect(c);
+  if ((unsigned)M[0] & kStRank) {
+    *msg = "build MPHF: internal error: a settled position fell outside its owner's slice";
+    return S3IMPH_ERR_INTERNAL;
+  }
+  d.seg.clear();
+  if (mine) d.seg.insert(d.seg.end(), {lo, mine, 0});
+  d.out_n = mine;
+  info->status = S3IMPH_OK;
+  info->num_levels = hs.nlevels;
+  info->total_words = hs.woff[hs.nlevels];
+  info->mph_bin_len = 8 * kPartitions + 8 + 8ull * hs.nlevels + 8ull * info->total_words;
+  info->big_levels = (uint64_t)Ls;
+  return S3IMPH_OK;
+}
+
 int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                uint64_t n_local, uint64_t key_base, uint64_t* fp_out, uint64_t* pos_out, uint64_t out_cap,
                uint64_t* out_n, hipStream_t s, s3imph_build_info* info, std::string* msg) {
@@ -1113,11 +1381,20 @@ int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
   ensure_dist_workspace(c, n_local, N);
   set_lds_attrs(c);
   int rc = S3IMPH_OK;
-  for (int attempt = 0; attempt < 2; ++attempt) {
+  // bitmap decomposition first when selected; its bound miss, and the routed build's
+  // geometry misses, fall back to the routed build and then to its conservative form
+  const int first = d.mode == kDistBitmap ? 0 : 1;
+  for (int attempt = first; attempt < 3; ++attempt) {
     ev_begin(c);
     ev_mark(c, s, "start");
-    rc = dist_attempt(c, blob, offsets, pos, n_local, key_base, N, fp_out, pos_out, out_cap, s, attempt > 0, info,
-                      msg);
+    rc = attempt == 0 ? dist_attempt_bitmap(c, blob, offsets, pos, n_local, key_base, N, fp_out, pos_out, out_cap, s,
+                                            info, msg)
+                      : dist_attempt(c, blob, offsets, pos, n_local, key_base, N, fp_out, pos_out, out_cap, s,
+                                     attempt > 1, info, msg);
+    if (rc == kDistRetry && attempt == 0 && std::getenv("S3IMPH_DIST_STRICT")) {
+      *msg = "build MPHF: the bitmap decomposition missed its size bounds (S3IMPH_DIST_STRICT: no fallback)";
+      return S3IMPH_ERR_INTERNAL;  // tests use this to prove the bitmap path built the index
+    }
     if (rc != kDistRetry) break;
   }
   if (rc != S3IMPH_OK) return rc;
@@ -1381,6 +1658,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     if (const char* m = std::getenv("S3IMPH_RES0")) c->res0 = std::atoi(m);
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);
+    if (const char* m = std::getenv("S3IMPH_DIST_MODE")) c->d.mode = std::strcmp(m, "bitmap") == 0 ? kDistBitmap : kDistRoute;
     // A blocking stream: implicitly ordered with the legacy NULL stream, so work a
     // caller queued there (e.g. torch's default stream) completes before ours starts.
     HIPCHECK(hipStreamCreate(&c->own_stream));
@@ -1580,6 +1858,13 @@ int s3imph_dist_segments(s3imph_ctx* c, uint64_t* seg, uint64_t cap, uint64_t* c
   if (!c->have_build) return S3IMPH_ERR_STATE;
   if (seg && cap) std::memcpy(seg, c->d.seg.data(), 8 * 3 * std::min(n, cap));
   return cap >= n || !seg ? S3IMPH_OK : S3IMPH_ERR_INVALID;
+}
+
+int s3imph_ctx_set_dist_mode(s3imph_ctx* c, int mode) {
+  if (!c || !c->dist || (mode != S3IMPH_DIST_ROUTE && mode != S3IMPH_DIST_BITMAP)) return S3IMPH_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->d.mode = mode == S3IMPH_DIST_BITMAP ? kDistBitmap : kDistRoute;
+  return S3IMPH_OK;
 }
 
 uint64_t s3imph_dist_out_cap(s3imph_ctx* c, uint64_t n_global) {

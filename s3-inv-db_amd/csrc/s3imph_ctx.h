@@ -56,6 +56,8 @@ struct Comm {
   virtual ~Comm() = default;
   // d_recv[r * bytes ..) <- rank r's d_send[0 .. bytes)
   virtual void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) = 0;
+  // d_recv[0 .. bytes) <- byte-wise sum over ranks of their d_send[rank * bytes ..) (u8, mod 256)
+  virtual void reduce_scatter_u8(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) = 0;
   // element-wise u64 sum over ranks
   virtual void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
                              hipStream_t s) = 0;
@@ -68,6 +70,10 @@ struct Comm {
 };
 
 constexpr uint64_t kDistSwitchKeysDefault = 2ull << 20;  // levels below this run replicated
+
+// Decomposition of the multi-GPU levels (s3imph_ctx_set_dist_mode / S3IMPH_DIST_MODE).
+constexpr int kDistRoute = 0;   // records routed to the owner of their position range (s3imph_dist.hip)
+constexpr int kDistBitmap = 1;  // count-lane reduction of the collision bitmap (s3imph_bitmap.hip)
 
 struct DistState {
   Comm* comm = nullptr;
@@ -82,6 +88,14 @@ struct DistState {
   unsigned long long* h_pinned = nullptr;    // host staging (64 x 64 + 256 u64)
   std::vector<uint64_t> seg;                 // last build: (p_lo, count, local_off) triples
   uint64_t out_n = 0;
+  // bitmap decomposition workspace: local A / C marks, count lanes, this rank's summed
+  // slice, the gathered final bits, their word prefix and block sums
+  uint64_t *bm_a = nullptr, *bm_c = nullptr, *bm_g = nullptr, *bm_dec = nullptr;
+  uint8_t *bm_lanes = nullptr, *bm_slice = nullptr;
+  unsigned* bm_wpre = nullptr;
+  unsigned long long* bm_bsum = nullptr;
+  uint64_t bm_cap_words = 0;
+  int mode = kDistRoute;
   // level 0's exchange runs on its own stream, chunk by chunk, beside the next chunk's hash
   hipStream_t xs = nullptr;
   hipEvent_t ev_route = nullptr, ev_counts = nullptr, ev_x = nullptr;
@@ -101,6 +115,9 @@ struct RcclComm final : Comm {
   }
   void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
     NCCLCHECK(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, s));
+  }
+  void reduce_scatter_u8(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
+    NCCLCHECK(ncclReduceScatter(d_send, d_recv, bytes, ncclUint8, ncclSum, comm, s));
   }
   void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
                      hipStream_t s) override {

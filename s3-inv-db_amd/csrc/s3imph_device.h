@@ -160,6 +160,28 @@ static __device__ __forceinline__ void fnv_window(const uint32_t* win, unsigned 
   hb = (uint64_t)blo | ((uint64_t)bhi << 32);
 }
 
+// fnv_window continuing a running state (alo:ahi FNV-1a, blo:bhi FNV-1): the bytes of a
+// key that arrive chunk by chunk.
+static __device__ __forceinline__ void fnv_window_cont(const uint32_t* win, unsigned o, unsigned len, uint32_t& alo,
+                                                       uint32_t& ahi, uint32_t& blo, uint32_t& bhi) {
+  const uint32_t* w = win + (o >> 2);
+  const unsigned sb = o & 3u;
+  const unsigned nfull = len >> 3;
+  uint32_t cur = w[0];
+  for (unsigned q = 0; q < nfull; ++q) {
+    const uint32_t n1 = w[2 * q + 1], n2 = w[2 * q + 2];
+    fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n1, cur, sb));
+    fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n2, n1, sb));
+    cur = n2;
+  }
+  const unsigned rem = len & 7u;
+  if (rem) {
+    const uint32_t n1 = w[2 * nfull + 1], n2 = w[2 * nfull + 2];
+    fnv_tail_b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n1, cur, sb), __builtin_amdgcn_alignbyte(n2, n1, sb),
+               rem);
+  }
+}
+
 // FNV-1a and FNV-1 over the 8 bytes of v, little-endian order.
 static __device__ __forceinline__ void fnv_8(uint64_t& a, uint64_t& b, uint64_t v) {
   uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);

@@ -144,6 +144,7 @@ constexpr unsigned kStTooManyLevels = 2u;  // level budget exhausted (duplicates
 constexpr unsigned kStOverflow = 4u;       // workspace capacity exceeded
 constexpr unsigned kStRank = 8u;           // a position landed outside [0, N)
 constexpr unsigned kStRouteOverflow = 256u;  // a multi-GPU send region overflowed (rerun bigger)
+constexpr unsigned kStBitmapBound = 512u;    // bitmap decomposition: a level outgrew the host's size bound
 // Any of these ends the level pipeline: later kernels return at once.
 constexpr unsigned kStStop = kStGeometry | kStOverflow | kStLookback | kStTooManyLevels;
 
@@ -270,6 +271,28 @@ void launch_dist_setup(LevelState* st, int L, const unsigned long long* gcount, 
 void launch_set_u64(unsigned long long* p, uint64_t v, hipStream_t s);
 void launch_route_flag(LevelState* st, unsigned long long* scnt, int P, hipStream_t s);
 void launch_dist_replicate(LevelState* st, int L, uint64_t n_all, uint64_t skip_from, hipStream_t s);
+
+// ---- the bitmap decomposition of the multi-GPU build (s3imph_bitmap.hip) --------------
+void launch_bm_check(LevelState* st, int level, uint64_t wmax, hipStream_t s);
+void launch_bm_mark(int level, const uint64_t* kh, uint64_t n_keys, const Rec* list, uint64_t n_pred,
+                    const LevelState* st, uint64_t* A, uint64_t* C, hipStream_t s);
+void launch_bm_lanes(const uint64_t* A, const uint64_t* C, uint64_t wpad, uint8_t* lanes, const LevelState* st,
+                     hipStream_t s);
+void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const LevelState* st, hipStream_t s);
+uint64_t bm_scan_blocks(uint64_t wpad);
+uint64_t bm_max_words();
+void launch_bm_level_end(int level, const uint64_t* g, uint64_t wpad, uint64_t* bits, unsigned long long* bsum,
+                         unsigned* wpre, LevelState* st, unsigned long long* gslot, hipStream_t s);
+void launch_bm_settle(int level, const uint64_t* kh, const uint64_t* fp, const uint64_t* pos, uint64_t pos_base,
+                      uint64_t n_keys, const Rec* list, uint64_t n_pred, LevelState* st, const uint64_t* g,
+                      const unsigned* wpre, Rec* out, unsigned long long* out_cnt, uint64_t out_cap, Rec* next,
+                      uint64_t next_cap, hipStream_t s);
+void launch_bm_route_out(const Rec* in, const unsigned long long* n_in, uint64_t n_pred, uint64_t slice, int P,
+                         Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, hipStream_t s);
+void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,
+                     LevelState* st, hipStream_t s);
+void launch_bm_tail_copy(const uint64_t* sfp, const uint64_t* spos, uint64_t g0, uint64_t total, uint64_t lo,
+                         uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s);
 
 // ---- host-memory builds (s3imph_build.hip, s3imph_multi.hip) -------------------------
 int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t n,

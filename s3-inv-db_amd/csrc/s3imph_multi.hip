@@ -87,6 +87,21 @@ struct ThreadComm final : Comm {
     HIPCHECK(hipStreamSynchronize(s));
     hub->barrier();  // every rank has read the slots before they are reused
   }
+  void reduce_scatter_u8(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
+    auto& mine = hub->slot[rank];
+    mine.resize(bytes * nranks + 1);
+    d2h(mine.data(), d_send, bytes * nranks, s);
+    HIPCHECK(hipStreamSynchronize(s));
+    hub->barrier();
+    std::vector<uint8_t> sum(bytes + 1, 0);
+    for (int r = 0; r < nranks; ++r) {
+      const uint8_t* q = hub->slot[r].data() + (uint64_t)rank * bytes;
+      for (uint64_t i = 0; i < bytes; ++i) sum[i] = (uint8_t)(sum[i] + q[i]);
+    }
+    h2d(d_recv, sum.data(), bytes, s);
+    HIPCHECK(hipStreamSynchronize(s));
+    hub->barrier();
+  }
   void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
                      hipStream_t s) override {
     const uint64_t bytes = 8 * count;
@@ -311,6 +326,11 @@ int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const ui
       return S3IMPH_ERR_RCCL;
     }
     if (mc->hub) mc->hub->reset();
+    {
+      const char* em = std::getenv("S3IMPH_DIST_MODE");
+      const bool bitmap = (flags & S3IMPH_MULTI_BITMAP) || (em && std::strcmp(em, "bitmap") == 0);
+      for (s3imph_ctx* c : mc->ctx) c->d.mode = bitmap ? kDistBitmap : kDistRoute;
+    }
     const std::vector<uint64_t> cuts = byte_cuts(offsets, n, P);
     // argument checks every rank would make alone, made here so that all ranks fail together
     for (int r = 0; r < P; ++r)

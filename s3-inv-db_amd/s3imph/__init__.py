@@ -47,6 +47,9 @@ ERR_STATE = 11
 
 MULTI_FORCE_SHARDED = 1   # the sharded (multi-GPU) build even for one GPU
 MULTI_HOST_TRANSPORT = 2  # in-process host-copy collectives instead of RCCL
+MULTI_BITMAP = 4          # the bitmap decomposition of the sharded levels
+DIST_ROUTE = 0            # sharded levels: records routed to their position-range owner
+DIST_BITMAP = 1           # sharded levels: count-lane reduction of the collision bitmap
 
 # Every entry point include/s3imph.h declares (checked by tests/test_capi.py).
 EXPORTS = (
@@ -58,7 +61,7 @@ EXPORTS = (
     "s3imph_ctx_create", "s3imph_ctx_destroy", "s3imph_ctx_reserve", "s3imph_build_device",
     "s3imph_ctx_mph_bin", "s3imph_ctx_set_profiling", "s3imph_ctx_stage_times",
     "s3imph_dist_unique_id", "s3imph_ctx_create_dist", "s3imph_ctx_create_dist_host", "s3imph_build_device_dist",
-    "s3imph_dist_segments", "s3imph_dist_out_cap", "s3imph_ctx_last_error",
+    "s3imph_dist_segments", "s3imph_dist_out_cap", "s3imph_ctx_last_error", "s3imph_ctx_set_dist_mode",
     "s3imph_ctx_load_mph_bin", "s3imph_lookup_device", "s3imph_gen_keys",
     "s3imph_finalize_index_host", "s3imph_finalize_index_device",
     "s3imph_write_manifest", "s3imph_verify_manifest", "s3imph_sha256_file",
@@ -133,6 +136,7 @@ def _load():
         "s3imph_build_device_dist": (i32, [vp, vp, vp, vp, u64, u64, vp, vp, u64, P(u64), vp, P(BuildInfo)]),
         "s3imph_dist_segments": (i32, [vp, P(u64), u64, P(u64)]),
         "s3imph_dist_out_cap": (u64, [vp, u64]),
+        "s3imph_ctx_set_dist_mode": (i32, [vp, i32]),
         "s3imph_ctx_last_error": (cp, [vp]),
         "s3imph_ctx_load_mph_bin": (i32, [vp, vp, u64]),
         "s3imph_lookup_device": (i32, [vp, vp, vp, u64, vp, vp, u64, vp, vp]),
@@ -562,6 +566,10 @@ class DistBuilder(DeviceBuilder):
 
     def out_cap(self, n_global: int) -> int:
         return LIB.s3imph_dist_out_cap(self._h, n_global)
+
+    def set_mode(self, mode: int) -> None:
+        """DIST_ROUTE or DIST_BITMAP (every rank of a build must choose the same)."""
+        _check(LIB.s3imph_ctx_set_dist_mode(self._h, mode), None, "set_dist_mode")
 
     def segments(self) -> list[tuple[int, int, int]]:
         """(global p, count, local offset) of this rank's outputs in the last build."""

@@ -11,12 +11,14 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def rank_main(rank, world, port, shard, n_global, switch, result_q):
+def rank_main(rank, world, port, shard, n_global, switch, result_q, mode="route"):
     try:
         for d in (os.path.join(ROOT, "s3-inv-db_amd"), os.path.join(ROOT, "oracle")):
             if d not in sys.path:
                 sys.path.insert(0, d)
         os.environ["S3IMPH_DIST_SWITCH"] = str(switch)
+        os.environ["S3IMPH_DIST_MODE"] = mode
+        os.environ["S3IMPH_DIST_STRICT"] = "1"  # a bitmap build may not fall back to routing
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         import torch
         import torch.distributed as dist

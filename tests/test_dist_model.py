@@ -12,6 +12,18 @@ dist_attempt):
   identically, rank 0 writing those outputs.  Each (level, rank) is one output segment
   whose global start is a prefix sum over (level, rank) settled counts.
 
+The second decomposition (s3-inv-db_amd/csrc/s3imph_bitmap.hip, s3imph_build.hip:
+dist_attempt_bitmap — the north_star's per-level collision-bitmap reduction):
+
+  every rank keeps its key shard; at level L it computes the count lane
+  min(local count, 2) of every global position, the lanes are summed over the ranks
+  (RCCL reduce-scatter of u8; here an all-reduce whose slice each rank keeps), the
+  slice owner sets final bit = (sum == 1), the final bits are all-gathered, and every
+  rank settles its own records (bit set at x: placed at lvl_base + popcount(A[0:x)));
+  the next level's global size is n_L - popcount(A_L).  Below the switch the remaining
+  records are replicated as above; at the end one all-to-all moves the settled
+  (p, fp, pos) triples to the owner of p's output slice [r*ceil(N/P), ...).
+
 The per-rank arithmetic is a numpy restatement of the kernels; the cross-rank
 exchange is real torch.distributed traffic.  The assembled result must equal the
 oracle's single-process build byte for byte, whatever the number of ranks.
@@ -168,8 +180,105 @@ def _rank_main(rank, world, port, blob, offs, switch, result_q):
     dist.destroy_process_group()
 
 
+def _bitmap_rank_main(rank, world, port, blob, offs, switch, result_q):
+    import torch
+    import torch.distributed as dist
+    import sys
+    for d in (os.path.join(os.path.dirname(__file__), "..", "s3-inv-db_amd"),
+              os.path.join(os.path.dirname(__file__), "..", "oracle")):
+        sys.path.insert(0, d)
+    import oracle as Orc
+    from s3imph import ShardPlan
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    N = len(offs) - 1
+    plan = ShardPlan(rank, world, N)
+    kh, fp = Orc.lib().hash_keys(blob, offs)
+    k, f = kh[plan.lo:plan.hi], fp[plan.lo:plan.hi]
+    p = np.arange(plan.lo, plan.hi, dtype=np.uint64)
+    out = []  # settled (p, fp, pos) of this rank's keys
+    bits_levels = []
+    nL, level, base = N, 0, 0
+    while True:
+        words = (2 * nL + 63) // 64
+        S = -(-words // world)
+        x = _positions(level, k, words)
+        lanes = np.minimum(np.bincount(x, minlength=64 * S * world), 2).astype(np.int32)
+        t = torch.from_numpy(lanes)
+        dist.all_reduce(t)  # the reduce-scatter's sums; this rank decides its slice only
+        mine = t.numpy()[64 * S * rank:64 * S * (rank + 1)] == 1
+        g = [torch.zeros(64 * S, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(g, torch.from_numpy(mine.astype(np.uint8)))
+        final = np.concatenate([a.numpy() for a in g]).astype(bool)
+        bits_levels.append(np.packbits(final[:64 * words], bitorder="little").view(np.uint64))
+        prefix = np.concatenate([[0], np.cumsum(final)])
+        ok = final[x]
+        out.append(np.stack([base + prefix[x[ok]].astype(np.uint64), f[ok], p[ok]]))
+        k, f, p = k[~ok], f[~ok], p[~ok]
+        pop = int(final.sum())
+        base += pop
+        nL -= pop  # known to every rank: no collective for the next level's size
+        level += 1
+        if nL <= switch:  # the production code compares its bound of n_{L+1}
+            break
+    # replicated tail (every rank runs it; outputs numbered from base)
+    cnts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(cnts, torch.tensor([len(k)], dtype=torch.int64))
+    maxc = max(int(c.item()) for c in cnts)
+    pad = np.zeros((3, maxc), np.uint64)
+    pad[:, :len(k)] = np.stack([k, f, p])
+    gat = [torch.zeros((3, maxc), dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(gat, torch.from_numpy(pad.view(np.int64).copy()))
+    k, f, p = np.concatenate([g.numpy().view(np.uint64)[:, :int(c.item())] for g, c in zip(gat, cnts)], axis=1)
+    tail = []
+    L = level
+    while len(k):
+        words = (2 * len(k) + 63) // 64
+        final, (sf, sp), (k, f, p) = _settle(L, k, f, p, words, 0, 64 * words)
+        tail.append(np.stack([base + np.arange(len(sf), dtype=np.uint64), sf, sp]))
+        base += len(sf)
+        bits_levels.append(np.packbits(final, bitorder="little").view(np.uint64))
+        L += 1
+    assert base == N
+    # settled triples -> the owner of p's slice (all-to-all); the tail is on every rank
+    sl = -(-N // world)
+    trip = np.concatenate(out, axis=1) if out else np.zeros((3, 0), np.uint64)
+    owner = (trip[0] // np.uint64(sl)).astype(np.int64)
+    send = [trip[:, owner == q] for q in range(world)]
+    allc = [torch.zeros(world, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(allc, torch.tensor([s.shape[1] for s in send], dtype=torch.int64))
+    recv, reqs = [None] * world, []
+    for q in range(world):
+        if q == rank:
+            recv[q] = torch.from_numpy(send[q].view(np.int64).copy())
+            continue
+        recv[q] = torch.zeros((3, int(allc[q][rank])), dtype=torch.int64)
+        reqs.append(dist.isend(torch.from_numpy(send[q].view(np.int64).copy()), q))
+        reqs.append(dist.irecv(recv[q], q))
+    for r in reqs:
+        r.wait()
+    lo, hi = min(rank * sl, N), min((rank + 1) * sl, N)
+    lf = np.zeros(hi - lo, np.uint64)
+    lp = np.zeros(hi - lo, np.uint64)
+    filled = np.zeros(hi - lo, bool)
+    for r in recv + [torch.from_numpy(t.view(np.int64)) for t in tail]:
+        a = r.numpy().view(np.uint64)
+        m = (a[0] >= lo) & (a[0] < hi)
+        idx = (a[0][m] - np.uint64(lo)).astype(np.int64)
+        lf[idx], lp[idx] = a[1][m], a[2][m]
+        filled[idx] = True
+    assert filled.all()
+    mph = np.uint64(1).tobytes() + np.uint64(len(bits_levels)).tobytes() + b"".join(
+        np.uint64(len(b)).tobytes() + b.tobytes() for b in bits_levels)
+    result_q.put((rank, lf, lp, [(lo, hi - lo, 0)] if hi > lo else [], mph, level))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["route", "bitmap"])
 @pytest.mark.parametrize("world,switch", [(2, 5000), (3, 5000), (3, 10 ** 9)])
-def test_position_range_ownership_matches_single_process(world, switch, oracle_lib):
+def test_position_range_ownership_matches_single_process(world, switch, mode, oracle_lib):
     import torch.multiprocessing as mp
     import s3imph
 
@@ -181,7 +290,8 @@ def test_position_range_ownership_matches_single_process(world, switch, oracle_l
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, blob, offs, switch, q)) for r in range(world)]
+    target = _rank_main if mode == "route" else _bitmap_rank_main
+    procs = [ctx.Process(target=target, args=(r, world, port, blob, offs, switch, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -191,7 +301,7 @@ def test_position_range_ownership_matches_single_process(world, switch, oracle_l
     res.sort(key=lambda r: r[0])
     assert all(r[4] == mph for r in res)
     if switch < n:
-        assert res[0][5] >= 3  # several routed levels before the replicated tail
+        assert res[0][5] >= 2  # several sharded levels before the replicated tail
     got_fp, got_pos = s3imph.assemble_dist([(r[1], r[2], r[3]) for r in res], n)
     assert np.array_equal(got_fp, fp)
     assert np.array_equal(got_pos, po)

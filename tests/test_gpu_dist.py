@@ -1,4 +1,5 @@
-"""Multi-GPU build (s3imph_build_device_dist) on the GPU, bit-exact against the oracle.
+"""Multi-GPU build (s3imph_build_device_dist) on the GPU, bit-exact against the oracle,
+for both decompositions of the sharded levels (route and bitmap, s3imph.h).
 
 Several ranks share the box's one GPU through the host-callback transport
 (tests/dist_worker.py: torch.distributed/gloo collectives on host copies); every
@@ -37,13 +38,13 @@ def _shards(blob, offs, cuts, pos=None):
     return out
 
 
-def _run(world, shards, n, switch):
+def _run(world, shards, n, switch, mode="route"):
     import torch.multiprocessing as mp
     import dist_worker
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=dist_worker.rank_main, args=(r, world, port, shards[r], n, switch, q))
+    procs = [ctx.Process(target=dist_worker.rank_main, args=(r, world, port, shards[r], n, switch, q, mode))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -66,29 +67,33 @@ def _check(res, n, fp, po, mph):
     assert np.array_equal(got_po, po)
 
 
+@pytest.mark.parametrize("mode", ["route", "bitmap"])
 @pytest.mark.parametrize("world,n,switch", [(2, 200_000, 20_000), (3, 120_000, 10_000), (2, 300_000, 2 << 20)])
-def test_dist_host_comm_matches_oracle(world, n, switch, oracle_lib):
+def test_dist_host_comm_matches_oracle(world, n, switch, mode, oracle_lib):
+    """Both decompositions of the sharded levels (route: records to position owners;
+    bitmap: count lanes reduce-scattered, final bits all-gathered) bit-exact."""
     import s3imph
     blob, offs = s3imph.gen_keys(0, 7, 32, 0, n)
     blob = blob[: int(offs[-1])]
     st, fp, po, mph = oracle_lib.build(blob, offs)
     assert st == 0
     cuts = [n * r // world for r in range(world + 1)]
-    res = _run(world, _shards(blob, offs, cuts), n, switch)
+    res = _run(world, _shards(blob, offs, cuts), n, switch, mode)
     assert res[0][6]["big_levels"] >= (3 if switch < 50_000 else 1)
     _check(res, n, fp, po, mph)
 
 
-def test_dist_unbalanced_shards_custom_pos(oracle_lib):
+@pytest.mark.parametrize("mode", ["route", "bitmap"])
+def test_dist_unbalanced_shards_custom_pos(oracle_lib, mode):
     import s3imph
     n, world = 90_000, 3
-    blob, offs = s3imph.gen_keys(1, 3, 0, 0, n)  # ragged lengths 1-1024 B
+    blob, offs = s3imph.gen_keys(1, 3, 0, 0, n)  # ragged lengths 5-1024 B
     blob = blob[: int(offs[-1])]
     pos = (np.random.default_rng(1).permutation(n).astype(np.uint64) + np.uint64(7_000_000))
     st, fp, po, mph = oracle_lib.build(blob, offs, pos)
     assert st == 0
     cuts = [0, 5_000, 70_000, n]
-    res = _run(world, _shards(blob, offs, cuts, pos), n, 8_000)
+    res = _run(world, _shards(blob, offs, cuts, pos), n, 8_000, mode)
     _check(res, n, fp, po, mph)
 
 
@@ -107,31 +112,38 @@ def test_dist_chunked_level0_unbalanced(oracle_lib):
     _check(res, n, fp, po, mph)
 
 
-def test_dist_tiny_set_and_empty_rank(oracle_lib):
+@pytest.mark.parametrize("mode", ["route", "bitmap"])
+def test_dist_tiny_set_and_empty_rank(oracle_lib, mode):
     """5 keys on 3 ranks (one rank holds none; most ranks own no level positions)."""
     keys = [b"", b"a/", b"data/", b"data/2024/", b"root/"]
     blob, offs = O.keys_to_blob(keys)
     st, fp, po, mph = oracle_lib.build(blob, offs)
-    res = _run(3, _shards(blob, offs, [0, 2, 2, 5]), 5, 1 << 20)
+    res = _run(3, _shards(blob, offs, [0, 2, 2, 5]), 5, 1 << 20, mode)
     _check(res, 5, fp, po, mph)
 
 
-def test_dist_duplicate_across_ranks_fails_everywhere():
+@pytest.mark.parametrize("mode", ["route", "bitmap"])
+def test_dist_duplicate_across_ranks_fails_everywhere(mode):
     keys = [b"x/%05d/" % i for i in range(3000)]
     keys[2500] = keys[10]  # the duplicate lives on the other rank
     blob, offs = O.keys_to_blob(keys)
-    res = _run(2, _shards(blob, offs, [0, 1500, 3000]), 3000, 1 << 20)
+    res = _run(2, _shards(blob, offs, [0, 1500, 3000]), 3000, 1 << 20, mode)
     import s3imph
     for r in res:
         assert r[1] == "error" and r[2] == s3imph.ERR_DUP_KEY_HASH, r
 
 
-def test_dist_rccl_single_rank_routes_levels(oracle_lib, monkeypatch):
-    """The RCCL transport (nranks = 1 on this box) through several routed levels."""
+@pytest.mark.parametrize("mode", ["route", "bitmap"])
+def test_dist_rccl_single_rank_routes_levels(oracle_lib, monkeypatch, mode):
+    """The RCCL transport (nranks = 1 on this box) through several sharded levels: route
+    (all-to-all, all-gathers) and bitmap (ncclReduceScatter of the count lanes,
+    ncclAllGather of the final bits, the output all-to-all)."""
     import torch
     import s3imph
     monkeypatch.setenv("S3IMPH_DIST_SWITCH", "20000")
+    monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
     d = s3imph.DistBuilder(0, s3imph.dist_unique_id(), 0, 1)
+    d.set_mode(s3imph.DIST_BITMAP if mode == "bitmap" else s3imph.DIST_ROUTE)
     n = 300_000
     blob, offs = s3imph.gen_keys(0, 11, 32, 0, n)
     st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)

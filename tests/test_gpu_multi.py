@@ -47,15 +47,31 @@ def test_one_gpu_sharded_over_rccl(s3, oracle_lib, monkeypatch):
         assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
 
 
-@pytest.mark.parametrize("ranks,kind,avg,n", [(2, 0, 32, 300_000), (3, 1, 0, 400_000), (4, 0, 64, 500_000)])
-def test_thread_per_rank_shared_gpu(s3, oracle_lib, monkeypatch, ranks, kind, avg, n):
-    """2-4 ranks in one process on the one GPU (host-copy transport), shards balanced by
-    key bytes, skewed lengths on one case: bit-exact."""
+@pytest.mark.parametrize("bitmap", [False, True])
+@pytest.mark.parametrize("ranks,kind,avg,n", [(2, 0, 32, 300_000), (3, 1, 0, 400_000), (4, 0, 64, 500_000),
+                                              (8, 0, 24, 2_000_000)])
+def test_thread_per_rank_shared_gpu(s3, oracle_lib, monkeypatch, ranks, kind, avg, n, bitmap):
+    """2-8 ranks in one process on the one GPU (host-copy transport), shards balanced by
+    key bytes, skewed lengths on one case, both decompositions (route / bitmap; the
+    bitmap build may not fall back, S3IMPH_DIST_STRICT): bit-exact."""
     monkeypatch.setenv("S3IMPH_DIST_SWITCH", "15000")
+    monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
     blob, offs = s3.gen_keys(kind, 8, avg, 0, n)
     fp, po, mph = _expect(oracle_lib, blob, offs)
-    g = s3.build_host(blob, offs, devices=[0] * ranks)
+    g = s3.build_host(blob, offs, devices=[0] * ranks, flags=s3.MULTI_BITMAP if bitmap else 0)
     assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+
+
+def test_one_gpu_sharded_bitmap_over_rccl(s3, oracle_lib, monkeypatch):
+    """The bitmap decomposition on an in-process RCCL communicator (one rank):
+    ncclReduceScatter of the count lanes and ncclAllGather of the final bits per level."""
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", "20000")
+    monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
+    blob, offs = s3.gen_keys(0, 16, 40, 0, 1_500_000)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    for _ in range(2):
+        g = s3.build_host(blob, offs, num_gpus=1, flags=s3.MULTI_FORCE_SHARDED | s3.MULTI_BITMAP)
+        assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
 
 
 @pytest.mark.parametrize("ranks", [2, 3])
