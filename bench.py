@@ -74,6 +74,9 @@ def main() -> None:
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
                     help="N>1 collectives: RCCL over xGMI (default), or host copies over gloo — a rehearsal "
                          "mode that lets several ranks share one GPU (not a measurement)")
+    ap.add_argument("--decomp", default="route", choices=["route", "bitmap"],
+                    help="sharded levels: records routed to position owners (route), or the per-level "
+                         "collision-bitmap count lanes reduce-scattered over RCCL (bitmap)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 line beside the C3 headline")
     ap.add_argument("--headline-only", action="store_true",
                     help="skip the lookup / finalize / host_e2e lines (profiling runs)")
@@ -121,6 +124,7 @@ def main() -> None:
             if dist is not None:
                 dist.broadcast_object_list(uid, src=0)
             ctx = s3imph.DistBuilder(local_rank, uid[0], rank, world)
+        ctx.set_mode(s3imph.DIST_BITMAP if args.decomp == "bitmap" else s3imph.DIST_ROUTE)
         ctx.reserve(n, plan.n_global)
         out_cap = ctx.out_cap(plan.n_global)
     d_fp = torch.empty(max(out_cap, 1), dtype=torch.int64, device=dev)
@@ -202,6 +206,7 @@ def main() -> None:
         "data": "synthetic (deterministic splitmix64 prefixes, byte-sorted, distinct)",
         "config": {"workload": cfg["workload"], "config": args.config, "keys": n_global,
                    "transport": args.transport if world > 1 else None,
+                   "decomposition": args.decomp if use_dist else None,
                    "key_bytes": key_bytes, "parallelism": f"shard{world}" if use_dist else "single",
                    "gamma": 2.0, "levels": info.get("num_levels")},
         "key_bytes_GBps": key_bytes / dt / 1e9,

@@ -467,17 +467,29 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
           uint64_t a, b;
           const unsigned j = sidx[slot];
           fnv_window(reinterpret_cast<const uint32_t*>(sw), soff[slot], slen[slot], a, b);
-          if (RT) {
-            ra[h] = a;
-            rb[h] = b;
-            rj[h] = j;
-            rv[h] = true;
-          } else {
-            kh[r0 + j] = a;
-            fp[r0 + j] = b;
-          }
+          ra[h] = a;
+          rb[h] = b;
+          rj[h] = j;
+          rv[h] = true;
           zero |= (a == 0);
         }
+      }
+    }
+    if (!RT && !alone) {  // ---- (kh, fp) back to key order through LDS, then coalesced stores
+      static_assert(2 * G * sizeof(uint64_t) <= sizeof(sw), "the result stage aliases the byte window");
+      __syncthreads();  // every lane has hashed: the window is free
+      uint64_t* sa = sw;
+      uint64_t* sb = sw + G;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (rv[h]) {
+          sa[rj[h]] = ra[h];
+          sb[rj[h]] = rb[h];
+        }
+      __syncthreads();
+      for (unsigned j = tid; j < m; j += NT) {
+        kh[r0 + j] = sa[j];
+        fp[r0 + j] = sb[j];
       }
     }
     if (RT) {  // ---- route the round's records to their owners (k_route's scheme)
@@ -658,52 +670,66 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
       if (k < m) sidx[cnt[cls[q]] + rk[q]] = (unsigned short)k;
     }
     __syncthreads();
-    // ---- batches of 64 sorted keys, longest first, one wave each
+    // ---- batches of 64 sorted keys, longest first, one wave each.  The wave takes its next
+    // ticket, reads that batch's keys and issues its first chunk's loads before it hashes the
+    // current batch's last chunk, so the dependent ticket -> sidx -> offsets -> bytes chain
+    // of a batch hides behind the previous batch's hashing.
     const unsigned nb = (m + 63) / 64;
-    for (;;) {
+    const unsigned u = lane & 3u;
+    struct Batch {
+      unsigned b, k, steps;
+      bool valid;
+      uint64_t ks, ke, kbase;
+      uint64_t lb[kSkU], le[kSkU];  // the keys this lane loads for: key 16t + lane/4, unit lane%4
+    };
+    auto take = [&](Batch& x) {
       unsigned b = 0;
       if (lane == 0) b = atomicAdd(next, 1u);
-      b = __shfl(b, 0);
-      if (b >= nb) break;
-      const int hi = (int)m - 64 * (int)b;  // sorted slots [hi - 64, hi)
+      x.b = __shfl(b, 0);
+      if (x.b >= nb) return;
+      const int hi = (int)m - 64 * (int)x.b;  // sorted slots [hi - 64, hi)
       const int slot = hi - 64 + (int)lane;
-      const bool valid = slot >= 0;
-      const unsigned k = valid ? sidx[slot] : 0u;
-      const uint64_t ks = valid ? offsets[grp + k] : 0, ke = valid ? offsets[grp + k + 1] : 0;
-      const uint64_t kbase = ks & ~15ull;
-      const uint64_t span = valid ? ke - kbase : 0;
+      x.valid = slot >= 0;
+      x.k = x.valid ? sidx[slot] : 0u;
+      x.ks = x.valid ? offsets[grp + x.k] : 0;
+      x.ke = x.valid ? offsets[grp + x.k + 1] : 0;
+      x.kbase = x.ks & ~15ull;
+      const uint64_t span = x.valid ? x.ke - x.kbase : 0;
       unsigned steps = (unsigned)((span + kSkC - 1) / kSkC);
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) steps = max(steps, (unsigned)__shfl_xor(steps, d));
-      // the keys this lane loads for: key 16t + lane/4, unit lane%4
-      uint64_t lb[kSkU], le[kSkU];
+      x.steps = max(steps, 1u);  // >= 1: the step loop takes the next ticket
 #pragma unroll
       for (int t = 0; t < kSkU; ++t) {
         const int src = 16 * t + (int)(lane >> 2);
-        lb[t] = __shfl(kbase, src);
-        le[t] = __shfl(valid ? ke : 0ull, src);
+        x.lb[t] = __shfl(x.kbase, src);
+        x.le[t] = __shfl(x.valid ? x.ke : 0ull, src);
       }
-      const unsigned u = lane & 3u;
-      uint4 r[kSkU];
-      auto load = [&](unsigned step) {
+    };
+    uint4 r[kSkU];
+    auto load = [&](const Batch& x, unsigned step) {
 #pragma unroll
-        for (int t = 0; t < kSkU; ++t) {
-          const uint64_t a = lb[t] + (uint64_t)step * kSkC + 16u * u;
-          r[t] = make_uint4(0, 0, 0, 0);
-          if (a < le[t]) {
-            if (a + 16 <= end8) {
-              r[t] = *reinterpret_cast<const uint4*>(blob + a);
-            } else {  // the blob's last 8 readable bytes
-              const uint2 h2 = *reinterpret_cast<const uint2*>(blob + a);
-              r[t].x = h2.x;
-              r[t].y = h2.y;
-            }
+      for (int t = 0; t < kSkU; ++t) {
+        const uint64_t a = x.lb[t] + (uint64_t)step * kSkC + 16u * u;
+        r[t] = make_uint4(0, 0, 0, 0);
+        if (a < x.le[t]) {
+          if (a + 16 <= end8) {
+            r[t] = *reinterpret_cast<const uint4*>(blob + a);
+          } else {  // the blob's last 8 readable bytes
+            const uint2 h2 = *reinterpret_cast<const uint2*>(blob + a);
+            r[t].x = h2.x;
+            r[t].y = h2.y;
           }
         }
-      };
+      }
+    };
+    Batch cur, nxt;
+    take(cur);
+    if (cur.b < nb) load(cur, 0);
+    while (cur.b < nb) {
       uint32_t alo = (uint32_t)kFnvOffset, ahi = (uint32_t)(kFnvOffset >> 32), blo = alo, bhi = ahi;
-      load(0);
-      for (unsigned step = 0; step < steps; ++step) {
+      nxt.b = nb;
+      for (unsigned step = 0; step < cur.steps; ++step) {
 #pragma unroll
         for (int t = 0; t < kSkU; ++t) wst[(16 * t + (lane >> 2)) * (kSkS / 16) + u] = r[t];
         // LDS operations of one wave complete in order: the lanes' reads below see every
@@ -711,21 +737,27 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (step + 1 < steps) load(step + 1);
-        const uint64_t clo = kbase + (uint64_t)step * kSkC;
-        if (ke > clo) {
-          const unsigned o = step == 0 ? (unsigned)(ks - kbase) : 0u;
-          const unsigned top = (unsigned)min<uint64_t>(ke - clo, kSkC);
+        if (step + 1 < cur.steps) {
+          load(cur, step + 1);
+        } else {
+          take(nxt);
+          if (nxt.b < nb) load(nxt, 0);
+        }
+        const uint64_t clo = cur.kbase + (uint64_t)step * kSkC;
+        if (cur.ke > clo) {
+          const unsigned o = step == 0 ? (unsigned)(cur.ks - cur.kbase) : 0u;
+          const unsigned top = (unsigned)min<uint64_t>(cur.ke - clo, kSkC);
           fnv_window_cont(wst32 + lane * (kSkS / 4), o, top - o, alo, ahi, blo, bhi);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
-      if (valid) {
-        res_a[k] = (uint64_t)alo | ((uint64_t)ahi << 32);
-        res_b[k] = (uint64_t)blo | ((uint64_t)bhi << 32);
+      if (cur.valid) {
+        res_a[cur.k] = (uint64_t)alo | ((uint64_t)ahi << 32);
+        res_b[cur.k] = (uint64_t)blo | ((uint64_t)bhi << 32);
       }
+      cur = nxt;
     }
     __syncthreads();
     for (unsigned k = tid; k < m; k += kSkT) {

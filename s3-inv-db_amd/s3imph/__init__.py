@@ -518,7 +518,8 @@ class MPHF:
         pad = np.zeros(((len(blob) + 7) // 8) * 8 + 8, np.uint8)
         pad[:len(blob)] = blob
         d_blob = torch.from_numpy(pad).to(self.dev)
-        d_offs = torch.from_numpy(np.ascontiguousarray(offsets, np.uint64).view(np.int64)).to(self.dev)
+        # offsets may be a read-only view of prefix_offsets.u64: copy before torch takes it
+        d_offs = torch.from_numpy(np.array(offsets, dtype=np.uint64).view(np.int64)).to(self.dev)
         res = torch.empty(max(n, 1), dtype=torch.int64, device=self.dev)
         self.ctx.lookup(d_blob, d_offs, n, self.d_fp, self.d_pos, self.count, res)
         return res[:n].cpu().numpy().view(np.uint64)
