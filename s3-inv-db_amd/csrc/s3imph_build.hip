@@ -1107,6 +1107,10 @@ void ensure_bm_workspace(s3imph_ctx* c, uint64_t N) {
   DistState& d = c->d;
   const uint64_t P = (uint64_t)d.nranks;
   const uint64_t w0 = level_words(N), S = (w0 + P - 1) / P, wpad = S * P;
+  if (d.bm_cap_out < d.cap_list) {  // a rank settles at most the records it holds (<= its list capacity)
+    dalloc(d.bm_out, d.cap_list);
+    d.bm_cap_out = d.cap_list;
+  }
   if (wpad <= d.bm_cap_words && d.bm_a) return;
   if (wpad > bm_max_words()) throw Fail{S3IMPH_ERR_INVALID, "build MPHF: key set too large for the bitmap decomposition"};
   dalloc(d.bm_a, wpad);
@@ -1123,7 +1127,9 @@ void ensure_bm_workspace(s3imph_ctx* c, uint64_t N) {
 void free_bm_workspace(DistState& d) {
   dfree(d.bm_a); dfree(d.bm_c); dfree(d.bm_g); dfree(d.bm_dec);
   dfree(d.bm_lanes); dfree(d.bm_slice); dfree(d.bm_wpre); dfree(d.bm_bsum);
+  dfree(d.bm_out);
   d.bm_cap_words = 0;
+  d.bm_cap_out = 0;
 }
 
 int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
@@ -1144,7 +1150,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     launch_hash0_only(blob, offsets, n_local, b, gh0, level_grids(n_local, 64 * level_words(N), gh0).gc, s);
   }
   ev_mark(c, s, "hash_count0");
-  Rec* const out = c->bucket;                  // this rank's settled (p, fp, pos) triples
+  Rec* const out = d.bm_out;                   // this rank's settled (p, fp, pos) triples
   unsigned long long* const out_cnt = d.small + 4096;
   HIPCHECK(hipMemsetAsync(out_cnt, 0, 8, s));
   // Level sizes: the host bounds n_L from above (mean q n + 6 sigma), so every collective's
@@ -1167,7 +1173,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     cm.allgather(d.bm_dec, d.bm_g, 8 * S, s);
     launch_bm_level_end(L, d.bm_g, wpad, c->bits, d.bm_bsum, d.bm_wpre, st, d.gslot, s);
     launch_bm_settle(L, c->kh, c->fp, pos, key_base, n_local, lin, np, st, d.bm_g, d.bm_wpre, out, out_cnt,
-                     c->bucket_cap, c->list[L & 1], d.cap_list, s);
+                     d.bm_cap_out, c->list[L & 1], d.cap_list, s);
     ev_mark(c, s, L == 0 ? "level0" : "levels");
     const double nbn = nb * q + 6.0 * std::sqrt(nb) + 64.0;
     npred *= q;
@@ -1194,6 +1200,9 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     total += cnt[r];
     maxc = std::max(maxc, cnt[r]);
   }
+  if (c->debug)
+    std::fprintf(stderr, "[s3imph] rank %d bitmap: %d sharded levels, replicated %llu records, flags 0x%x\n", R, Ls,
+                 (unsigned long long)total, flags);
   if (flags & kStBitmapBound) return kDistRetry;  // a global fact: every rank returns here
   if (flags & kStOverflow) {
     *msg = "build MPHF: bitmap decomposition: list capacity exceeded";
@@ -1248,6 +1257,13 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     settled += M[3 * r + 2];
   }
   const LevelState& hs = *c->h_st;
+  if (c->debug) {
+    std::fprintf(stderr, "[s3imph] rank %d bitmap: after tail flags 0x%x settled %llu tail ranked %llu nlevels %u\n  n:",
+                 R, flags, (unsigned long long)settled, (unsigned long long)hs.rank_total, hs.nlevels);
+    for (int l = 0; l <= (int)hs.nlevels + 1 && l < kMaxLevels; ++l)
+      std::fprintf(stderr, " %llu/%llu", (unsigned long long)hs.n[l], (unsigned long long)hs.lvl_base[l]);
+    std::fprintf(stderr, "\n");
+  }
   if (flags & (kStGeometry | kStTailOverflow | kStResOverflow)) return kDistRetry;
   if (flags & kStTooManyLevels) {
     const unsigned nl = hs.stop_level ? hs.stop_level : hs.nlevels;

@@ -95,6 +95,8 @@ struct DistState {
   unsigned* bm_wpre = nullptr;
   unsigned long long* bm_bsum = nullptr;
   uint64_t bm_cap_words = 0;
+  Rec* bm_out = nullptr;  // this rank's settled (p, fp, pos) triples (the tail's tile kernels own the bucket)
+  uint64_t bm_cap_out = 0;
   int mode = kDistRoute;
   // level 0's exchange runs on its own stream, chunk by chunk, beside the next chunk's hash
   hipStream_t xs = nullptr;

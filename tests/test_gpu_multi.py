@@ -62,12 +62,15 @@ def test_thread_per_rank_shared_gpu(s3, oracle_lib, monkeypatch, ranks, kind, av
     assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
 
 
-def test_one_gpu_sharded_bitmap_over_rccl(s3, oracle_lib, monkeypatch):
+@pytest.mark.parametrize("switch,n", [(20_000, 1_500_000), (2 << 20, 4_000_000)])
+def test_one_gpu_sharded_bitmap_over_rccl(s3, oracle_lib, monkeypatch, switch, n):
     """The bitmap decomposition on an in-process RCCL communicator (one rank):
-    ncclReduceScatter of the count lanes and ncclAllGather of the final bits per level."""
-    monkeypatch.setenv("S3IMPH_DIST_SWITCH", "20000")
+    ncclReduceScatter of the count lanes and ncclAllGather of the final bits per level;
+    a tiny replicated tail (switch 20k) and a 1.5M-record one (the default 2M switch: the
+    tail's scatter / tile kernels run beside the held settled triples)."""
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", str(switch))
     monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
-    blob, offs = s3.gen_keys(0, 16, 40, 0, 1_500_000)
+    blob, offs = s3.gen_keys(0, 16, 40, 0, n)
     fp, po, mph = _expect(oracle_lib, blob, offs)
     for _ in range(2):
         g = s3.build_host(blob, offs, num_gpus=1, flags=s3.MULTI_FORCE_SHARDED | s3.MULTI_BITMAP)
