@@ -597,9 +597,14 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
                                                        uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
                                                        unsigned long long* __restrict__ flags,
                                                        unsigned long long* __restrict__ sflags, LevelState* st,
-                                                       unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt) {
+                                                       unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt,
+                                                       unsigned long long* __restrict__ prof) {
   extern __shared__ __align__(16) unsigned char sk_lds[];
   if (!st->skew) return;  // k_hash0_pair hashed this near-uniform set
+  // prof (S3IMPH_DEBUG): per wave, shader cycles total / hashing / waiting for a chunk's
+  // loads / the rest (sort, tickets, barriers, write-back)
+  const unsigned long long pt0 = __builtin_amdgcn_s_memtime(), prt0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long p_hash = 0, p_wait = 0, p_sort = 0, p_end = 0;
   uint4* stage = reinterpret_cast<uint4*>(sk_lds);
   uint64_t* res_a = reinterpret_cast<uint64_t*>(sk_lds + kSkStage);
   uint64_t* res_b = res_a + kSkG;
@@ -627,6 +632,7 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
   bool zero = false;
   constexpr int KPT = kSkG / kSkT;  // keys per thread in the sort
   for (uint64_t grp = gbeg; grp < gend; grp += kSkG) {
+    const unsigned long long g0t = prof ? __builtin_amdgcn_s_memtime() : 0;
     const unsigned m = (unsigned)min<uint64_t>(kSkG, gend - grp);
     // ---- counting sort of the group's keys by length (ascending)
     for (unsigned c = tid; c < kSkLB; c += kSkT) cnt[c] = 0;
@@ -682,7 +688,8 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
       uint64_t ks, ke, kbase;
       uint64_t lb[kSkU], le[kSkU];  // the keys this lane loads for: key 16t + lane/4, unit lane%4
     };
-    auto take = [&](Batch& x) {
+    // issue: the ticket, the batch's sorted slots and its keys' offsets (loads in flight)
+    auto take_issue = [&](Batch& x) {
       unsigned b = 0;
       if (lane == 0) b = atomicAdd(next, 1u);
       x.b = __shfl(b, 0);
@@ -693,6 +700,10 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
       x.k = x.valid ? sidx[slot] : 0u;
       x.ks = x.valid ? offsets[grp + x.k] : 0;
       x.ke = x.valid ? offsets[grp + x.k + 1] : 0;
+    };
+    // finish (uses the offsets): the wave's step count and the cooperative load addresses
+    auto take_finish = [&](Batch& x) {
+      if (x.b >= nb) return;
       x.kbase = x.ks & ~15ull;
       const uint64_t span = x.valid ? x.ke - x.kbase : 0;
       unsigned steps = (unsigned)((span + kSkC - 1) / kSkC);
@@ -707,29 +718,38 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
       }
     };
     uint4 r[kSkU];
+    // One 16-byte load per unit.  Units are 16-byte aligned; only a unit at end8 - 8 (when
+    // end8 = 8 mod 16) would run past the readable blob: it takes the 8 bytes left in a
+    // separate (non-temporal) load, so the compiler cannot fold the two into one split load.
     auto load = [&](const Batch& x, unsigned step) {
 #pragma unroll
       for (int t = 0; t < kSkU; ++t) {
         const uint64_t a = x.lb[t] + (uint64_t)step * kSkC + 16u * u;
-        r[t] = make_uint4(0, 0, 0, 0);
-        if (a < x.le[t]) {
-          if (a + 16 <= end8) {
-            r[t] = *reinterpret_cast<const uint4*>(blob + a);
-          } else {  // the blob's last 8 readable bytes
-            const uint2 h2 = *reinterpret_cast<const uint2*>(blob + a);
-            r[t].x = h2.x;
-            r[t].y = h2.y;
-          }
+        const bool in = a < x.le[t], full = a + 16 <= end8;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (in && full) v = *reinterpret_cast<const uint4*>(blob + a);
+        if (in && !full) {
+          const uint64_t h = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(blob + a));
+          v = make_uint4((uint32_t)h, (uint32_t)(h >> 32), 0u, 0u);
         }
+        r[t] = v;
       }
     };
+    if (prof) p_sort += __builtin_amdgcn_s_memtime() - g0t;
+    // Two batches in flight: the next batch's ticket and offsets are requested at the current
+    // batch's first step, its first chunk at the current batch's last step (before hashing it).
     Batch cur, nxt;
-    take(cur);
+    take_issue(cur);
+    take_finish(cur);
     if (cur.b < nb) load(cur, 0);
     while (cur.b < nb) {
       uint32_t alo = (uint32_t)kFnvOffset, ahi = (uint32_t)(kFnvOffset >> 32), blo = alo, bhi = ahi;
-      nxt.b = nb;
       for (unsigned step = 0; step < cur.steps; ++step) {
+        if (prof) {
+          const unsigned long long w0 = __builtin_amdgcn_s_memtime();
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          p_wait += __builtin_amdgcn_s_memtime() - w0;
+        }
 #pragma unroll
         for (int t = 0; t < kSkU; ++t) wst[(16 * t + (lane >> 2)) * (kSkS / 16) + u] = r[t];
         // LDS operations of one wave complete in order: the lanes' reads below see every
@@ -737,18 +757,21 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (step == 0) take_issue(nxt);
         if (step + 1 < cur.steps) {
           load(cur, step + 1);
         } else {
-          take(nxt);
+          take_finish(nxt);
           if (nxt.b < nb) load(nxt, 0);
         }
         const uint64_t clo = cur.kbase + (uint64_t)step * kSkC;
+        const unsigned long long h0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         if (cur.ke > clo) {
           const unsigned o = step == 0 ? (unsigned)(cur.ks - cur.kbase) : 0u;
           const unsigned top = (unsigned)min<uint64_t>(cur.ke - clo, kSkC);
           fnv_window_cont(wst32 + lane * (kSkS / 4), o, top - o, alo, ahi, blo, bhi);
         }
+        if (prof) p_hash += __builtin_amdgcn_s_memtime() - h0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -759,6 +782,7 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
       }
       cur = nxt;
     }
+    const unsigned long long e0t = prof ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();
     for (unsigned k = tid; k < m; k += kSkT) {
       const uint64_t a = res_a[k];
@@ -767,6 +791,19 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
       zero |= a == 0;
     }
     __syncthreads();  // the next group reuses cnt / sidx / res
+    if (prof) p_end += __builtin_amdgcn_s_memtime() - e0t;
+  }
+  if (prof && lane == 0 && (uint64_t)blockIdx.x * (kSkT / 64) + wave < 8192) {
+    const unsigned long long tot = __builtin_amdgcn_s_memtime() - pt0, prt1 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* q = prof + ((uint64_t)blockIdx.x * (kSkT / 64) + wave) * 8;
+    q[0] = tot;
+    q[1] = p_hash;
+    q[2] = p_wait;
+    q[3] = tot - p_hash - p_wait;
+    q[4] = prt1 - prt0;
+    q[5] = prt0;
+    q[6] = prt1;
+    q[7] = (p_sort << 32) | (p_end & 0xffffffffull);  // group phases: sort | barrier + write-back
   }
   if (zero) atomicOr(&st->status, kStKeyZero);
 }
@@ -2990,7 +3027,7 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       k_hash0_pair<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
                                                              g.tb, g.chunk, b.tcnt, prof);
       k_hash_skew<<<256, kSkT, kSkLds, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk,
-                                            b.tcnt);
+                                            b.tcnt, prof);
       return;
     }
     k_hash_count0<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, histogram ? b.hist : nullptr,
@@ -3007,7 +3044,7 @@ void launch_hash0_only(const uint8_t* blob, const uint64_t* offsets, uint64_t n,
     k_hash0_pair<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
                                                            g.tb, g.chunk, b.tcnt, nullptr);
     k_hash_skew<<<256, kSkT, kSkLds, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk,
-                                          b.tcnt);
+                                          b.tcnt, nullptr);
     return;
   }
   k_hash_count0<<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
@@ -3021,7 +3058,7 @@ void launch_hash0_route(const uint8_t* blob, const uint64_t* offsets, uint64_t n
                                                                  b.st, g.tb, g.chunk, b.tcnt, nullptr, rt);
     // a skewed set (st->skew): k_hash_skew's length-sorted batches, then k_route
     k_hash_skew<<<256, kSkT, kSkLds, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk,
-                                          b.tcnt);
+                                          b.tcnt, nullptr);
     launch_route0_arrays(b.kh, b.fp, n, rt, b.st, true, s);
     return;
   }

@@ -225,7 +225,12 @@ __global__ __launch_bounds__(kBT) void k_bm_pass3(const uint64_t* __restrict__ g
 
 // Settle this rank's level-L records against the final bits: placed records leave as
 // (p, fp, pos) triples (Rec with k = p) in `out`, the others go to the next level's list
-// (st->n[L+1] counts them).  Slots are taken one atomic per wave.
+// (st->n[L+1] counts them).  A block takes kSetQ x kBT consecutive records at a time:
+// the first sweep counts each (wave, round)'s placed / collided records, one atomic per
+// counter reserves the block's runs, and the second sweep (records and final-bit words
+// again, from L2) writes every wave-round as one contiguous run.  Same-address device
+// atomics serialise (~12 ns each): one per wave made this stage 20x slower.
+constexpr int kSetQ = 16;
 template <int kSrc>
 __global__ __launch_bounds__(kBT) void k_bm_settle(int level, const uint64_t* __restrict__ kh,
                                                    const uint64_t* __restrict__ fp, const uint64_t* __restrict__ pos,
@@ -234,55 +239,92 @@ __global__ __launch_bounds__(kBT) void k_bm_settle(int level, const uint64_t* __
                                                    const unsigned* __restrict__ wpre, Rec* __restrict__ out,
                                                    unsigned long long* __restrict__ out_cnt, uint64_t out_cap,
                                                    Rec* __restrict__ next, uint64_t next_cap) {
+  constexpr int NW = kBT / 64;
+  __shared__ unsigned s_cp[NW * kSetQ], s_cn[NW * kSetQ];
+  __shared__ unsigned long long s_bp, s_bn;
   if (bm_dead(st)) return;
   const uint64_t n = bm_count<kSrc>(level, n_keys, st);
   const uint64_t words = st->words[level], magic = st->magic[level], seed = level_seed(level);
   const uint64_t base = st->lvl_base[level];
-  const unsigned lane = lane_id();
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   bool over = false;
-  const uint64_t stride = (uint64_t)gridDim.x * kBT;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * kBT + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
-    const uint64_t i = i0 + lane;
-    const bool valid = i < n;
-    Rec r{0, 0, 0};
-    bool placed = false;
-    uint64_t p = 0;
-    if (valid) {
-      if (kSrc == 2) {
-        r = Rec{kh[i], fp[i], pos ? pos[i] : pos_base + i};
-      } else {
-        r = ilist[i];
+  auto rec_at = [&](uint64_t i) -> Rec {
+    if (kSrc == 2) return Rec{kh[i], fp[i], pos ? pos[i] : pos_base + i};
+    return ilist[i];
+  };
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kSetQ * kBT; c0 < n; c0 += (uint64_t)gridDim.x * kSetQ * kBT) {
+    // sweep 1: counts per (wave, round)
+#pragma unroll 4
+    for (int q = 0; q < kSetQ; ++q) {
+      const uint64_t i = c0 + (uint64_t)q * kBT + tid;
+      bool placed = false;
+      if (i < n) {
+        const uint64_t x = bb_index(seed, kSrc == 2 ? kh[i] : ilist[i].k, words, magic);
+        placed = (g[x >> 6] >> (x & 63)) & 1ull;
       }
-      const uint64_t x = bb_index(seed, r.k, words, magic);
-      const uint64_t v = g[x >> 6];
-      const unsigned b = (unsigned)(x & 63);
-      placed = (v >> b) & 1ull;
-      if (placed) p = base + wpre[x >> 6] + (uint64_t)__popcll(v & ((1ull << b) - 1ull));
+      const uint64_t pm = __ballot(i < n && placed), nm = __ballot(i < n && !placed);
+      if (lane == 0) {
+        s_cp[wave * kSetQ + q] = (unsigned)__popcll(pm);
+        s_cn[wave * kSetQ + q] = (unsigned)__popcll(nm);
+      }
     }
-    const uint64_t pm = __ballot(valid && placed), nm = __ballot(valid && !placed);
-    unsigned long long po = 0, no = 0;
-    if (lane == 0) {
-      if (pm) po = atomicAdd(out_cnt, (unsigned long long)__popcll(pm));
-      if (nm) no = atomicAdd(&st->n[level + 1], (unsigned long long)__popcll(nm));
+    __syncthreads();
+    if (tid < 64) {  // exclusive scans of the NW x kSetQ (<= 64) entries, and the reservations
+      const unsigned cp = tid < NW * kSetQ ? s_cp[tid] : 0u, cn = tid < NW * kSetQ ? s_cn[tid] : 0u;
+      unsigned xp = cp, xn = cn;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned yp = __shfl_up(xp, d), yn = __shfl_up(xn, d);
+        if (tid >= (unsigned)d) {
+          xp += yp;
+          xn += yn;
+        }
+      }
+      if (tid < NW * kSetQ) {
+        s_cp[tid] = xp - cp;
+        s_cn[tid] = xn - cn;
+      }
+      const unsigned tp = __shfl(xp, 63), tn = __shfl(xn, 63);
+      if (tid == 0) {
+        s_bp = tp ? atomicAdd(out_cnt, (unsigned long long)tp) : 0ull;
+        s_bn = tn ? atomicAdd(&st->n[level + 1], (unsigned long long)tn) : 0ull;
+      }
     }
-    po = __shfl(po, 0);
-    no = __shfl(no, 0);
-    if (valid) {
+    __syncthreads();
+    // sweep 2: every wave-round writes its runs
+#pragma unroll 2
+    for (int q = 0; q < kSetQ; ++q) {
+      const uint64_t i = c0 + (uint64_t)q * kBT + tid;
+      Rec r{0, 0, 0};
+      bool placed = false;
+      uint64_t p = 0;
+      if (i < n) {
+        r = rec_at(i);
+        const uint64_t x = bb_index(seed, r.k, words, magic);
+        const uint64_t v = g[x >> 6];
+        const unsigned b = (unsigned)(x & 63);
+        placed = (v >> b) & 1ull;
+        if (placed) p = base + wpre[x >> 6] + (uint64_t)__popcll(v & ((1ull << b) - 1ull));
+      }
+      const uint64_t pm = __ballot(i < n && placed), nm = __ballot(i < n && !placed);
       const uint64_t lt = lanemask_lt();
-      if (placed) {
-        const uint64_t slot = po + (uint64_t)__popcll(pm & lt);
-        if (slot < out_cap)
-          out[slot] = Rec{p, r.f, r.p};
-        else
-          over = true;
-      } else {
-        const uint64_t slot = no + (uint64_t)__popcll(nm & lt);
-        if (slot < next_cap)
-          next[slot] = r;
-        else
-          over = true;
+      if (i < n) {
+        if (placed) {
+          const uint64_t slot = s_bp + s_cp[wave * kSetQ + q] + (uint64_t)__popcll(pm & lt);
+          if (slot < out_cap)
+            out[slot] = Rec{p, r.f, r.p};
+          else
+            over = true;
+        } else {
+          const uint64_t slot = s_bn + s_cn[wave * kSetQ + q] + (uint64_t)__popcll(nm & lt);
+          if (slot < next_cap)
+            next[slot] = r;
+          else
+            over = true;
+        }
       }
     }
+    __syncthreads();  // s_cp / s_cn / s_bp / s_bn are reused by the next chunk
   }
   if (over) atomicOr(&st->status, kStOverflow);
 }
@@ -434,11 +476,12 @@ void launch_bm_settle(int level, const uint64_t* kh, const uint64_t* fp, const u
                       const unsigned* wpre, Rec* out, unsigned long long* out_cnt, uint64_t out_cap, Rec* next,
                       uint64_t next_cap, hipStream_t s) {
   if (level == 0)
-    k_bm_settle<2><<<grid_for(n_keys, kBT, 8192), kBT, 0, s>>>(0, kh, fp, pos, pos_base, n_keys, nullptr, st, g,
-                                                                wpre, out, out_cnt, out_cap, next, next_cap);
+    k_bm_settle<2><<<grid_for(n_keys, kBT * kSetQ, 2048), kBT, 0, s>>>(0, kh, fp, pos, pos_base, n_keys, nullptr, st,
+                                                                        g, wpre, out, out_cnt, out_cap, next, next_cap);
   else
-    k_bm_settle<1><<<grid_for(n_pred, kBT, 8192), kBT, 0, s>>>(level, nullptr, nullptr, nullptr, 0, 0, list, st, g,
-                                                                wpre, out, out_cnt, out_cap, next, next_cap);
+    k_bm_settle<1><<<grid_for(n_pred, kBT * kSetQ, 2048), kBT, 0, s>>>(level, nullptr, nullptr, nullptr, 0, 0, list,
+                                                                        st, g, wpre, out, out_cnt, out_cap, next,
+                                                                        next_cap);
 }
 
 void launch_bm_route_out(const Rec* in, const unsigned long long* n_in, uint64_t n_pred, uint64_t slice, int P,

@@ -485,6 +485,17 @@ void print_tile_profile(s3imph_ctx* c) {
                    "%.1f%%, rest %.1f%%\n",
                    cnt, a[0] / cnt, a[4] / cnt / 100.0, a[4] ? 100.0 * a[0] / a[4] : 0.0, 100 * a[1] / a[0],
                    100 * a[2] / a[0], 100 * a[3] / a[0]);
+    if (cnt) {  // k_hash_skew: q[7] = group sort cycles << 32 | group-end (barrier + write-back) cycles
+      double gs = 0, ge = 0;
+      for (int w = 0; w < (int)(2 * kMaxTiles * 8 / 8); ++w)
+        if (q[8 * w]) {
+          gs += (double)(q[8 * w + 7] >> 32);
+          ge += (double)(q[8 * w + 7] & 0xffffffffull);
+        }
+      if (gs + ge > 0)
+        std::fprintf(stderr, "  hash_skew groups: sort %.1f%%, end barrier + write-back %.1f%% (wait = chunk loads)\n",
+                     100 * gs / a[0], 100 * ge / a[0]);
+    }
   }
   {  // k_mid_levels phase stamps: workgroup 0 and the last one, 8 per level
     const unsigned long long* m = &h[(size_t)(kMaxLevels - 4) * kMaxTiles * 8];

@@ -143,19 +143,21 @@ static __device__ __forceinline__ void fnv_window(const uint32_t* win, unsigned 
   const uint32_t* w = win + (o >> 2);
   const unsigned sb = o & 3u;
   const unsigned nfull = len >> 3;
-  uint32_t cur = w[0];
+  // the next stream word's dwords are read one iteration ahead, so the LDS latency hides
+  // behind the current word's 64 steps (reads stay within w[0 .. 2 nfull + 2], as the tail's)
+  uint32_t cur = w[0], n1 = w[1], n2 = w[2];
   for (unsigned q = 0; q < nfull; ++q) {
-    const uint32_t n1 = w[2 * q + 1], n2 = w[2 * q + 2];
+    const uint32_t m1 = w[2 * q + 3], m2 = w[2 * q + 4];
     fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n1, cur, sb));
     fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n2, n1, sb));
     cur = n2;
+    n1 = m1;
+    n2 = m2;
   }
   const unsigned rem = len & 7u;
-  if (rem) {
-    const uint32_t n1 = w[2 * nfull + 1], n2 = w[2 * nfull + 2];
+  if (rem)
     fnv_tail_b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n1, cur, sb), __builtin_amdgcn_alignbyte(n2, n1, sb),
                rem);
-  }
   ha = (uint64_t)alo | ((uint64_t)ahi << 32);
   hb = (uint64_t)blo | ((uint64_t)bhi << 32);
 }
@@ -167,19 +169,19 @@ static __device__ __forceinline__ void fnv_window_cont(const uint32_t* win, unsi
   const uint32_t* w = win + (o >> 2);
   const unsigned sb = o & 3u;
   const unsigned nfull = len >> 3;
-  uint32_t cur = w[0];
+  uint32_t cur = w[0], n1 = w[1], n2 = w[2];  // one stream word ahead, as fnv_window
   for (unsigned q = 0; q < nfull; ++q) {
-    const uint32_t n1 = w[2 * q + 1], n2 = w[2 * q + 2];
+    const uint32_t m1 = w[2 * q + 3], m2 = w[2 * q + 4];
     fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n1, cur, sb));
     fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n2, n1, sb));
     cur = n2;
+    n1 = m1;
+    n2 = m2;
   }
   const unsigned rem = len & 7u;
-  if (rem) {
-    const uint32_t n1 = w[2 * nfull + 1], n2 = w[2 * nfull + 2];
+  if (rem)
     fnv_tail_b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n1, cur, sb), __builtin_amdgcn_alignbyte(n2, n1, sb),
                rem);
-  }
 }
 
 // FNV-1a and FNV-1 over the 8 bytes of v, little-endian order.
