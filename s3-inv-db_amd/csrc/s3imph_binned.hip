@@ -580,32 +580,40 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
 // chunk from LDS with the funnel step of fnv_window.  Results go to LDS by key and leave
 // in key order with coalesced stores.  (Simulated over C5's lengths: 95 % of lane-steps do
 // work with 4096-key groups, 82 % with 1024.)
-constexpr int kSkT = 1024;             // threads (16 waves, one block per CU)
-constexpr int kSkG = 4096;             // keys per sorted group
 constexpr int kSkC = 64;               // chunk bytes per key per step
 constexpr int kSkS = kSkC + 16;        // LDS stride per key (16-B aligned for ds_write_b128)
 constexpr int kSkU = kSkC / 16;        // 16-byte units per key chunk = loads per step
 constexpr unsigned kSkLB = 256;        // length classes (4 B each)
-constexpr size_t kSkStage = (size_t)(kSkT / 64) * 64 * kSkS;
-constexpr size_t kSkLds = kSkStage + 2 * kSkG * sizeof(uint64_t) + kSkG * sizeof(unsigned short) +
-                          kSkLB * sizeof(unsigned) + 16;
-static_assert(kSkLds <= 160 * 1024, "k_hash_skew's LDS");
+// kSkT threads, kSkG keys per sorted group: 1024 / 4096 (one block per CU) or 512 / 2048
+// (two per CU: one block's sort and group barrier overlap the other's hashing)
+template <int kSkT, int kSkG>
+constexpr size_t sk_stage_bytes() { return (size_t)(kSkT / 64) * 64 * kSkS; }
+template <int kSkT, int kSkG>
+constexpr size_t sk_lds_bytes() {
+  return sk_stage_bytes<kSkT, kSkG>() + 2 * kSkG * sizeof(uint64_t) + kSkG * sizeof(unsigned short) +
+         kSkLB * sizeof(unsigned) + 16;
+}
+static_assert(sk_lds_bytes<1024, 4096>() <= 160 * 1024, "k_hash_skew's LDS");
+static_assert(2 * sk_lds_bytes<512, 2048>() <= 160 * 1024, "k_hash_skew's LDS, two blocks per CU");
 static_assert(kSkU * 16 == 64, "a load instruction covers 16 keys x 64 B");
 
-__global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict__ blob,
+template <int kSkT, int kSkG>
+__global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict__ blob,
                                                        const uint64_t* __restrict__ offsets, uint64_t n,
                                                        uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
                                                        unsigned long long* __restrict__ flags,
                                                        unsigned long long* __restrict__ sflags, LevelState* st,
                                                        unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt,
-                                                       unsigned long long* __restrict__ prof) {
+                                                       unsigned long long* __restrict__ prof, int order) {
   extern __shared__ __align__(16) unsigned char sk_lds[];
   if (!st->skew) return;  // k_hash0_pair hashed this near-uniform set
+  const bool interleave = order == 0;
   // prof (S3IMPH_DEBUG): per wave, shader cycles total / hashing / waiting for a chunk's
   // loads / the rest (sort, tickets, barriers, write-back)
   const unsigned long long pt0 = __builtin_amdgcn_s_memtime(), prt0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long p_hash = 0, p_wait = 0, p_sort = 0, p_end = 0;
   uint4* stage = reinterpret_cast<uint4*>(sk_lds);
+  constexpr size_t kSkStage = sk_stage_bytes<kSkT, kSkG>();
   uint64_t* res_a = reinterpret_cast<uint64_t*>(sk_lds + kSkStage);
   uint64_t* res_b = res_a + kSkG;
   unsigned short* sidx = reinterpret_cast<unsigned short*>(res_b + kSkG);
@@ -682,31 +690,44 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
     // of a batch hides behind the previous batch's hashing.
     const unsigned nb = (m + 63) / 64;
     const unsigned u = lane & 3u;
+    // Key offsets relative to the group's 16-byte aligned first byte gb fit 32 bits (a group
+    // of more than 4 GiB of key bytes is refused), which keeps two batches in registers.
+    const uint64_t gb = uniform64(offsets[grp] & ~15ull);
+    const uint64_t gspan = offsets[grp + m] - gb;
+    if (gspan >= 0xffff0000ull) {
+      if (tid == 0) atomicOr(&st->status, kStGeometry);
+      break;
+    }
+    const uint8_t* gblob = blob + gb;
+    const uint32_t end8r = (uint32_t)min<uint64_t>(end8 - gb, 0xffffffffull);
     struct Batch {
       unsigned b, k, steps;
       bool valid;
-      uint64_t ks, ke, kbase;
-      uint64_t lb[kSkU], le[kSkU];  // the keys this lane loads for: key 16t + lane/4, unit lane%4
+      uint32_t ks, ke, kbase;
+      uint32_t lb[kSkU], le[kSkU];  // the keys this lane loads for: key 16t + lane/4, unit lane%4
     };
     // issue: the ticket, the batch's sorted slots and its keys' offsets (loads in flight)
     auto take_issue = [&](Batch& x) {
-      unsigned b = 0;
-      if (lane == 0) b = atomicAdd(next, 1u);
-      x.b = __shfl(b, 0);
+      unsigned t = 0;
+      if (lane == 0) t = atomicAdd(next, 1u);
+      t = __shfl(t, 0);
+      // longest batch first (LPT); the alternative alternates the longest and the shortest
+      // batch left (measured worse on C5: the group barrier waited 33 % vs 17 %)
+      x.b = t >= nb ? nb : (!interleave ? t : (t & 1u) ? nb - 1 - (t >> 1) : (t >> 1));
       if (x.b >= nb) return;
       const int hi = (int)m - 64 * (int)x.b;  // sorted slots [hi - 64, hi)
       const int slot = hi - 64 + (int)lane;
       x.valid = slot >= 0;
       x.k = x.valid ? sidx[slot] : 0u;
-      x.ks = x.valid ? offsets[grp + x.k] : 0;
-      x.ke = x.valid ? offsets[grp + x.k + 1] : 0;
+      x.ks = x.valid ? (uint32_t)(offsets[grp + x.k] - gb) : 0u;
+      x.ke = x.valid ? (uint32_t)(offsets[grp + x.k + 1] - gb) : 0u;
     };
     // finish (uses the offsets): the wave's step count and the cooperative load addresses
     auto take_finish = [&](Batch& x) {
       if (x.b >= nb) return;
-      x.kbase = x.ks & ~15ull;
-      const uint64_t span = x.valid ? x.ke - x.kbase : 0;
-      unsigned steps = (unsigned)((span + kSkC - 1) / kSkC);
+      x.kbase = x.ks & ~15u;
+      const uint32_t span = x.valid ? x.ke - x.kbase : 0u;
+      unsigned steps = (span + kSkC - 1) / kSkC;
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) steps = max(steps, (unsigned)__shfl_xor(steps, d));
       x.steps = max(steps, 1u);  // >= 1: the step loop takes the next ticket
@@ -714,7 +735,7 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
       for (int t = 0; t < kSkU; ++t) {
         const int src = 16 * t + (int)(lane >> 2);
         x.lb[t] = __shfl(x.kbase, src);
-        x.le[t] = __shfl(x.valid ? x.ke : 0ull, src);
+        x.le[t] = __shfl(x.valid ? x.ke : 0u, src);
       }
     };
     uint4 r[kSkU];
@@ -724,12 +745,12 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
     auto load = [&](const Batch& x, unsigned step) {
 #pragma unroll
       for (int t = 0; t < kSkU; ++t) {
-        const uint64_t a = x.lb[t] + (uint64_t)step * kSkC + 16u * u;
-        const bool in = a < x.le[t], full = a + 16 <= end8;
+        const uint32_t a = x.lb[t] + step * kSkC + 16u * u;
+        const bool in = a < x.le[t], full = (uint64_t)a + 16 <= end8r;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (in && full) v = *reinterpret_cast<const uint4*>(blob + a);
+        if (in && full) v = *reinterpret_cast<const uint4*>(gblob + a);
         if (in && !full) {
-          const uint64_t h = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(blob + a));
+          const uint64_t h = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(gblob + a));
           v = make_uint4((uint32_t)h, (uint32_t)(h >> 32), 0u, 0u);
         }
         r[t] = v;
@@ -764,11 +785,11 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
           take_finish(nxt);
           if (nxt.b < nb) load(nxt, 0);
         }
-        const uint64_t clo = cur.kbase + (uint64_t)step * kSkC;
+        const uint32_t clo = cur.kbase + step * kSkC;
         const unsigned long long h0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         if (cur.ke > clo) {
-          const unsigned o = step == 0 ? (unsigned)(cur.ks - cur.kbase) : 0u;
-          const unsigned top = (unsigned)min<uint64_t>(cur.ke - clo, kSkC);
+          const unsigned o = step == 0 ? cur.ks - cur.kbase : 0u;
+          const unsigned top = min(cur.ke - clo, (uint32_t)kSkC);
           fnv_window_cont(wst32 + lane * (kSkS / 4), o, top - o, alo, ahi, blo, bhi);
         }
         if (prof) p_hash += __builtin_amdgcn_s_memtime() - h0;
@@ -776,6 +797,9 @@ __global__ __launch_bounds__(kSkT, 1) void k_hash_skew(const uint8_t* __restrict
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
+      // results by key in LDS, written back in key order with coalesced stores (each lane's
+      // own 8-byte stores cost more: they count against vmcnt, which every step waits on,
+      // 1.64 -> 2.11 ms on C5 even with 8192-key groups in the freed LDS)
       if (cur.valid) {
         res_a[cur.k] = (uint64_t)alo | ((uint64_t)ahi << 32);
         res_b[cur.k] = (uint64_t)blo | ((uint64_t)bhi << 32);
@@ -3005,8 +3029,33 @@ size_t tile_lds_bytes(unsigned tb) {
 
 uint64_t split_scratch_records() { return split_scratch_recs(); }
 
+// The skewed-length level-0 hash (a no-op launch unless st->skew).  A/B knobs:
+// S3IMPH_SKEW_CFG=0 selects two 512-thread blocks per CU (2048-key groups) instead of one
+// 1024-thread block (4096-key groups; measured 1.64 vs 1.75 ms on C5), S3IMPH_SKEW_ORDER=0
+// alternates the longest and the shortest batch instead of longest first.
+void launch_hash_skew(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
+                      unsigned long long* prof, hipStream_t s) {
+  static const int cfg = [] {
+    const char* e = std::getenv("S3IMPH_SKEW_CFG");
+    return e ? std::atoi(e) : 1;
+  }();
+  static const int order = [] {  // 1: longest first; 0: alternating longest / shortest
+    const char* e = std::getenv("S3IMPH_SKEW_ORDER");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (cfg == 1)
+    k_hash_skew<1024, 4096><<<256, 1024, sk_lds_bytes<1024, 4096>(), s>>>(
+        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order);
+  else
+    k_hash_skew<512, 2048><<<512, 512, sk_lds_bytes<512, 2048>(), s>>>(
+        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order);
+}
+
 void binned_set_lds_limits() {
-  (void)hipFuncSetAttribute((const void*)k_hash_skew, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSkLds);
+  (void)hipFuncSetAttribute((const void*)k_hash_skew<1024, 4096>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sk_lds_bytes<1024, 4096>());
+  (void)hipFuncSetAttribute((const void*)k_hash_skew<512, 2048>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sk_lds_bytes<512, 2048>());
   (void)hipFuncSetAttribute((const void*)k_tile<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)std::max(tile_lds_bytes(kTileMaxBits), tile_lds_bytes(kCacheBits)));
   (void)hipFuncSetAttribute((const void*)k_tile_reg<512, 20, 2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3026,8 +3075,7 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       unsigned long long* prof = b.tile_prof ? b.tile_prof + (uint64_t)(kMaxLevels - 3) * kMaxTiles * 8 : nullptr;
       k_hash0_pair<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
                                                              g.tb, g.chunk, b.tcnt, prof);
-      k_hash_skew<<<256, kSkT, kSkLds, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk,
-                                            b.tcnt, prof);
+      launch_hash_skew(blob, offsets, n, b, g, prof, s);
       return;
     }
     k_hash_count0<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, histogram ? b.hist : nullptr,
@@ -3043,8 +3091,7 @@ void launch_hash0_only(const uint8_t* blob, const uint64_t* offsets, uint64_t n,
   if (((uintptr_t)blob & 15) == 0) {  // as the single-GPU level 0: pair rounds unless st->skew
     k_hash0_pair<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
                                                            g.tb, g.chunk, b.tcnt, nullptr);
-    k_hash_skew<<<256, kSkT, kSkLds, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk,
-                                          b.tcnt, nullptr);
+    launch_hash_skew(blob, offsets, n, b, g, nullptr, s);
     return;
   }
   k_hash_count0<<<grid, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, nullptr, b.flags, b.sflags, b.st, g.tb,
@@ -3057,8 +3104,7 @@ void launch_hash0_route(const uint8_t* blob, const uint64_t* offsets, uint64_t n
     k_hash0_pair<kH0T, kH0B, true, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags,
                                                                  b.st, g.tb, g.chunk, b.tcnt, nullptr, rt);
     // a skewed set (st->skew): k_hash_skew's length-sorted batches, then k_route
-    k_hash_skew<<<256, kSkT, kSkLds, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk,
-                                          b.tcnt, nullptr);
+    launch_hash_skew(blob, offsets, n, b, g, nullptr, s);
     launch_route0_arrays(b.kh, b.fp, n, rt, b.st, true, s);
     return;
   }
