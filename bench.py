@@ -182,6 +182,12 @@ def main() -> None:
         key_bytes = key_bytes_local
     n_global = plan.n_global
     stages = {k: v / prof_steps for k, v in stage_sum.items()}
+    # The other decomposition of the sharded levels, timed the same way on the same keys
+    # (N > 1 only; beside `value`, never as it): the driver's multi-GPU runs then measure
+    # both the routed build and the per-level collision-bitmap reduction over RCCL.
+    alt = None
+    if world > 1 and not args.headline_only:
+        alt = alt_decomposition(s3imph, ctx, step, args, barrier, dist)
 
     if rank != 0:
         if dist is not None:
@@ -245,6 +251,9 @@ def main() -> None:
                                        "unit": "T byte-steps/s", "frac": steps_per_s / 1e12 / FNV_STEP_PEAK_T,
                                        "hbm": hbm})
         result["dominant_stage"] = max(stages, key=stages.get)
+    if alt is not None:
+        result["alt_decomposition"] = {**alt, "keys_per_s": n_global / alt["ms_per_step"] * 1e3
+                                       if alt.get("ms_per_step") else None}
     if world == 1 and not use_dist and not args.headline_only:
         result["lookup"] = lookup_rate(ctx, d_blob, d_offs, n, d_fp, d_po)
         result["finalize"] = finalize_rate(ctx, d_blob, d_offs, n)
@@ -261,6 +270,43 @@ def main() -> None:
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def alt_decomposition(s3imph, ctx, step, args, barrier, dist) -> dict:
+    """Time the decomposition bench.py was not asked for (route <-> bitmap) over the same
+    shards: min(steps, 5) builds after one warm-up, max over ranks.  The bitmap attempt runs
+    with S3IMPH_DIST_STRICT so a miss of its size bounds is reported, not timed as routing."""
+    import torch
+    other = "bitmap" if args.decomp == "route" else "route"
+    ctx.set_mode(s3imph.DIST_BITMAP if other == "bitmap" else s3imph.DIST_ROUTE)
+    os.environ["S3IMPH_DIST_STRICT"] = "1"
+    res = {"decomposition": other}
+    dt, err = -1.0, None
+    try:
+        step()
+        k = min(args.steps, 5)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        dt = (time.perf_counter() - t0) / k
+        res["steps"] = k
+    except s3imph.MPHFError as e:  # a bound miss is a global fact: every rank lands here
+        err = str(e)
+    finally:
+        del os.environ["S3IMPH_DIST_STRICT"]
+        ctx.set_mode(s3imph.DIST_BITMAP if args.decomp == "bitmap" else s3imph.DIST_ROUTE)
+    tt = torch.tensor([dt if err is None else -1.0], dtype=torch.float64)
+    fl = torch.tensor([0 if err is None else 1], dtype=torch.int64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dist.all_reduce(fl)
+    res["ms_per_step"] = float(tt.item()) * 1e3 if int(fl.item()) == 0 else None
+    if err is not None:
+        res["error"] = err
+    return res
 
 
 def lookup_rate(ctx, d_blob, d_offs, n: int, d_fp, d_po, reps: int = 5) -> dict:

@@ -31,61 +31,10 @@ namespace s3imph {
 namespace {
 
 constexpr int kBT = 256;
-constexpr int kBScanPer = 8;                     // words per thread in the word-prefix passes
-constexpr int kBScanBlock = kBT * kBScanPer;     // 2048 words per block
-constexpr int kBTopT = 1024;                     // the single-block scan of block sums
-constexpr int kBTopPer = 32;                     // ... 32 per thread: up to 32768 blocks (67M words)
-
-// Level L's records: kSrc 2 = level 0 from the hash kernel's key-order arrays (n_keys of
-// them, positions pos[i] or pos_base + i); kSrc 1 = the list of this rank's records that
-// collided at L-1 (st->n[L] of them).
-template <int kSrc>
-__device__ __forceinline__ uint64_t bm_count(int level, uint64_t n_keys, const LevelState* st) {
-  return kSrc == 2 ? n_keys : st->n[level];
-}
+constexpr int kBTopT = 1024;                     // the single-block scan of tile totals
 
 // The level's size is outside the host's bound (or the level flagged earlier): skip.
 __device__ __forceinline__ bool bm_dead(const LevelState* st) { return (st->status & kStBitmapBound) != 0; }
-
-template <int kSrc>
-__global__ __launch_bounds__(kBT) void k_bm_mark(int level, const uint64_t* __restrict__ kh, uint64_t n_keys,
-                                                 const Rec* __restrict__ ilist, const LevelState* st,
-                                                 unsigned* __restrict__ A32, unsigned* __restrict__ C32) {
-  if (bm_dead(st)) return;
-  const uint64_t n = bm_count<kSrc>(level, n_keys, st);
-  const uint64_t words = st->words[level], magic = st->magic[level], seed = level_seed(level);
-  for (uint64_t i = (uint64_t)blockIdx.x * kBT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBT) {
-    const uint64_t k = kSrc == 2 ? kh[i] : ilist[i].k;
-    const uint64_t x = bb_index(seed, k, words, magic);
-    const unsigned bit = 1u << (x & 31);
-    const unsigned old = atomicOr(&A32[x >> 5], bit);
-    if (old & bit) atomicOr(&C32[x >> 5], bit);  // a second key here: local count >= 2
-  }
-}
-
-// 4 bits -> 4 bytes (bit j of v -> byte j)
-__device__ __forceinline__ unsigned spread4(unsigned v) {
-  return (v & 1u) | ((v & 2u) << 7) | ((v & 4u) << 14) | ((v & 8u) << 21);
-}
-
-// Count lanes: byte x = A bit x + C bit x = min(local count, 2), for words [0, wpad).
-__global__ __launch_bounds__(kBT) void k_bm_lanes(const uint64_t* __restrict__ A, const uint64_t* __restrict__ C,
-                                                  uint64_t wpad, uint4* __restrict__ lanes, const LevelState* st) {
-  if (bm_dead(st)) return;
-  for (uint64_t w = (uint64_t)blockIdx.x * kBT + threadIdx.x; w < wpad; w += (uint64_t)gridDim.x * kBT) {
-    const uint64_t a = A[w], c = C[w];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {  // bytes 16q .. 16q+15
-      const unsigned as = (unsigned)(a >> (16 * q)), cs = (unsigned)(c >> (16 * q));
-      uint4 v;
-      v.x = spread4(as & 15u) + spread4(cs & 15u);
-      v.y = spread4((as >> 4) & 15u) + spread4((cs >> 4) & 15u);
-      v.z = spread4((as >> 8) & 15u) + spread4((cs >> 8) & 15u);
-      v.w = spread4((as >> 12) & 15u) + spread4((cs >> 12) & 15u);
-      lanes[4 * w + q] = v;
-    }
-  }
-}
 
 // bytes of v equal to 1 -> their high bits (exact per byte)
 __device__ __forceinline__ unsigned ones_mask(unsigned v) {
@@ -114,48 +63,62 @@ __global__ __launch_bounds__(kBT) void k_bm_decide(const uint4* __restrict__ sli
   }
 }
 
-// Pass 1 over the gathered final bits: copy the level's words to bits + woff[L] (mph.bin's
-// level L), and per 2048-word block the popcount total.
-__global__ __launch_bounds__(kBT) void k_bm_pass1(int level, const uint64_t* __restrict__ g, uint64_t wpad,
-                                                  uint64_t* __restrict__ bits, unsigned long long* __restrict__ bsum,
-                                                  const LevelState* st) {
+// ---- level end: tile totals over the gathered final bits -------------------------------
+// Tile t (2^tb positions, W = 2^(tb-6) words) -> tsum[t] = popcount(g) << 32 | popcount(g & A)
+// over its words (the level's keys placed in the tile, and this rank's share of them); g is
+// also copied to bits + woff[L] (mph.bin's level L).
+__global__ __launch_bounds__(kBT) void k_bm_tsum(int level, const uint64_t* __restrict__ g,
+                                                 const uint64_t* __restrict__ A, unsigned tb,
+                                                 uint64_t* __restrict__ bits, unsigned long long* __restrict__ tsum,
+                                                 const LevelState* st) {
   __shared__ unsigned long long s_w[kBT / 64];
-  if (bm_dead(st)) return;
+  if (bm_dead(st) || (st->status & kStStop)) return;
   const uint64_t words = st->words[level], woff = st->woff[level];
-  const uint64_t b0 = (uint64_t)blockIdx.x * kBScanBlock;
-  unsigned long long s = 0;
-#pragma unroll
-  for (int t = 0; t < kBScanPer; ++t) {
-    const uint64_t w = b0 + (uint64_t)t * kBT + threadIdx.x;
-    if (w < wpad) {
+  const uint64_t W = 1ull << (tb - 6);
+  const uint64_t T = (words + W - 1) / W;
+  for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
+    const uint64_t w0 = t * W, w1 = min<uint64_t>(words, w0 + W);
+    unsigned long long s = 0;
+    for (uint64_t w = w0 + threadIdx.x; w < w1; w += kBT) {
       const uint64_t v = g[w];
-      s += __popcll(v);
-      if (w < words) bits[woff + w] = v;
+      s += ((unsigned long long)__popcll(v) << 32) | (unsigned)__popcll(v & A[w]);
+      bits[woff + w] = v;
     }
-  }
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
-  if (lane_id() == 0) s_w[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long t = 0;
-    for (int k = 0; k < kBT / 64; ++k) t += s_w[k];
-    bsum[blockIdx.x] = t;
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+    if (lane_id() == 0) s_w[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long tt = 0;
+      for (int k = 0; k < kBT / 64; ++k) tt += s_w[k];
+      tsum[t] = tt;
+    }
+    __syncthreads();
   }
 }
 
-// Pass 2 (one block): exclusive scan of the block totals in place; the level's total
-// settles the next level's global size and rank base.
-__global__ __launch_bounds__(kBTopT) void k_bm_pass2(int level, unsigned long long* __restrict__ bsum, uint64_t nblk,
-                                                     LevelState* st, unsigned long long* __restrict__ gslot) {
+// One block: exclusive scans of the tile totals -> tbase[2t] (the tile's first rank within
+// the level) and tbase[2t + 1] (its first slot in this rank's settled list, which runs on
+// from *out_cnt: the list is in (level, position) order, so sorted by p).  The level's
+// total settles the next level's global size and rank base.
+constexpr int kTsPer = (int)(kScatterTiles / kBTopT);
+__global__ __launch_bounds__(kBTopT) void k_bm_tscan(int level, const unsigned long long* __restrict__ tsum,
+                                                     unsigned tb, unsigned long long* __restrict__ tbase,
+                                                     LevelState* st, unsigned long long* __restrict__ gslot,
+                                                     unsigned long long* __restrict__ out_cnt) {
   __shared__ unsigned long long s_w[kBTopT / 64];
-  if (bm_dead(st)) return;
+  __shared__ unsigned long long s_base;
+  if (bm_dead(st) || (st->status & kStStop)) return;
+  const uint64_t words = st->words[level];
+  const uint64_t W = 1ull << (tb - 6);
+  const uint64_t T = (words + W - 1) / W;
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  unsigned long long v[kBTopPer], sum = 0;
+  if (tid == 0) s_base = *out_cnt;
+  unsigned long long v[kTsPer], sum = 0;
 #pragma unroll
-  for (int q = 0; q < kBTopPer; ++q) {
-    const uint64_t i = (uint64_t)tid * kBTopPer + q;
-    v[q] = i < nblk ? bsum[i] : 0ull;
+  for (int q = 0; q < kTsPer; ++q) {
+    const uint64_t i = (uint64_t)tid * kTsPer + q;
+    v[q] = i < T ? tsum[i] : 0ull;
     sum += v[q];
   }
   unsigned long long x = sum;
@@ -173,160 +136,286 @@ __global__ __launch_bounds__(kBTopT) void k_bm_pass2(int level, unsigned long lo
     tot += s_w[w];
   }
   unsigned long long ex = pre + x - sum;
+  const unsigned long long ob = s_base;
 #pragma unroll
-  for (int q = 0; q < kBTopPer; ++q) {
-    const uint64_t i = (uint64_t)tid * kBTopPer + q;
-    if (i < nblk) bsum[i] = ex;
+  for (int q = 0; q < kTsPer; ++q) {
+    const uint64_t i = (uint64_t)tid * kTsPer + q;
+    if (i < T) {
+      tbase[2 * i] = ex >> 32;
+      tbase[2 * i + 1] = ob + (ex & 0xffffffffull);
+    }
     ex += v[q];
   }
   if (tid == 0) {
-    const unsigned long long n = st->gn[level];
-    if (tot > n) atomicOr(&st->status, kStRank);  // cannot happen: each set bit is one key
-    gslot[level + 1] = n - tot;                   // keys entering level L + 1, globally
-    st->lvl_base[level + 1] = st->lvl_base[level] + tot;
+    const unsigned long long n = st->gn[level], placed = tot >> 32;
+    if (placed > n) atomicOr(&st->status, kStRank);  // cannot happen: each set bit is one key
+    gslot[level + 1] = n - placed;                    // keys entering level L + 1, globally
+    st->lvl_base[level + 1] = st->lvl_base[level] + placed;
+    *out_cnt = ob + (tot & 0xffffffffull);
   }
 }
 
-// Pass 3: per-word exclusive prefix of set bits within the level (u32: n_L < 2^32).
-__global__ __launch_bounds__(kBT) void k_bm_pass3(const uint64_t* __restrict__ g, uint64_t wpad,
-                                                  const unsigned long long* __restrict__ bsum,
-                                                  unsigned* __restrict__ wpre, const LevelState* st) {
-  __shared__ unsigned s_w[kBT / 64];
-  if (bm_dead(st)) return;
-  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  const uint64_t b0 = (uint64_t)blockIdx.x * kBScanBlock + (uint64_t)tid * kBScanPer;  // this thread's 8 words
-  unsigned c[kBScanPer], sum = 0;
-#pragma unroll
-  for (int t = 0; t < kBScanPer; ++t) {
-    const uint64_t w = b0 + t;
-    c[t] = w < wpad ? (unsigned)__popcll(g[w]) : 0u;
-    sum += c[t];
-  }
-  unsigned x = sum;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const unsigned y = __shfl_up(x, d);
-    if (lane >= (unsigned)d) x += y;
-  }
-  if (lane == 63) s_w[wave] = x;
-  __syncthreads();
-  unsigned pre = 0;
-#pragma unroll
-  for (int w = 0; w < kBT / 64; ++w)
-    if ((unsigned)w < wave) pre += s_w[w];
-  unsigned ex = (unsigned)bsum[blockIdx.x] + pre + x - sum;
-#pragma unroll
-  for (int t = 0; t < kBScanPer; ++t) {
-    const uint64_t w = b0 + t;
-    if (w < wpad) wpre[w] = ex;
-    ex += c[t];
-  }
+// ---- per-tile kernels over the reservation scatter's buckets ---------------------------
+// Level L's records were scattered by k_scatter_res into tiles of 2^tb positions over the
+// level's WHOLE position range (tile t: kResShards shard slots of scap records from
+// t * cap, fills in tc).  Marking and settling then touch only tile-local state in LDS.
+// Both read a tile's records as one flattened index range over its shards, kU records
+// per thread in flight.
+constexpr int kTT = 1024;
+constexpr int kU = 4;
+
+__device__ __forceinline__ uint32_t spread4(uint32_t v) {  // 4 bits -> 4 bytes (bit j -> byte j)
+  return (v & 1u) | ((v & 2u) << 7) | ((v & 4u) << 14) | ((v & 8u) << 21);
 }
 
-// Settle this rank's level-L records against the final bits: placed records leave as
-// (p, fp, pos) triples (Rec with k = p) in `out`, the others go to the next level's list
-// (st->n[L+1] counts them).  A block takes kSetQ x kBT consecutive records at a time:
-// the first sweep counts each (wave, round)'s placed / collided records, one atomic per
-// counter reserves the block's runs, and the second sweep (records and final-bit words
-// again, from L2) writes every wave-round as one contiguous run.  Same-address device
-// atomics serialise (~12 ns each): one per wave made this stage 20x slower.
-constexpr int kSetQ = 16;
-template <int kSrc>
-__global__ __launch_bounds__(kBT) void k_bm_settle(int level, const uint64_t* __restrict__ kh,
-                                                   const uint64_t* __restrict__ fp, const uint64_t* __restrict__ pos,
-                                                   uint64_t pos_base, uint64_t n_keys, const Rec* __restrict__ ilist,
-                                                   LevelState* st, const uint64_t* __restrict__ g,
-                                                   const unsigned* __restrict__ wpre, Rec* __restrict__ out,
-                                                   unsigned long long* __restrict__ out_cnt, uint64_t out_cap,
-                                                   Rec* __restrict__ next, uint64_t next_cap) {
-  constexpr int NW = kBT / 64;
-  __shared__ unsigned s_cp[NW * kSetQ], s_cn[NW * kSetQ];
-  __shared__ unsigned long long s_bp, s_bn;
-  if (bm_dead(st)) return;
-  const uint64_t n = bm_count<kSrc>(level, n_keys, st);
+// shard fills of tile t -> exclusive prefix fo[0..8] (fo[8] = the tile's records)
+__device__ __forceinline__ void shard_prefix(const unsigned* __restrict__ tc, uint64_t t, unsigned* fo) {
+  unsigned a = 0;
+#pragma unroll
+  for (int sh = 0; sh < kResShards; ++sh) {
+    fo[sh] = a;
+    a += tc[t * kResShards + sh];
+  }
+  fo[kResShards] = a;
+}
+__device__ __forceinline__ uint64_t rec_index(unsigned i, const unsigned* fo, uint64_t tslot, uint64_t scap) {
+  unsigned sh = 0;
+#pragma unroll
+  for (int k = 1; k < kResShards; ++k) sh += i >= fo[k] ? 1u : 0u;
+  unsigned base = fo[0];
+#pragma unroll
+  for (int k = 1; k < kResShards; ++k)
+    if (sh == (unsigned)k) base = fo[k];
+  return tslot + (uint64_t)sh * scap + (i - base);
+}
+
+// Mark: this rank's records of tile t -> local A (>= 1 key) / C (>= 2 keys) in LDS ->
+// the tile's count lanes (byte x = A + C = min(local count, 2)) and its A words (kept
+// for the settle).  Lanes of positions past the level's true size are zeroed here too.
+__global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const Rec* __restrict__ bucket,
+                                                      const unsigned* __restrict__ tc, uint64_t bucket_cap,
+                                                      unsigned tb, const LevelState* st, uint64_t wpad,
+                                                      uint8_t* __restrict__ lanes, uint32_t* __restrict__ A32) {
+  extern __shared__ uint32_t bm_lds[];
+  __shared__ unsigned s_fo[kResShards + 1];
+  if (bm_dead(st) || (st->status & kStStop)) return;
   const uint64_t words = st->words[level], magic = st->magic[level], seed = level_seed(level);
-  const uint64_t base = st->lvl_base[level];
-  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  bool over = false;
-  auto rec_at = [&](uint64_t i) -> Rec {
-    if (kSrc == 2) return Rec{kh[i], fp[i], pos ? pos[i] : pos_base + i};
-    return ilist[i];
-  };
-  for (uint64_t c0 = (uint64_t)blockIdx.x * kSetQ * kBT; c0 < n; c0 += (uint64_t)gridDim.x * kSetQ * kBT) {
-    // sweep 1: counts per (wave, round)
-#pragma unroll 4
-    for (int q = 0; q < kSetQ; ++q) {
-      const uint64_t i = c0 + (uint64_t)q * kBT + tid;
-      bool placed = false;
-      if (i < n) {
-        const uint64_t x = bb_index(seed, kSrc == 2 ? kh[i] : ilist[i].k, words, magic);
-        placed = (g[x >> 6] >> (x & 63)) & 1ull;
-      }
-      const uint64_t pm = __ballot(i < n && placed), nm = __ballot(i < n && !placed);
-      if (lane == 0) {
-        s_cp[wave * kSetQ + q] = (unsigned)__popcll(pm);
-        s_cn[wave * kSetQ + q] = (unsigned)__popcll(nm);
-      }
-    }
+  const uint64_t T = (64 * words + (1ull << tb) - 1) >> tb;
+  const unsigned W32 = 1u << (tb - 5);  // u32 words of a tile's bit vector
+  uint32_t* sA = bm_lds;
+  uint32_t* sC = bm_lds + W32;
+  const unsigned tid = threadIdx.x;
+  // zero the lanes of [64 words, 64 wpad): no tile covers them
+  for (uint64_t q = 64 * words / 16 + (uint64_t)blockIdx.x * kTT + tid; q < 64 * wpad / 16;
+       q += (uint64_t)gridDim.x * kTT)
+    reinterpret_cast<uint4*>(lanes)[q] = make_uint4(0, 0, 0, 0);
+  if (T == 0) return;
+  const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
+  for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
+    for (unsigned j = tid; j < W32; j += kTT) sA[j] = sC[j] = 0;
+    if (tid == 0) shard_prefix(tc, t, s_fo);
     __syncthreads();
-    if (tid < 64) {  // exclusive scans of the NW x kSetQ (<= 64) entries, and the reservations
-      const unsigned cp = tid < NW * kSetQ ? s_cp[tid] : 0u, cn = tid < NW * kSetQ ? s_cn[tid] : 0u;
-      unsigned xp = cp, xn = cn;
+    unsigned fo[kResShards + 1];
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const unsigned yp = __shfl_up(xp, d), yn = __shfl_up(xn, d);
-        if (tid >= (unsigned)d) {
-          xp += yp;
-          xn += yn;
+    for (int k = 0; k <= kResShards; ++k) fo[k] = s_fo[k];
+    const uint64_t t0 = t << tb;
+    for (unsigned i0 = 0; i0 < fo[kResShards]; i0 += kTT * kU) {
+      uint64_t kk[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const unsigned i = i0 + u * kTT + tid;
+        kk[u] = i < fo[kResShards] ? bucket[rec_index(i, fo, t * cap, scap)].k : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (i0 + u * kTT + tid < fo[kResShards]) {
+          const uint64_t lx = bb_index(seed, kk[u], words, magic) - t0;
+          const uint32_t bit = 1u << (lx & 31);
+          if (atomicOr(&sA[lx >> 5], bit) & bit) atomicOr(&sC[lx >> 5], bit);
         }
       }
-      if (tid < NW * kSetQ) {
-        s_cp[tid] = xp - cp;
-        s_cn[tid] = xn - cn;
-      }
-      const unsigned tp = __shfl(xp, 63), tn = __shfl(xn, 63);
-      if (tid == 0) {
-        s_bp = tp ? atomicAdd(out_cnt, (unsigned long long)tp) : 0ull;
-        s_bn = tn ? atomicAdd(&st->n[level + 1], (unsigned long long)tn) : 0ull;
+    }
+    __syncthreads();
+    // the tile's lanes and A words (positions below 64 words only)
+    const uint64_t wend = min<uint64_t>((uint64_t)W32, (64 * words - t0 + 31) / 32);
+    for (unsigned j = tid; j < wend; j += kTT) {
+      const uint32_t a = sA[j], c = sC[j];
+      A32[(t0 >> 5) + j] = a;
+      uint4* dst = reinterpret_cast<uint4*>(lanes + t0 + 32ull * j);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {  // bytes 16q .. 16q + 15 of this word's 32 lanes
+        const uint32_t as = a >> (16 * q), cs = c >> (16 * q);
+        dst[q] = make_uint4(spread4(as & 15u) + spread4(cs & 15u), spread4((as >> 4) & 15u) + spread4((cs >> 4) & 15u),
+                            spread4((as >> 8) & 15u) + spread4((cs >> 8) & 15u),
+                            spread4((as >> 12) & 15u) + spread4((cs >> 12) & 15u));
       }
     }
     __syncthreads();
-    // sweep 2: every wave-round writes its runs
-#pragma unroll 2
-    for (int q = 0; q < kSetQ; ++q) {
-      const uint64_t i = c0 + (uint64_t)q * kBT + tid;
-      Rec r{0, 0, 0};
-      bool placed = false;
-      uint64_t p = 0;
-      if (i < n) {
-        r = rec_at(i);
-        const uint64_t x = bb_index(seed, r.k, words, magic);
-        const uint64_t v = g[x >> 6];
-        const unsigned b = (unsigned)(x & 63);
-        placed = (v >> b) & 1ull;
-        if (placed) p = base + wpre[x >> 6] + (uint64_t)__popcll(v & ((1ull << b) - 1ull));
+  }
+}
+
+// Settle: with the tile's final bits g (gathered) and this rank's A bits a, a record at x is
+// placed iff g bit x is set (exactly one key there, so this rank's); its
+//   p    = lvl_base[L] + tbase[2t] + popcount(g over the tile below x)
+//   slot = tbase[2t + 1] + popcount(g & a over the tile below x)
+// so this rank's settled list is in p order whatever order the records arrive in.  The
+// tile keeps g and g & a (16 B per word) and, per group of 4 words, both prefixes (2 B per
+// word): 144 KiB at 2^19 positions.  Collided records go to the next level's list at one
+// atomic per tile plus an LDS cursor.
+constexpr unsigned kGrp = 4;
+__global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const Rec* __restrict__ bucket,
+                                                        const unsigned* __restrict__ tc, uint64_t bucket_cap,
+                                                        unsigned tb, LevelState* st, const uint64_t* __restrict__ g,
+                                                        const uint64_t* __restrict__ A,
+                                                        const unsigned long long* __restrict__ tbase,
+                                                        Rec* __restrict__ out, uint64_t out_cap,
+                                                        Rec* __restrict__ next, uint64_t next_cap) {
+  extern __shared__ uint64_t bm_lds64[];
+  __shared__ unsigned long long s_w[kTT / 64];
+  __shared__ unsigned s_fo[kResShards + 1];
+  __shared__ unsigned long long s_nb, s_tg, s_ta;
+  __shared__ unsigned s_ncur;
+  if (bm_dead(st) || (st->status & kStStop)) return;
+  const uint64_t words = st->words[level], magic = st->magic[level], seed = level_seed(level);
+  const uint64_t base = st->lvl_base[level];
+  const uint64_t T = (64 * words + (1ull << tb) - 1) >> tb;
+  if (T == 0) return;
+  const unsigned W = 1u << (tb - 6), G = W / kGrp;  // words, groups of a tile
+  uint64_t* sg = bm_lds64;
+  uint64_t* sga = sg + W;
+  unsigned* gpg = reinterpret_cast<unsigned*>(sga + W);  // per group: popcount(g) before it
+  unsigned* gpa = gpg + G;                               // ... popcount(g & a)
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
+  constexpr int kGper = 2;  // groups per thread in the tile scan (G <= 2048)
+  bool over = false;
+  for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
+    const uint64_t w0 = t * W;
+    const unsigned nw = (unsigned)min<uint64_t>(W, words - w0);
+    unsigned long long c[kGper], sum = 0;
+#pragma unroll
+    for (int q = 0; q < kGper; ++q) {
+      const unsigned grp = tid * kGper + q;
+      unsigned cg = 0, ca = 0;
+      if (grp < G) {
+        const unsigned j0 = grp * kGrp;
+        uint64_t gv[kGrp], av[kGrp];
+        if (j0 + kGrp <= nw) {
+          const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(g + w0 + j0);
+          const ulonglong2* a2 = reinterpret_cast<const ulonglong2*>(A + w0 + j0);
+          const ulonglong2 x0 = g2[0], x1 = g2[1], y0 = a2[0], y1 = a2[1];
+          gv[0] = x0.x; gv[1] = x0.y; gv[2] = x1.x; gv[3] = x1.y;
+          av[0] = y0.x; av[1] = y0.y; av[2] = y1.x; av[3] = y1.y;
+        } else {
+#pragma unroll
+          for (int k = 0; k < (int)kGrp; ++k) {
+            gv[k] = j0 + k < nw ? g[w0 + j0 + k] : 0ull;
+            av[k] = j0 + k < nw ? A[w0 + j0 + k] : 0ull;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < (int)kGrp; ++k) {
+          const uint64_t ga = gv[k] & av[k];
+          sg[j0 + k] = gv[k];
+          sga[j0 + k] = ga;
+          cg += (unsigned)__popcll(gv[k]);
+          ca += (unsigned)__popcll(ga);
+        }
       }
-      const uint64_t pm = __ballot(i < n && placed), nm = __ballot(i < n && !placed);
-      const uint64_t lt = lanemask_lt();
-      if (i < n) {
-        if (placed) {
-          const uint64_t slot = s_bp + s_cp[wave * kSetQ + q] + (uint64_t)__popcll(pm & lt);
+      c[q] = ((unsigned long long)cg << 32) | ca;
+      sum += c[q];
+    }
+    unsigned long long x = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long y = __shfl_up(x, d);
+      if (lane >= (unsigned)d) x += y;
+    }
+    if (lane == 63) s_w[wave] = x;
+    __syncthreads();
+    unsigned long long pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kTT / 64; ++w) {
+      if ((unsigned)w < wave) pre += s_w[w];
+      tot += s_w[w];
+    }
+    unsigned long long ex = pre + x - sum;
+#pragma unroll
+    for (int q = 0; q < kGper; ++q) {
+      const unsigned grp = tid * kGper + q;
+      if (grp < G) {
+        gpg[grp] = (unsigned)(ex >> 32);
+        gpa[grp] = (unsigned)ex;
+      }
+      ex += c[q];
+    }
+    if (tid == 0) {
+      shard_prefix(tc, t, s_fo);
+      const unsigned nrec = s_fo[kResShards], placed = (unsigned)tot;
+      s_nb = nrec > placed ? atomicAdd(&st->n[level + 1], (unsigned long long)(nrec - placed)) : 0ull;
+      s_ncur = 0;
+      s_tg = tbase[2 * t];
+      s_ta = tbase[2 * t + 1];
+    }
+    __syncthreads();
+    unsigned fo[kResShards + 1];
+#pragma unroll
+    for (int k = 0; k <= kResShards; ++k) fo[k] = s_fo[k];
+    const uint64_t t0 = t << tb, pb = base + s_tg, ob = s_ta, nb = s_nb;
+    for (unsigned i0 = 0; i0 < fo[kResShards]; i0 += kTT * kU) {
+      Rec r[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const unsigned i = i0 + u * kTT + tid;
+        if (i < fo[kResShards]) r[u] = bucket[rec_index(i, fo, t * cap, scap)];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (i0 + u * kTT + tid >= fo[kResShards]) continue;
+        const uint64_t lx = bb_index(seed, r[u].k, words, magic) - t0;
+        const unsigned j = (unsigned)(lx >> 6), b = (unsigned)(lx & 63), grp = j / kGrp;
+        const uint64_t below = (1ull << b) - 1ull, v = sg[j];
+        if ((v >> b) & 1ull) {
+          const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(sg + grp * kGrp);
+          const ulonglong2* a2 = reinterpret_cast<const ulonglong2*>(sga + grp * kGrp);
+          const ulonglong2 x0 = g2[0], x1 = g2[1], y0 = a2[0], y1 = a2[1];
+          const uint64_t gw[kGrp] = {x0.x, x0.y, x1.x, x1.y}, aw[kGrp] = {y0.x, y0.y, y1.x, y1.y};
+          unsigned pg = gpg[grp], pa = gpa[grp];
+          const unsigned jr = j % kGrp;
+#pragma unroll
+          for (int k = 0; k < (int)kGrp; ++k)
+            if ((unsigned)k < jr) {
+              pg += (unsigned)__popcll(gw[k]);
+              pa += (unsigned)__popcll(aw[k]);
+            }
+          pg += (unsigned)__popcll(v & below);
+          pa += (unsigned)__popcll(sga[j] & below);
+          const uint64_t slot = ob + pa;
           if (slot < out_cap)
-            out[slot] = Rec{p, r.f, r.p};
+            out[slot] = Rec{pb + pg, r[u].f, r[u].p};
           else
             over = true;
         } else {
-          const uint64_t slot = s_bn + s_cn[wave * kSetQ + q] + (uint64_t)__popcll(nm & lt);
+          const uint64_t slot = nb + atomicAdd(&s_ncur, 1u);
           if (slot < next_cap)
-            next[slot] = r;
+            next[slot] = r[u];
           else
             over = true;
         }
       }
     }
-    __syncthreads();  // s_cp / s_cn / s_bp / s_bn are reused by the next chunk
+    __syncthreads();  // the tile's LDS state is reused by the next tile
   }
   if (over) atomicOr(&st->status, kStOverflow);
+}
+
+// Bitmap levels cover the level's whole position range on every rank (the routed build's
+// k_dist_setup gave this rank a slice): the scatter and the tile kernels see [0, 64 words).
+__global__ void k_bm_range(LevelState* st, int level) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    st->wlo[level] = 0;
+    st->rw[level] = st->words[level];
+  }
 }
 
 // The level's true size against the host's bound (words_L <= wmax), after k_dist_setup.
@@ -334,71 +423,30 @@ __global__ void k_bm_check(LevelState* st, int level, uint64_t wmax) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && st->words[level] > wmax) atomicOr(&st->status, kStBitmapBound);
 }
 
-// Settled triples -> per-owner send regions (owner of p = p / slice): rounds of kRR
-// records counting-sorted by owner in LDS, one atomic per (round, owner), runs written
-// whole (as k_route).
-constexpr int kRR = 2048;
-__global__ __launch_bounds__(1024) void k_bm_route_out(const Rec* __restrict__ in, const unsigned long long* n_in,
-                                                       uint64_t slice, int P, Rec* __restrict__ send, uint64_t cap,
-                                                       unsigned long long* __restrict__ scnt, LevelState* st) {
-  __shared__ Rec stage[kRR];
-  __shared__ unsigned char sdst[kRR];
-  __shared__ unsigned cnt[kMaxRanks], start[kMaxRanks];
-  __shared__ uint64_t rbase[kMaxRanks];
-  __shared__ unsigned s_over;
-  const unsigned tid = threadIdx.x;
-  if (tid == 0) s_over = 0;
-  const uint64_t n = *n_in;
-  for (uint64_t r0 = (uint64_t)blockIdx.x * kRR; r0 < n; r0 += (uint64_t)gridDim.x * kRR) {
-    if (tid < kMaxRanks) cnt[tid] = 0;
-    __syncthreads();
-    Rec rec[2];
-    unsigned d[2] = {0, 0}, rk[2] = {0, 0};
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const uint64_t i = r0 + (uint64_t)q * 1024 + tid;
-      if (i < n) {
-        rec[q] = in[i];
-        d[q] = (unsigned)min<uint64_t>(rec[q].k / slice, (uint64_t)(P - 1));
-        rk[q] = atomicAdd(&cnt[d[q]], 1u);
+// This rank's settled list is sorted by p: the run for output slice t ([t slice, (t+1)
+// slice)) is [lower_bound(t slice), lower_bound((t+1) slice)).  One thread per slice
+// boundary; scnt[t] = the run's length, scnt[P] = 0 (no overflow: nothing is copied).
+__global__ void k_bm_bounds(const Rec* __restrict__ out, const unsigned long long* __restrict__ n_out, uint64_t slice,
+                            int P, unsigned long long* __restrict__ scnt) {
+  __shared__ uint64_t s_b[kMaxRanks + 1];
+  const unsigned t = threadIdx.x;
+  const uint64_t n = *n_out;
+  if (t <= (unsigned)P) {
+    uint64_t lo = 0, hi = n;
+    if (t == (unsigned)P) lo = n;
+    else if (t > 0) {
+      const uint64_t key = (uint64_t)t * slice;
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (out[mid].k < key) lo = mid + 1;
+        else hi = mid;
       }
     }
-    __syncthreads();
-    if (tid < 64) {
-      const unsigned c = tid < (unsigned)P ? cnt[tid] : 0u;
-      unsigned x = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const unsigned y = __shfl_up(x, o);
-        if (tid >= (unsigned)o) x += y;
-      }
-      start[tid] = x - c;
-      if (c) {
-        const unsigned long long at = atomicAdd(&scnt[tid], (unsigned long long)c);
-        if (at + c > cap) s_over = 1;
-        rbase[tid] = (uint64_t)tid * cap + at;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const uint64_t i = r0 + (uint64_t)q * 1024 + tid;
-      if (i < n) {
-        const unsigned slot = start[d[q]] + rk[q];
-        stage[slot] = rec[q];
-        sdst[slot] = (unsigned char)d[q];
-      }
-    }
-    __syncthreads();
-    const unsigned m = (unsigned)min<uint64_t>(kRR, n - r0);
-    if (!s_over)
-      for (unsigned j = tid; j < m; j += 1024) {
-        const unsigned o = sdst[j];
-        send[rbase[o] + (j - start[o])] = stage[j];
-      }
-    __syncthreads();
+    s_b[t] = lo;
   }
-  if (tid == 0 && s_over) atomicOr(&st->status, kStRouteOverflow);
+  __syncthreads();
+  if (t < (unsigned)P) scnt[t] = s_b[t + 1] - s_b[t];
+  if (t == (unsigned)P) scnt[P] = 0;
 }
 
 // Received triples of this rank's output slice [lo, lo + cnt) -> fp_out / pos_out.
@@ -441,52 +489,51 @@ void launch_bm_check(LevelState* st, int level, uint64_t wmax, hipStream_t s) {
   k_bm_check<<<1, 64, 0, s>>>(st, level, wmax);
 }
 
-void launch_bm_mark(int level, const uint64_t* kh, uint64_t n_keys, const Rec* list, uint64_t n_pred,
-                    const LevelState* st, uint64_t* A, uint64_t* C, hipStream_t s) {
-  unsigned* a = reinterpret_cast<unsigned*>(A);
-  unsigned* c = reinterpret_cast<unsigned*>(C);
-  if (level == 0)
-    k_bm_mark<2><<<grid_for(n_keys, kBT, 8192), kBT, 0, s>>>(0, kh, n_keys, nullptr, st, a, c);
-  else
-    k_bm_mark<1><<<grid_for(n_pred, kBT, 8192), kBT, 0, s>>>(level, nullptr, 0, list, st, a, c);
-}
-
-void launch_bm_lanes(const uint64_t* A, const uint64_t* C, uint64_t wpad, uint8_t* lanes, const LevelState* st,
-                     hipStream_t s) {
-  k_bm_lanes<<<grid_for(wpad, kBT, 8192), kBT, 0, s>>>(A, C, wpad, reinterpret_cast<uint4*>(lanes), st);
-}
-
 void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const LevelState* st, hipStream_t s) {
   k_bm_decide<<<grid_for(S, kBT, 8192), kBT, 0, s>>>(reinterpret_cast<const uint4*>(slice), S, out, st);
 }
 
-uint64_t bm_scan_blocks(uint64_t wpad) { return (wpad + kBScanBlock - 1) / kBScanBlock; }
-uint64_t bm_max_words() { return (uint64_t)kBTopT * kBTopPer * kBScanBlock; }
-
-void launch_bm_level_end(int level, const uint64_t* g, uint64_t wpad, uint64_t* bits, unsigned long long* bsum,
-                         unsigned* wpre, LevelState* st, unsigned long long* gslot, hipStream_t s) {
-  const uint64_t nblk = bm_scan_blocks(wpad);
-  k_bm_pass1<<<(int)std::max<uint64_t>(nblk, 1), kBT, 0, s>>>(level, g, wpad, bits, bsum, st);
-  k_bm_pass2<<<1, kBTopT, 0, s>>>(level, bsum, nblk, st, gslot);
-  k_bm_pass3<<<(int)std::max<uint64_t>(nblk, 1), kBT, 0, s>>>(g, wpad, bsum, wpre, st);
+void launch_bm_level_end(int level, const uint64_t* g, const uint64_t* A, unsigned tb, uint64_t tiles, uint64_t* bits,
+                         unsigned long long* tsum, unsigned long long* tbase, LevelState* st,
+                         unsigned long long* gslot, unsigned long long* out_cnt, hipStream_t s) {
+  k_bm_tsum<<<(int)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4096)), kBT, 0, s>>>(level, g, A, tb, bits, tsum, st);
+  k_bm_tscan<<<1, kBTopT, 0, s>>>(level, tsum, tb, tbase, st, gslot, out_cnt);
 }
 
-void launch_bm_settle(int level, const uint64_t* kh, const uint64_t* fp, const uint64_t* pos, uint64_t pos_base,
-                      uint64_t n_keys, const Rec* list, uint64_t n_pred, LevelState* st, const uint64_t* g,
-                      const unsigned* wpre, Rec* out, unsigned long long* out_cnt, uint64_t out_cap, Rec* next,
-                      uint64_t next_cap, hipStream_t s) {
-  if (level == 0)
-    k_bm_settle<2><<<grid_for(n_keys, kBT * kSetQ, 2048), kBT, 0, s>>>(0, kh, fp, pos, pos_base, n_keys, nullptr, st,
-                                                                        g, wpre, out, out_cnt, out_cap, next, next_cap);
-  else
-    k_bm_settle<1><<<grid_for(n_pred, kBT * kSetQ, 2048), kBT, 0, s>>>(level, nullptr, nullptr, nullptr, 0, 0, list,
-                                                                        st, g, wpre, out, out_cnt, out_cap, next,
-                                                                        next_cap);
+size_t bm_tile_lds(unsigned tb, bool settle) {
+  const size_t W = (size_t)1 << (tb - 6);
+  return settle ? W * 16 + (W / kGrp) * 8 : W * 16;
 }
 
-void launch_bm_route_out(const Rec* in, const unsigned long long* n_in, uint64_t n_pred, uint64_t slice, int P,
-                         Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, hipStream_t s) {
-  k_bm_route_out<<<grid_for(n_pred, kRR, 2048), 1024, 0, s>>>(in, n_in, slice, P, send, cap, scnt, st);
+void bm_set_lds_limits() {
+  (void)hipFuncSetAttribute((const void*)k_bm_tile_mark, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)bm_tile_lds(kBmMaxTb, false));
+  (void)hipFuncSetAttribute((const void*)k_bm_tile_settle, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)bm_tile_lds(kBmMaxTb, true));
+}
+
+void launch_bm_range(LevelState* st, int level, hipStream_t s) { k_bm_range<<<1, 64, 0, s>>>(st, level); }
+
+void launch_bm_tile_mark(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
+                         uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A,
+                         hipStream_t s) {
+  const int grid = (int)std::max<uint64_t>(256, std::min<uint64_t>(tiles, 1024));
+  k_bm_tile_mark<<<grid, kTT, bm_tile_lds(tb, false), s>>>(level, bucket, tc, bucket_cap, tb, st, wpad, lanes,
+                                                          reinterpret_cast<uint32_t*>(A));
+}
+
+void launch_bm_tile_settle(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
+                           uint64_t tiles, LevelState* st, const uint64_t* g, const uint64_t* A,
+                           const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next, uint64_t next_cap,
+                           hipStream_t s) {
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1024));
+  k_bm_tile_settle<<<grid, kTT, bm_tile_lds(tb, true), s>>>(level, bucket, tc, bucket_cap, tb, st, g, A, tbase, out,
+                                                            out_cap, next, next_cap);
+}
+
+void launch_bm_bounds(const Rec* out, const unsigned long long* n_out, uint64_t slice, int P, unsigned long long* scnt,
+                      hipStream_t s) {
+  k_bm_bounds<<<1, 64, 0, s>>>(out, n_out, slice, P, scnt);
 }
 
 void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,

@@ -429,6 +429,7 @@ void set_lds_attrs(s3imph_ctx* c) {
   if (c->lds_attr_set) return;
   // The tile kernels take up to 2 x 64 KiB of dynamic LDS (tiles of 2^19 positions).
   binned_set_lds_limits();
+  bm_set_lds_limits();
   c->lds_attr_set = true;
 }
 
@@ -1123,21 +1124,19 @@ void ensure_bm_workspace(s3imph_ctx* c, uint64_t N) {
     d.bm_cap_out = d.cap_list;
   }
   if (wpad <= d.bm_cap_words && d.bm_a) return;
-  if (wpad > bm_max_words()) throw Fail{S3IMPH_ERR_INVALID, "build MPHF: key set too large for the bitmap decomposition"};
   dalloc(d.bm_a, wpad);
-  dalloc(d.bm_c, wpad);
   dalloc(d.bm_g, wpad);
   dalloc(d.bm_dec, S);
   dalloc(d.bm_lanes, 64 * wpad);
   dalloc(d.bm_slice, 64 * S);
-  dalloc(d.bm_wpre, wpad);
-  dalloc(d.bm_bsum, bm_scan_blocks(wpad) + 2);
+  if (!d.bm_tsum) dalloc(d.bm_tsum, kScatterTiles);
+  if (!d.bm_tbase) dalloc(d.bm_tbase, 2 * kScatterTiles);
   d.bm_cap_words = wpad;
 }
 
 void free_bm_workspace(DistState& d) {
-  dfree(d.bm_a); dfree(d.bm_c); dfree(d.bm_g); dfree(d.bm_dec);
-  dfree(d.bm_lanes); dfree(d.bm_slice); dfree(d.bm_wpre); dfree(d.bm_bsum);
+  dfree(d.bm_a); dfree(d.bm_g); dfree(d.bm_dec);
+  dfree(d.bm_lanes); dfree(d.bm_slice); dfree(d.bm_tsum); dfree(d.bm_tbase);
   dfree(d.bm_out);
   d.bm_cap_words = 0;
   d.bm_cap_out = 0;
@@ -1150,6 +1149,8 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   Comm& cm = *d.comm;
   const int P = d.nranks, R = d.rank;
   LevelState* st = c->d_st;
+  // level 0 beyond kScatterTiles tiles of 2^kBmMaxTb positions (N > ~2^30): the routed build
+  if (tiles_of(level_words(N), kBmMaxTb, 0) > kScatterTiles) return kDistRetry;
   ensure_bm_workspace(c, N);
   const BinBuffers b = make_bufs(c, nullptr, fp_out, pos_out, s);
   const double q = 1.0 - std::exp(-0.5);
@@ -1164,6 +1165,15 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   Rec* const out = d.bm_out;                   // this rank's settled (p, fp, pos) triples
   unsigned long long* const out_cnt = d.small + 4096;
   HIPCHECK(hipMemsetAsync(out_cnt, 0, 8, s));
+  HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kMaxDistLevels * kScatterTiles * kResShards * sizeof(unsigned), s));
+  // The level's records go through the reservation scatter into tiles over the level's
+  // whole position range (this rank's records only); the tile kernels then mark and
+  // settle a tile at a time in LDS.  Level 0 reads the hash kernel's key-order arrays.
+  BinBuffers bs = b;
+  bs.dist = false;
+  bs.split = nullptr;
+  bs.pos = pos;
+  bs.pos_base = key_base;
   // Level sizes: the host bounds n_L from above (mean q n + 6 sigma), so every collective's
   // size is known without a host round trip; a level outgrowing its bound sets
   // kStBitmapBound and the build reruns on the routed decomposition.
@@ -1171,20 +1181,29 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   int L = 0;
   for (;;) {
     const uint64_t wmax = level_words((uint64_t)std::ceil(nb)), S = (wmax + P - 1) / P, wpad = S * (uint64_t)P;
+    // tiles of 2^tb positions: the smallest tile leaving at most kScatterTiles tiles
+    unsigned tb = kBmMinTb;
+    while (tb < kBmMaxTb && tiles_of(wmax, tb, 0) > kScatterTiles) ++tb;
+    const uint64_t tiles = tiles_of(wmax, tb, 0);
+    if (tiles > kScatterTiles) return kDistRetry;  // > 2^30 positions: the routed build (same on every rank)
     if (L > 0) launch_dist_setup(st, L, d.gslot + L, 0, R, P, s);
+    launch_bm_range(st, L, s);
     launch_bm_check(st, L, wmax, s);
-    HIPCHECK(hipMemsetAsync(d.bm_a, 0, 8 * wpad, s));
-    HIPCHECK(hipMemsetAsync(d.bm_c, 0, 8 * wpad, s));
-    const Rec* lin = L ? c->list[(L - 1) & 1] : nullptr;
     const uint64_t np = (uint64_t)(npred * 1.1) + 4096;
-    launch_bm_mark(L, c->kh, n_local, lin, np, st, d.bm_a, d.bm_c, s);
-    launch_bm_lanes(d.bm_a, d.bm_c, wpad, d.bm_lanes, st, s);
+    LevelGeom g{};
+    g.tb = tb;
+    g.chunk = kTargetChunks;
+    g.ts = 0;
+    const int gsr = (int)std::max<uint64_t>(1, std::min<uint64_t>((np + kSubRound - 1) / kSubRound, 256));
+    launch_binned_scatter_res(L, bs, g, gsr, s);
+    const unsigned* tc = c->tcnt + (uint64_t)L * kScatterTiles * kResShards;
+    launch_bm_tile_mark(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, s);
     cm.reduce_scatter_u8(d.bm_lanes, d.bm_slice, 64 * S, s);
     launch_bm_decide(d.bm_slice, S, d.bm_dec, st, s);
     cm.allgather(d.bm_dec, d.bm_g, 8 * S, s);
-    launch_bm_level_end(L, d.bm_g, wpad, c->bits, d.bm_bsum, d.bm_wpre, st, d.gslot, s);
-    launch_bm_settle(L, c->kh, c->fp, pos, key_base, n_local, lin, np, st, d.bm_g, d.bm_wpre, out, out_cnt,
-                     d.bm_cap_out, c->list[L & 1], d.cap_list, s);
+    launch_bm_level_end(L, d.bm_g, d.bm_a, tb, tiles, c->bits, d.bm_tsum, d.bm_tbase, st, d.gslot, out_cnt, s);
+    launch_bm_tile_settle(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
+                          d.bm_cap_out, c->list[L & 1], d.cap_list, s);
     ev_mark(c, s, L == 0 ? "level0" : "levels");
     const double nbn = nb * q + 6.0 * std::sqrt(nb) + 64.0;
     npred *= q;
@@ -1214,7 +1233,9 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   if (c->debug)
     std::fprintf(stderr, "[s3imph] rank %d bitmap: %d sharded levels, replicated %llu records, flags 0x%x\n", R, Ls,
                  (unsigned long long)total, flags);
-  if (flags & kStBitmapBound) return kDistRetry;  // a global fact: every rank returns here
+  // global facts (the flags are gathered): every rank returns here.  A reservation slot
+  // overflow (a skewed tile) or a level beyond its bound reruns on the routed build.
+  if (flags & (kStBitmapBound | kStResOverflow | kStGeometry)) return kDistRetry;
   if (flags & kStOverflow) {
     *msg = "build MPHF: bitmap decomposition: list capacity exceeded";
     return S3IMPH_ERR_INTERNAL;
@@ -1306,52 +1327,39 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     *msg = "build MPHF: output capacity " + std::to_string(out_cap) + " < " + std::to_string(mine);
     return S3IMPH_ERR_INVALID;
   }
+  // this rank's settled list is sorted by p: its run for slice t goes to rank t as it lies
+  // (the own run is placed straight from the list)
+  launch_bm_bounds(out, out_cnt, slice, P, d.scnt, s);
+  cm.allgather(d.scnt, d.mat, 8ull * (P + 1), s);
+  HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
   std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
-  uint64_t C = n_out / P + n_out / (4 * (uint64_t)P) + 4096;
-  uint64_t got = 0;
-  for (int tries = 0;; ++tries) {
-    if ((uint64_t)P * C > d.cap_send) {
-      HIPCHECK(hipStreamSynchronize(s));
-      dalloc(d.send, (uint64_t)P * C);
-      d.cap_send = (uint64_t)P * C;
-    }
-    HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
-    launch_bm_route_out(out, out_cnt, n_out, slice, P, d.send, C, d.scnt, st, s);
-    launch_route_flag(st, d.scnt, P, s);
-    cm.allgather(d.scnt, d.mat, 8ull * (P + 1), s);
-    HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    bool over = false;
-    uint64_t need = 0;
-    for (int r = 0; r < P; ++r) over |= M[(uint64_t)r * (P + 1) + P] != 0;
-    for (int t = 0; t < P; ++t) need = std::max<uint64_t>(need, M[(uint64_t)R * (P + 1) + t]);
-    if (!over) break;
-    if (tries >= 3) {
-      *msg = "build MPHF: output route regions keep overflowing";
-      return S3IMPH_ERR_INTERNAL;
-    }
-    // every rank sees the overflow; each grows to its own need (the regions are per rank)
-    C = std::max<uint64_t>(need, C) + C / 2 + 4096;
-  }
-  uint64_t acc = 0;
+  uint64_t acc = 0, got = 0, own_off = 0, sent = 0;
   for (int t = 0; t < P; ++t) {
-    soff[t] = (uint64_t)t * C * sizeof(Rec);
-    sbytes[t] = M[(uint64_t)R * (P + 1) + t] * sizeof(Rec);
+    const uint64_t cnt_t = M[(uint64_t)R * (P + 1) + t];
+    if (t < R) own_off += cnt_t;
+    soff[t] = sent * sizeof(Rec);
+    sbytes[t] = t == R ? 0 : cnt_t * sizeof(Rec);
+    sent += cnt_t;
+    const uint64_t in_t = M[(uint64_t)t * (P + 1) + R];
     roff[t] = acc;
-    rbytes[t] = M[(uint64_t)t * (P + 1) + R] * sizeof(Rec);
+    rbytes[t] = t == R ? 0 : in_t * sizeof(Rec);
     acc += rbytes[t];
-    got += M[(uint64_t)t * (P + 1) + R];
+    if (t != R) got += in_t;
   }
+  const uint64_t own = M[(uint64_t)R * (P + 1) + R];
   const uint64_t g0 = N - total;
   const uint64_t tail_mine = std::min<uint64_t>(N, lo + mine) > std::max(g0, lo)
                                  ? std::min<uint64_t>(N, lo + mine) - std::max(g0, lo) : 0;
-  if (got + tail_mine != mine || got > d.cap_list) {
+  if (sent != n_out || got + own + tail_mine != mine || got > d.cap_list) {
     *msg = "build MPHF: internal error: output slice of rank " + std::to_string(R) + " receives " +
-           std::to_string(got) + " + " + std::to_string(tail_mine) + " of " + std::to_string(mine) + " entries";
+           std::to_string(got) + " + " + std::to_string(own) + " + " + std::to_string(tail_mine) + " of " +
+           std::to_string(mine) + " entries";
     return S3IMPH_ERR_INTERNAL;
   }
   Rec* recv = c->list[Ls & 1];
-  cm.alltoallv(d.send, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), s);
+  if (P > 1) cm.alltoallv(out, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), s);
+  launch_bm_place(out + own_off, own, lo, mine, fp_out, pos_out, st, s);
   launch_bm_place(recv, got, lo, mine, fp_out, pos_out, st, s);
   launch_bm_tail_copy(c->kh, c->fp, g0, total, lo, mine, fp_out, pos_out, s);
   ev_mark(c, s, "exchange_out");

@@ -90,10 +90,10 @@ struct DistState {
   uint64_t out_n = 0;
   // bitmap decomposition workspace: local A / C marks, count lanes, this rank's summed
   // slice, the gathered final bits, their word prefix and block sums
-  uint64_t *bm_a = nullptr, *bm_c = nullptr, *bm_g = nullptr, *bm_dec = nullptr;
+  uint64_t *bm_a = nullptr, *bm_g = nullptr, *bm_dec = nullptr;
   uint8_t *bm_lanes = nullptr, *bm_slice = nullptr;
-  unsigned* bm_wpre = nullptr;
-  unsigned long long* bm_bsum = nullptr;
+  unsigned long long* bm_tsum = nullptr;   // per-tile totals of a level (kScatterTiles)
+  unsigned long long* bm_tbase = nullptr;  // per-tile (rank, slot) bases (2 kScatterTiles)
   uint64_t bm_cap_words = 0;
   Rec* bm_out = nullptr;  // this rank's settled (p, fp, pos) triples (the tail's tile kernels own the bucket)
   uint64_t bm_cap_out = 0;

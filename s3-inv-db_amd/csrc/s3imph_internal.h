@@ -274,21 +274,28 @@ void launch_dist_replicate(LevelState* st, int L, uint64_t n_all, uint64_t skip_
 
 // ---- the bitmap decomposition of the multi-GPU build (s3imph_bitmap.hip) --------------
 void launch_bm_check(LevelState* st, int level, uint64_t wmax, hipStream_t s);
-void launch_bm_mark(int level, const uint64_t* kh, uint64_t n_keys, const Rec* list, uint64_t n_pred,
-                    const LevelState* st, uint64_t* A, uint64_t* C, hipStream_t s);
-void launch_bm_lanes(const uint64_t* A, const uint64_t* C, uint64_t wpad, uint8_t* lanes, const LevelState* st,
-                     hipStream_t s);
 void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const LevelState* st, hipStream_t s);
-uint64_t bm_scan_blocks(uint64_t wpad);
-uint64_t bm_max_words();
-void launch_bm_level_end(int level, const uint64_t* g, uint64_t wpad, uint64_t* bits, unsigned long long* bsum,
-                         unsigned* wpre, LevelState* st, unsigned long long* gslot, hipStream_t s);
-void launch_bm_settle(int level, const uint64_t* kh, const uint64_t* fp, const uint64_t* pos, uint64_t pos_base,
-                      uint64_t n_keys, const Rec* list, uint64_t n_pred, LevelState* st, const uint64_t* g,
-                      const unsigned* wpre, Rec* out, unsigned long long* out_cnt, uint64_t out_cap, Rec* next,
-                      uint64_t next_cap, hipStream_t s);
-void launch_bm_route_out(const Rec* in, const unsigned long long* n_in, uint64_t n_pred, uint64_t slice, int P,
-                         Rec* send, uint64_t cap, unsigned long long* scnt, LevelState* st, hipStream_t s);
+// Bitmap levels are scattered into tiles of 2^tb positions, kBmMinTb <= tb <= kBmMaxTb, at
+// most kScatterTiles of them (levels of up to 2^31 positions); the settle kernel keeps 18 B
+// per tile word in LDS: 144 KiB at 2^19 positions.
+constexpr unsigned kBmMinTb = 14, kBmMaxTb = 19;
+// level end: per-tile totals of the final bits -> tbase[2t] (rank within the level), tbase[2t+1]
+// (first slot in this rank's settled list, continuing *out_cnt, which it then advances)
+void launch_bm_level_end(int level, const uint64_t* g, const uint64_t* A, unsigned tb, uint64_t tiles, uint64_t* bits,
+                         unsigned long long* tsum, unsigned long long* tbase, LevelState* st,
+                         unsigned long long* gslot, unsigned long long* out_cnt, hipStream_t s);
+void bm_set_lds_limits();
+void launch_bm_range(LevelState* st, int level, hipStream_t s);
+void launch_bm_tile_mark(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
+                         uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A,
+                         hipStream_t s);
+void launch_bm_tile_settle(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
+                           uint64_t tiles, LevelState* st, const uint64_t* g, const uint64_t* A,
+                           const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next, uint64_t next_cap,
+                           hipStream_t s);
+// the settled list (sorted by p) -> scnt[t] = its run for output slice t, scnt[P] = 0
+void launch_bm_bounds(const Rec* out, const unsigned long long* n_out, uint64_t slice, int P, unsigned long long* scnt,
+                      hipStream_t s);
 void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,
                      LevelState* st, hipStream_t s);
 void launch_bm_tail_copy(const uint64_t* sfp, const uint64_t* spos, uint64_t g0, uint64_t total, uint64_t lo,
