@@ -1069,7 +1069,8 @@ __device__ __forceinline__ void r20_split(const R20& r, uint64_t pos_base, uint6
 // <2048, 2048> (two blocks per CU, so one block's atomics and barriers overlap the other's
 // memory phases) measured slower on C2: level-0 scatter 0.156 -> 0.214 ms.
 // kSrc: 0 records from ilist; 1 level-0 arrays ik / ifp with caller positions ipos;
-// 2 level-0 arrays with identity positions.  A compile-time source keeps the loads
+// 2 level-0 arrays with identity positions; 3 records from ilist with padding records
+// (k = 0) to skip: the multi-GPU build's fixed-size exchange regions (k_route_pad).  A compile-time source keeps the loads
 // straight-line: with run-time selects the compiler waited out every record's loads
 // before issuing the next record's (four round trips per round).
 // kP20 (kSrc 2 only): bucket records are R20 (the split kernel reads them).
@@ -1161,7 +1162,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   // Level 0 reads the hash kernel's key-order arrays instead of a record list.
   uint64_t rk_[kKPT], rf_[kKPT], rp_[kKPT];
   auto load = [&](uint64_t i, int q) {
-    if constexpr (kSrc == 0) {
+    if constexpr (kSrc == 0 || kSrc == 3) {
       rk_[q] = ilist[i].k;
       rf_[q] = ilist[i].f;
       rp_[q] = ilist[i].p;
@@ -1185,7 +1186,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
 #pragma unroll
     for (int q = 0; q < kKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
-      if (i < n) {
+      if (i < n && (kSrc != 3 || rk_[q] != 0)) {  // kSrc 3: k = 0 is a padding record (k_route_pad)
         const uint64_t lp = bb_index(seed, rk_[q], words, magic) - rg.plo;
         tt[q] = ts ? __umulhi((uint32_t)(lp >> kSplitSubBitsDev), ts_mul) : (unsigned)(lp >> tb);
         rk[q] = atomicAdd(&cnt[tt[q]], 1u);
@@ -1225,7 +1226,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
 #pragma unroll
     for (int q = 0; q < kKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
-      if (i < n) {
+      if (i < n && (kSrc != 3 || rk_[q] != 0)) {
         const unsigned slot = start[tt[q]] + rk[q];
         if constexpr (kP20) stage20[slot] = r20_make(rk_[q], rf_[q], (uint32_t)(rp_[q] - pos_base));
         else stage[slot] = Rec{rk_[q], rf_[q], rp_[q]};
@@ -1235,7 +1236,8 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     // The next round's loads are issued before any atomic result is used, so the two
     // latencies overlap; one tile at a time waited out each round trip in turn (C3 level
     // 0: ~10 of ~20 us per round).
-    const unsigned m = (unsigned)min<uint64_t>(kR, n - r0);
+    // the round's staged records (kSrc 3: its padding records were not staged)
+    const unsigned m = kSrc == 3 ? start[T - 1] + cnt[T - 1] : (unsigned)min<uint64_t>(kR, n - r0);
     r0 += stride;
     const bool more = r0 < n;
 #pragma unroll
@@ -3170,7 +3172,7 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
   // level 0 whose tiles go to the split kernel, identity positions: R20 records (the
   // split launch makes the same choice)
   const bool p20 = l0 && !b.pos && b.split && g.tb > kRegMaxBits && g.tb <= kSplitMaxBits;
-  auto kern = !l0    ? k_scatter_res<kSubRound, kLdsTiles, 0>
+  auto kern = !l0    ? (b.padded ? k_scatter_res<kSubRound, kLdsTiles, 3> : k_scatter_res<kSubRound, kLdsTiles, 0>)
               : b.pos ? k_scatter_res<kSubRound, kLdsTiles, 1>
               : p20   ? k_scatter_res<kSubRound, kLdsTiles, 2, true>
                       : k_scatter_res<kSubRound, kLdsTiles, 2>;

@@ -904,12 +904,54 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
                                        chunks0(std::max<uint64_t>(n_local, 1)), kTileMaxBits);
   const int gc0 = level_grids(std::max<uint64_t>(n_local, 1), 64 * level_words(N), gh0).gc;
   bool have_kh = false;  // kh / fp written (a retried level-0 route reads them)
-  std::vector<uint64_t> hw, hS;  // words and per-rank range of each distributed level
   std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
   double src_pred = (double)n_local;  // records this rank routes at the current level
   unsigned long long* M = d.h_pinned;  // (P + 1) x P gathered counts, row r = rank r's [scnt, overflow]
   int L = 0;
   for (;;) {
+    // ---- routed levels >= 1 with device-side counts: every (sender, owner) region has a
+    // fixed size C derived from N alone (identical on every rank), the route pads each
+    // region's unused tail with k = 0 records that the reservation scatter skips, and the
+    // regions are exchanged whole, so no count crosses to the host until the build ends.
+    // A region that overflows sets kStRouteOverflow and the attempt reruns on the
+    // host-counted path (conservative).
+    if (L >= 1 && !conservative) {
+      const double mean_l = (double)N * std::pow(q, L);           // level L's global keys
+      const double pair = mean_l / ((double)P * P);                // records per (sender, owner)
+      const uint64_t Cf = (uint64_t)std::ceil(pair * 1.03 + 8.0 * std::sqrt(pair)) + 1024;
+      const uint64_t list_n = (uint64_t)P * Cf;
+      const uint64_t wpred = level_words((uint64_t)(mean_l * 1.02 + 6.0 * std::sqrt(mean_l)) + 1024);
+      const uint64_t Spred = (wpred + P - 1) / P;
+      const bool dev = list_n <= d.cap_list && list_n <= c->res_max_keys && L < kResLevels &&
+                       res_fits(c, list_n, 64 * Spred);
+      if (dev) {
+        if (list_n > d.cap_send) {
+          HIPCHECK(hipStreamSynchronize(s));
+          dalloc(d.send, list_n);
+          d.cap_send = list_n;
+        }
+        HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
+        Rec* const own = lin + (uint64_t)R * Cf;
+        launch_route(L, lredo, (uint64_t)(mean_l / P * 1.05) + 4096, d.send, Cf, d.scnt, st, P, R, own, Cf, s);
+        launch_route_pad(d.send, Cf, d.scnt, P, R, own, s);
+        for (int t = 0; t < P; ++t) {
+          soff[t] = roff[t] = (uint64_t)t * Cf * sizeof(Rec);
+          sbytes[t] = rbytes[t] = t == R ? 0 : Cf * sizeof(Rec);
+        }
+        if (P > 1) cm.alltoallv(d.send, soff.data(), sbytes.data(), lin, roff.data(), rbytes.data(), s);
+        launch_set_u64(&st->n[L], list_n, s);  // the list's length, padding included
+        ev_mark(c, s, "route");
+        BinBuffers bp = (L & 1) ? bsw : b;
+        bp.padded = true;
+        enqueue_list_level(c, bp, L, list_n, 64 * Spred, false, nullptr, s, false);
+        ev_mark(c, s, "levels");
+        cm.allreduce_u64(&st->n[L + 1], d.gslot + L + 1, 1, s);
+        if (L + 1 >= kMaxDistLevels || mean_l * q <= (double)c->dist_switch) break;
+        ++L;
+        launch_dist_setup(st, L, d.gslot + L, 0, R, P, s);
+        continue;
+      }
+    }
     // ---- route level L's records to their owners
     uint64_t C = (uint64_t)(src_pred / P * 1.15) + 4096;
     uint64_t m_chunked = 0;
@@ -965,8 +1007,6 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
     for (int r = 0; r < P; ++r) m += M[(uint64_t)r * (P + 1) + R];
     const uint64_t w = level_words(nL), S = (w + P - 1) / P;
     const uint64_t lo = std::min<uint64_t>((uint64_t)R * S, w), rw = std::min<uint64_t>(S, w - lo);
-    hw.push_back(w);
-    hS.push_back(S);
     if (m > d.cap_list) {
       *msg = "build MPHF: rank " + std::to_string(R) + " received " + std::to_string(m) + " records (capacity " +
              std::to_string(d.cap_list) + ")";
@@ -1036,17 +1076,26 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   ev_mark(c, s, "gather");
   const LevelGeom gcons = choose_geom(std::max<uint64_t>(total, 1), kTargetTiles, kTargetChunks, kRegTileMaxBits);
   enqueue_levels_from(c, b, Ls, total, gcons, conservative, s);
-  // ---- level bit vectors of the distributed levels: all-gather each rank's word range
-  uint64_t woff = 0;
-  for (int l = 0; l < Ls; ++l) {
-    cm.allgather(c->bits + woff + (uint64_t)R * hS[l], d.stage_bits, hS[l] * 8, s);
-    HIPCHECK(hipMemcpyAsync(c->bits + woff, d.stage_bits, hw[l] * 8, hipMemcpyDeviceToDevice, s));
-    woff += hw[l];
-  }
-  ev_mark(c, s, "bits");
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipMemcpyAsync(c->h_st, st, sizeof(LevelState), hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
+  // ---- level bit vectors of the distributed levels: all-gather each rank's word range
+  // (level sizes from the device state: the routed levels >= 1 never sent them to the host)
+  {
+    uint64_t woff = 0;
+    for (int l = 0; l < Ls; ++l) {
+      const uint64_t w = c->h_st->words[l], S = (w + P - 1) / P;
+      if (w > d.cap_stage_words || (uint64_t)P * S > d.cap_stage_words) {
+        *msg = "build MPHF: internal error: level " + std::to_string(l) + " of " + std::to_string(w) +
+               " words exceeds the bit-vector stage";
+        return S3IMPH_ERR_INTERNAL;
+      }
+      cm.allgather(c->bits + woff + (uint64_t)R * S, d.stage_bits, S * 8, s);
+      HIPCHECK(hipMemcpyAsync(c->bits + woff, d.stage_bits, w * 8, hipMemcpyDeviceToDevice, s));
+      woff += w;
+    }
+  }
+  ev_mark(c, s, "bits");
   // ---- per-rank level bases, totals and flags -> this rank's output segments
   const LevelState& hs = *c->h_st;
   const int K = Ls + 3;
@@ -1061,7 +1110,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   auto lb = [&](int r, int l) { return M[(uint64_t)r * K + l]; };
   unsigned flags = 0;
   for (int r = 0; r < P; ++r) flags |= (unsigned)lb(r, Ls + 2);
-  if (flags & (kStGeometry | kStTailOverflow | kStResOverflow)) return conservative ? S3IMPH_ERR_INTERNAL : kDistRetry;
+  if (flags & (kStGeometry | kStTailOverflow | kStResOverflow | kStRouteOverflow)) return conservative ? S3IMPH_ERR_INTERNAL : kDistRetry;
   if (flags & kStTooManyLevels) {
     const unsigned nl = hs.stop_level ? hs.stop_level : hs.nlevels;
     const uint64_t rem = nl < (unsigned)kMaxLevels + 2 ? hs.n[nl] : 0;

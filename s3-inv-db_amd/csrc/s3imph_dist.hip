@@ -177,6 +177,21 @@ __global__ void k_route_flag(LevelState* st, unsigned long long* scnt, int P) {
   st->status &= ~kStRouteOverflow;
 }
 
+// Fixed-size exchange regions (routed levels >= 1): the tail [min(scnt[t], C), C) of every
+// region — send region t, or this rank's own region in the level's input list — is
+// filled with k = 0 records, which the reservation scatter skips (no key hashes to 0:
+// level 0 rejects it), so every region can be sent whole and the receivers need no
+// counts on the host.
+__global__ __launch_bounds__(256) void k_route_pad(Rec* __restrict__ send, uint64_t C,
+                                                   const unsigned long long* __restrict__ scnt, int rank,
+                                                   Rec* __restrict__ self_region) {
+  const int t = blockIdx.y;
+  Rec* reg = t == rank ? self_region : send + (uint64_t)t * C;
+  const uint64_t c0 = min<uint64_t>(scnt[t], C);
+  for (uint64_t i = c0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; i < C; i += (uint64_t)gridDim.x * 256)
+    reg[i] = Rec{0, 0, 0};
+}
+
 }  // namespace
 
 void launch_route_flag(LevelState* st, unsigned long long* scnt, int P, hipStream_t s) {
@@ -203,6 +218,12 @@ void launch_route(int level, const Rec* list, uint64_t n_pred, Rec* send, uint64
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n_pred + kRRound - 1) / kRRound + 8, 2048));
   k_route<1><<<grid, kRT, 0, s>>>(level, nullptr, nullptr, nullptr, 0, 0, list, send, cap, scnt, st,
                                    P, rank, self_dst, self_cap, nullptr, 0);
+}
+
+void launch_route_pad(Rec* send, uint64_t C, const unsigned long long* scnt, int P, int rank, Rec* self_region,
+                      hipStream_t s) {
+  const unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((C / 8 + 255) / 256, 256));
+  k_route_pad<<<dim3(gx, (unsigned)P), 256, 0, s>>>(send, C, scnt, rank, self_region);
 }
 
 void launch_dist_setup(LevelState* st, int L, const unsigned long long* gcount, uint64_t n_value, int rank, int P,

@@ -212,6 +212,7 @@ struct BinBuffers {
   uint64_t* pos_out;
   LevelState* st;
   bool dist;                            // multi-GPU owner levels: level 0 reads list[1] too
+  bool padded = false;                  // list levels hold k = 0 padding records (fixed exchange regions)
   uint32_t* mid;                        // k_mid_levels scratch (kMidScratchU32)
   Rec* split;                           // k_tile_split scratch (split_scratch_records()), or null
 };
@@ -270,6 +271,8 @@ void launch_dist_setup(LevelState* st, int L, const unsigned long long* gcount, 
                        hipStream_t s);
 void launch_set_u64(unsigned long long* p, uint64_t v, hipStream_t s);
 void launch_route_flag(LevelState* st, unsigned long long* scnt, int P, hipStream_t s);
+void launch_route_pad(Rec* send, uint64_t C, const unsigned long long* scnt, int P, int rank, Rec* self_region,
+                      hipStream_t s);
 void launch_dist_replicate(LevelState* st, int L, uint64_t n_all, uint64_t skip_from, hipStream_t s);
 
 // ---- the bitmap decomposition of the multi-GPU build (s3imph_bitmap.hip) --------------
