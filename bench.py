@@ -238,6 +238,16 @@ def main() -> None:
                 traffic = ent["hbm_bytes_per_launch"]
         except (OSError, ValueError):
             pass
+        try:  # the whole build's counter bytes (tools/gpu_pmc_all.sh), one GPU
+            with open(args.traffic) as f:
+                pl = json.load(f).get(args.config, {}).get("_pipeline")
+            if pl and pl.get("n_gpus", 1) == world and not use_dist:
+                result["pipeline_traffic"] = {"hbm_bytes_per_step": pl["hbm_bytes_per_build"],
+                                              "read_bytes": pl["read_bytes"], "write_bytes": pl["write_bytes"],
+                                              "alg_bytes": b_alg, "ratio": pl["hbm_bytes_per_build"] / b_alg,
+                                              "source": os.path.relpath(args.traffic, ROOT)}
+        except (OSError, ValueError, KeyError):
+            pass
         hbm = {"achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS}
         result["roofline"] = {"kernel": dom, "bound": "hbm", **hbm, "traffic": traffic, "alg_bytes": alg,
                               "avg_ms": dom_ms, "timed_region_events": dom in timed_stages}

@@ -39,7 +39,7 @@ constexpr int kH0Grid = 4096;         // ... blocks: 4 per resident slot, a cont
 constexpr int kSB = 1024;             // scatter block
 constexpr int kTailT = 1024;          // tail block
 constexpr unsigned kLenBuckets = 256;  // key-length classes (4 B each) of the level-0 hash sort
-constexpr uint64_t kTcntWords = (uint64_t)kResLevels * kScatterTiles * kResShards;
+constexpr uint64_t kTcntWords = (uint64_t)kResLevels * kTcntStride;
 constexpr uint64_t kLdsTiles = kScatterTiles;  // count / start / cursor entries of the LDS-staged scatters
 constexpr unsigned long long kGate = kTailKeys;
 constexpr int kTailW32 = (int)(2 * ((kGammaNum * kTailKeys + 63) / 64));  // A/C words of the largest tail level
@@ -3128,7 +3128,7 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
   if (g.tb <= kRegMaxBits) {
     // records per tile ~2^(tb-1): pick the variant whose NT x R covers it with margin
     // (lighter variants keep several tiles resident per CU)
-    const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kScatterTiles * kResShards : nullptr;
+    const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kTcntStride : nullptr;
     const size_t lds = tile_reg_lds_bytes(g.tb);
 #define S3_TILE_REG(NT_, R_, W_)                                                                             \
   (tc ? k_tile_reg<NT_, R_, W_, true> : k_tile_reg<NT_, R_, W_, false>)<<<grid_tiles, NT_, lds, s>>>(level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags, \
@@ -3148,7 +3148,7 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
 #undef S3_TILE_REG
     return;
   }
-  const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kScatterTiles * kResShards : nullptr;
+  const unsigned* tc = reserved ? b.tcnt + (uint64_t)level * kTcntStride : nullptr;
   // 2^15 / 2^16 tiles: the split kernel (k_tile stays for contexts without its scratch
   // and for the 2^17+ tiles of oversized conservative reruns)
   if (b.split && g.tb > kRegMaxBits && g.tb <= kSplitMaxBits) {
@@ -3168,7 +3168,7 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
                                uint64_t i_hi) {
   const bool l0 = level == 0 && !b.dist;
   const Rec* il = l0 ? nullptr : b.list[(level - 1) & 1];
-  unsigned* tc = b.tcnt + (uint64_t)level * kScatterTiles * kResShards;
+  unsigned* tc = b.tcnt + (uint64_t)level * kTcntStride;
   // level 0 whose tiles go to the split kernel, identity positions: R20 records (the
   // split launch makes the same choice)
   const bool p20 = l0 && !b.pos && b.split && g.tb > kRegMaxBits && g.tb <= kSplitMaxBits;

@@ -86,7 +86,7 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   dalloc(c->scan_sums, kHistCap / 2048 + 2);
   dalloc(c->flags, kMaxTiles + 2);
   dalloc(c->sflags, kHistCap / kScanSeg + 2);
-  dalloc(c->tcnt, (uint64_t)kResLevels * kScatterTiles * kResShards);
+  dalloc(c->tcnt, (uint64_t)kResLevels * kTcntStride);
   alloc_common(c, cap);
   dalloc(c->bits, c->cap_words);
   dalloc(c->rank_base, 2 * c->cap_words);  // rank directory: (word, rank) pairs
@@ -364,7 +364,11 @@ int enqueue_levels_from(s3imph_ctx* c, const BinBuffers& b, int L0, uint64_t n0,
     }
     launched = L;
     const uint64_t nb = conservative ? n0 : (uint64_t)(pred * 1.1) + 4096;
-    enqueue_list_level(c, b, L, nb, 64 * level_words(nb), conservative, conservative ? &gcons : nullptr, s);
+    // geometry from a tight bound on the level's size (level sizes concentrate: sigma ~ sqrt(n));
+    // a level past it flags kStGeometry and the build reruns conservatively
+    const uint64_t nsz = conservative ? n0 : (uint64_t)(pred * 1.02 + 6.0 * std::sqrt(pred)) + 1024;
+    enqueue_list_level(c, b, L, nb, 64 * level_words(nsz), conservative, conservative ? &gcons : nullptr, s,
+                       !conservative);
   }
   ev_mark(c, s, "levels");
   launch_binned_tail(L0, launched, b, s);
@@ -749,7 +753,7 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
   dalloc(c->scan_sums, kHistCap / 2048 + 2);
   dalloc(c->flags, kMaxTiles + 2);
   dalloc(c->sflags, kHistCap / kScanSeg + 2);
-  dalloc(c->tcnt, (uint64_t)kResLevels * kScatterTiles * kResShards);
+  dalloc(c->tcnt, (uint64_t)kResLevels * kTcntStride);
   c->cap_words = capw;
   dalloc(c->bits, capw);
   dalloc(c->rank_base, 2 * capw);  // rank directory: (word, rank) pairs
@@ -891,9 +895,10 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   std::swap(bsw.list[0], bsw.list[1]);
   Rec* const lin = c->list[1];
   Rec* const lredo = c->list[0];
+  Rec* redo = lredo;  // where the last level's collided records are (one rank: ping-pong)
   const double q = 1.0 - std::exp(-0.5);
   launch_init_state(st, n_local, out_cap, s, n_local ? offsets : nullptr);  // samples key lengths (st->skew)
-  HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kScatterTiles * kResShards * sizeof(unsigned), s));
+  HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kTcntStride * sizeof(unsigned), s));
   launch_dist_setup(st, 0, nullptr, N, R, P, s);
   ev_mark(c, s, "init");
   // level 0's key hashes and fingerprints, once (the routing below may be retried); a big
@@ -924,6 +929,25 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
       const uint64_t Spred = (wpred + P - 1) / P;
       const bool dev = list_n <= d.cap_list && list_n <= c->res_max_keys && L < kResLevels &&
                        res_fits(c, list_n, 64 * Spred);
+      if (dev && P == 1) {
+        // one rank: every record is its own, so nothing is routed — the level reads the
+        // previous level's collided records where they lie and writes its own to the other
+        // list (the single-GPU ping-pong)
+        Rec* const other = redo == c->list[0] ? c->list[1] : c->list[0];
+        BinBuffers bp = b;
+        bp.list[(L - 1) & 1] = redo;
+        bp.list[L & 1] = other;
+        ev_mark(c, s, "route");
+        enqueue_list_level(c, bp, L, (uint64_t)(mean_l * 1.02 + 6.0 * std::sqrt(mean_l)) + 1024, 64 * Spred, false,
+                           nullptr, s, false);
+        ev_mark(c, s, "levels");
+        redo = other;
+        cm.allreduce_u64(&st->n[L + 1], d.gslot + L + 1, 1, s);
+        if (L + 1 >= kMaxDistLevels || mean_l * q <= (double)c->dist_switch) break;
+        ++L;
+        launch_dist_setup(st, L, d.gslot + L, 0, R, P, s);
+        continue;
+      }
       if (dev) {
         if (list_n > d.cap_send) {
           HIPCHECK(hipStreamSynchronize(s));
@@ -951,6 +975,39 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
         launch_dist_setup(st, L, d.gslot + L, 0, R, P, s);
         continue;
       }
+    }
+    if (L == 0 && P == 1 && !conservative && n_local) {
+      // one rank: level 0 is the single-GPU level 0 (nothing to route) — the pair-round hash
+      // into kh / fp, the reservation scatter from them (20-byte records when positions are
+      // identities), the tile kernels writing outputs and collided records (into lredo)
+      const LevelGeom g0 = choose_geom(n_local, kTargetTiles0, chunks0(n_local), kRegTileMaxBits);
+      const uint64_t T0 = tiles_of(level_words(N), g0.tb, 0);
+      if (N == n_local && T0 <= kScatterTiles && c->res0 && res_fits(c, n_local, 64 * level_words(N), T0)) {
+        BinBuffers b0 = b;
+        b0.dist = false;
+        b0.pos = pos;
+        b0.pos_base = key_base;
+        launch_hash0_only(blob, offsets, n_local, b0, gh0, gc0, s);
+        ev_mark(c, s, "hash_count0");
+        LevelGeom gr0 = g0;
+        if (b0.split && g0.tb > kRegTileMaxBits && g0.tb <= kSplitMaxBits) gr0.ts = choose_split_ts(64 * level_words(N), true);
+        launch_binned_scatter_res(0, b0, gr0, 256, s);
+        launch_binned_tile(0, b0, gr0, level_grids(n_local, 64 * level_words(N), g0).gt, s, true);
+        ev_mark(c, s, "level0");
+        cm.allreduce_u64(&st->n[1], d.gslot + 1, 1, s);
+        src_pred = (double)n_local * q * 1.05 + 1024;
+        if (1 >= kMaxDistLevels || (double)N * q <= (double)c->dist_switch) break;
+        ++L;
+        launch_dist_setup(st, L, d.gslot + L, 0, R, P, s);
+        continue;
+      }
+    }
+    if (redo != lredo) {  // a one-rank level ping-ponged before this host-counted one: the route reads lredo
+      HIPCHECK(hipStreamSynchronize(s));
+      unsigned long long nr = 0;
+      HIPCHECK(hipMemcpy(&nr, &st->n[L], 8, hipMemcpyDeviceToHost));
+      HIPCHECK(hipMemcpyAsync(lredo, redo, nr * sizeof(Rec), hipMemcpyDeviceToDevice, s));
+      redo = lredo;
     }
     // ---- route level L's records to their owners
     uint64_t C = (uint64_t)(src_pred / P * 1.15) + 4096;
@@ -1064,7 +1121,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
       dalloc(d.send, (uint64_t)P * maxc);
       d.cap_send = (uint64_t)P * maxc;
     }
-    cm.allgather(lredo, d.send, maxc * sizeof(Rec), s);
+    cm.allgather(redo, d.send, maxc * sizeof(Rec), s);
     uint64_t o = 0;
     for (int r = 0; r < P; ++r) {
       if (cnt[r])
@@ -1214,7 +1271,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   Rec* const out = d.bm_out;                   // this rank's settled (p, fp, pos) triples
   unsigned long long* const out_cnt = d.small + 4096;
   HIPCHECK(hipMemsetAsync(out_cnt, 0, 8, s));
-  HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kMaxDistLevels * kScatterTiles * kResShards * sizeof(unsigned), s));
+  HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kMaxDistLevels * kTcntStride * sizeof(unsigned), s));
   // The level's records go through the reservation scatter into tiles over the level's
   // whole position range (this rank's records only); the tile kernels then mark and
   // settle a tile at a time in LDS.  Level 0 reads the hash kernel's key-order arrays.
@@ -1245,7 +1302,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     g.ts = 0;
     const int gsr = (int)std::max<uint64_t>(1, std::min<uint64_t>((np + kSubRound - 1) / kSubRound, 256));
     launch_binned_scatter_res(L, bs, g, gsr, s);
-    const unsigned* tc = c->tcnt + (uint64_t)L * kScatterTiles * kResShards;
+    const unsigned* tc = c->tcnt + (uint64_t)L * kTcntStride;
     launch_bm_tile_mark(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, s);
     cm.reduce_scatter_u8(d.bm_lanes, d.bm_slice, 64 * S, s);
     launch_bm_decide(d.bm_slice, S, d.bm_dec, st, s);

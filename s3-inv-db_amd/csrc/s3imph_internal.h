@@ -115,6 +115,7 @@ constexpr uint64_t kResMaxKeys = 1ull << 32;
 constexpr uint64_t kResSmallKeys = 2ull << 20;  // ... with 4x slot headroom up to this size, 2x above
 constexpr int kResShards = 8;                 // per-tile reservation counters (one per XCD)
 constexpr int kResLevels = 32;                // levels that may use the reservation path
+constexpr uint64_t kTcntStride = kScatterTiles * kResShards;  // tcnt words per level
 constexpr double kTailMargin = 1.1;
 constexpr uint64_t kTargetChunks = 768;  // 3 resident 1024-thread count blocks x 256 CUs
 constexpr uint64_t kBigChunksKeys = 20ull << 20;  // level-0 hash of this many keys or more: 2x the chunks

@@ -52,13 +52,26 @@ def main():
         ent = tr.setdefault(cfg, {})
         scatter0 = "k_scatter_res" if "k_scatter_res" in first and "k_hscan" not in first else "k_scatter"
         tile0 = next((o["kernel"] for o in out if o["kernel"] in ("k_tile_reg", "k_tile_split", "k_tile")), "k_tile_reg")
-        hash0 = "k_hash0_pair" if "k_hash0_pair" in first else "k_hash_count0"  # skewed sets: k_hash_count0
+        # the level-0 hash that did the work (the others are no-op launches for this set's skew)
+        hash0 = max((k for k in ("k_hash0_pair", "k_hash_skew", "k_hash_count0") if k in first),
+                    key=lambda k: first[k]["read_bytes_corrected"] + first[k]["write_bytes"], default="k_hash0_pair")
         for stage, kern in (("hash_count0", hash0), ("scatter0", scatter0), ("tile0", tile0)):
             if kern in first:
                 o = first[kern]
                 ent[stage] = {"kernel": kern, "n_gpus": 1,
                               "hbm_bytes_per_launch": int(o["read_bytes_corrected"] + o["write_bytes"]),
                               "read_bytes": int(o["read_bytes_corrected"]), "write_bytes": int(o["write_bytes"])}
+        # the whole build: every dispatch of the last build summed (bench.py's pipeline_traffic)
+        per = {}
+        for o in out:
+            e = per.setdefault(o["kernel"], [0, 0])
+            e[0] += int(o["read_bytes_corrected"])
+            e[1] += int(o["write_bytes"])
+        rd = sum(v[0] for v in per.values())
+        wr = sum(v[1] for v in per.values())
+        ent["_pipeline"] = {"n_gpus": 1, "hbm_bytes_per_build": rd + wr, "read_bytes": rd, "write_bytes": wr,
+                            "dispatches": len(out),
+                            "by_kernel": {k: {"read_bytes": v[0], "write_bytes": v[1]} for k, v in sorted(per.items())}}
         json.dump(tr, open(path, "w"), indent=1, sort_keys=True)
 
 
