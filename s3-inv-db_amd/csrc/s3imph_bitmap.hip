@@ -4,8 +4,9 @@
 // Each rank keeps its key shard for the whole build.  At a distributed level L (global
 // key count n_L, words_L = ceil(2 n_L / 64)) every rank hashes its active records over the
 // WHOLE level and marks a local 2-bit count per position (A: >= 1 key, C: >= 2 keys) with
-// atomics; the count lanes min(local count, 2) are expanded to one byte per position and
-// summed over the ranks by an RCCL reduce-scatter (u8 sum: at most 2P <= 128), so rank r
+// in LDS; the count lanes min(local count, 2) are expanded to one nibble per position (P <= 7
+// ranks: sums <= 14, no carry out of a nibble) or one byte (P >= 8: sums <= 2P <= 128) and
+// summed over the ranks by an RCCL reduce-scatter (u8 sum), so rank r
 // holds the global counts of its slice of the level's words; it decides the final bits
 // there (exactly one key: count == 1) and an all-gather gives every rank the level's final
 // bit vector — mph.bin's level L, the same bytes a single GPU writes.  Every rank then
@@ -46,18 +47,40 @@ __device__ __forceinline__ unsigned gather4(unsigned m) {  // high bits of the 4
   return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
 }
 
-// This rank's slice of the summed lanes (S words) -> final bits: exactly one key.
+// nibbles of v equal to 1 -> 8 bits (nibble j -> bit j)
+__device__ __forceinline__ unsigned nib_ones8(unsigned v) {
+  const unsigned t = v ^ 0x11111111u;
+  const unsigned y = ~(((t & 0x77777777u) + 0x77777777u) | t | 0x77777777u);  // bit 3 of each zero nibble of t
+  unsigned m = (y >> 3) & 0x11111111u;
+  m = (m | (m >> 3)) & 0x03030303u;
+  m = (m | (m >> 6)) & 0x000f000fu;
+  return (m | (m >> 12)) & 0xffu;
+}
+
+// This rank's slice of the summed lanes (S words) -> final bits: exactly one key.  kNib: a
+// lane is one nibble (two positions per byte: P <= 7 ranks sum to at most 14), else a byte.
+template <bool kNib>
 __global__ __launch_bounds__(kBT) void k_bm_decide(const uint4* __restrict__ slice, uint64_t S,
                                                    uint64_t* __restrict__ out, const LevelState* st) {
   if (bm_dead(st)) return;
   for (uint64_t w = (uint64_t)blockIdx.x * kBT + threadIdx.x; w < S; w += (uint64_t)gridDim.x * kBT) {
     uint64_t bits = 0;
+    if (kNib) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint4 v = slice[4 * w + q];
-      const uint64_t b16 = gather4(ones_mask(v.x)) | (gather4(ones_mask(v.y)) << 4) |
-                           (gather4(ones_mask(v.z)) << 8) | (gather4(ones_mask(v.w)) << 12);
-      bits |= b16 << (16 * q);
+      for (int q = 0; q < 2; ++q) {
+        const uint4 v = slice[2 * w + q];
+        const uint64_t b32 = (uint64_t)nib_ones8(v.x) | ((uint64_t)nib_ones8(v.y) << 8) |
+                             ((uint64_t)nib_ones8(v.z) << 16) | ((uint64_t)nib_ones8(v.w) << 24);
+        bits |= b32 << (32 * q);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = slice[4 * w + q];
+        const uint64_t b16 = gather4(ones_mask(v.x)) | (gather4(ones_mask(v.y)) << 4) |
+                             (gather4(ones_mask(v.z)) << 8) | (gather4(ones_mask(v.w)) << 12);
+        bits |= b16 << (16 * q);
+      }
     }
     out[w] = bits;
   }
@@ -167,6 +190,12 @@ constexpr int kU = 4;
 __device__ __forceinline__ uint32_t spread4(uint32_t v) {  // 4 bits -> 4 bytes (bit j -> byte j)
   return (v & 1u) | ((v & 2u) << 7) | ((v & 4u) << 14) | ((v & 8u) << 21);
 }
+__device__ __forceinline__ uint32_t spread8n(uint32_t v) {  // 8 bits -> 8 nibbles (bit j -> nibble j)
+  v &= 0xffu;
+  v = (v | (v << 12)) & 0x000f000fu;
+  v = (v | (v << 6)) & 0x03030303u;
+  return (v | (v << 3)) & 0x11111111u;
+}
 
 // shard fills of tile t -> exclusive prefix fo[0..8] (fo[8] = the tile's records)
 __device__ __forceinline__ void shard_prefix(const unsigned* __restrict__ tc, uint64_t t, unsigned* fo) {
@@ -192,6 +221,7 @@ __device__ __forceinline__ uint64_t rec_index(unsigned i, const unsigned* fo, ui
 // Mark: this rank's records of tile t -> local A (>= 1 key) / C (>= 2 keys) in LDS ->
 // the tile's count lanes (byte x = A + C = min(local count, 2)) and its A words (kept
 // for the settle).  Lanes of positions past the level's true size are zeroed here too.
+template <bool kNib>
 __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const Rec* __restrict__ bucket,
                                                       const unsigned* __restrict__ tc, uint64_t bucket_cap,
                                                       unsigned tb, const LevelState* st, uint64_t wpad,
@@ -205,9 +235,9 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const Rec* __re
   uint32_t* sA = bm_lds;
   uint32_t* sC = bm_lds + W32;
   const unsigned tid = threadIdx.x;
-  // zero the lanes of [64 words, 64 wpad): no tile covers them
-  for (uint64_t q = 64 * words / 16 + (uint64_t)blockIdx.x * kTT + tid; q < 64 * wpad / 16;
-       q += (uint64_t)gridDim.x * kTT)
+  // zero the lanes of [64 words, 64 wpad): no tile covers them (64 positions: 4 or 2 uint4)
+  constexpr uint64_t kU4 = kNib ? 2 : 4;
+  for (uint64_t q = kU4 * words + (uint64_t)blockIdx.x * kTT + tid; q < kU4 * wpad; q += (uint64_t)gridDim.x * kTT)
     reinterpret_cast<uint4*>(lanes)[q] = make_uint4(0, 0, 0, 0);
   if (T == 0) return;
   const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
@@ -241,13 +271,19 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const Rec* __re
     for (unsigned j = tid; j < wend; j += kTT) {
       const uint32_t a = sA[j], c = sC[j];
       A32[(t0 >> 5) + j] = a;
-      uint4* dst = reinterpret_cast<uint4*>(lanes + t0 + 32ull * j);
+      if (kNib) {  // 32 lanes in 16 bytes
+        uint4* dst = reinterpret_cast<uint4*>(lanes + t0 / 2 + 16ull * j);
+        dst[0] = make_uint4(spread8n(a) + spread8n(c), spread8n(a >> 8) + spread8n(c >> 8),
+                            spread8n(a >> 16) + spread8n(c >> 16), spread8n(a >> 24) + spread8n(c >> 24));
+      } else {
+        uint4* dst = reinterpret_cast<uint4*>(lanes + t0 + 32ull * j);
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {  // bytes 16q .. 16q + 15 of this word's 32 lanes
-        const uint32_t as = a >> (16 * q), cs = c >> (16 * q);
-        dst[q] = make_uint4(spread4(as & 15u) + spread4(cs & 15u), spread4((as >> 4) & 15u) + spread4((cs >> 4) & 15u),
-                            spread4((as >> 8) & 15u) + spread4((cs >> 8) & 15u),
-                            spread4((as >> 12) & 15u) + spread4((cs >> 12) & 15u));
+        for (int q = 0; q < 2; ++q) {  // bytes 16q .. 16q + 15 of this word's 32 lanes
+          const uint32_t as = a >> (16 * q), cs = c >> (16 * q);
+          dst[q] = make_uint4(spread4(as & 15u) + spread4(cs & 15u), spread4((as >> 4) & 15u) + spread4((cs >> 4) & 15u),
+                              spread4((as >> 8) & 15u) + spread4((cs >> 8) & 15u),
+                              spread4((as >> 12) & 15u) + spread4((cs >> 12) & 15u));
+        }
       }
     }
     __syncthreads();
@@ -489,8 +525,9 @@ void launch_bm_check(LevelState* st, int level, uint64_t wmax, hipStream_t s) {
   k_bm_check<<<1, 64, 0, s>>>(st, level, wmax);
 }
 
-void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const LevelState* st, hipStream_t s) {
-  k_bm_decide<<<grid_for(S, kBT, 8192), kBT, 0, s>>>(reinterpret_cast<const uint4*>(slice), S, out, st);
+void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const LevelState* st, bool nib, hipStream_t s) {
+  if (nib) k_bm_decide<true><<<grid_for(S, kBT, 8192), kBT, 0, s>>>(reinterpret_cast<const uint4*>(slice), S, out, st);
+  else k_bm_decide<false><<<grid_for(S, kBT, 8192), kBT, 0, s>>>(reinterpret_cast<const uint4*>(slice), S, out, st);
 }
 
 void launch_bm_level_end(int level, const uint64_t* g, const uint64_t* A, unsigned tb, uint64_t tiles, uint64_t* bits,
@@ -506,7 +543,9 @@ size_t bm_tile_lds(unsigned tb, bool settle) {
 }
 
 void bm_set_lds_limits() {
-  (void)hipFuncSetAttribute((const void*)k_bm_tile_mark, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_bm_tile_mark<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)bm_tile_lds(kBmMaxTb, false));
+  (void)hipFuncSetAttribute((const void*)k_bm_tile_mark<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)bm_tile_lds(kBmMaxTb, false));
   (void)hipFuncSetAttribute((const void*)k_bm_tile_settle, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)bm_tile_lds(kBmMaxTb, true));
@@ -515,11 +554,12 @@ void bm_set_lds_limits() {
 void launch_bm_range(LevelState* st, int level, hipStream_t s) { k_bm_range<<<1, 64, 0, s>>>(st, level); }
 
 void launch_bm_tile_mark(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
-                         uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A,
+                         uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A, bool nib,
                          hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(256, std::min<uint64_t>(tiles, 1024));
-  k_bm_tile_mark<<<grid, kTT, bm_tile_lds(tb, false), s>>>(level, bucket, tc, bucket_cap, tb, st, wpad, lanes,
-                                                          reinterpret_cast<uint32_t*>(A));
+  auto kern = nib ? k_bm_tile_mark<true> : k_bm_tile_mark<false>;
+  kern<<<grid, kTT, bm_tile_lds(tb, false), s>>>(level, bucket, tc, bucket_cap, tb, st, wpad, lanes,
+                                                 reinterpret_cast<uint32_t*>(A));
 }
 
 void launch_bm_tile_settle(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,

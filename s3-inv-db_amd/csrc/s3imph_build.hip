@@ -366,9 +366,9 @@ int enqueue_levels_from(s3imph_ctx* c, const BinBuffers& b, int L0, uint64_t n0,
     const uint64_t nb = conservative ? n0 : (uint64_t)(pred * 1.1) + 4096;
     // geometry from a tight bound on the level's size (level sizes concentrate: sigma ~ sqrt(n));
     // a level past it flags kStGeometry and the build reruns conservatively
-    const uint64_t nsz = conservative ? n0 : (uint64_t)(pred * 1.02 + 6.0 * std::sqrt(pred)) + 1024;
-    enqueue_list_level(c, b, L, nb, 64 * level_words(nsz), conservative, conservative ? &gcons : nullptr, s,
-                       !conservative);
+    const bool tight = !conservative && !c->loose_geom;
+    const uint64_t nsz = tight ? (uint64_t)(pred * 1.02 + 6.0 * std::sqrt(pred)) + 1024 : nb;
+    enqueue_list_level(c, b, L, nb, 64 * level_words(nsz), conservative, conservative ? &gcons : nullptr, s, tight);
   }
   ev_mark(c, s, "levels");
   launch_binned_tail(L0, launched, b, s);
@@ -1284,6 +1284,8 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   // size is known without a host round trip; a level outgrowing its bound sets
   // kStBitmapBound and the build reruns on the routed decomposition.
   double nb = (double)N, npred = (double)n_local;
+  // count lanes: a nibble per position while the rank sums cannot carry out of it (2P <= 14)
+  const bool nib = P <= kBmNibRanks;
   int L = 0;
   for (;;) {
     const uint64_t wmax = level_words((uint64_t)std::ceil(nb)), S = (wmax + P - 1) / P, wpad = S * (uint64_t)P;
@@ -1303,9 +1305,9 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     const int gsr = (int)std::max<uint64_t>(1, std::min<uint64_t>((np + kSubRound - 1) / kSubRound, 256));
     launch_binned_scatter_res(L, bs, g, gsr, s);
     const unsigned* tc = c->tcnt + (uint64_t)L * kTcntStride;
-    launch_bm_tile_mark(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, s);
-    cm.reduce_scatter_u8(d.bm_lanes, d.bm_slice, 64 * S, s);
-    launch_bm_decide(d.bm_slice, S, d.bm_dec, st, s);
+    launch_bm_tile_mark(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, nib, s);
+    cm.reduce_scatter_u8(d.bm_lanes, d.bm_slice, (nib ? 32 : 64) * S, s);
+    launch_bm_decide(d.bm_slice, S, d.bm_dec, st, nib, s);
     cm.allgather(d.bm_dec, d.bm_g, 8 * S, s);
     launch_bm_level_end(L, d.bm_g, d.bm_a, tb, tiles, c->bits, d.bm_tsum, d.bm_tbase, st, d.gslot, out_cnt, s);
     launch_bm_tile_settle(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
@@ -1797,6 +1799,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     if (const char* m = std::getenv("S3IMPH_RES_MAX")) c->res_max_keys = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_RES_FILL")) c->res_fill = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_RES0")) c->res0 = std::atoi(m);
+    c->loose_geom = std::getenv("S3IMPH_LOOSE_GEOM") != nullptr;  // A/B knob: list-level geometry from 1.1x bounds
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_DIST_MODE")) c->d.mode = std::strcmp(m, "bitmap") == 0 ? kDistBitmap : kDistRoute;

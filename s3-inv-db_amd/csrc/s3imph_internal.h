@@ -278,7 +278,9 @@ void launch_dist_replicate(LevelState* st, int L, uint64_t n_all, uint64_t skip_
 
 // ---- the bitmap decomposition of the multi-GPU build (s3imph_bitmap.hip) --------------
 void launch_bm_check(LevelState* st, int level, uint64_t wmax, hipStream_t s);
-void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const LevelState* st, hipStream_t s);
+// nib: count lanes are nibbles (two positions per byte; P <= kBmNibRanks), else bytes
+constexpr int kBmNibRanks = 7;
+void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const LevelState* st, bool nib, hipStream_t s);
 // Bitmap levels are scattered into tiles of 2^tb positions, kBmMinTb <= tb <= kBmMaxTb, at
 // most kScatterTiles of them (levels of up to 2^31 positions); the settle kernel keeps 18 B
 // per tile word in LDS: 144 KiB at 2^19 positions.
@@ -291,7 +293,7 @@ void launch_bm_level_end(int level, const uint64_t* g, const uint64_t* A, unsign
 void bm_set_lds_limits();
 void launch_bm_range(LevelState* st, int level, hipStream_t s);
 void launch_bm_tile_mark(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
-                         uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A,
+                         uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A, bool nib,
                          hipStream_t s);
 void launch_bm_tile_settle(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
                            uint64_t tiles, LevelState* st, const uint64_t* g, const uint64_t* A,
