@@ -896,6 +896,9 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   Rec* const lin = c->list[1];
   Rec* const lredo = c->list[0];
   Rec* redo = lredo;  // where the last level's collided records are (one rank: ping-pong)
+  // one rank routes nothing (S3IMPH_DIST_ROUTE_SELF: route anyway, so tests drive the routed
+  // kernels and the RCCL exchange with nranks = 1)
+  const bool one = P == 1 && !c->route_self;
   const double q = 1.0 - std::exp(-0.5);
   launch_init_state(st, n_local, out_cap, s, n_local ? offsets : nullptr);  // samples key lengths (st->skew)
   HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kResLevels * kTcntStride * sizeof(unsigned), s));
@@ -929,7 +932,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
       const uint64_t Spred = (wpred + P - 1) / P;
       const bool dev = list_n <= d.cap_list && list_n <= c->res_max_keys && L < kResLevels &&
                        res_fits(c, list_n, 64 * Spred);
-      if (dev && P == 1) {
+      if (dev && one) {
         // one rank: every record is its own, so nothing is routed — the level reads the
         // previous level's collided records where they lie and writes its own to the other
         // list (the single-GPU ping-pong)
@@ -976,7 +979,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
         continue;
       }
     }
-    if (L == 0 && P == 1 && !conservative && n_local) {
+    if (L == 0 && one && !conservative && n_local) {
       // one rank: level 0 is the single-GPU level 0 (nothing to route) — the pair-round hash
       // into kh / fp, the reservation scatter from them (20-byte records when positions are
       // identities), the tile kernels writing outputs and collided records (into lredo)
@@ -1799,7 +1802,8 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     if (const char* m = std::getenv("S3IMPH_RES_MAX")) c->res_max_keys = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_RES_FILL")) c->res_fill = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_RES0")) c->res0 = std::atoi(m);
-    c->loose_geom = std::getenv("S3IMPH_LOOSE_GEOM") != nullptr;  // A/B knob: list-level geometry from 1.1x bounds
+    c->loose_geom = std::getenv("S3IMPH_LOOSE_GEOM") != nullptr;
+    c->route_self = std::getenv("S3IMPH_DIST_ROUTE_SELF") != nullptr;  // A/B knob: list-level geometry from 1.1x bounds
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_DIST_MODE")) c->d.mode = std::strcmp(m, "bitmap") == 0 ? kDistBitmap : kDistRoute;

@@ -133,15 +133,19 @@ def test_dist_duplicate_across_ranks_fails_everywhere(mode):
         assert r[1] == "error" and r[2] == s3imph.ERR_DUP_KEY_HASH, r
 
 
-@pytest.mark.parametrize("mode", ["route", "bitmap"])
+@pytest.mark.parametrize("mode", ["route", "route_self", "bitmap"])
 def test_dist_rccl_single_rank_routes_levels(oracle_lib, monkeypatch, mode):
     """The RCCL transport (nranks = 1 on this box) through several sharded levels: route
-    (all-to-all, all-gathers) and bitmap (ncclReduceScatter of the count lanes,
-    ncclAllGather of the final bits, the output all-to-all)."""
+    (one rank: nothing to route, the single-GPU level 0 and ping-ponged levels), route_self
+    (S3IMPH_DIST_ROUTE_SELF: the fused level-0 route, the padded fixed-region routes of levels
+    >= 1 and their all-to-alls, as with P > 1) and bitmap (ncclReduceScatter of the count
+    lanes, ncclAllGather of the final bits, the output all-to-all)."""
     import torch
     import s3imph
     monkeypatch.setenv("S3IMPH_DIST_SWITCH", "20000")
     monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
+    if mode == "route_self":
+        monkeypatch.setenv("S3IMPH_DIST_ROUTE_SELF", "1")
     d = s3imph.DistBuilder(0, s3imph.dist_unique_id(), 0, 1)
     d.set_mode(s3imph.DIST_BITMAP if mode == "bitmap" else s3imph.DIST_ROUTE)
     n = 300_000
