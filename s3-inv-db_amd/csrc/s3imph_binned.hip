@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
                                                      uint64_t i_hi, unsigned ts) {
   constexpr int kKPT = kR / kSB;
   static_assert(!kP20 || kSrc == 2, "20-byte records carry identity positions");
-  __shared__ uint64_t stage_raw[kR * 3];  // kR Rec, or kR R20
+  __shared__ uint64_t stage_raw[kP20 ? (kR * 5 + 1) / 2 : kR * 3];  // kR Rec, or kR R20
   Rec* const stage = reinterpret_cast<Rec*>(stage_raw);
   R20* const stage20 = reinterpret_cast<R20*>(stage_raw);
   R20* const bucket20 = reinterpret_cast<R20*>(bucket);
@@ -2384,8 +2384,10 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, LevelS
     int ok = 1;
     unsigned spins = 0;
     while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++spins > (1u << 22)) {  // bounded: a missing workgroup must not hang the GPU
-        atomicOr(&st->status, kStLookback);
+      if (++spins > (1u << 22)) {  // bounded: a missing workgroup must not hang the GPU.  Workgroups
+        // that never become resident (another build's persistent kernel holds the CUs) are the
+        // likely cause: the attempt reruns on the conservative path, which has no grid barrier.
+        atomicOr(&st->status, kStTailOverflow);
         ok = 0;
         break;
       }
@@ -2422,7 +2424,7 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
   __shared__ int s_go, s_ok;
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const unsigned g = blockIdx.x, G = gridDim.x;
-  unsigned* bar = mid;
+  unsigned* bar = &st->mid_bar;  // zeroed by k_init_state: one mid launch per build attempt
   unsigned* xc = mid + kMidXc;  // [owner][sender] segment counts
   unsigned long long* tot = reinterpret_cast<unsigned long long*>(mid + kMidTot);
   const uint64_t N = st->out_cap;
@@ -3165,23 +3167,51 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
 }
 
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s, uint64_t i_lo,
-                               uint64_t i_hi) {
+                               uint64_t i_hi, uint64_t tmax) {
   const bool l0 = level == 0 && !b.dist;
   const Rec* il = l0 ? nullptr : b.list[(level - 1) & 1];
   unsigned* tc = b.tcnt + (uint64_t)level * kTcntStride;
   // level 0 whose tiles go to the split kernel, identity positions: R20 records (the
   // split launch makes the same choice)
   const bool p20 = l0 && !b.pos && b.split && g.tb > kRegMaxBits && g.tb <= kSplitMaxBits;
-  auto kern = !l0    ? (b.padded ? k_scatter_res<kSubRound, kLdsTiles, 3> : k_scatter_res<kSubRound, kLdsTiles, 0>)
-              : b.pos ? k_scatter_res<kSubRound, kLdsTiles, 1>
-              : p20   ? k_scatter_res<kSubRound, kLdsTiles, 2, true>
-                      : k_scatter_res<kSubRound, kLdsTiles, 2>;
+  // LDS count / start / cursor arrays sized to the level's tiles (tmax: the host's bound;
+  // a level past it flags kStGeometry and reruns), the freed LDS taken by longer rounds
+  // (more records per tile per round: longer runs, fewer reservation atomics per record).
+  // S3IMPH_SCAT_CFG (A/B knob): 0 the 4096-tile / 4096-record kernel for every level;
+  // 1 tiles by tmax, 4096-record rounds; 2 (default) tiles by tmax, longer rounds.
+  static const int cfg = [] {
+    const char* e = std::getenv("S3IMPH_SCAT_CFG");
+    return e ? std::atoi(e) : 2;
+  }();
+  const int kt = cfg == 0 || tmax == 0 || tmax > 2048 ? 4096 : tmax > 1024 ? 2048 : 1024;
+  auto pick = [&](auto r4096, auto r_long) {
+    return cfg == 2 ? r_long : r4096;
+  };
+  using KFn = decltype(&k_scatter_res<kSubRound, kLdsTiles, 0>);
+  KFn kern;
+  if (kt == 1024) {
+    kern = !l0    ? (b.padded ? pick(k_scatter_res<4096, 1024, 3>, k_scatter_res<5120, 1024, 3>)
+                              : pick(k_scatter_res<4096, 1024, 0>, k_scatter_res<5120, 1024, 0>))
+           : b.pos ? pick(k_scatter_res<4096, 1024, 1>, k_scatter_res<5120, 1024, 1>)
+           : p20   ? pick(k_scatter_res<4096, 1024, 2, true>, k_scatter_res<5120, 1024, 2, true>)
+                   : pick(k_scatter_res<4096, 1024, 2>, k_scatter_res<5120, 1024, 2>);
+  } else if (kt == 2048) {
+    kern = !l0    ? (b.padded ? pick(k_scatter_res<4096, 2048, 3>, k_scatter_res<5120, 2048, 3>)
+                              : pick(k_scatter_res<4096, 2048, 0>, k_scatter_res<5120, 2048, 0>))
+           : b.pos ? pick(k_scatter_res<4096, 2048, 1>, k_scatter_res<5120, 2048, 1>)
+           : p20   ? pick(k_scatter_res<4096, 2048, 2, true>, k_scatter_res<5120, 2048, 2, true>)
+                   : pick(k_scatter_res<4096, 2048, 2>, k_scatter_res<5120, 2048, 2>);
+  } else {
+    kern = !l0    ? (b.padded ? k_scatter_res<kSubRound, kLdsTiles, 3> : k_scatter_res<kSubRound, kLdsTiles, 0>)
+           : b.pos ? k_scatter_res<kSubRound, kLdsTiles, 1>
+           : p20   ? k_scatter_res<kSubRound, kLdsTiles, 2, true>
+                   : k_scatter_res<kSubRound, kLdsTiles, 2>;
+  }
   kern<<<grid, kSB, 0, s>>>(level, il, b.kh, b.fp, b.pos, b.pos_base, tc, b.bucket, b.bucket_cap, b.flags, b.st, g.tb,
                             b.cap_words, b.tile_prof, i_lo, i_hi, b.split ? g.ts : 0u);
 }
 
 void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s) {
-  (void)hipMemsetAsync(b.mid, 0, 64 * sizeof(uint32_t), s);  // the barrier counter
   k_mid_levels<<<kMidG, kMidT, 0, s>>>(L0, L1, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out, b.pos_out, b.st,
                                        b.mid, reinterpret_cast<Rec*>(b.mid + kMidXb), b.tile_prof);
 }

@@ -329,7 +329,7 @@ void enqueue_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, 
   const Grids gr = level_grids(nb, size, g);
   if (res) {
     const int gsr = (int)std::min<uint64_t>((nb + kSubRound - 1) / kSubRound, 256);
-    launch_binned_scatter_res(L, b, g, std::max(gsr, 1), s);
+    launch_binned_scatter_res(L, b, g, std::max(gsr, 1), s, 0, 0, tiles_of((size + 63) / 64, g.tb, b.split ? g.ts : 0));
     launch_binned_tile(L, b, g, gr.gt, s, true);
   } else {
     launch_binned_count(L, nullptr, nullptr, 0, b, g, gr.gc, s);
@@ -413,7 +413,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   if (res0) {
     LevelGeom gr0 = g0;  // split-kernel level 0: tiles in whole rounds over the CUs (exact size)
     if (b.split && g0.tb > kRegTileMaxBits && g0.tb <= kSplitMaxBits) gr0.ts = choose_split_ts(64 * level_words(n), true);
-    launch_binned_scatter_res(0, b, gr0, 256, s);
+    launch_binned_scatter_res(0, b, gr0, 256, s, 0, 0, tiles_of(level_words(n), gr0.tb, b.split ? gr0.ts : 0));
     ev_mark(c, s, "scatter0");
     launch_binned_tile(0, b, gr0, gr.gt, s, true);
     ev_mark(c, s, "tile0");
@@ -994,7 +994,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
         ev_mark(c, s, "hash_count0");
         LevelGeom gr0 = g0;
         if (b0.split && g0.tb > kRegTileMaxBits && g0.tb <= kSplitMaxBits) gr0.ts = choose_split_ts(64 * level_words(N), true);
-        launch_binned_scatter_res(0, b0, gr0, 256, s);
+        launch_binned_scatter_res(0, b0, gr0, 256, s, 0, 0, tiles_of(level_words(N), gr0.tb, b0.split ? gr0.ts : 0));
         launch_binned_tile(0, b0, gr0, level_grids(n_local, 64 * level_words(N), g0).gt, s, true);
         ev_mark(c, s, "level0");
         cm.allreduce_u64(&st->n[1], d.gslot + 1, 1, s);

@@ -27,6 +27,8 @@ struct LevelState {
   unsigned int skew;                         // sampled key lengths are skewed: hash length-sorted
   unsigned int stop_level;  // kStTooManyLevels: the level whose n[stop_level] keys could not be
                             // placed; they are left in list[(stop_level - 1) & 1]
+  unsigned int mid_bar;     // k_mid_levels' grid-barrier counter (zeroed with the rest by k_init_state)
+  unsigned int pad0_;
   // Binned pipeline (s3imph_binned.hip).
   unsigned long long lvl_base[kMaxLevels + 2];  // set bits in all levels < L (= ranks[L] - 1)
   unsigned long long ntiles[kMaxLevels + 2];    // position tiles of level L
@@ -162,7 +164,7 @@ constexpr unsigned kMidSeg = 512;          // exchange records per (owner, sende
 constexpr unsigned kMidStage = 6144;       // settled records staged per owner (LDS)
 constexpr unsigned long long kMidMaxKeys = 440ull << 10;  // owners average <= 6.9k of 8k slots
 constexpr uint64_t kMidW32 = 2 * ((2 * kMidMaxKeys + 63) / 64);  // u32 words of the largest mid level
-// scratch (u32 units): barrier counter [64], segment counts [kMidG][kMidG], per-owner
+// scratch (u32 units): 64 unused (the barrier counter is LevelState::mid_bar), segment counts [kMidG][kMidG], per-owner
 // totals [kMidG] u64, then the exchange area [kMidG][kMidG][kMidSeg] Rec
 constexpr uint64_t kMidXc = 64;
 constexpr uint64_t kMidTot = kMidXc + (uint64_t)kMidG * kMidG;  // even: u64-aligned
@@ -225,8 +227,9 @@ void launch_binned_scan(int level, const BinBuffers& b, int grid, hipStream_t s)
 void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStream_t s);
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s,
                         bool reserved = false);
+// tmax: an upper bound on the level's tiles (0: unknown, the 4096-tile kernel)
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s,
-                               uint64_t i_lo = 0, uint64_t i_hi = 0);
+                               uint64_t i_lo = 0, uint64_t i_hi = 0, uint64_t tmax = 0);
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s);
 // levels L0..L1 (each predicted above the tail and at most kMidMaxKeys keys) in one launch
 void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s);

@@ -79,6 +79,7 @@ def test_dist_host_comm_matches_oracle(world, n, switch, mode, oracle_lib):
     assert st == 0
     cuts = [n * r // world for r in range(world + 1)]
     res = _run(world, _shards(blob, offs, cuts), n, switch, mode)
+    assert res[0][1] == "ok", res[0]
     assert res[0][6]["big_levels"] >= (3 if switch < 50_000 else 1)
     _check(res, n, fp, po, mph)
 
