@@ -1169,7 +1169,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     } else {
       rk_[q] = ik[i];
       rf_[q] = ifp[i];
-      rp_[q] = kSrc == 1 ? ipos[i] : pos_base + i;
+      if constexpr (kSrc == 1) rp_[q] = ipos[i];
     }
   };
 #pragma unroll
@@ -1182,14 +1182,17 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   if (tid == 0) s_over = 0;
   __syncthreads();
   for (;;) {
-    unsigned tt[kKPT], rk[kKPT];
+    // a record's tile (< 2^12) and its rank among the round's records of that tile (< 2^13)
+    // packed into one register: tt << 13 | rk
+    static_assert(kT <= 4096 && kR <= 8192, "tile / rank packing");
+    unsigned trk[kKPT];
 #pragma unroll
     for (int q = 0; q < kKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < n && (kSrc != 3 || rk_[q] != 0)) {  // kSrc 3: k = 0 is a padding record (k_route_pad)
         const uint64_t lp = bb_index(seed, rk_[q], words, magic) - rg.plo;
-        tt[q] = ts ? __umulhi((uint32_t)(lp >> kSplitSubBitsDev), ts_mul) : (unsigned)(lp >> tb);
-        rk[q] = atomicAdd(&cnt[tt[q]], 1u);
+        const unsigned t = ts ? __umulhi((uint32_t)(lp >> kSplitSubBitsDev), ts_mul) : (unsigned)(lp >> tb);
+        trk[q] = (t << 13) | atomicAdd(&cnt[t], 1u);
       }
     }
     __syncthreads();
@@ -1197,29 +1200,29 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     constexpr int kTPT = (int)(kT / kSB);
     // The round's returning reservation atomics (one per tile present; thread tid takes
     // tiles q kSB + tid) go out as soon as the counts are final, so their round trip
-    // overlaps the count scan, the stage writes and the next round's loads.
-    unsigned ac[kTPT], at[kTPT];
+    // overlaps the count scan, the stage writes and the next round's loads.  Counts are
+    // re-read from LDS where they are used (cnt[] holds them until the next round) rather
+    // than kept in registers: the 2048 / 4096-tile forms spilled 8-13 VGPRs in this loop.
+    unsigned at[kTPT];
 #pragma unroll
     for (int q = 0; q < kTPT; ++q) {
       const uint64_t t = (uint64_t)q * kSB + tid;
-      ac[q] = t < T ? cnt[t] : 0u;
+      const unsigned c = t < T ? cnt[t] : 0u;
       at[q] = 0;
-      if (ac[q]) at[q] = atomicAdd(&tcnt[t * kResShards + shard], ac[q]);
+      if (c) at[q] = atomicAdd(&tcnt[t * kResShards + shard], c);
     }
     const uint64_t t0 = (uint64_t)kTPT * tid;
-    unsigned a[kTPT];
     uint64_t sum = 0;
 #pragma unroll
-    for (int q = 0; q < kTPT; ++q) {
-      a[q] = t0 + q < T ? cnt[t0 + q] : 0u;
-      sum += a[q];
-    }
+    for (int q = 0; q < kTPT; ++q) sum += t0 + q < T ? cnt[t0 + q] : 0u;
     uint64_t tot;
     uint64_t ex = block_exscan<kSB>(sum, &tot);
 #pragma unroll
     for (int q = 0; q < kTPT; ++q) {
-      if (t0 + q < T) start[t0 + q] = (unsigned)ex;
-      ex += a[q];
+      if (t0 + q < T) {
+        start[t0 + q] = (unsigned)ex;
+        ex += cnt[t0 + q];
+      }
     }
     __syncthreads();  // start[] complete
     SPROF(2);
@@ -1227,10 +1230,11 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     for (int q = 0; q < kKPT; ++q) {
       const uint64_t i = r0 + (uint64_t)q * kSB + tid;
       if (i < n && (kSrc != 3 || rk_[q] != 0)) {
-        const unsigned slot = start[tt[q]] + rk[q];
-        if constexpr (kP20) stage20[slot] = r20_make(rk_[q], rf_[q], (uint32_t)(rp_[q] - pos_base));
-        else stage[slot] = Rec{rk_[q], rf_[q], rp_[q]};
-        stile[slot] = (unsigned short)tt[q];
+        const unsigned t = trk[q] >> 13, slot = start[t] + (trk[q] & 8191u);
+        // identity positions (kSrc 2) are the record's index, recomputed rather than held
+        if constexpr (kP20) stage20[slot] = r20_make(rk_[q], rf_[q], (uint32_t)i);
+        else stage[slot] = Rec{rk_[q], rf_[q], kSrc == 2 ? pos_base + i : rp_[q]};
+        stile[slot] = (unsigned short)t;
       }
     }
     // The next round's loads are issued before any atomic result is used, so the two
@@ -1247,9 +1251,10 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     }
 #pragma unroll
     for (int q = 0; q < kTPT; ++q) {
-      if (ac[q]) {
-        const uint64_t t = (uint64_t)q * kSB + tid;
-        if (at[q] + ac[q] > scap) s_over = 1;
+      const uint64_t t = (uint64_t)q * kSB + tid;
+      const unsigned c = t < T ? cnt[t] : 0u;
+      if (c) {
+        if (at[q] + c > scap) s_over = 1;
         cur[t] = (unsigned)(t * cap + shard * scap + at[q]);
       }
     }
