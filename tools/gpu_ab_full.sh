@@ -15,7 +15,7 @@ if [ -n "$PYT_ENV" ]; then
     --timeout 300 --timeout-method thread > $OUT/pytest_knob.log 2>&1 || true
 fi
 L=s3-inv-db_amd/s3imph/_lib/libs3imph.so
-for cfg in c2 c3; do
+for cfg in ${CFGS:-c2 c3}; do
   for v in old new old new; do
     cp ab/libs3imph_$v.so $L
     timeout -k 10 200 python bench.py --no-cpu-baseline --headline-only --no-secondary --config $cfg --steps 20 \
