@@ -3182,13 +3182,13 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
   // LDS count / start / cursor arrays sized to the level's tiles (tmax: the host's bound;
   // a level past it flags kStGeometry and reruns), the freed LDS taken by longer rounds
   // (more records per tile per round: longer runs, fewer reservation atomics per record).
-  // S3IMPH_SCAT_CFG (A/B knob): 0 the 4096-tile / 4096-record kernel for every level;
-  // 1 tiles by tmax, 4096-record rounds; 2 (default) tiles by tmax, longer rounds.
-  static const int cfg = [] {
-    const char* e = std::getenv("S3IMPH_SCAT_CFG");
-    return e ? std::atoi(e) : 2;
-  }();
+  // b.scat_cfg (S3IMPH_SCAT_CFG at context creation; A/B knob and test hook): 0 the 4096-tile /
+  // 4096-record kernel for every level; 1 tiles by tmax, 4096-record rounds; 2 (default) tiles
+  // by tmax, longer rounds.
+  const int cfg = b.scat_cfg;
   const int kt = cfg == 0 || tmax == 0 || tmax > 2048 ? 4096 : tmax > 1024 ? 2048 : 1024;
+  // (longer rounds with 2048 counters too: they spill 6-8 VGPRs against 0-4, yet measured
+  // faster on C2's level 0 than 4096-record rounds there, 0.144-0.149 vs 0.152-0.154 ms)
   auto pick = [&](auto r4096, auto r_long) {
     return cfg == 2 ? r_long : r4096;
   };

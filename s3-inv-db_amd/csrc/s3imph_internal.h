@@ -218,6 +218,7 @@ struct BinBuffers {
   bool padded = false;                  // list levels hold k = 0 padding records (fixed exchange regions)
   uint32_t* mid;                        // k_mid_levels scratch (kMidScratchU32)
   Rec* split;                           // k_tile_split scratch (split_scratch_records()), or null
+  int scat_cfg = 2;                     // k_scatter_res forms (launch_binned_scatter_res)
 };
 uint64_t split_scratch_records();  // sub-tile segments of the split big-tile kernel
 void binned_set_lds_limits();

@@ -359,6 +359,27 @@ def test_small_level_paths_bit_exact(s3, oracle_lib, res_max, monkeypatch):
         c.close()
 
 
+@pytest.mark.parametrize("cfg", ["0", "1"])
+def test_scatter_forms_bit_exact(s3, oracle_lib, cfg, monkeypatch):
+    """The reservation scatter's other LDS forms (S3IMPH_SCAT_CFG 0: 4096 tile counters and
+    4096-record rounds for every level; 1: counters sized to the level's tiles, 4096-record
+    rounds) on a set whose levels take 1221 / 481 / 189 tiles: bit-exact with the oracle,
+    like the default form (5120-record rounds) in test_c2_10m_bit_exact."""
+    monkeypatch.setenv("S3IMPH_SCAT_CFG", cfg)
+    c = s3.DeviceBuilder(0)
+    try:
+        n = 10_000_000
+        blob, offs = s3.gen_keys(0, 42, 32, 0, n)
+        st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)
+        assert st == 0
+        gfp, gpo, gmph, info = _device_build(s3, c, blob, offs)
+        assert gmph == mph
+        assert np.array_equal(gfp, fp)
+        assert np.array_equal(gpo, po)
+    finally:
+        c.close()
+
+
 def test_c2_10m_bit_exact(s3, oracle_lib, ctx):
     """BASELINE config 2: 10M synthetic prefixes, avg 32 B — full bit-exact comparison."""
     n = 10_000_000
