@@ -1603,8 +1603,67 @@ void stager_init(s3imph_ctx* c) {
 // conv 1 (h2d): host u64 words, minus bias, stored as device u32 (`bytes` = device
 // bytes); conv 2 (d2h): device u32 words widened to host u64.  Both halve the PCIe bytes
 // of an array whose values fit 32 bits.
+// Device -> pageable host copies of one or more arrays through the pinned buffers, all
+// their chunks dealt over one worker pool: each worker issues its next chunk's DMA, then
+// copies out (conv 2: widens u32 -> u64) the chunk that landed, so the CPU copies of one
+// worker overlap the DMA of the others and the arrays' transfers share the link.
+struct D2HJob {
+  void* dst;
+  const void* src;
+  uint64_t bytes;  // device bytes
+  int conv;        // 0 copy, 2 widen u32 -> u64
+};
+void staged_d2h(s3imph_ctx* c, const std::vector<D2HJob>& jobs) {
+  stager_init(c);
+  Stager& g = c->stager;
+  std::vector<uint64_t> first(jobs.size() + 1, 0);  // first global chunk of each job
+  for (size_t j = 0; j < jobs.size(); ++j) first[j + 1] = first[j] + (jobs[j].bytes + kStageChunk - 1) / kStageChunk;
+  const uint64_t nch = first.back();
+  if (!nch) return;
+  const int nw = (int)std::min<uint64_t>(kStageWorkers, nch);
+  std::vector<std::string> errs(nw);
+  auto work = [&](int w) {
+    try {
+      HIPCHECK(hipSetDevice(c->device));
+      auto job = [&](uint64_t ch) { return (size_t)(std::upper_bound(first.begin(), first.end(), ch) - first.begin() - 1); };
+      auto issue = [&](uint64_t ch, int buf) {
+        const D2HJob& J = jobs[job(ch)];
+        const uint64_t off = (ch - first[job(ch)]) * kStageChunk, len = std::min(kStageChunk, J.bytes - off);
+        HIPCHECK(hipMemcpyAsync(g.pin[w][buf], static_cast<const uint8_t*>(J.src) + off, len, hipMemcpyDeviceToHost,
+                                g.st[w]));
+        HIPCHECK(hipEventRecord(g.ev[w][buf], g.st[w]));
+      };
+      int b = 0;
+      if ((uint64_t)w < nch) issue(w, 0);
+      for (uint64_t ch = w; ch < nch; ch += nw, b ^= 1) {
+        if (ch + nw < nch) issue(ch + nw, b ^ 1);
+        HIPCHECK(hipEventSynchronize(g.ev[w][b]));
+        const D2HJob& J = jobs[job(ch)];
+        const uint64_t off = (ch - first[job(ch)]) * kStageChunk, len = std::min(kStageChunk, J.bytes - off);
+        if (J.conv == 2) {
+          const uint32_t* s32 = static_cast<const uint32_t*>(g.pin[w][b]);
+          uint64_t* d64 = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(J.dst) + 2 * off);
+          for (uint64_t i = 0; i < len / 4; ++i) d64[i] = s32[i];
+        } else {
+          std::memcpy(static_cast<uint8_t*>(J.dst) + off, g.pin[w][b], len);
+        }
+      }
+      HIPCHECK(hipStreamSynchronize(g.st[w]));
+    } catch (const Fail& f) {
+      errs[w] = f.msg.empty() ? "staged copy failed" : f.msg;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int w = 1; w < nw; ++w) th.emplace_back(work, w);
+  work(0);
+  for (auto& t : th) t.join();
+  for (const auto& e : errs)
+    if (!e.empty()) throw Fail{S3IMPH_ERR_HIP, e};
+}
+
 void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias, int conv) {
   if (!bytes) return;
+  if (!h2d) return staged_d2h(c, {D2HJob{dst, src, bytes, conv}});
   // Pageable H2D through the runtime already runs at the PCIe rate (C2: 400 MB in
   // 7.4 ms, 54 GB/s); pageable D2H does not (17 GB/s), and neither does rebasing.
   if (!bias && !conv && h2d) {
@@ -1639,25 +1698,6 @@ void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t b
           HIPCHECK(hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, g.pin[w][b], len, hipMemcpyHostToDevice,
                                   g.st[w]));
           HIPCHECK(hipEventRecord(g.ev[w][b], g.st[w]));
-        }
-      } else {
-        // prefetch the worker's first chunk, then: issue chunk i+1's DMA, copy out chunk i
-        auto issue = [&](uint64_t ch, int buf) {
-          HIPCHECK(hipMemcpyAsync(g.pin[w][buf], static_cast<const uint8_t*>(src) + ch * kStageChunk, clen(ch),
-                                  hipMemcpyDeviceToHost, g.st[w]));
-          HIPCHECK(hipEventRecord(g.ev[w][buf], g.st[w]));
-        };
-        if ((uint64_t)w < nch) issue(w, 0);
-        for (uint64_t ch = w; ch < nch; ch += nw, b ^= 1) {
-          if (ch + nw < nch) issue(ch + nw, b ^ 1);
-          HIPCHECK(hipEventSynchronize(g.ev[w][b]));
-          if (conv == 2) {
-            const uint32_t* s32 = static_cast<const uint32_t*>(g.pin[w][b]);
-            uint64_t* d64 = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(dst) + 2 * ch * kStageChunk);
-            for (uint64_t i = 0; i < clen(ch) / 4; ++i) d64[i] = s32[i];
-          } else {
-            std::memcpy(static_cast<uint8_t*>(dst) + ch * kStageChunk, g.pin[w][b], clen(ch));
-          }
         }
       }
       HIPCHECK(hipStreamSynchronize(g.st[w]));
@@ -1702,16 +1742,29 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
     hipStream_t s = c->own_stream;
     HIPCHECK(hipStreamSynchronize(s));  // staging buffers may be in use by the last build
     const auto t0 = clk::now();
-    staged_copy(c, true, c->s_blob, blob + b0, nbytes);
     // offsets cross PCIe as u32 when the blob is under 4 GiB (widened on the device, in
-    // s_fp's space: the build writes s_fp only later on the same stream)
-    if (nbytes < (1ull << 32)) {
-      uint32_t* tmp32 = reinterpret_cast<uint32_t*>(c->s_fp);
-      staged_copy(c, true, tmp32, offsets, (n + 1) * 4, b0, 1);
-      launch_widen32(tmp32, c->s_offsets, n + 1, s);
-    } else {
-      staged_copy(c, true, c->s_offsets, offsets, (n + 1) * 8, b0);
+    // s_fp's space: the build writes s_fp only later on the same stream); their rebasing /
+    // narrowing and pinned copies run on a second thread beside the blob's runtime copy
+    const bool off32 = nbytes < (1ull << 32);
+    uint32_t* tmp32 = reinterpret_cast<uint32_t*>(c->s_fp);
+    Fail off_err{S3IMPH_OK, ""};
+    std::thread toff([&]() {
+      try {
+        if (off32) staged_copy(c, true, tmp32, offsets, (n + 1) * 4, b0, 1);
+        else staged_copy(c, true, c->s_offsets, offsets, (n + 1) * 8, b0);
+      } catch (const Fail& f) {
+        off_err = f;
+      }
+    });
+    try {
+      staged_copy(c, true, c->s_blob, blob + b0, nbytes);
+    } catch (...) {
+      toff.join();
+      throw;
     }
+    toff.join();
+    if (off_err.code != S3IMPH_OK) throw off_err;
+    if (off32) launch_widen32(tmp32, c->s_offsets, n + 1, s);
     if (pos) staged_copy(c, true, c->s_pos, pos, n * 8);
     const auto t1 = clk::now();
     s3imph_build_info info;
@@ -1719,14 +1772,15 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
                           &info, msg);
     if (rc != S3IMPH_OK) return rc;
     const auto t2 = clk::now();
-    staged_copy(c, false, fp_out, c->s_fp, n * 8);
-    if (!pos) {  // identity positions are < n < 2^32: u32 over PCIe (offsets' space is free now)
-      uint32_t* tmp32 = reinterpret_cast<uint32_t*>(c->s_offsets);
-      launch_narrow32(c->s_posout, tmp32, n, s);
+    // both output arrays in one pass over the pinned workers (identity positions are < n <
+    // 2^32: u32 over PCIe, narrowed into the offsets' space, which is free now)
+    if (!pos) {
+      uint32_t* pos32 = reinterpret_cast<uint32_t*>(c->s_offsets);
+      launch_narrow32(c->s_posout, pos32, n, s);
       HIPCHECK(hipStreamSynchronize(s));
-      staged_copy(c, false, pos_out, tmp32, n * 4, 0, 2);
+      staged_d2h(c, {D2HJob{fp_out, c->s_fp, n * 8, 0}, D2HJob{pos_out, pos32, n * 4, 2}});
     } else {
-      staged_copy(c, false, pos_out, c->s_posout, n * 8);
+      staged_d2h(c, {D2HJob{fp_out, c->s_fp, n * 8, 0}, D2HJob{pos_out, c->s_posout, n * 8, 0}});
     }
     const auto t3 = clk::now();
     mph->resize(info.mph_bin_len);

@@ -1,11 +1,13 @@
 """Phase split of the one-shot host-memory build (s3imph_build_host) on C2: H2D, build, D2H
-and marshal times from the library's debug report (S3IMPH_DEBUG), after two warm-up builds.
-  python tools/host_phase.py [n] [avg]"""
+and marshal times from the library's debug report (--debug: S3IMPH_DEBUG), and the wall time of
+repeated builds.   python tools/host_phase.py [n] [avg] [--debug]"""
 import os
 import sys
 import time
 
-os.environ["S3IMPH_DEBUG"] = "1"
+if "--debug" in sys.argv:
+    sys.argv.remove("--debug")
+    os.environ["S3IMPH_DEBUG"] = "1"
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "s3-inv-db_amd"))
 import s3imph  # noqa: E402
 
@@ -15,7 +17,7 @@ blob, offs = s3imph.gen_keys(0, 42, avg, 0, n)
 blob = blob[: int(offs[-1])].copy()
 import numpy as np  # noqa: E402
 out = (np.zeros(n, np.uint64), np.zeros(n, np.uint64))  # reused, as bench.py's host_e2e
-for i in range(4):
+for i in range(6):
     t = time.perf_counter()
     s3imph.build_host(blob, offs, out=out)
     print(f"build_host {i}: {(time.perf_counter() - t) * 1e3:.2f} ms", file=sys.stderr, flush=True)
