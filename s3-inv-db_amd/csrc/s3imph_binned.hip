@@ -584,8 +584,13 @@ constexpr int kSkC = 64;               // chunk bytes per key per step
 constexpr int kSkS = kSkC + 16;        // LDS stride per key (16-B aligned for ds_write_b128)
 constexpr int kSkU = kSkC / 16;        // 16-byte units per key chunk = loads per step
 constexpr unsigned kSkLB = 256;        // length classes (4 B each)
-// kSkT threads, kSkG keys per sorted group: 1024 / 4096 (one block per CU) or 512 / 2048
-// (two per CU: one block's sort and group barrier overlap the other's hashing)
+// kSkT threads, kSkG keys per sorted group: 768 / 5120 (one block per CU, three waves per
+// SIMD), 1024 / 4096 (four waves per SIMD) or 512 / 2048 (two blocks per CU: one block's
+// sort and group barrier overlap the other's hashing).  A group's makespan is at least its
+// longest batch (C5: 16 chunk steps for 1024-byte keys); 4096 keys give each of 16 waves
+// ~12.5 steps on average, so the group barrier waited ~17 % of a wave's life; 5120 keys
+// over 12 waves give ~21 (C5 hash 1.65-1.66 -> 1.60-1.62 ms, `profiles/r3_skew*/`; 11, 10 and
+// 13 waves, and 8 waves with 4096 keys, measured slower).
 template <int kSkT, int kSkG>
 constexpr size_t sk_stage_bytes() { return (size_t)(kSkT / 64) * 64 * kSkS; }
 template <int kSkT, int kSkG>
@@ -595,6 +600,7 @@ constexpr size_t sk_lds_bytes() {
 }
 static_assert(sk_lds_bytes<1024, 4096>() <= 160 * 1024, "k_hash_skew's LDS");
 static_assert(2 * sk_lds_bytes<512, 2048>() <= 160 * 1024, "k_hash_skew's LDS, two blocks per CU");
+static_assert(sk_lds_bytes<768, 5120>() <= 160 * 1024, "k_hash_skew's LDS, 12 waves");
 static_assert(kSkU * 16 == 64, "a load instruction covers 16 keys x 64 B");
 
 template <int kSkT, int kSkG>
@@ -638,7 +644,7 @@ __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict
   uint4* wst = stage + (size_t)wave * 64 * (kSkS / 16);  // this wave's 64 key regions
   const uint32_t* wst32 = reinterpret_cast<const uint32_t*>(wst);
   bool zero = false;
-  constexpr int KPT = kSkG / kSkT;  // keys per thread in the sort
+  constexpr int KPT = (kSkG + kSkT - 1) / kSkT;  // keys per thread in the sort
   for (uint64_t grp = gbeg; grp < gend; grp += kSkG) {
     const unsigned long long g0t = prof ? __builtin_amdgcn_s_memtime() : 0;
     const unsigned m = (unsigned)min<uint64_t>(kSkG, gend - grp);
@@ -3039,14 +3045,15 @@ size_t tile_lds_bytes(unsigned tb) {
 uint64_t split_scratch_records() { return split_scratch_recs(); }
 
 // The skewed-length level-0 hash (a no-op launch unless st->skew).  A/B knobs:
-// S3IMPH_SKEW_CFG=0 selects two 512-thread blocks per CU (2048-key groups) instead of one
-// 1024-thread block (4096-key groups; measured 1.64 vs 1.75 ms on C5), S3IMPH_SKEW_ORDER=0
+// S3IMPH_SKEW_CFG selects the block / group shape: 2 (default) one 768-thread block per CU
+// with 5120-key groups, 1 one 1024-thread block with 4096-key groups (C5 1.65 vs 1.61 ms),
+// 0 two 512-thread blocks per CU with 2048-key groups (1.75 ms); S3IMPH_SKEW_ORDER=0
 // alternates the longest and the shortest batch instead of longest first.
 void launch_hash_skew(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                       unsigned long long* prof, hipStream_t s) {
   static const int cfg = [] {
     const char* e = std::getenv("S3IMPH_SKEW_CFG");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 2;
   }();
   static const int order = [] {  // 1: longest first; 0: alternating longest / shortest
     const char* e = std::getenv("S3IMPH_SKEW_ORDER");
@@ -3054,6 +3061,9 @@ void launch_hash_skew(const uint8_t* blob, const uint64_t* offsets, uint64_t n, 
   }();
   if (cfg == 1)
     k_hash_skew<1024, 4096><<<256, 1024, sk_lds_bytes<1024, 4096>(), s>>>(
+        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order);
+  else if (cfg == 2)
+    k_hash_skew<768, 5120><<<256, 768, sk_lds_bytes<768, 5120>(), s>>>(
         blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order);
   else
     k_hash_skew<512, 2048><<<512, 512, sk_lds_bytes<512, 2048>(), s>>>(
@@ -3065,6 +3075,8 @@ void binned_set_lds_limits() {
                             (int)sk_lds_bytes<1024, 4096>());
   (void)hipFuncSetAttribute((const void*)k_hash_skew<512, 2048>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sk_lds_bytes<512, 2048>());
+  (void)hipFuncSetAttribute((const void*)k_hash_skew<768, 5120>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sk_lds_bytes<768, 5120>());
   (void)hipFuncSetAttribute((const void*)k_tile<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)std::max(tile_lds_bytes(kTileMaxBits), tile_lds_bytes(kCacheBits)));
   (void)hipFuncSetAttribute((const void*)k_tile_reg<512, 20, 2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
