@@ -250,8 +250,8 @@ int rank_build(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
     c->s_blob_cap = bcap;
   }
   const uint64_t need = std::max(cap, nl + 1);
-  if (need > c->s_cap) {
-    dalloc(c->s_offsets, need);
+  if (need > c->s_cap) {  // s_cap keys: s_offsets holds s_cap + 1 words (as build_from_host's)
+    dalloc(c->s_offsets, need + 1);
     dalloc(c->s_pos, need);
     dalloc(c->s_fp, need);
     dalloc(c->s_posout, need);

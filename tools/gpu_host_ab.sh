@@ -1,6 +1,6 @@
 #!/bin/bash
 # Host-memory build A/B (ab/libs3imph_{old,new}.so alternating): tools/host_phase.py wall
-# times on C2, plus the host-path parity tests on the new library.   bash tools/gpu_host_ab.sh TAG
+# times on C2, plus the whole -m gpu suite on the new library.   bash tools/gpu_host_ab.sh TAG
 set -e
 OUT=gpurun_out/$1; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -10,6 +10,12 @@ for v in old new old new; do
   timeout -k 10 200 python tools/host_phase.py >> $OUT/host_$v.log 2>&1
 done
 cp ab/libs3imph_new.so $L
+# the new library under each A/B knob setting (AB_ENV="S3IMPH_HOST_OVERLAP=0")
+for kv in $AB_ENV; do
+  env $kv timeout -k 10 200 python tools/host_phase.py >> $OUT/host_knob_$kv.log 2>&1
+done
+timeout -k 10 200 python tools/host_phase.py 10000000 32 --debug > $OUT/host_new_debug.log 2>&1
+[ -n "$NO_PYTEST" ] && { echo done > $OUT/DONE; exit 0; }
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-  -k "host or builder or multi" > $OUT/pytest.log 2>&1
+  > $OUT/pytest.log 2>&1
 echo done > $OUT/DONE
