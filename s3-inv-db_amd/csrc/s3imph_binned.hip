@@ -3045,16 +3045,14 @@ size_t tile_lds_bytes(unsigned tb) {
 uint64_t split_scratch_records() { return split_scratch_recs(); }
 
 // The skewed-length level-0 hash (a no-op launch unless st->skew).  A/B knobs:
-// S3IMPH_SKEW_CFG selects the block / group shape: 2 (default) one 768-thread block per CU
-// with 5120-key groups, 1 one 1024-thread block with 4096-key groups (C5 1.65 vs 1.61 ms),
-// 0 two 512-thread blocks per CU with 2048-key groups (1.75 ms); S3IMPH_SKEW_ORDER=0
-// alternates the longest and the shortest batch instead of longest first.
+// b.skew_cfg (S3IMPH_SKEW_CFG at context creation) selects the block / group shape: 2
+// (default) one 768-thread block per CU with 5120-key groups, 1 one 1024-thread block with
+// 4096-key groups (C5 1.65 vs 1.61 ms), 0 two 512-thread blocks per CU with 2048-key groups
+// (1.75 ms); S3IMPH_SKEW_ORDER=0 alternates the longest and the shortest batch instead of
+// longest first.
 void launch_hash_skew(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                       unsigned long long* prof, hipStream_t s) {
-  static const int cfg = [] {
-    const char* e = std::getenv("S3IMPH_SKEW_CFG");
-    return e ? std::atoi(e) : 2;
-  }();
+  const int cfg = b.skew_cfg;
   static const int order = [] {  // 1: longest first; 0: alternating longest / shortest
     const char* e = std::getenv("S3IMPH_SKEW_ORDER");
     return e ? std::atoi(e) : 1;

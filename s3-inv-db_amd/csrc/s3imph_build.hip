@@ -252,6 +252,7 @@ BinBuffers make_bufs(s3imph_ctx* c, const uint64_t* pos, uint64_t* fp_out, uint6
   if (!c->split && c->cap_keys > (kMaxTiles << kRegTileMaxBits) / 2) dalloc(c->split, split_scratch_records());
   b.split = c->split;
   b.scat_cfg = c->scat_cfg;
+  b.skew_cfg = c->skew_cfg;
   b.bits = c->bits;
   b.cap_words = c->cap_words;
   b.fp_out = fp_out;
@@ -1861,6 +1862,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     c->route_self = std::getenv("S3IMPH_DIST_ROUTE_SELF") != nullptr;  // A/B knob: list-level geometry from 1.1x bounds
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     if (const char* m = std::getenv("S3IMPH_SCAT_CFG")) c->scat_cfg = std::atoi(m);
+    if (const char* m = std::getenv("S3IMPH_SKEW_CFG")) c->skew_cfg = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_DIST_MODE")) c->d.mode = std::strcmp(m, "bitmap") == 0 ? kDistBitmap : kDistRoute;
     // A blocking stream: implicitly ordered with the legacy NULL stream, so work a

@@ -198,6 +198,7 @@ struct s3imph_ctx {
   int res0 = 1;  // level 0 through the reservation scatter when its tiles are large
   bool route_self = false;  // S3IMPH_DIST_ROUTE_SELF: a one-rank sharded build routes like P > 1 (tests)
   int scat_cfg = 2;         // S3IMPH_SCAT_CFG: reservation-scatter forms (launch_binned_scatter_res)
+  int skew_cfg = 2;         // S3IMPH_SKEW_CFG: skewed-length hash block / group shape (launch_hash_skew)
   bool loose_geom = false;  // S3IMPH_LOOSE_GEOM: list levels sized from 1.1x (not 1.02x + 6 sigma) bounds
   bool debug = false;
   unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps

@@ -380,6 +380,27 @@ def test_scatter_forms_bit_exact(s3, oracle_lib, cfg, monkeypatch):
         c.close()
 
 
+@pytest.mark.parametrize("cfg", ["0", "1"])
+def test_skew_shapes_bit_exact(s3, oracle_lib, cfg, monkeypatch):
+    """The skewed-length hash's other block / group shapes (S3IMPH_SKEW_CFG 0: two 512-thread
+    blocks per CU with 2048-key groups; 1: 1024 threads with 4096-key groups) on a C5-style
+    log-uniform 1-1024 B set: bit-exact with the oracle, like the default 768 / 5120 shape
+    in test_c5_one_gpu_share_bit_exact."""
+    monkeypatch.setenv("S3IMPH_SKEW_CFG", cfg)
+    c = s3.DeviceBuilder(0)
+    try:
+        n = 3_000_000
+        blob, offs = s3.gen_keys(1, 23, 0, 0, n)
+        st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)
+        assert st == 0
+        gfp, gpo, gmph, info = _device_build(s3, c, blob, offs)
+        assert gmph == mph
+        assert np.array_equal(gfp, fp)
+        assert np.array_equal(gpo, po)
+    finally:
+        c.close()
+
+
 def test_c2_10m_bit_exact(s3, oracle_lib, ctx):
     """BASELINE config 2: 10M synthetic prefixes, avg 32 B — full bit-exact comparison."""
     n = 10_000_000
