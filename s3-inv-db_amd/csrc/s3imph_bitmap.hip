@@ -462,7 +462,8 @@ __global__ void k_bm_check(LevelState* st, int level, uint64_t wmax) {
 // This rank's settled list is sorted by p: the run for output slice t ([t slice, (t+1)
 // slice)) is [lower_bound(t slice), lower_bound((t+1) slice)).  One thread per slice
 // boundary; scnt[t] = the run's length, scnt[P] = 0 (no overflow: nothing is copied).
-__global__ void k_bm_bounds(const Rec* __restrict__ out, const unsigned long long* __restrict__ n_out, uint64_t slice,
+constexpr int kBmBoundsT = 128;
+__global__ __launch_bounds__(kBmBoundsT) void k_bm_bounds(const Rec* __restrict__ out, const unsigned long long* __restrict__ n_out, uint64_t slice,
                             int P, unsigned long long* __restrict__ scnt) {
   __shared__ uint64_t s_b[kMaxRanks + 1];
   const unsigned t = threadIdx.x;
@@ -573,7 +574,10 @@ void launch_bm_tile_settle(int level, const Rec* bucket, const unsigned* tc, uin
 
 void launch_bm_bounds(const Rec* out, const unsigned long long* n_out, uint64_t slice, int P, unsigned long long* scnt,
                       hipStream_t s) {
-  k_bm_bounds<<<1, 64, 0, s>>>(out, n_out, slice, P, scnt);
+  // thread t <= P finds boundary t: P + 1 threads, up to kMaxRanks + 1 (a 64-thread launch
+  // left boundary 64, and so the last slice's count, unset at P = 64)
+  static_assert(kMaxRanks + 1 <= kBmBoundsT, "one thread per slice boundary");
+  k_bm_bounds<<<1, kBmBoundsT, 0, s>>>(out, n_out, slice, P, scnt);
 }
 
 void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,

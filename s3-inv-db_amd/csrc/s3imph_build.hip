@@ -174,43 +174,65 @@ int predict_big_levels(uint64_t n) {
   return std::min(big + 1, kMaxLevels - 2);
 }
 
-bool has_duplicates(const uint64_t* d_keys, uint64_t n) {
-  std::vector<uint64_t> h(n);
-  if (n) HIPCHECK(hipMemcpy(h.data(), d_keys, n * 8, hipMemcpyDeviceToHost));
-  std::sort(h.begin(), h.end());
-  return std::adjacent_find(h.begin(), h.end()) != h.end();
-}
-
-bool records_have_duplicates(const Rec* d_list, uint64_t n) {
+// Values that occur more than once among n device records' key hashes (sorted, distinct,
+// at most `cap` of them): the keys a stopped build could not place.
+std::vector<uint64_t> record_dup_values(const Rec* d_list, uint64_t n, size_t cap) {
   std::vector<Rec> h(n);
   if (n) HIPCHECK(hipMemcpy(h.data(), d_list, n * sizeof(Rec), hipMemcpyDeviceToHost));
   std::vector<uint64_t> k(n);
   for (uint64_t i = 0; i < n; ++i) k[i] = h[i].k;
   std::sort(k.begin(), k.end());
-  return std::adjacent_find(k.begin(), k.end()) != k.end();
+  std::vector<uint64_t> out;
+  for (uint64_t i = 1; i < n && out.size() < cap; ++i)
+    if (k[i] == k[i - 1] && (out.empty() || out.back() != k[i])) out.push_back(k[i]);
+  return out;
 }
 
-// Duplicate key hashes, judged from the records the build could not place (the stop
-// level's input list) when it stopped on them, else from every key hash.
-bool stopped_on_duplicates(s3imph_ctx* c, unsigned flags, uint64_t n) {
+// The ORIGINAL key hashes, recomputed from the key bytes (c->kh is scratch here: the
+// level-0 pipeline may keep them only in its record layouts), sorted, on the host.
+std::vector<uint64_t> original_key_hashes(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, uint64_t n,
+                                          hipStream_t s) {
+  std::vector<uint64_t> h(n);
+  if (n) {
+    launch_key_hashes(blob, offsets, n, c->kh, s);
+    HIPCHECK(hipMemcpyAsync(h.data(), c->kh, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+  }
+  std::sort(h.begin(), h.end());
+  return h;
+}
+
+// A build that stopped (kStTooManyLevels: a level placed no key) or overflowed blames the
+// caller's keys (DUP_KEY_HASH, the reference's bbhash failure on equal hashes) only when
+// equal FNV-1a hashes exist among the ORIGINAL keys.  Leftover records with equal hashes
+// while every key hash is distinct mean a record was duplicated inside the build: an
+// internal fault, reported as one (with the level), never as the user's duplicates.
+int classify_stop(s3imph_ctx* c, unsigned flags, const uint8_t* blob, const uint64_t* offsets, uint64_t n,
+                  hipStream_t s, std::string* msg) {
   const LevelState& h = *c->h_st;
   const unsigned S = h.stop_level;
+  std::vector<uint64_t> left;
   if ((flags & kStTooManyLevels) && S >= 1 && S < (unsigned)kMaxLevels + 2 && h.n[S])
-    return records_have_duplicates(c->list[(S - 1) & 1], h.n[S]);
-  return has_duplicates(c->kh, n);
+    left = record_dup_values(c->list[(S - 1) & 1], h.n[S], 1);
+  const std::vector<uint64_t> orig = original_key_hashes(c, blob, offsets, n, s);
+  if (std::adjacent_find(orig.begin(), orig.end()) != orig.end()) {
+    *msg = "build MPHF: duplicate FNV-1a key hashes: bbhash cannot place them";
+    return S3IMPH_ERR_DUP_KEY_HASH;
+  }
+  if (!left.empty()) {
+    *msg = "build MPHF: internal error: level " + std::to_string(S) +
+           " holds records with equal key hashes although every key hash is distinct (a record was duplicated)";
+    return S3IMPH_ERR_INTERNAL;
+  }
+  *msg = (flags & kStTooManyLevels) ? "build MPHF: can't find minimal perfect hash after " +
+                                          std::to_string(kMaxLevels) + " levels"
+                                    : "build MPHF: workspace overflow";
+  return (flags & kStTooManyLevels) ? S3IMPH_ERR_TOO_MANY_LEVELS : S3IMPH_ERR_INTERNAL;
 }
 
-int map_status(s3imph_ctx* c, unsigned flags, uint64_t n, std::string* msg) {
-  if (flags & (kStTooManyLevels | kStOverflow)) {
-    if (stopped_on_duplicates(c, flags, n)) {
-      *msg = "build MPHF: duplicate FNV-1a key hashes: bbhash cannot place them";
-      return S3IMPH_ERR_DUP_KEY_HASH;
-    }
-    *msg = (flags & kStTooManyLevels) ? "build MPHF: can't find minimal perfect hash after " +
-                                            std::to_string(kMaxLevels) + " levels"
-                                      : "build MPHF: workspace overflow";
-    return (flags & kStTooManyLevels) ? S3IMPH_ERR_TOO_MANY_LEVELS : S3IMPH_ERR_INTERNAL;
-  }
+int map_status(s3imph_ctx* c, unsigned flags, const uint8_t* blob, const uint64_t* offsets, uint64_t n,
+               hipStream_t s, std::string* msg) {
+  if (flags & (kStTooManyLevels | kStOverflow)) return classify_stop(c, flags, blob, offsets, n, s, msg);
   if (flags & kStKeyZero) {
     *msg = "MPHF Key(...) returned 0, possible hash collision with sentinel";
     return S3IMPH_ERR_KEY_HASH_ZERO;
@@ -220,6 +242,13 @@ int map_status(s3imph_ctx* c, unsigned flags, uint64_t n, std::string* msg) {
     return S3IMPH_ERR_INTERNAL;
   }
   return S3IMPH_OK;
+}
+
+// Test hook (S3IMPH_FAULT_DUP_REC, read at context creation): copy record 0 of a list over
+// record 1, as a kernel race that duplicated a record would, so the tests can check that the
+// stop it causes is reported as an internal fault and not as the caller's duplicate keys.
+void fault_dup_record(s3imph_ctx* c, Rec* list, hipStream_t s) {
+  if (c->fault_dup) HIPCHECK(hipMemcpyAsync(list + 1, list, sizeof(Rec), hipMemcpyDeviceToDevice, s));
 }
 
 BinBuffers make_bufs(s3imph_ctx* c, const uint64_t* pos, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s) {
@@ -419,6 +448,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
     ev_mark(c, s, "scatter0");
     launch_binned_tile(0, b, gr0, gr.gt, s, true);
     ev_mark(c, s, "tile0");
+    fault_dup_record(c, c->list[0], s);
     enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
     return;
   }
@@ -428,6 +458,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   ev_mark(c, s, "scatter0");
   launch_binned_tile(0, b, g0, gr.gt, s);
   ev_mark(c, s, "tile0");
+  fault_dup_record(c, c->list[0], s);
   enqueue_levels_from(c, b, 1, conservative ? n : (uint64_t)((double)n * q), g0, conservative, s);
 }
 
@@ -604,7 +635,7 @@ int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
     break;
   }
   const LevelState& st = *c->h_st;
-  int rc = map_status(c, st.status, n, msg);
+  int rc = map_status(c, st.status, blob, offsets, n, s, msg);
   if (rc != S3IMPH_OK) return rc;
   if (st.rank_total != n || st.nlevels == 0) {
     *msg = "build MPHF: internal error: ranked " + std::to_string(st.rank_total) + " of " +
@@ -719,6 +750,31 @@ void ensure_dist_small(s3imph_ctx* c) {
   }
 }
 
+// Rank-local checks in front of a collective: every rank learns whether ANY rank failed
+// (an all-reduce of per-status flags on stream s), so all of them return at the same point
+// instead of the healthy ones blocking in the next collective.  A rank that did not fail
+// itself returns the failing ranks' lowest status, saying so.  Scratch: the last 32 words
+// of d.small and the 256 spare words of the pinned stage.
+int dist_agree(s3imph_ctx* c, int rc, hipStream_t s, std::string* msg) {
+  DistState& d = c->d;
+  constexpr int kCodes = 16;
+  unsigned long long* h = d.h_pinned + kSmallWords;
+  unsigned long long* dv = d.small + kSmallWords - 2 * kCodes;
+  std::fill(h, h + kCodes, 0ull);
+  if (rc > 0 && rc < kCodes) h[rc] = 1;
+  HIPCHECK(hipMemcpyAsync(dv, h, 8 * kCodes, hipMemcpyHostToDevice, s));
+  d.comm->allreduce_u64(dv, dv + kCodes, kCodes, s);
+  HIPCHECK(hipMemcpyAsync(h, dv + kCodes, 8 * kCodes, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  if (rc > 0) return rc;
+  for (int k = 1; k < kCodes; ++k)
+    if (h[k]) {
+      *msg = "build MPHF: another rank failed (" + std::string(status_name(k)) + ")";
+      return k;
+    }
+  return S3IMPH_OK;
+}
+
 // Output entries one rank may need: its share of the positions settles about N/P keys
 // (binomial spread), and rank 0 also writes the replicated tail levels.
 uint64_t dist_out_cap(const s3imph_ctx* c, uint64_t n_global) {
@@ -797,6 +853,7 @@ int route0_chunked(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, 
     HIPCHECK(hipEventCreateWithFlags(&d.ev_x, hipEventDisableTiming));
   }
   const int K = kRoute0Chunks;
+  d.agree_msg.clear();
   const uint64_t per = (n_local + K - 1) / K;
   const LevelGeom gh = choose_geom_sz(n_local, 64 * level_words(N), kTargetTiles0, chunks0(n_local), kTileMaxBits);
   HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
@@ -857,10 +914,13 @@ int route0_chunked(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, 
         got += rn;
       }
     }
-    if (at(M, R, R) + received + got > d.cap_list) {
-      HIPCHECK(hipStreamSynchronize(d.xs));
-      HIPCHECK(hipStreamSynchronize(s));
-      return S3IMPH_ERR_NOMEM;
+    {  // a local capacity check: agreed on the exchange stream before its all-to-all
+      const int rc = dist_agree(c, at(M, R, R) + received + got > d.cap_list ? S3IMPH_ERR_NOMEM : S3IMPH_OK, d.xs,
+                                &d.agree_msg);
+      if (rc != S3IMPH_OK) {
+        HIPCHECK(hipStreamSynchronize(s));
+        return rc;
+      }
     }
     cm.alltoallv(d.send, soff.data(), sbytes.data(), lin, roff.data(), rbytes.data(), d.xs);
     received += got;
@@ -875,6 +935,61 @@ int route0_chunked(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, 
     std::fprintf(stderr, "[s3imph] rank %d: level 0 exchanged in %d chunks (%llu records)\n", R, K,
                  (unsigned long long)*recv_total);
   return S3IMPH_OK;
+}
+
+// kStTooManyLevels on a sharded build, decided on every rank together (the flags are
+// gathered, so every rank calls this): each rank's leftover duplicate hash values (at most
+// 32) are all-gathered, every rank counts them among its ORIGINAL key hashes (recomputed),
+// and the counts are summed over ranks.  DUP_KEY_HASH only if some value occurs twice among
+// the original keys; leftovers with equal hashes otherwise are an internal fault.
+int dist_classify_stop(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, uint64_t n_local, hipStream_t s,
+                       std::string* msg) {
+  DistState& d = c->d;
+  Comm& cm = *d.comm;
+  const int P = d.nranks;
+  constexpr int kCand = 32;
+  const LevelState& hs = *c->h_st;
+  const unsigned nl = hs.stop_level ? hs.stop_level : hs.nlevels;
+  const uint64_t rem = nl >= 1 && nl < (unsigned)kMaxLevels + 2 ? hs.n[nl] : 0;
+  const std::vector<uint64_t> mine = rem ? record_dup_values(c->list[(nl - 1) & 1], rem, kCand) : std::vector<uint64_t>{};
+  unsigned long long* M = d.h_pinned;
+  std::fill(M, M + kCand + 1, 0ull);
+  M[0] = mine.size();
+  std::copy(mine.begin(), mine.end(), M + 1);
+  HIPCHECK(hipMemcpyAsync(d.small, M, 8ull * (kCand + 1), hipMemcpyHostToDevice, s));
+  cm.allgather(d.small, d.small + 64, 8ull * (kCand + 1), s);
+  HIPCHECK(hipMemcpyAsync(M, d.small + 64, 8ull * (kCand + 1) * P, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  std::vector<uint64_t> u;
+  for (int r = 0; r < P; ++r) {
+    const unsigned long long* row = M + (uint64_t)r * (kCand + 1);
+    for (uint64_t i = 0; i < std::min<uint64_t>(row[0], kCand); ++i) u.push_back(row[1 + i]);
+  }
+  std::sort(u.begin(), u.end());
+  u.erase(std::unique(u.begin(), u.end()), u.end());
+  if (u.empty()) {
+    *msg = "build MPHF: can't find minimal perfect hash after " + std::to_string(kMaxLevels) + " levels";
+    return S3IMPH_ERR_TOO_MANY_LEVELS;
+  }
+  const std::vector<uint64_t> orig = original_key_hashes(c, blob, offsets, n_local, s);
+  std::vector<unsigned long long> cnt(u.size(), 0);
+  for (size_t i = 0; i < u.size(); ++i) {
+    const auto r = std::equal_range(orig.begin(), orig.end(), u[i]);
+    cnt[i] = (unsigned long long)(r.second - r.first);
+  }
+  unsigned long long* ds = d.small + 4000;  // |u| <= 32 P <= 2048 entries each way (below dist_agree's words)
+  HIPCHECK(hipMemcpyAsync(ds, cnt.data(), 8 * cnt.size(), hipMemcpyHostToDevice, s));
+  cm.allreduce_u64(ds, ds + 2048, cnt.size(), s);
+  HIPCHECK(hipMemcpyAsync(cnt.data(), ds + 2048, 8 * cnt.size(), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  for (unsigned long long v : cnt)
+    if (v >= 2) {
+      *msg = "build MPHF: duplicate FNV-1a key hashes: bbhash cannot place them";
+      return S3IMPH_ERR_DUP_KEY_HASH;
+    }
+  *msg = "build MPHF: internal error: level " + std::to_string(nl) +
+         " holds records with equal key hashes although every key hash is distinct (a record was duplicated)";
+  return S3IMPH_ERR_INTERNAL;
 }
 
 // One attempt of the multi-GPU build (see s3imph_dist.hip for the decomposition).
@@ -1026,6 +1141,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
       const int rc = route0_chunked(c, blob, offsets, pos, n_local, key_base, N, b, C, lin, s, M, &m_chunked);
       if (rc != S3IMPH_OK) {
         if (rc == S3IMPH_ERR_NOMEM) *msg = "build MPHF: rank " + std::to_string(R) + " received too many records";
+        if (rc > 0 && !d.agree_msg.empty()) *msg = d.agree_msg;
         return rc;
       }
     }
@@ -1069,19 +1185,22 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
     for (int r = 0; r < P; ++r) m += M[(uint64_t)r * (P + 1) + R];
     const uint64_t w = level_words(nL), S = (w + P - 1) / P;
     const uint64_t lo = std::min<uint64_t>((uint64_t)R * S, w), rw = std::min<uint64_t>(S, w - lo);
-    if (m > d.cap_list) {
-      *msg = "build MPHF: rank " + std::to_string(R) + " received " + std::to_string(m) + " records (capacity " +
-             std::to_string(d.cap_list) + ")";
-      return S3IMPH_ERR_NOMEM;
-    }
-    // ---- exchange: the received records follow this rank's own ones in list[1]
-    if (L == 0 && chunked) {
-      if (m_chunked != m) {
+    {  // rank-local checks, agreed before the exchange
+      int lrc = S3IMPH_OK;
+      if (m > d.cap_list) {
+        *msg = "build MPHF: rank " + std::to_string(R) + " received " + std::to_string(m) + " records (capacity " +
+               std::to_string(d.cap_list) + ")";
+        lrc = S3IMPH_ERR_NOMEM;
+      } else if (L == 0 && chunked && m_chunked != m) {
         *msg = "build MPHF: internal error: chunked level-0 exchange received " + std::to_string(m_chunked) +
                " of " + std::to_string(m) + " records";
-        return S3IMPH_ERR_INTERNAL;
+        lrc = S3IMPH_ERR_INTERNAL;
       }
-    } else {
+      const int rc = dist_agree(c, lrc, s, msg);
+      if (rc != S3IMPH_OK) return rc;
+    }
+    // ---- exchange: the received records follow this rank's own ones in list[1]
+    if (!(L == 0 && chunked)) {
       uint64_t acc = M[(uint64_t)R * (P + 1) + R] * sizeof(Rec);
       for (int t = 0; t < P; ++t) {
         soff[t] = (uint64_t)t * C * sizeof(Rec);
@@ -1116,9 +1235,14 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
     total += cnt[r];
     maxc = std::max(maxc, cnt[r]);
   }
-  if (total > d.cap_list) {
-    *msg = "build MPHF: replicated level of " + std::to_string(total) + " records exceeds the workspace";
-    return S3IMPH_ERR_NOMEM;
+  {  // the list capacity is per rank (it follows n_local): agreed before the gather
+    int lrc = S3IMPH_OK;
+    if (total > d.cap_list) {
+      *msg = "build MPHF: replicated level of " + std::to_string(total) + " records exceeds the workspace";
+      lrc = S3IMPH_ERR_NOMEM;
+    }
+    const int rc = dist_agree(c, lrc, s, msg);
+    if (rc != S3IMPH_OK) return rc;
   }
   Rec* rl = c->list[(Ls - 1) & 1];
   if (total) {
@@ -1134,6 +1258,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
       o += cnt[r];
     }
   }
+  if (total >= 2) fault_dup_record(c, rl, s);
   launch_dist_replicate(st, Ls, total, R == 0 ? 0 : (uint64_t)Ls, s);
   ev_mark(c, s, "gather");
   const LevelGeom gcons = choose_geom(std::max<uint64_t>(total, 1), kTargetTiles, kTargetChunks, kRegTileMaxBits);
@@ -1173,16 +1298,7 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   unsigned flags = 0;
   for (int r = 0; r < P; ++r) flags |= (unsigned)lb(r, Ls + 2);
   if (flags & (kStGeometry | kStTailOverflow | kStResOverflow | kStRouteOverflow)) return conservative ? S3IMPH_ERR_INTERNAL : kDistRetry;
-  if (flags & kStTooManyLevels) {
-    const unsigned nl = hs.stop_level ? hs.stop_level : hs.nlevels;
-    const uint64_t rem = nl < (unsigned)kMaxLevels + 2 ? hs.n[nl] : 0;
-    if (records_have_duplicates(c->list[(nl - 1) & 1], rem)) {
-      *msg = "build MPHF: duplicate FNV-1a key hashes: bbhash cannot place them";
-      return S3IMPH_ERR_DUP_KEY_HASH;
-    }
-    *msg = "build MPHF: can't find minimal perfect hash after " + std::to_string(kMaxLevels) + " levels";
-    return S3IMPH_ERR_TOO_MANY_LEVELS;
-  }
+  if (flags & kStTooManyLevels) return dist_classify_stop(c, blob, offsets, n_local, s, msg);
   if (flags & kStKeyZero) {
     *msg = "MPHF Key(...) returned 0, possible hash collision with sentinel";
     return S3IMPH_ERR_KEY_HASH_ZERO;
@@ -1353,9 +1469,14 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     *msg = "build MPHF: bitmap decomposition: list capacity exceeded";
     return S3IMPH_ERR_INTERNAL;
   }
-  if (total > d.cap_list || total > c->cap_keys) {
-    *msg = "build MPHF: replicated level of " + std::to_string(total) + " records exceeds the workspace";
-    return S3IMPH_ERR_NOMEM;
+  {  // per-rank capacities: agreed before the gather
+    int lrc = S3IMPH_OK;
+    if (total > d.cap_list || total > c->cap_keys) {
+      *msg = "build MPHF: replicated level of " + std::to_string(total) + " records exceeds the workspace";
+      lrc = S3IMPH_ERR_NOMEM;
+    }
+    const int rc = dist_agree(c, lrc, s, msg);
+    if (rc != S3IMPH_OK) return rc;
   }
   Rec* rl = c->list[(Ls - 1) & 1];
   if (total) {
@@ -1371,6 +1492,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
       o += cnt[r];
     }
   }
+  if (total >= 2) fault_dup_record(c, rl, s);
   launch_dist_replicate(st, Ls, total, 0, s);
   launch_set_u64(&st->lvl_base[Ls], 0, s);  // tail ranks count from 0: scratch index = p - (N - total)
   ev_mark(c, s, "gather");
@@ -1410,16 +1532,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     std::fprintf(stderr, "\n");
   }
   if (flags & (kStGeometry | kStTailOverflow | kStResOverflow)) return kDistRetry;
-  if (flags & kStTooManyLevels) {
-    const unsigned nl = hs.stop_level ? hs.stop_level : hs.nlevels;
-    const uint64_t rem = nl < (unsigned)kMaxLevels + 2 ? hs.n[nl] : 0;
-    if (records_have_duplicates(c->list[(nl - 1) & 1], rem)) {
-      *msg = "build MPHF: duplicate FNV-1a key hashes: bbhash cannot place them";
-      return S3IMPH_ERR_DUP_KEY_HASH;
-    }
-    *msg = "build MPHF: can't find minimal perfect hash after " + std::to_string(kMaxLevels) + " levels";
-    return S3IMPH_ERR_TOO_MANY_LEVELS;
-  }
+  if (flags & kStTooManyLevels) return dist_classify_stop(c, blob, offsets, n_local, s, msg);
   if (flags & kStKeyZero) {
     *msg = "MPHF Key(...) returned 0, possible hash collision with sentinel";
     return S3IMPH_ERR_KEY_HASH_ZERO;
@@ -1436,9 +1549,14 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   // ---- settled triples to the owners of their output slices
   const uint64_t slice = (N + P - 1) / P;
   const uint64_t lo = std::min<uint64_t>((uint64_t)R * slice, N), mine = std::min<uint64_t>(N, lo + slice) - lo;
-  if (mine > out_cap) {
-    *msg = "build MPHF: output capacity " + std::to_string(out_cap) + " < " + std::to_string(mine);
-    return S3IMPH_ERR_INVALID;
+  {  // out_cap is the caller's, per rank: agreed before the bounds gather
+    int lrc = S3IMPH_OK;
+    if (mine > out_cap) {
+      *msg = "build MPHF: output capacity " + std::to_string(out_cap) + " < " + std::to_string(mine);
+      lrc = S3IMPH_ERR_INVALID;
+    }
+    const int rc = dist_agree(c, lrc, s, msg);
+    if (rc != S3IMPH_OK) return rc;
   }
   // this rank's settled list is sorted by p: its run for slice t goes to rank t as it lies
   // (the own run is placed straight from the list)
@@ -1464,11 +1582,16 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   const uint64_t g0 = N - total;
   const uint64_t tail_mine = std::min<uint64_t>(N, lo + mine) > std::max(g0, lo)
                                  ? std::min<uint64_t>(N, lo + mine) - std::max(g0, lo) : 0;
-  if (sent != n_out || got + own + tail_mine != mine || got > d.cap_list) {
-    *msg = "build MPHF: internal error: output slice of rank " + std::to_string(R) + " receives " +
-           std::to_string(got) + " + " + std::to_string(own) + " + " + std::to_string(tail_mine) + " of " +
-           std::to_string(mine) + " entries";
-    return S3IMPH_ERR_INTERNAL;
+  {  // rank-local consistency of the output exchange: agreed before the all-to-all
+    int lrc = S3IMPH_OK;
+    if (sent != n_out || got + own + tail_mine != mine || got > d.cap_list) {
+      *msg = "build MPHF: internal error: output slice of rank " + std::to_string(R) + " receives " +
+             std::to_string(got) + " + " + std::to_string(own) + " + " + std::to_string(tail_mine) + " of " +
+             std::to_string(mine) + " entries";
+      lrc = S3IMPH_ERR_INTERNAL;
+    }
+    const int rc = dist_agree(c, lrc, s, msg);
+    if (rc != S3IMPH_OK) return rc;
   }
   Rec* recv = c->list[Ls & 1];
   if (P > 1) cm.alltoallv(out, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), s);
@@ -1479,9 +1602,14 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   HIPCHECK(hipMemcpyAsync(M, &st->status, 4, hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   ev_collect(c);
-  if ((unsigned)M[0] & kStRank) {
-    *msg = "build MPHF: internal error: a settled position fell outside its owner's slice";
-    return S3IMPH_ERR_INTERNAL;
+  {  // this rank's placement flag: agreed, so every rank returns the same way
+    int lrc = S3IMPH_OK;
+    if ((unsigned)M[0] & kStRank) {
+      *msg = "build MPHF: internal error: a settled position fell outside its owner's slice";
+      lrc = S3IMPH_ERR_INTERNAL;
+    }
+    const int rc = dist_agree(c, lrc, s, msg);
+    if (rc != S3IMPH_OK) return rc;
   }
   d.seg.clear();
   if (mine) d.seg.insert(d.seg.end(), {lo, mine, 0});
@@ -1861,6 +1989,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     c->loose_geom = std::getenv("S3IMPH_LOOSE_GEOM") != nullptr;
     c->route_self = std::getenv("S3IMPH_DIST_ROUTE_SELF") != nullptr;  // A/B knob: list-level geometry from 1.1x bounds
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
+    c->fault_dup = std::getenv("S3IMPH_FAULT_DUP_REC") != nullptr;
     if (const char* m = std::getenv("S3IMPH_SCAT_CFG")) c->scat_cfg = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_SKEW_CFG")) c->skew_cfg = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);

@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -101,32 +102,47 @@ struct DistState {
   // level 0's exchange runs on its own stream, chunk by chunk, beside the next chunk's hash
   hipStream_t xs = nullptr;
   hipEvent_t ev_route = nullptr, ev_counts = nullptr, ev_x = nullptr;
+  std::string agree_msg;  // message of a failure agreed inside route0_chunked
 };
 
 // RCCL over xGMI: all-to-all as grouped point-to-point send/recv (xGMI is a full mesh
 // of point-to-point links, so every pair streams on its own link), all-gathers and
 // all-reduces as RCCL collectives; the rank's own share is a device-to-device copy.
 struct RcclComm final : Comm {
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr;  // written once, before any collective; never reset (abort keeps it)
+  std::atomic<bool> aborted{false};
   ~RcclComm() override {
-    if (comm) (void)ncclCommDestroy(comm);
+    if (comm && !aborted.load()) (void)ncclCommDestroy(comm);
   }
+  // Called from a failing peer's thread (s3imph_multi.hip): ncclCommAbort makes this rank's
+  // pending collectives return.  The handle is left as it is — the owning rank thread may be
+  // reading it — and the owning thread's next collective throws instead of enqueueing on the
+  // aborted communicator (a collective already being enqueued when the abort lands fails
+  // inside RCCL and throws the same way).
   void abort() override {
-    if (comm) (void)ncclCommAbort(comm);
-    comm = nullptr;
+    bool expected = false;
+    if (comm && aborted.compare_exchange_strong(expected, true)) (void)ncclCommAbort(comm);
+  }
+  void live() const {
+    if (aborted.load(std::memory_order_acquire))
+      throw Fail{S3IMPH_ERR_RCCL, "RCCL communicator aborted: a peer rank failed"};
   }
   void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
+    live();
     NCCLCHECK(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, s));
   }
   void reduce_scatter_u8(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
+    live();
     NCCLCHECK(ncclReduceScatter(d_send, d_recv, bytes, ncclUint8, ncclSum, comm, s));
   }
   void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
                      hipStream_t s) override {
+    live();
     NCCLCHECK(ncclAllReduce(d_in, d_out, count, ncclUint64, ncclSum, comm, s));
   }
   void alltoallv(const void* d_send, const uint64_t* soff, const uint64_t* sbytes, void* d_recv,
                  const uint64_t* roff, const uint64_t* rbytes, hipStream_t s) override {
+    live();
     const char* sb = static_cast<const char*>(d_send);
     char* rb = static_cast<char*>(d_recv);
     NCCLCHECK(ncclGroupStart());
@@ -201,6 +217,7 @@ struct s3imph_ctx {
   int skew_cfg = 2;         // S3IMPH_SKEW_CFG: skewed-length hash block / group shape (launch_hash_skew)
   bool loose_geom = false;  // S3IMPH_LOOSE_GEOM: list levels sized from 1.1x (not 1.02x + 6 sigma) bounds
   bool debug = false;
+  bool fault_dup = false;   // S3IMPH_FAULT_DUP_REC: test hook, duplicates a record mid-build (fault_dup_record)
   unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps
   bool lds_attr_set = false;
 
@@ -244,6 +261,8 @@ void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t b
                  int conv = 0);
 void launch_widen32(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);
 void launch_narrow32(const uint64_t* in, uint32_t* out, uint64_t n, hipStream_t s);
+// FNV-1a of keys [0, n) into out (the error path's recount of the original key hashes)
+void launch_key_hashes(const uint8_t* blob, const uint64_t* offsets, uint64_t n, uint64_t* out, hipStream_t s);
 int marshal_locked(s3imph_ctx* c, uint8_t* out, uint64_t cap, uint64_t* len, std::string* msg);
 // Index finalize arrays (s3imph_finalize.hip): device pass over keys in HBM, and the
 // host-memory form that writes the five files.

@@ -16,6 +16,10 @@
 // writeArraysParallel, :546-596) each handing chunk k to the caller's sink while the DMA
 // of chunk k+1 runs.  The sink (the output files) is opened only once the build has
 // succeeded: like the reference's Build, a failed bbhash.New leaves out_dir untouched.
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -31,7 +35,20 @@ namespace {
 
 constexpr uint64_t kMinChunk = 256ull << 10;  // first chunk of an arena; each next one doubles
 constexpr uint64_t kMaxChunk = 64ull << 20;   // ... up to this
-constexpr uint64_t kPoolKeep = 16ull << 30;   // pinned bytes the pool keeps cached between builders
+constexpr uint64_t kPoolKeep = 16ull << 30;   // pinned bytes the pool keeps cached between builders (at most)
+
+// The pool's cap: 16 GiB, or an eighth of physical memory if that is less, or
+// S3IMPH_PINNED_KEEP bytes.  Page-locked memory a long-lived host process (the cgo caller)
+// keeps between builds is memory the rest of the box cannot page.
+uint64_t pool_keep() {
+  static const uint64_t keep = [] {
+    if (const char* e = std::getenv("S3IMPH_PINNED_KEEP")) return (uint64_t)std::strtoull(e, nullptr, 10);
+    const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGE_SIZE);
+    const uint64_t phys = pages > 0 && psz > 0 ? (uint64_t)pages * (uint64_t)psz : 0;
+    return phys ? std::min<uint64_t>(kPoolKeep, phys / 8) : kPoolKeep;
+  }();
+  return keep;
+}
 
 // Process-wide cache of pinned host chunks by size.  hipHostMalloc pins (and zeroes) every
 // page: ~5 GB/s, the cost that dominated round 2's Add.  Chunks come back at Build / close.
@@ -57,7 +74,7 @@ struct PinnedPool {
   void put(void* p, uint64_t sz) {
     {
       std::lock_guard<std::mutex> lk(mu);
-      if (cached + sz <= kPoolKeep) {
+      if (cached + sz <= pool_keep()) {
         idle[sz].push_back(p);
         cached += sz;
         return;
@@ -65,7 +82,25 @@ struct PinnedPool {
     }
     (void)hipHostFree(p);
   }
+  // Unpin idle chunks, largest first, until at most `keep` bytes stay cached.
+  void trim(uint64_t keep) {
+    std::vector<std::pair<void*, uint64_t>> drop;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (auto it = idle.rbegin(); it != idle.rend() && cached > keep; ++it)
+        while (!it->second.empty() && cached > keep) {
+          drop.emplace_back(it->second.back(), it->first);
+          it->second.pop_back();
+          cached -= it->first;
+        }
+    }
+    for (auto& d : drop) (void)hipHostFree(d.first);
+  }
 };
+// Builders alive (feed_new .. feed_free): when the last one closes, the pool keeps only the
+// chunks of one typical builder (1 GiB) pinned, not the largest build's working set.
+std::atomic<int> g_live_feeds{0};
+constexpr uint64_t kPoolKeepIdle = 1ull << 30;
 
 PinnedPool& pool() {
   static PinnedPool* p = new PinnedPool();  // never destroyed: chunks may return during exit
@@ -106,6 +141,20 @@ struct Arena {
     fill = 0;
     return true;
   }
+  // copies the whole arena to dst chunk by chunk, giving each chunk back (pool or heap) as
+  // soon as it is copied: the host copy moves instead of doubling
+  void drain(uint8_t* dst) {
+    for (size_t k = 0; k < ch.size(); ++k) {
+      const uint64_t m = k + 1 < ch.size() ? ch[k].size : fill;
+      std::memcpy(dst + ch[k].start, ch[k].p, m);
+      if (ch[k].pinned)
+        pool().put(ch[k].p, ch[k].size);
+      else
+        std::free(ch[k].p);
+    }
+    ch.clear();
+    fill = 0;
+  }
   // reads [a, a+n) of the arena into dst
   void read(uint64_t a, uint8_t* dst, uint64_t n) const {
     size_t k = 0;
@@ -133,6 +182,7 @@ struct Feed {
   uint64_t n = 0;
   uint64_t reserve_keys = 0, reserve_bytes = 0;
   uint64_t* d_out[2] = {nullptr, nullptr};  // fp_out, pos_out
+  bool host_taken = false;  // feed_take_host moved the host chunks out: no more Adds
   uint64_t out_cap = 0;
 
   void drop_device() {
@@ -231,6 +281,7 @@ struct Feed {
 
 Feed* feed_new(int device, bool use_gpu) {
   Feed* f = new Feed();
+  g_live_feeds.fetch_add(1);
   f->device = device;
   f->ends.dev_base = 8;  // device offsets array = [0, ends...]
   if (use_gpu) {
@@ -247,7 +298,10 @@ Feed* feed_new(int device, bool use_gpu) {
   return f;
 }
 
-void feed_free(Feed* f) { delete f; }
+void feed_free(Feed* f) {
+  delete f;  // its chunks go back to the pool
+  if (g_live_feeds.fetch_sub(1) == 1) pool().trim(std::min(pool_keep(), kPoolKeepIdle));
+}
 
 void feed_drop_device(Feed* f) {
   if (!f->dev_on) return;
@@ -326,14 +380,14 @@ void feed_flush(Feed* f) {
 
 bool feed_on_device(const Feed* f) { return f && f->dev_on; }
 
-void feed_materialize(const Feed* f, std::vector<uint8_t>* blob, std::vector<uint64_t>* offsets,
-                      std::vector<uint64_t>* pos) {
-  blob->resize(((f->blob.total + 7) & ~7ull) + 16);  // the host build's staging reads whole words
-  f->blob.read(0, blob->data(), f->blob.total);
+void feed_take_host(Feed* f, std::vector<uint8_t>* blob, std::vector<uint64_t>* offsets, std::vector<uint64_t>* pos) {
+  blob->assign(((f->blob.total + 7) & ~7ull) + 16, 0);  // the host build's staging reads whole words
+  f->blob.drain(blob->data());
   offsets->assign(f->n + 1, 0);
-  f->ends.read(0, reinterpret_cast<uint8_t*>(offsets->data() + 1), 8 * f->n);
+  f->ends.drain(reinterpret_cast<uint8_t*>(offsets->data() + 1));
   pos->resize(f->n);
-  f->pos.read(0, reinterpret_cast<uint8_t*>(pos->data()), 8 * f->n);
+  f->pos.drain(reinterpret_cast<uint8_t*>(pos->data()));
+  f->host_taken = true;
 }
 
 // prefix_blob.bin / prefix_offsets.u64 straight from the chunks (writePrefixBlobPreorder,

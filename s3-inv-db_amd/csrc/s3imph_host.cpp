@@ -374,6 +374,11 @@ struct s3imph_builder {
   Feed* feed = nullptr;
   uint64_t count = 0;
   bool built = false;
+  // the host path's contiguous copy, moved out of the feed's chunks by the first host-path
+  // Build (kept for a retried Build; Adds are refused after it)
+  bool host_taken = false;
+  std::vector<uint8_t> h_blob;
+  std::vector<uint64_t> h_offsets, h_pos;
   ~s3imph_builder() { feed_free(feed); }
   Feed* store() {
     if (!feed) feed = feed_new(device, devices.empty());
@@ -406,8 +411,9 @@ int s3imph_builder_new(const char* temp_dir, int device, s3imph_builder** out, c
 int s3imph_builder_add(s3imph_builder* b, const uint8_t* prefix, uint64_t len, uint64_t pos, char* err,
                        size_t errlen) {
   if (!b || (len && !prefix)) return S3IMPH_ERR_INVALID;
-  if (b->built) {
-    set_err(err, errlen, "add to MPHF builder: builder already built");
+  if (b->built || b->host_taken) {
+    set_err(err, errlen, b->built ? "add to MPHF builder: builder already built"
+                                  : "add to MPHF builder: a failed Build already took the keys");
     return S3IMPH_ERR_STATE;
   }
   if (!feed_add(b->store(), prefix, len, pos)) {
@@ -421,8 +427,9 @@ int s3imph_builder_add(s3imph_builder* b, const uint8_t* prefix, uint64_t len, u
 int s3imph_builder_add_batch(s3imph_builder* b, const uint8_t* blob, const uint64_t* offsets,
                              const uint64_t* pos, uint64_t n, char* err, size_t errlen) {
   if (!b) return S3IMPH_ERR_INVALID;
-  if (b->built) {
-    set_err(err, errlen, "add to MPHF builder: builder already built");
+  if (b->built || b->host_taken) {
+    set_err(err, errlen, b->built ? "add to MPHF builder: builder already built"
+                                  : "add to MPHF builder: a failed Build already took the keys");
     return S3IMPH_ERR_STATE;
   }
   if (n == 0) return S3IMPH_OK;  // an empty batch may pass NULL blob / offsets
@@ -502,9 +509,13 @@ int s3imph_builder_build(s3imph_builder* b, const char* out_dir, char* err, size
       return S3IMPH_OK;
     }
     // host path: several GPUs, or the device feed is off (it failed, or there is no GPU)
-    std::vector<uint8_t> blob;
-    std::vector<uint64_t> offsets, pos;
-    feed_materialize(f, &blob, &offsets, &pos);
+    if (!b->host_taken) {
+      feed_take_host(f, &b->h_blob, &b->h_offsets, &b->h_pos);
+      b->host_taken = true;
+    }
+    const std::vector<uint8_t>& blob = b->h_blob;
+    const std::vector<uint64_t>& offsets = b->h_offsets;
+    const std::vector<uint64_t>& pos = b->h_pos;
     std::vector<uint64_t> fp(n), pos_out(n);
     std::vector<uint8_t> mph;
     if (n) {

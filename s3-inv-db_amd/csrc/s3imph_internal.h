@@ -339,9 +339,10 @@ bool feed_add_batch(Feed* f, const uint8_t* blob, const uint64_t* offsets, const
 uint64_t feed_count(const Feed* f);
 void feed_flush(Feed* f);              // enqueue the partial chunks (may turn the device path off)
 bool feed_on_device(const Feed* f);
-// contiguous copies (offsets N+1 from 0; blob padded to whole words + 16 B) for the host builds
-void feed_materialize(const Feed* f, std::vector<uint8_t>* blob, std::vector<uint64_t>* offsets,
-                      std::vector<uint64_t>* pos);
+// contiguous copies (offsets N+1 from 0; blob padded to whole words + 16 B) for the host
+// builds, MOVED out of the chunks (each chunk is released as it is copied, so the host copy
+// never exists twice); the feed takes no more keys afterwards
+void feed_take_host(Feed* f, std::vector<uint8_t>* blob, std::vector<uint64_t>* offsets, std::vector<uint64_t>* pos);
 int feed_write_prefix_files(const Feed* f, const std::string& dir, std::string* msg);
 // the single-GPU build on the fed arrays; open_sink() is called only once the build succeeded
 int feed_build(Feed* f, std::vector<uint8_t>* mph, const std::function<FeedSink*()>& open_sink, std::string* msg);

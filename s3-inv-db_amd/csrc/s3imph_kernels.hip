@@ -249,6 +249,18 @@ __global__ __launch_bounds__(256) void k_narrow32(const uint64_t* __restrict__ i
     out[i] = (uint32_t)in[i];
 }
 
+// FNV-1a hash of every key (mphf.go:349-369), nothing else: the error path's recount of
+// the ORIGINAL key hashes (the level-0 pipeline keeps them only in its own layouts).
+__global__ __launch_bounds__(kBlock) void k_key_hash(const uint8_t* __restrict__ blob,
+                                                     const uint64_t* __restrict__ offsets, uint64_t n,
+                                                     uint64_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    uint64_t a, b;
+    fnv_both_pf(blob, offsets[i], offsets[i + 1], a, b);
+    out[i] = a;
+  }
+}
+
 }  // namespace
 
 // ================================ launchers =======================================
@@ -285,6 +297,10 @@ void launch_widen32(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s
 }
 void launch_narrow32(const uint64_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
   if (n) k_narrow32<<<(unsigned)std::min<uint64_t>(8192, (n + 255) / 256), 256, 0, s>>>(in, out, n);
+}
+
+void launch_key_hashes(const uint8_t* blob, const uint64_t* offsets, uint64_t n, uint64_t* out, hipStream_t s) {
+  if (n) k_key_hash<<<(unsigned)std::min<uint64_t>(4096, (n + kBlock - 1) / kBlock), kBlock, 0, s>>>(blob, offsets, n, out);
 }
 
 }  // namespace s3imph

@@ -134,6 +134,21 @@ def test_dist_duplicate_across_ranks_fails_everywhere(mode):
         assert r[1] == "error" and r[2] == s3imph.ERR_DUP_KEY_HASH, r
 
 
+@pytest.mark.parametrize("mode", ["route", "bitmap"])
+def test_dist_duplicated_record_is_an_internal_fault(mode, monkeypatch):
+    """A record duplicated inside the sharded build (S3IMPH_FAULT_DUP_REC: the gathered
+    replicated level's record 0 copied over record 1) stops it on leftovers with one key
+    hash; the ranks count that value among their ORIGINAL key hashes, sum the counts, find
+    it once, and every rank reports ERR_INTERNAL (not the caller's duplicate keys)."""
+    monkeypatch.setenv("S3IMPH_FAULT_DUP_REC", "1")
+    keys = [b"x/%05d/" % i for i in range(3000)]
+    blob, offs = O.keys_to_blob(keys)
+    res = _run(2, _shards(blob, offs, [0, 1500, 3000]), 3000, 1 << 20, mode)
+    import s3imph
+    for r in res:
+        assert r[1] == "error" and r[2] == s3imph.ERR_INTERNAL and "duplicated" in r[3], r
+
+
 @pytest.mark.parametrize("mode", ["route", "route_self", "bitmap"])
 def test_dist_rccl_single_rank_routes_levels(oracle_lib, monkeypatch, mode):
     """The RCCL transport (nranks = 1 on this box) through several sharded levels: route

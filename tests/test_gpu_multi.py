@@ -62,6 +62,18 @@ def test_thread_per_rank_shared_gpu(s3, oracle_lib, monkeypatch, ranks, kind, av
     assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
 
 
+def test_thread_per_rank_64_ranks_bitmap(s3, oracle_lib, monkeypatch):
+    """kMaxRanks = 64 ranks (the API's limit) on the bitmap decomposition: the output
+    exchange's slice bounds need P + 1 = 65 boundaries (k_bm_bounds), the last slice's
+    count included; bit-exact."""
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", "15000")
+    monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
+    blob, offs = s3.gen_keys(0, 12, 24, 0, 640_000)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    g = s3.build_host(blob, offs, devices=[0] * 64, flags=s3.MULTI_BITMAP)
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+
+
 @pytest.mark.parametrize("switch,n", [(20_000, 1_500_000), (2 << 20, 4_000_000)])
 def test_one_gpu_sharded_bitmap_over_rccl(s3, oracle_lib, monkeypatch, switch, n):
     """The bitmap decomposition on an in-process RCCL communicator (one rank):

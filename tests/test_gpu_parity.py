@@ -315,6 +315,26 @@ def test_duplicates_stop_the_build_early(s3, ctx):
     assert time.perf_counter() - t0 < 5.0
 
 
+def test_duplicated_record_is_an_internal_fault(s3, monkeypatch):
+    """A record duplicated inside the build (S3IMPH_FAULT_DUP_REC copies level 1's record 0
+    over record 1, as a kernel race would) stops the build on two records with one key
+    hash; every ORIGINAL key hash is distinct, so the error is ERR_INTERNAL naming the
+    level, never the caller's ERR_DUP_KEY_HASH.  A context without the hook builds the
+    same keys."""
+    monkeypatch.setenv("S3IMPH_FAULT_DUP_REC", "1")
+    blob, offs = s3.gen_keys(0, 5, 32, 0, 200_000)
+    faulty = s3.DeviceBuilder(0)
+    with pytest.raises(s3.MPHFError) as e:
+        _device_build(s3, faulty, blob, offs)
+    faulty.close()
+    assert e.value.status == s3.ERR_INTERNAL, e.value
+    assert "duplicated" in str(e.value) and "level" in str(e.value)
+    monkeypatch.delenv("S3IMPH_FAULT_DUP_REC")
+    clean = s3.DeviceBuilder(0)
+    _device_build(s3, clean, blob, offs)
+    clean.close()
+
+
 def test_duplicate_group_overflowing_a_reservation_slot(s3, ctx):
     """150k copies of one key all land in one tile of every level: the small-level
     reservation slot overflows, the build reruns on the counted path, and the result is

@@ -140,6 +140,48 @@ def test_c_vs_python_random_keysets(oracle_lib):
         assert list(map(int, fp)) == pfp and list(map(int, pos)) == ppos
 
 
+@pytest.mark.parametrize("threads", [1, 3, 8, 16])
+def test_build_mt_and_revmap_equal_build(oracle_lib, threads):
+    """The big-config checkers: orc_build_mt (FNV and placement on several threads, used by
+    every >= 10M-key GPU parity test) and orc_build_revmap (the reference-shaped reverse-map
+    build, bench.py's CPU baseline) give orc_build's exact outputs, with identity and custom
+    positions, around word / thread-split boundaries."""
+    rng = random.Random(99 + threads)
+    for n in [1, 2, 63, 64, 65, 1000, 4097, 120_000]:
+        keys = [b"t/%d/%08x/" % (i, rng.getrandbits(32)) for i in range(n)]
+        blob, offs = O.keys_to_blob(keys)
+        pos = np.array([rng.getrandbits(63) for _ in range(n)], np.uint64)
+        for pv in (None, pos):
+            st, fp, po, mph = oracle_lib.build(blob, offs, pv)
+            assert st == 0
+            st2, fp2, po2, mph2 = oracle_lib.build_mt(blob, offs, pv, threads=threads)
+            assert st2 == 0 and mph2 == mph and np.array_equal(fp2, fp) and np.array_equal(po2, po), (n, threads)
+            st3, fp3, po3 = oracle_lib.build_revmap(blob, offs, pv)
+            assert st3 == 0 and np.array_equal(fp3, fp) and np.array_equal(po3, po), n
+
+
+def test_build_mt_and_revmap_equal_python_restatement(oracle_lib):
+    """The same checkers against the independent pure-Python restatement (small sets)."""
+    rng = random.Random(4321)
+    for n in [1, 5, 33, 200, 1500]:
+        keys = list({bytes(rng.randrange(256) for _ in range(rng.randrange(0, 24))) for _ in range(n)})
+        blob, offs = O.keys_to_blob(keys)
+        pfp, ppos, pmph = O.py_build(keys)
+        st, fp, po, mph = oracle_lib.build_mt(blob, offs, threads=4)
+        assert st == 0 and mph == pmph and list(map(int, fp)) == pfp and list(map(int, po)) == ppos
+        st, fp, po = oracle_lib.build_revmap(blob, offs)
+        assert st == 0 and list(map(int, fp)) == pfp and list(map(int, po)) == ppos
+
+
+def test_build_mt_and_revmap_report_duplicates(oracle_lib):
+    keys = [b"a/%d" % i for i in range(5000)] + [b"a/17"]
+    blob, offs = O.keys_to_blob(keys)
+    st = oracle_lib.build(blob, offs)[0]
+    assert st != 0
+    assert oracle_lib.build_mt(blob, offs, threads=8)[0] == st
+    assert oracle_lib.build_revmap(blob, offs)[0] == st
+
+
 def test_custom_pos_permutes_with_keys(oracle_lib):
     """Add(prefix, pos) accepts arbitrary pos (mphf_streaming.go:68); pos_out[p] = pos_i."""
     keys = [("k%d/" % i).encode() for i in range(300)]

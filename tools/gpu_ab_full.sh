@@ -1,5 +1,5 @@
 #!/bin/bash
-# Full -m gpu suite on the in-tree build, then an old/new library A/B (ab/libs3imph_{old,new}.so,
+# Full -m gpu suite on the in-tree build, then an old/new library A/B (abx/libs3imph_{old,new}.so,
 # alternating) on C2 and C3.   bash tools/gpu_ab_full.sh TAG [pytest -k expr]
 set -e
 OUT=gpurun_out/$1; mkdir -p $OUT
@@ -17,12 +17,12 @@ fi
 L=s3-inv-db_amd/s3imph/_lib/libs3imph.so
 for cfg in ${CFGS:-c2 c3}; do
   for v in old new old new; do
-    cp ab/libs3imph_$v.so $L
+    cp abx/libs3imph_$v.so $L
     timeout -k 10 200 python bench.py --no-cpu-baseline --headline-only --no-secondary --config $cfg --steps 20 \
       >> $OUT/${cfg}_$v.log 2>&1
   done
 done
-cp ab/libs3imph_new.so $L
+cp abx/libs3imph_new.so $L
 # the new library once more per A/B knob setting (AB_ENV="S3IMPH_MID_FENCE=1 S3IMPH_SCAT_CFG=0": one run each)
 i=0
 for kv in $AB_ENV; do
