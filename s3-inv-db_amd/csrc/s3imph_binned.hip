@@ -1052,9 +1052,6 @@ constexpr unsigned kSplitSubBitsDev = 14;  // = kSplitSubBits (sub-tile of the s
 // instead of Rec's 24, so the level-0 scatter writes and the split kernel's bucket reads,
 // scratch writes and scratch reads move 4 bytes less per key (1.6 GB less at C3).  Only
 // the reservation scatter and the split big-tile kernel use it; the next list stays Rec.
-struct R20 {
-  uint32_t w[5];
-};
 __device__ __forceinline__ R20 r20_make(uint64_t k, uint64_t f, uint32_t i) {
   return R20{{(uint32_t)k, (uint32_t)(k >> 32), (uint32_t)f, (uint32_t)(f >> 32), i}};
 }
@@ -1286,6 +1283,155 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     tp[7] = c;
   }
 #undef SPROF
+}
+
+// ------------------------------------------- level 0 in 2^14-position tiles (P0) --------
+// Level 0 of a set with more than kP0MinTiles 2^14-position tiles (C3: 12.2k) takes
+// register-resident tiles too, without the split kernel's 2^14 sub-tile scratch round trip:
+// its positions are cut into S super-tiles of tps tiles each (tps <= kT), the level-0 records
+// (R20: k, f, key index) first land in per-(super-tile, XCD shard) slots of `sup` — written by
+// the level-0 hash itself (k_hash0_pair<..., PT>) or, for skewed / unaligned sets, by a
+// k_scatter_res pass over kh / fp — and this kernel gives each super-tile bps blocks that
+// scatter its records into the slots of their 2^14-position tiles: an LDS counting sort by
+// tile inside the super-tile's window, one reservation atomic per (round, tile, XCD shard),
+// runs written whole (k_scatter_res's scheme).  A record reads 20 B and writes 20 B here, and
+// k_tile_p0 reads it once more: the 40 B per record of the split kernel's scratch are gone.
+template <int kR, int kT>
+__global__ __launch_bounds__(kSB) void k_scatter_p0(const R20* __restrict__ sup, uint64_t sup_scap,
+                                                    const unsigned* __restrict__ scnt, unsigned bps, unsigned tps,
+                                                    R20* __restrict__ bucket, uint64_t bcap, unsigned* __restrict__ tcnt,
+                                                    unsigned long long* __restrict__ flags, LevelState* st) {
+  constexpr int kKPT = kR / kSB;
+  __shared__ uint64_t stage_raw[(kR * 5 + 1) / 2];
+  R20* const stage = reinterpret_cast<R20*>(stage_raw);
+  __shared__ unsigned short stile[kR];
+  __shared__ unsigned cnt[kT];
+  __shared__ unsigned start[kT];
+  __shared__ unsigned cur[kT];
+  __shared__ unsigned s_over;
+  if (st->status & kStStop) return;
+  const unsigned tid = threadIdx.x;
+  const uint64_t words = st->words[0], magic = st->magic[0];
+  const uint64_t T = tiles_of(words, kRegTileMaxBits, 0);
+  if (blockIdx.x == 0 && tid == 0) {
+    st->ntiles[0] = T;
+    st->nchunks[0] = 0;
+  }
+  for (uint64_t t = (uint64_t)blockIdx.x * kSB + tid; t < T; t += (uint64_t)gridDim.x * kSB) flags[t] = 0;
+  const unsigned sidx = blockIdx.x / bps, part = blockIdx.x % bps;
+  const uint64_t t0 = (uint64_t)sidx * tps;
+  if (t0 >= T) return;
+  const unsigned tn = (unsigned)min<uint64_t>(tps, T - t0);
+  if (tn > (unsigned)kT) {
+    if (tid == 0) atomicOr(&st->status, kStGeometry);
+    return;
+  }
+  // the super-tile's records: its kResShards slots back to back (index j)
+  unsigned pre[kResShards + 1];
+  pre[0] = 0;
+#pragma unroll
+  for (int x = 0; x < kResShards; ++x) pre[x + 1] = pre[x] + scnt[sidx * kResShards + x];
+  const uint64_t m = pre[kResShards];
+  const uint64_t lo = m * part / bps, hi = m * (part + 1) / bps;
+  const R20* sbase = sup + (uint64_t)sidx * kResShards * sup_scap;
+  auto src = [&](uint64_t j) -> const R20& {
+    uint64_t o = j;
+#pragma unroll
+    for (int x = 1; x < kResShards; ++x)
+      if (j >= pre[x]) o = (uint64_t)x * sup_scap + (j - pre[x]);
+    return sbase[o];
+  };
+  const uint64_t cap = bcap / T, scap = cap / kResShards;
+  const unsigned shard = blockIdx.x % kResShards;
+  const uint64_t seed = level_seed(0);
+  uint64_t r0 = lo;
+  if (r0 >= hi) return;
+  R20 rr[kKPT];
+#pragma unroll
+  for (int u = 0; u < kKPT; ++u) {
+    const uint64_t j = r0 + (uint64_t)u * kSB + tid;
+    rr[u] = R20{{0, 0, 0, 0, 0}};
+    if (j < hi) rr[u] = src(j);
+  }
+  for (unsigned t = tid; t < kT; t += kSB) cnt[t] = 0;
+  if (tid == 0) s_over = 0;
+  __syncthreads();
+  bool geo = false;
+  for (;;) {
+    unsigned trk[kKPT];  // tile in the window << 13 | rank in the round's run of that tile
+#pragma unroll
+    for (int u = 0; u < kKPT; ++u) {
+      const uint64_t j = r0 + (uint64_t)u * kSB + tid;
+      trk[u] = 0xffffffffu;
+      if (j < hi) {
+        const uint64_t k = (uint64_t)rr[u].w[0] | ((uint64_t)rr[u].w[1] << 32);
+        const uint64_t t = (bb_index(seed, k, words, magic) >> kRegTileMaxBits) - t0;
+        if (t < tn) trk[u] = ((unsigned)t << 13) | atomicAdd(&cnt[t], 1u);
+        else geo = true;
+      }
+    }
+    __syncthreads();
+    constexpr int kTPT = (int)(kT / kSB);
+    unsigned at[kTPT];
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      const unsigned t = (unsigned)q * kSB + tid;
+      const unsigned c = t < tn ? cnt[t] : 0u;
+      at[q] = 0;
+      if (c) at[q] = atomicAdd(&tcnt[(t0 + t) * kResShards + shard], c);
+    }
+    const unsigned tb0 = (unsigned)kTPT * tid;
+    uint64_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) sum += tb0 + q < tn ? cnt[tb0 + q] : 0u;
+    uint64_t tot;
+    uint64_t ex = block_exscan<kSB>(sum, &tot);
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      if (tb0 + q < tn) {
+        start[tb0 + q] = (unsigned)ex;
+        ex += cnt[tb0 + q];
+      }
+    }
+    __syncthreads();  // start[] complete
+#pragma unroll
+    for (int u = 0; u < kKPT; ++u) {
+      if (trk[u] != 0xffffffffu) {
+        const unsigned t = trk[u] >> 13, slot = start[t] + (trk[u] & 8191u);
+        stage[slot] = rr[u];
+        stile[slot] = (unsigned short)t;
+      }
+    }
+    const unsigned mr = (unsigned)tot;
+    r0 += kR;
+    const bool more = r0 < hi;
+#pragma unroll
+    for (int u = 0; u < kKPT; ++u) {
+      const uint64_t j = r0 + (uint64_t)u * kSB + tid;
+      if (j < hi) rr[u] = src(j);
+    }
+#pragma unroll
+    for (int q = 0; q < kTPT; ++q) {
+      const unsigned t = (unsigned)q * kSB + tid;
+      const unsigned c = t < tn ? cnt[t] : 0u;
+      if (c) {
+        if (at[q] + c > scap) s_over = 1;
+        cur[t] = (unsigned)((t0 + t) * cap + shard * scap + at[q]);
+      }
+    }
+    __syncthreads();
+    if (s_over) break;
+    for (unsigned j = tid; j < mr; j += kSB) {
+      const unsigned t = stile[j];
+      bucket[cur[t] + (j - start[t])] = stage[j];
+    }
+    __syncthreads();
+    if (!more) break;
+    for (unsigned t = tid; t < tn; t += kSB) cnt[t] = 0;
+    __syncthreads();
+  }
+  if (geo) atomicOr(&st->status, kStGeometry);
+  if (s_over && tid == 0) atomicOr(&st->status, kStOverflow | kStResOverflow);
 }
 
 // --------------------------------------------------------------------- tile --------
@@ -2360,6 +2506,356 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kWaves))) vo
   if (bad) atomicOr(&st->status, kStRank);
 }
 
+// ----------------------------------------------------- P0 level-0 register tiles ------
+// Level 0's 2^14-position tiles after k_scatter_p0 (R20 records, identity positions): one
+// persistent 1024-thread workgroup per CU takes tiles by ticket, nine records per thread in
+// registers, and overlaps each tile's memory traffic with LDS phases of its own:
+//   mark      A / C of tile t in LDS (its records arrived during the previous tile's work)
+//   finalize  A & ~C -> LDS + global bits, per-word rank prefix; the tile's aggregate is
+//             published for the look-back at once, its collided records' slots reserved
+//   classify  settled (f, i) -> the LDS stage by in-tile rank; collided -> the next list
+//   prefetch  the next tile's records into the registers just freed (its ticket was taken
+//             and its slot fills read during the mark)
+//   resolve   tile t's look-back, well after its predecessors published: its rank base
+//   write     the stage -> fp_out / pos_out[base + rank] in runs, beside the prefetch
+// k_tile_reg keeps one tile per CU and leaves HBM idle through every finalize, look-back and
+// output phase.  A tile holding more records than the registers (never at load 1/2: 11
+// sigma) or more settled keys than the stage (30 sigma) is finished from the bucket with
+// its base resolved first.
+constexpr int kP0T = 768;
+constexpr int kP0R = 12;                                  // 9216 >= 8192 + 11 sigma
+constexpr unsigned kP0Stage = 6144;                       // settled ranks staged (mean ~4965)
+constexpr unsigned kP0W32 = 1u << (kRegTileMaxBits - 5);  // A / C words of a tile
+
+__device__ __forceinline__ void lb_publish(unsigned long long* flags, uint64_t t, uint64_t pop) {
+  __hip_atomic_store(&flags[t], (t == 0 ? kFlagInc : kFlagAgg) | pop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// look_back_wave without its first store (the aggregate went out with lb_publish)
+__device__ __forceinline__ uint64_t lb_resolve(unsigned long long* flags, uint64_t t, uint64_t pop, LevelState* st) {
+  if (t == 0) return 0;
+  const unsigned lane = lane_id();
+  uint64_t excl = 0;
+  int64_t top = (int64_t)t - 1;
+  uint64_t spins = 0;
+  while (top >= 0) {
+    const int64_t q = top - (int64_t)lane;
+    unsigned long long v = kFlagInc;
+    if (q >= 0) v = __hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t not_ready = __ballot((v & ~kFlagVal) == 0);
+    const uint64_t inc = __ballot((v & ~kFlagVal) == kFlagInc);
+    const uint64_t upto = inc ? (inc & (~inc + 1)) * 2 - 1 : ~0ull;
+    if (not_ready & upto) {
+      if (++spins > (1ull << 24)) {
+        if (lane == 0) atomicOr(&st->status, kStLookback);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    uint64_t part = ((upto >> lane) & 1ull) && q >= 0 ? (v & kFlagVal) : 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d);
+    excl += part;
+    if (inc) break;
+    top -= 64;
+  }
+  if (lane == 0) __hip_atomic_store(&flags[t], kFlagInc | (excl + pop), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
+__global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket, uint64_t bucket_cap,
+                                                  const unsigned* __restrict__ tcnt, unsigned long long* flags,
+                                                  uint64_t* __restrict__ bits, Rec* __restrict__ next,
+                                                  uint64_t* __restrict__ fp_out, uint64_t* __restrict__ pos_out,
+                                                  LevelState* st, uint64_t pos_base) {
+  __shared__ uint64_t sf[kP0Stage];
+  __shared__ uint32_t si[kP0Stage];
+  __shared__ uint32_t sA[kP0W32], sC[kP0W32];
+  __shared__ unsigned s_wc[kP0T / 64];
+  __shared__ unsigned s_cnt[2][kResShards];
+  __shared__ unsigned long long s_t[2], s_b0, s_excl;
+  __shared__ unsigned s_late;
+  if (!level_active(0, st)) return;
+  const uint64_t N = st->out_cap;
+  const bool out_on = level_out_on(st, 0);
+  const uint64_t words = st->words[0], magic = st->magic[0];
+  const uint64_t T = st->ntiles[0];
+  const uint64_t w32_level = 2 * words;
+  uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[0]);
+  const uint64_t seed = level_seed(0);
+  const uint64_t lvl_base = st->lvl_base[0];
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint64_t lt = lanemask_lt();
+  const uint64_t cap = bucket_cap / T, shcap = cap / kResShards;
+  constexpr unsigned kCntT = kP0T - kResShards;  // the last wave's lanes read a tile's slot fills
+  // a tile's slot fills as wave-uniform exclusive prefixes (scalar registers)
+  struct Fills {
+    unsigned pre[kResShards];
+    unsigned n;
+  };
+  auto fills = [&](const unsigned* c) {
+    Fills F;
+    unsigned a = 0;
+#pragma unroll
+    for (int x = 0; x < kResShards; ++x) {
+      F.pre[x] = a;
+      a += __builtin_amdgcn_readfirstlane(c[x]);
+    }
+    F.n = a;
+    return F;
+  };
+  // tile t's record j as (k, f, key index)
+  auto rec = [&](uint64_t t, const Fills& F, unsigned j, uint64_t& k_, uint64_t& f_, uint32_t& p_) {
+    uint32_t o = j;
+#pragma unroll
+    for (int x = 1; x < kResShards; ++x)
+      if (j >= F.pre[x]) o = (uint32_t)(x * shcap) + (j - F.pre[x]);
+    const R20* q = bucket + t * cap + o;
+    const R20 r = *q;
+    k_ = (uint64_t)r.w[0] | ((uint64_t)r.w[1] << 32);
+    f_ = (uint64_t)r.w[2] | ((uint64_t)r.w[3] << 32);
+    p_ = r.w[4];
+  };
+  uint64_t k[kP0R], f[kP0R];
+  uint32_t p[kP0R];
+  auto load_regs = [&](uint64_t t, const Fills& F, unsigned me) {
+#pragma unroll
+    for (int r = 0; r < kP0R; ++r) {
+      const unsigned j = (unsigned)r * kP0T + me;
+      k[r] = f[r] = 0;
+      p[r] = 0;
+      if (j < F.n) rec(t, F, j, k[r], f[r], p[r]);
+    }
+  };
+  if (tid == 0) s_t[0] = atomicAdd(&st->ticket[0], 1ull);
+  for (unsigned w = tid; w < kP0W32; w += kP0T) {
+    sA[w] = 0;
+    sC[w] = 0;
+  }
+  __syncthreads();
+  uint64_t t = s_t[0];
+  if (tid >= kCntT && t < T) s_cnt[0][tid - kCntT] = tcnt[t * kResShards + (tid - kCntT)];
+  __syncthreads();
+  int cb = 0;
+  Fills F = fills(s_cnt[0]);
+  if (t < T && F.n <= (unsigned)kP0R * kP0T) load_regs(t, F, tid);
+  bool bad = false;
+  while (t < T) {
+    const int nb = cb ^ 1;
+    const unsigned nk = F.n;
+    // the thread index, opaque per iteration: per-thread record indices and addresses are
+    // recomputed each tile instead of hoisted out of the loop and kept live (they spilled)
+    unsigned me = tid;
+    asm volatile("" : "+v"(me));
+    const bool fits = nk <= (unsigned)kP0R * kP0T;
+    const uint64_t tbase = t << kRegTileMaxBits;
+    if (tid == 0) s_t[nb] = atomicAdd(&st->ticket[0], 1ull);
+    // ---- mark
+    unsigned loc2[(kP0R + 1) / 2];
+#define LOC(r) ((loc2[(r) >> 1] >> (((r) & 1) * 16)) & 0xffffu)
+#pragma unroll
+    for (int r = 0; r < (kP0R + 1) / 2; ++r) loc2[r] = 0;
+    if (fits) {
+#pragma unroll
+      for (int r = 0; r < kP0R; ++r) {
+        const unsigned j = (unsigned)r * kP0T + me;
+        if (j < nk) {
+          const unsigned x = (unsigned)(bb_index(seed, k[r], words, magic) - tbase);
+          loc2[r >> 1] |= x << ((r & 1) * 16);
+          const uint32_t bit = 1u << (x & 31);
+          const uint32_t old = atomicOr(&sA[x >> 5], bit);
+          if (old & bit) atomicOr(&sC[x >> 5], bit);
+        }
+      }
+    } else {
+      #pragma unroll 1
+      for (unsigned j = me; j < nk; j += kP0T) {
+        uint64_t jk, jf;
+        uint32_t jp;
+        rec(t, F, j, jk, jf, jp);
+        const unsigned x = (unsigned)(bb_index(seed, jk, words, magic) - tbase);
+        const uint32_t bit = 1u << (x & 31);
+        const uint32_t old = atomicOr(&sA[x >> 5], bit);
+        if (old & bit) atomicOr(&sC[x >> 5], bit);
+      }
+    }
+    __syncthreads();  // A / C complete; the next ticket is in s_t[nb]
+    const uint64_t tn = s_t[nb];
+    if (tid >= kCntT && tn < T) s_cnt[nb][tid - kCntT] = tcnt[tn * kResShards + (tid - kCntT)];
+    // ---- finalize: A & ~C -> LDS + global bits; per-word rank prefix into C
+    uint64_t cntw = 0;
+    uint32_t v = 0;
+    if (tid < kP0W32) {
+      v = sA[tid] & ~sC[tid];
+      sA[tid] = v;
+      const uint64_t gw = t * kP0W32 + tid;
+      if (gw < w32_level) g32[gw] = v;
+      cntw = __popc(v);
+    }
+    uint64_t pop;
+    const uint64_t run = block_exscan<kP0T>(cntw, &pop);
+    if (tid < kP0W32) sC[tid] = (uint32_t)run;
+    if (tid == 0) {
+      lb_publish(flags, t, pop);
+      s_late = 0;
+    }
+    if (tid == 64) s_b0 = nk > pop ? atomicAdd(&st->n[1], (unsigned long long)(nk - pop)) : 0ull;
+    __syncthreads();  // rank prefix, slot reservation
+    // ---- classify: settled -> stage[rank]; collided counted per wave
+    unsigned wc = 0;
+    uint32_t late = 0;
+    if (fits) {
+#pragma unroll
+      for (int r = 0; r < kP0R; ++r) {
+        const unsigned j = (unsigned)r * kP0T + me;
+        bool redo = false;
+        if (j < nk) {
+          const unsigned x = LOC(r);
+          const uint32_t wv = sA[x >> 5];
+          const uint32_t bit = 1u << (x & 31);
+          if (wv & bit) {
+            const unsigned rank = sC[x >> 5] + __popc(wv & (bit - 1));
+            if (rank < kP0Stage) {
+              sf[rank] = f[r];
+              si[rank] = p[r];
+            } else {
+              late |= 1u << r;
+            }
+          } else {
+            redo = true;
+          }
+        }
+        wc += __popcll(__ballot(redo));
+      }
+      if (late) s_late = 1;
+    } else {
+      #pragma unroll 1
+      for (unsigned jb = wave * 64; jb < nk; jb += kP0T) {
+        const unsigned j = jb + lane;
+        bool redo = false;
+        if (j < nk) {
+          uint64_t jk, jf;
+          uint32_t jp;
+          rec(t, F, j, jk, jf, jp);
+          const unsigned x = (unsigned)(bb_index(seed, jk, words, magic) - tbase);
+          redo = !((sA[x >> 5] >> (x & 31)) & 1u);
+        }
+        wc += __popcll(__ballot(redo));
+      }
+    }
+    if (lane == 0) s_wc[wave] = wc;
+    __syncthreads();
+    // ---- collided records -> next level
+    {
+      uint64_t o = s_b0;
+      #pragma unroll 1
+      for (unsigned w = 0; w < wave; ++w) o += s_wc[w];
+      if (fits) {
+#pragma unroll
+        for (int r = 0; r < kP0R; ++r) {
+          const unsigned j = (unsigned)r * kP0T + me;
+          const unsigned x = LOC(r);
+          const bool redo = j < nk && !((sA[x >> 5] >> (x & 31)) & 1u);
+          const uint64_t m = __ballot(redo);
+          if (redo) next[o + __popcll(m & lt)] = Rec{k[r], f[r], pos_base + p[r]};
+          o += __popcll(m);
+        }
+      } else {
+        #pragma unroll 1
+        for (unsigned jb = wave * 64; jb < nk; jb += kP0T) {
+          const unsigned j = jb + lane;
+          bool redo = false;
+          uint64_t jk = 0, jf = 0;
+          uint32_t jp = 0;
+          if (j < nk) {
+            rec(t, F, j, jk, jf, jp);
+            const unsigned x = (unsigned)(bb_index(seed, jk, words, magic) - tbase);
+            redo = !((sA[x >> 5] >> (x & 31)) & 1u);
+          }
+          const uint64_t m = __ballot(redo);
+          if (redo) next[o + __popcll(m & lt)] = Rec{jk, jf, pos_base + jp};
+          o += __popcll(m);
+        }
+      }
+    }
+    // ---- the rare tiles: base first, then the records the stage does not hold
+    const bool early = !fits || s_late;
+    if (early) {
+      if (wave == 0) {
+        const uint64_t excl = lb_resolve(flags, t, pop, st);
+        if (lane == 0) {
+          if (t == T - 1) st->lvl_base[1] = lvl_base + excl + pop;
+          s_excl = excl;
+        }
+      }
+      __syncthreads();
+      const uint64_t base = lvl_base + s_excl;
+      const bool wr = out_on && base + pop <= N;
+      if (fits) {
+#pragma unroll
+        for (int r = 0; r < kP0R; ++r)
+          if (wr && ((late >> r) & 1u)) {
+            const unsigned x = LOC(r);
+            const uint32_t wv = sA[x >> 5];
+            const uint64_t q = base + sC[x >> 5] + __popc(wv & ((1u << (x & 31)) - 1));
+            fp_out[q] = f[r];
+            pos_out[q] = pos_base + p[r];
+          }
+      } else {
+        #pragma unroll 1
+        for (unsigned j = me; wr && j < nk; j += kP0T) {
+          uint64_t jk, jf;
+          uint32_t jp;
+          rec(t, F, j, jk, jf, jp);
+          const unsigned x = (unsigned)(bb_index(seed, jk, words, magic) - tbase);
+          const uint32_t wv = sA[x >> 5];
+          const uint32_t bit = 1u << (x & 31);
+          if (wv & bit) {
+            const uint64_t q = base + sC[x >> 5] + __popc(wv & (bit - 1));
+            fp_out[q] = jf;
+            pos_out[q] = pos_base + jp;
+          }
+        }
+      }
+    }
+#undef LOC
+    __syncthreads();  // s_cnt[nb] visible; every register record consumed
+    // ---- prefetch the next tile's records
+    const Fills Fn = fills(s_cnt[nb]);
+    if (tn < T && Fn.n <= (unsigned)kP0R * kP0T) load_regs(tn, Fn, me);
+    // ---- resolve the look-back, write the stage
+    if (!early) {
+      if (wave == 0) {
+        const uint64_t excl = lb_resolve(flags, t, pop, st);
+        if (lane == 0) {
+          if (t == T - 1) st->lvl_base[1] = lvl_base + excl + pop;
+          s_excl = excl;
+        }
+      }
+      __syncthreads();
+    }
+    const uint64_t base = lvl_base + s_excl;
+    if (base + pop > N && out_on) bad = true;
+    if (fits && out_on && base + pop <= N) {
+      const unsigned ns = (unsigned)min<uint64_t>(pop, kP0Stage);
+      #pragma unroll 1
+      for (unsigned i = me; i < ns; i += kP0T) {
+        fp_out[base + i] = sf[i];
+        pos_out[base + i] = pos_base + si[i];
+      }
+    }
+    for (unsigned w = tid; w < kP0W32; w += kP0T) {
+      sA[w] = 0;
+      sC[w] = 0;
+    }
+    __syncthreads();  // stage read, A / C cleared before the next mark
+    t = tn;
+    F = Fn;
+    cb = nb;
+  }
+  if (bad) atomicOr(&st->status, kStRank);
+}
+
 // ------------------------------------------------------------ mid-size levels --------
 // Levels between the single-workgroup tail (<= kTailKeys keys) and the binned pipeline's
 // scatter + tile kernels, where the latter pay mostly fixed latency (two launches, a
@@ -3234,6 +3730,27 @@ void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s) {
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s) {
   k_bin_tail<<<1, kTailT, 0, s>>>(first_level, big_launched, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out, b.pos_out,
                                   b.st, b.tile_prof);
+}
+
+// ---- P0: level 0 through super-tiles into 2^14-position register tiles ----------------
+// The records' first partition, into the super-tiles' slots of p.sup, when the level-0 hash
+// did not write them there (kh / fp from k_hash_count0 or k_hash_skew): k_scatter_res with
+// the super-tiles as its tiles (tile = (position >> 14) / tps, exact by the reciprocal).
+void launch_p0_partition(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
+  k_scatter_res<5120, 1024, 2, true><<<256, kSB, 0, s>>>(0, nullptr, b.kh, b.fp, nullptr, b.pos_base, p.scnt,
+                                                        reinterpret_cast<Rec*>(p.sup), p.sup_cap, p.flags, b.st,
+                                                        kRegTileMaxBits, b.cap_words, nullptr, 0, 0, p.tps);
+}
+
+void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
+  const unsigned bps = std::max(1u, 256u / p.S);
+  k_scatter_p0<5120, 1024><<<p.S * bps, kSB, 0, s>>>(p.sup, p.sup_cap / ((uint64_t)p.S * kResShards), p.scnt, bps,
+                                                     p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st);
+}
+
+void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
+  k_tile_p0<<<256, kP0T, 0, s>>>(p.bucket, p.bucket_cap, p.tcnt, p.flags, b.bits, b.list[0], b.fp_out, b.pos_out, b.st,
+                                 b.pos_base);
 }
 
 }  // namespace s3imph

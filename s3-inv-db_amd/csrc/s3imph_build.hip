@@ -105,6 +105,8 @@ void free_workspace(s3imph_ctx* c) {
   dfree(c->block_sums); dfree(c->d_st);
   dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
   dfree(c->tcnt);
+  dfree(c->p0_tcnt); dfree(c->p0_flags); dfree(c->p0_scnt);
+  c->p0_tiles = 0;
   dfree(c->tile_prof);
   dfree(c->hist); dfree(c->hoff); dfree(c->tile_start); dfree(c->scan_sums); dfree(c->flags); dfree(c->sflags);
   if (c->h_st) (void)hipHostFree(c->h_st);
@@ -426,10 +428,55 @@ bool hash_only_knob() {
   return on;
 }
 
+// P0 geometry and buffers for level 0 of n keys (identity positions): T 2^14-position tiles
+// in S super-tiles of tps; the super-tile slots live in list[1] (unused until level 1's tile
+// pass writes its collided records there), the tile slots in the bucket, both as R20.
+P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, hipStream_t s) {
+  const uint64_t T = tiles_of(level_words(n), kRegTileMaxBits, 0);
+  P0Bufs p;
+  p.S = (unsigned)((T + kP0MaxTps - 1) / kP0MaxTps);
+  p.tps = (unsigned)((T + p.S - 1) / p.S);
+  if (T > c->p0_tiles) {
+    dalloc(c->p0_tcnt, T * kResShards);
+    dalloc(c->p0_flags, T);
+    if (!c->p0_scnt) dalloc(c->p0_scnt, 256 * kResShards);
+    c->p0_tiles = T;
+  }
+  p.sup = reinterpret_cast<R20*>(c->list[1]);
+  p.sup_cap = c->cap_keys * sizeof(Rec) / sizeof(R20);
+  p.scnt = c->p0_scnt;
+  p.bucket = reinterpret_cast<R20*>(c->bucket);
+  p.bucket_cap = c->bucket_cap * sizeof(Rec) / sizeof(R20);
+  p.tcnt = c->p0_tcnt;
+  p.flags = c->p0_flags;
+  HIPCHECK(hipMemsetAsync(p.tcnt, 0, T * kResShards * sizeof(unsigned), s));
+  HIPCHECK(hipMemsetAsync(p.scnt, 0, (uint64_t)p.S * kResShards * sizeof(unsigned), s));
+  return p;
+}
+
 void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
   const BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
   const double q = 1.0 - std::exp(-0.5);
+  if (!conservative && c->p0 && !pos && n <= kP0MaxKeys && !hash_only_knob() &&
+      tiles_of(level_words(n), kRegTileMaxBits, 0) > kP0MinTiles) {
+    // level 0 in 2^14-position register tiles through super-tiles (s3imph_internal.h, P0)
+    const P0Bufs p = p0_bufs(c, n, s);
+    const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
+    launch_init_state(c->d_st, n, n, s, offsets);
+    ev_mark(c, s, "init");
+    launch_binned_count(0, blob, offsets, n, b, g0, 256, s, false);
+    ev_mark(c, s, "hash_count0");
+    launch_p0_partition(b, p, s);
+    ev_mark(c, s, "part0");
+    launch_p0_scatter(b, p, s);
+    ev_mark(c, s, "scatter0");
+    launch_p0_tile(b, p, s);
+    ev_mark(c, s, "tile0");
+    fault_dup_record(c, c->list[0], s);
+    enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
+    return;
+  }
   const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
   launch_init_state(c->d_st, n, n, s, offsets);
   ev_mark(c, s, "init");
@@ -1990,6 +2037,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     c->route_self = std::getenv("S3IMPH_DIST_ROUTE_SELF") != nullptr;  // A/B knob: list-level geometry from 1.1x bounds
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     c->fault_dup = std::getenv("S3IMPH_FAULT_DUP_REC") != nullptr;
+    if (const char* m = std::getenv("S3IMPH_P0")) c->p0 = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_SCAT_CFG")) c->scat_cfg = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_SKEW_CFG")) c->skew_cfg = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);

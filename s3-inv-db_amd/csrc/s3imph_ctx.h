@@ -216,6 +216,14 @@ struct s3imph_ctx {
   int scat_cfg = 2;         // S3IMPH_SCAT_CFG: reservation-scatter forms (launch_binned_scatter_res)
   int skew_cfg = 2;         // S3IMPH_SKEW_CFG: skewed-length hash block / group shape (launch_hash_skew)
   bool loose_geom = false;  // S3IMPH_LOOSE_GEOM: list levels sized from 1.1x (not 1.02x + 6 sigma) bounds
+  // P0 level 0 (s3imph_internal.h): tile slot fills / look-back words for up to p0_tiles
+  // 2^14-position tiles, super-tile slot fills; made on first use.  S3IMPH_P0=0 keeps such
+  // sets on the split kernel (A/B knob).
+  int p0 = 1;
+  uint64_t p0_tiles = 0;
+  unsigned* p0_tcnt = nullptr;
+  unsigned long long* p0_flags = nullptr;
+  unsigned* p0_scnt = nullptr;
   bool debug = false;
   bool fault_dup = false;   // S3IMPH_FAULT_DUP_REC: test hook, duplicates a record mid-build (fault_dup_record)
   unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps

@@ -222,6 +222,32 @@ struct BinBuffers {
   int skew_cfg = 2;                     // k_hash_skew block / group shape (launch_hash_skew)
 };
 uint64_t split_scratch_records();  // sub-tile segments of the split big-tile kernel
+
+// ---- P0: level 0 of a big set in 2^14-position register tiles (s3imph_binned.hip) ----
+// Sets whose level 0 has more than kP0MinTiles 2^14-position tiles (the ones the split
+// kernel took) with identity positions: the level's tiles are grouped into S super-tiles of
+// tps tiles (tps <= kP0MaxTps); records (R20: k, f, key index) go to per-(super-tile, XCD
+// shard) slots of `sup`, then to per-(tile, shard) slots of `bucket`, then k_tile_reg.
+constexpr uint64_t kP0MinTiles = 2048;
+constexpr uint64_t kP0MaxTps = 1024;
+constexpr uint64_t kP0MaxKeys = 1ull << 31;  // bucket slot indices stay below 2^32
+// A level-0 record with an identity position: k (2 dwords), f (2), key index i (p = pos_base + i).
+struct R20 {
+  uint32_t w[5];
+};
+struct P0Bufs {
+  unsigned S = 0, tps = 0;     // super-tiles, 2^14 tiles per super-tile
+  R20* sup = nullptr;          // super-tile slots (S x kResShards slots of sup_cap / (S kResShards) records)
+  uint64_t sup_cap = 0;        // R20 records in sup
+  unsigned* scnt = nullptr;    // super-tile slot fills (S x kResShards), zeroed before the build
+  R20* bucket = nullptr;       // tile slots (T x kResShards)
+  uint64_t bucket_cap = 0;     // R20 records in bucket
+  unsigned* tcnt = nullptr;    // tile slot fills (T x kResShards), zeroed before the build
+  unsigned long long* flags = nullptr;  // look-back words, one per tile
+};
+void launch_p0_partition(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
+void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
+void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
 void binned_set_lds_limits();
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s, bool histogram = true);

@@ -492,9 +492,9 @@ def test_level0_ragged_and_c2_custom_positions(s3, oracle_lib, ctx, n, kind, avg
 
 
 def test_big_tiles_bit_exact(s3, oracle_lib):
-    """70M keys: level 0 needs 2^16-position tiles to stay within 4096 tiles, so it runs
-    the generic tile kernel with only the in-tile positions cached in LDS; level 1
-    (2^15-position tiles) the fully cached one.  Bit-exact with the oracle."""
+    """70M keys, short (avg 12 B): level 0 (8.5k tiles of 2^14 positions) through the P0
+    super-tiles and the pipelined register tiles, level 1 on the split kernel.  Bit-exact
+    with the oracle."""
     c = s3.DeviceBuilder(0)
     try:
         n = 70_000_000
@@ -506,6 +506,32 @@ def test_big_tiles_bit_exact(s3, oracle_lib):
         assert np.array_equal(gfp, fp) and np.array_equal(gpo, po)
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("n,unaligned", [(16_800_000, False), (20_000_000, True)])
+def test_p0_level0_bit_exact(s3, oracle_lib, n, unaligned):
+    """Level 0 with more than 2048 tiles of 2^14 positions (P0, s3imph_internal.h): the
+    records go to super-tile slots, then to their tiles' slots, then the pipelined register
+    tiles (k_tile_p0).  Just past the threshold (2051 tiles), and an unaligned blob whose
+    level-0 hash is k_hash_count0 (kh / fp, then the partition pass).  Bit-exact."""
+    c = s3.DeviceBuilder(0)
+    try:
+        blob, offs = s3.gen_keys(0, 19, 20, 0, n)
+        blob = blob[: int(offs[-1])]
+        st, fp, po, mph = oracle_lib.build_mt(blob, offs, threads=16)
+        assert st == 0
+        if unaligned:
+            gfp, gpo, gmph, _ = _device_build(s3, c, np.concatenate([np.frombuffer(b"q", np.uint8), blob]), offs + 1)
+        else:
+            gfp, gpo, gmph, _ = _device_build(s3, c, blob, offs)
+        assert gmph == mph and np.array_equal(gfp, fp) and np.array_equal(gpo, po)
+    finally:
+        c.close()
+
+
+def test_p0_off_split_kernel_bit_exact(s3, oracle_lib):
+    """S3IMPH_P0=0 (A/B knob): the same big level 0 on the split kernel instead: bit-exact."""
+    _parity_subprocess({"S3IMPH_P0": "0"}, [(40_000_000, 0, 12)])
 
 
 def test_big_tiles_counted_path(s3, oracle_lib):
