@@ -53,6 +53,12 @@ def stage_alg_bytes(stage: str, n: int, key_bytes: int, info: dict) -> int | Non
     settled = math.exp(-0.5)
     if stage == "hash_count0":  # key bytes + offsets read once; kh + fp written once
         return key_bytes + 8 * (n + 1) + 16 * n
+    if stage == "hash_part0":   # P0: key bytes + offsets read once; R20 record (k, f, index) to its super-tile
+        return key_bytes + 8 * (n + 1) + 20 * n
+    if stage == "scatter0_p0":  # P0: R20 record read from its super-tile slot, written to its 2^14 tile's slot
+        return 20 * n + 20 * n
+    if stage == "tile0_p0":     # P0: R20 read once; fp_out/pos_out or the next-level record; bits
+        return int(20 * n + 16 * settled * n + 24 * (1 - settled) * n + n // 4)
     if stage == "hash_route0":  # sharded build: key bytes + offsets read; (kh, fp, pos) records written once
         return key_bytes + 8 * (n + 1) + 24 * n
     if stage == "scatter0":     # kh + fp read, (kh, fp, pos) record written to its tile bucket
@@ -251,7 +257,7 @@ def main() -> None:
         hbm = {"achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS}
         result["roofline"] = {"kernel": dom, "bound": "hbm", **hbm, "traffic": traffic, "alg_bytes": alg,
                               "avg_ms": dom_ms, "timed_region_events": dom in timed_stages}
-        if dom in ("hash_count0", "hash_route0"):
+        if dom in ("hash_count0", "hash_route0", "hash_part0"):
             # The hash is bounded by VALU before HBM: every key byte is one FNV-1a + FNV-1 step
             # (two 64-bit multiplies by the FNV prime); tools/ubench_fnv.hip measured the chip's
             # ceiling for that step from registers.  Its HBM rate rides

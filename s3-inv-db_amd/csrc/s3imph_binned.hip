@@ -248,6 +248,16 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
   if (zero) atomicOr(&st->status, kStKeyZero);
 }
 
+// R20 (s3imph_internal.h): a level-0 record with an identity position, in five dwords.
+__device__ __forceinline__ R20 r20_make(uint64_t k, uint64_t f, uint32_t i) {
+  return R20{{(uint32_t)k, (uint32_t)(k >> 32), (uint32_t)f, (uint32_t)(f >> 32), i}};
+}
+__device__ __forceinline__ void r20_split(const R20& r, uint64_t pos_base, uint64_t& k, uint64_t& f, uint64_t& p) {
+  k = (uint64_t)r.w[0] | ((uint64_t)r.w[1] << 32);
+  f = (uint64_t)r.w[2] | ((uint64_t)r.w[3] << 32);
+  p = pos_base + r.w[4];
+}
+
 // ------------------------------------------------ level-0 hash, LDS-staged ----------
 // FNV-1a + FNV-1 of every key (StreamingMPHFBuilder.Add, mphf_streaming.go:73,80;
 // mphf.go:349-369) for near-uniform key lengths (st->skew == 0; skewed sets go to
@@ -275,7 +285,19 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
 // the kernel's limit: same-address device atomics serialise at ~12 ns each
 // (tools/ubench_atomics.hip); 1024-key rounds (512 threads, 64 KiB windows) halve them
 // but measured slower (C3 3.02 -> 3.51 ms: register spills, the larger rounds' tail).
-template <int NT, int BB, bool PF, bool RT = false>
+//
+// PT (P0 level 0, s3imph_internal.h): the same in-LDS counting sort, by SUPER-TILE (the
+// record's level-0 position >> 14, divided by tps), and the runs go to the super-tiles'
+// per-XCD-shard slots as R20 records (k, f, key index) — the first of P0's two partition
+// passes rides on the hash, whose HBM share is half idle, instead of a k_scatter_res pass
+// that reads kh / fp back (16 B per key written and read again).
+struct P0Part {
+  R20* sup;
+  uint64_t sup_scap;  // records per (super-tile, shard) slot
+  unsigned* scnt;     // slot fills
+  unsigned tps, S;
+};
+template <int NT, int BB, bool PF, bool RT = false, bool PT = false>
 __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(const uint8_t* __restrict__ blob,
                                                   const uint64_t* __restrict__ offsets, uint64_t n,
                                                   uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
@@ -283,7 +305,8 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
                                                   unsigned long long* __restrict__ sflags, LevelState* st,
                                                   unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt,
                                                   unsigned long long* __restrict__ prof = nullptr,
-                                                  Route0 rt = Route0{}) {
+                                                  Route0 rt = Route0{}, P0Part pt = P0Part{}) {
+  static_assert(!(RT && PT), "route or partition, not both");
   unsigned long long pt0 = __builtin_amdgcn_s_memtime(), ph = 0, pw = 0;  // debug phase clock
   const unsigned long long prt0 = __builtin_amdgcn_s_memrealtime();
   constexpr int G = 2 * NT;                    // keys per round
@@ -297,8 +320,8 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   __shared__ unsigned s_cnt[NW];
   // RT: per-owner counts / run starts of the round, the owners' reserved run bases (record
   // offsets into self_dst or send), the block's sticky overflow flag
-  __shared__ unsigned r_cnt[RT ? kMaxRanks : 1], r_start[RT ? kMaxRanks : 1];
-  __shared__ uint64_t r_base[RT ? kMaxRanks : 1];
+  __shared__ unsigned r_cnt[RT || PT ? kMaxRanks : 1], r_start[RT || PT ? kMaxRanks : 1];
+  __shared__ uint64_t r_base[RT || PT ? kMaxRanks : 1];
   __shared__ unsigned r_over;
   if (st->skew) return;  // k_hash_count0 hashes skewed sets (and clears the tile state)
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -306,6 +329,13 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   // RT: level 0's geometry and owner ranges; this rank's own-record shift (records received
   // for earlier key chunks sit before its own ones)
   uint64_t r_words = 0, r_magic = 0, r_S = 1, r_mS = 0, r_rb = 0;
+  uint32_t p_mul = 0;
+  if (PT) {
+    if (tid == 0) r_over = 0;
+    r_words = st->words[0];
+    r_magic = st->magic[0];
+    p_mul = 0xffffffffu / pt.tps + 1;  // exact for (position >> 14) < 2^18, tps <= 2^14
+  }
   if (RT) {
     if (tid == 0) r_over = 0;
     r_words = st->words[0];
@@ -378,7 +408,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
       }
     }
     for (unsigned b = tid; b < kLB; b += NT) lcnt[b] = 0;
-    if (RT && tid < kMaxRanks) r_cnt[tid] = 0;
+    if ((RT || PT) && tid < kMaxRanks) r_cnt[tid] = 0;
     const uint64_t rw = wlo;
     const uint64_t t_b0[2] = {kb0[0], kb0[1]}, t_b1[2] = {kb1[0], kb1[1]};
     // keys whose bytes all lie in the window: a prefix of the round (offsets ascend)
@@ -449,9 +479,10 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
       if (tid == 0) {
         uint64_t a, b;
         fnv_both_pf(blob, t_b0[0], t_b1[0], a, b);
-        if (RT) {
+        if (RT || PT) {
           ra[0] = a;
           rb[0] = b;
+          rj[0] = 0;
           rv[0] = true;
         } else {
           kh[r0] = a;
@@ -475,7 +506,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
         }
       }
     }
-    if (!RT && !alone) {  // ---- (kh, fp) back to key order through LDS, then coalesced stores
+    if (!RT && !PT && !alone) {  // ---- (kh, fp) back to key order through LDS, then coalesced stores
       static_assert(2 * G * sizeof(uint64_t) <= sizeof(sw), "the result stage aliases the byte window");
       __syncthreads();  // every lane has hashed: the window is free
       uint64_t* sa = sw;
@@ -539,6 +570,52 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
         }
       }
     }
+    if (PT) {  // ---- the round's R20 records to their super-tiles' slots (this block's XCD shard)
+      static_assert(G * sizeof(R20) + G <= sizeof(sw), "the partition stage aliases the byte window");
+      unsigned od[2] = {0, 0}, ork[2] = {0, 0};
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (rv[h]) {
+          const uint64_t x = bb_index(level_seed(0), ra[h], r_words, r_magic);
+          od[h] = __umulhi((uint32_t)(x >> kRegTileMaxBits), p_mul);
+          if (od[h] >= pt.S) od[h] = pt.S - 1;  // unreachable: positions < 64 words
+          ork[h] = atomicAdd(&r_cnt[od[h]], 1u);
+        }
+      __syncthreads();  // every lane has hashed (the window is free) and counted
+      if (tid < 64) {
+        const unsigned c = tid < pt.S ? r_cnt[tid] : 0u;
+        unsigned x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const unsigned y = __shfl_up(x, o);
+          if (tid >= (unsigned)o) x += y;
+        }
+        r_start[tid] = x - c;
+        if (c) {
+          const unsigned slot = tid * kResShards + blockIdx.x % kResShards;
+          const unsigned at = atomicAdd(&pt.scnt[slot], c);
+          if (at + c > pt.sup_scap) r_over = 1;
+          r_base[tid] = (uint64_t)slot * pt.sup_scap + at;
+        }
+      }
+      __syncthreads();
+      R20* stg = reinterpret_cast<R20*>(sw);
+      unsigned char* sdst = reinterpret_cast<unsigned char*>(stg + G);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (rv[h]) {
+          const unsigned slot = r_start[od[h]] + ork[h];
+          stg[slot] = r20_make(ra[h], rb[h], (uint32_t)(r0 + rj[h]));
+          sdst[slot] = (unsigned char)od[h];
+        }
+      __syncthreads();
+      if (!r_over) {
+        for (unsigned j = tid; j < m; j += NT) {
+          const unsigned o = sdst[j];
+          pt.sup[r_base[o] + (j - r_start[o])] = stg[j];
+        }
+      }
+    }
     unsigned long long ptb = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (!more) break;
     __syncthreads();  // every lane is done with sw / sidx before the next round overwrites them
@@ -561,6 +638,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   }
   if (zero) atomicOr(&st->status, kStKeyZero);
   if (RT && tid == 0 && r_over) atomicOr(&st->status, kStRouteOverflow);
+  if (PT && tid == 0 && r_over) atomicOr(&st->status, kStOverflow | kStResOverflow);
 }
 
 // ------------------------------------------- level-0 hash, skewed key lengths --------
@@ -1052,14 +1130,6 @@ constexpr unsigned kSplitSubBitsDev = 14;  // = kSplitSubBits (sub-tile of the s
 // instead of Rec's 24, so the level-0 scatter writes and the split kernel's bucket reads,
 // scratch writes and scratch reads move 4 bytes less per key (1.6 GB less at C3).  Only
 // the reservation scatter and the split big-tile kernel use it; the next list stays Rec.
-__device__ __forceinline__ R20 r20_make(uint64_t k, uint64_t f, uint32_t i) {
-  return R20{{(uint32_t)k, (uint32_t)(k >> 32), (uint32_t)f, (uint32_t)(f >> 32), i}};
-}
-__device__ __forceinline__ void r20_split(const R20& r, uint64_t pos_base, uint64_t& k, uint64_t& f, uint64_t& p) {
-  k = (uint64_t)r.w[0] | ((uint64_t)r.w[1] << 32);
-  f = (uint64_t)r.w[2] | ((uint64_t)r.w[3] << 32);
-  p = pos_base + r.w[4];
-}
 
 // ---------------------------------------------------------- reservation scatter ------
 // Small levels (a few 10^5 .. 10^6 keys) skip the count and histogram-scan kernels:
@@ -1085,8 +1155,9 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
                                                      uint64_t bucket_cap, unsigned long long* __restrict__ flags,
                                                      LevelState* st, unsigned tb, uint64_t cap_words,
                                                      unsigned long long* __restrict__ prof, uint64_t i_lo,
-                                                     uint64_t i_hi, unsigned ts) {
+                                                     uint64_t i_hi, unsigned ts, unsigned gate) {
   constexpr int kKPT = kR / kSB;
+  if (gate && !st->skew) return;  // gate: only for a skewed set (the fused P0 hash partitioned the rest)
   static_assert(!kP20 || kSrc == 2, "20-byte records carry identity positions");
   __shared__ uint64_t stage_raw[kP20 ? (kR * 5 + 1) / 2 : kR * 3];  // kR Rec, or kR R20
   Rec* const stage = reinterpret_cast<Rec*>(stage_raw);
@@ -3719,7 +3790,7 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
                    : k_scatter_res<kSubRound, kLdsTiles, 2>;
   }
   kern<<<grid, kSB, 0, s>>>(level, il, b.kh, b.fp, b.pos, b.pos_base, tc, b.bucket, b.bucket_cap, b.flags, b.st, g.tb,
-                            b.cap_words, b.tile_prof, i_lo, i_hi, b.split ? g.ts : 0u);
+                            b.cap_words, b.tile_prof, i_lo, i_hi, b.split ? g.ts : 0u, 0u);
 }
 
 void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s) {
@@ -3736,10 +3807,29 @@ void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, 
 // The records' first partition, into the super-tiles' slots of p.sup, when the level-0 hash
 // did not write them there (kh / fp from k_hash_count0 or k_hash_skew): k_scatter_res with
 // the super-tiles as its tiles (tile = (position >> 14) / tps, exact by the reciprocal).
-void launch_p0_partition(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
+void launch_p0_partition(const BinBuffers& b, const P0Bufs& p, hipStream_t s, bool only_skew) {
   k_scatter_res<5120, 1024, 2, true><<<256, kSB, 0, s>>>(0, nullptr, b.kh, b.fp, nullptr, b.pos_base, p.scnt,
                                                         reinterpret_cast<Rec*>(p.sup), p.sup_cap, p.flags, b.st,
-                                                        kRegTileMaxBits, b.cap_words, nullptr, 0, 0, p.tps);
+                                                        kRegTileMaxBits, b.cap_words, nullptr, 0, 0, p.tps,
+                                                        only_skew ? 1u : 0u);
+}
+
+// P0 level 0's hash and first partition: fused (k_hash0_pair<..., PT>) for an aligned blob
+// of up to kMaxRanks super-tiles, with k_hash_skew + the partition pass standing by for a
+// set the device finds skewed; otherwise kh / fp, then the partition pass.
+void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
+                    const P0Bufs& p, hipStream_t s) {
+  if (((uintptr_t)blob & 15) == 0 && p.S <= (unsigned)kMaxRanks) {
+    unsigned long long* prof = b.tile_prof ? b.tile_prof + (uint64_t)(kMaxLevels - 3) * kMaxTiles * 8 : nullptr;
+    const P0Part pt{p.sup, p.sup_cap / ((uint64_t)p.S * kResShards), p.scnt, p.tps, p.S};
+    k_hash0_pair<kH0T, kH0B, true, false, true><<<kH0Grid, kH0T, 0, s>>>(
+        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, Route0{}, pt);
+    launch_hash_skew(blob, offsets, n, b, g, prof, s);
+    launch_p0_partition(b, p, s, true);
+    return;
+  }
+  launch_binned_count(0, blob, offsets, n, b, g, 256, s, false);
+  launch_p0_partition(b, p, s, false);
 }
 
 void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {

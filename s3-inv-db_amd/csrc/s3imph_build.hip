@@ -142,6 +142,7 @@ void ev_begin(s3imph_ctx* c) {
 void ev_mark(s3imph_ctx* c, hipStream_t s, const char* name) {
   if (!c->profiling) return;
   if (c->profiling == 2 && std::strcmp(name, "init") != 0 && std::strcmp(name, "hash_count0") != 0 &&
+      std::strcmp(name, "hash_part0") != 0 &&
       std::strcmp(name, "hash_route0") != 0 && std::strcmp(name, "route0") != 0)
     return;  // light mode: two events per build, around the dominant kernel
   if (c->ev_used >= (int)c->events.size()) {
@@ -465,14 +466,12 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
     const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
     launch_init_state(c->d_st, n, n, s, offsets);
     ev_mark(c, s, "init");
-    launch_binned_count(0, blob, offsets, n, b, g0, 256, s, false);
-    ev_mark(c, s, "hash_count0");
-    launch_p0_partition(b, p, s);
-    ev_mark(c, s, "part0");
+    launch_p0_hash(blob, offsets, n, b, g0, p, s);
+    ev_mark(c, s, "hash_part0");
     launch_p0_scatter(b, p, s);
-    ev_mark(c, s, "scatter0");
+    ev_mark(c, s, "scatter0_p0");
     launch_p0_tile(b, p, s);
-    ev_mark(c, s, "tile0");
+    ev_mark(c, s, "tile0_p0");
     fault_dup_record(c, c->list[0], s);
     enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
     return;
@@ -1027,6 +1026,10 @@ int dist_classify_stop(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offse
   unsigned long long* ds = d.small + 4000;  // |u| <= 32 P <= 2048 entries each way (below dist_agree's words)
   HIPCHECK(hipMemcpyAsync(ds, cnt.data(), 8 * cnt.size(), hipMemcpyHostToDevice, s));
   cm.allreduce_u64(ds, ds + 2048, cnt.size(), s);
+  if (c->debug)
+    for (size_t i = 0; i < u.size(); ++i)
+      std::fprintf(stderr, "[s3imph] rank %d stop level %u: leftover hash %016llx occurs %llu times in %llu local keys\n",
+                   d.rank, nl, (unsigned long long)u[i], cnt[i], (unsigned long long)n_local);
   HIPCHECK(hipMemcpyAsync(cnt.data(), ds + 2048, 8 * cnt.size(), hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   for (unsigned long long v : cnt)

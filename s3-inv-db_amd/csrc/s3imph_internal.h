@@ -245,7 +245,10 @@ struct P0Bufs {
   unsigned* tcnt = nullptr;    // tile slot fills (T x kResShards), zeroed before the build
   unsigned long long* flags = nullptr;  // look-back words, one per tile
 };
-void launch_p0_partition(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
+void launch_p0_partition(const BinBuffers& b, const P0Bufs& p, hipStream_t s, bool only_skew);
+// level 0's hash with the first partition fused in where it can be (else hash, then partition)
+void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
+                    const P0Bufs& p, hipStream_t s);
 void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
 void binned_set_lds_limits();
