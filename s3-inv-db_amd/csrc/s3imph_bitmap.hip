@@ -86,6 +86,23 @@ __global__ __launch_bounds__(kBT) void k_bm_decide(const uint4* __restrict__ sli
   }
 }
 
+// The all-to-all's P (A, C) plane slices of this rank's words (rank q's at 2 S q) -> final
+// bits: the associative merge (A, C) + (a, c) = (A | a, C | c | (A & a)) over the ranks,
+// then exactly one key = A & ~C.  Two bits per position cross xGMI instead of a count byte.
+__global__ __launch_bounds__(kBT) void k_bm_merge(const uint64_t* __restrict__ recv, uint64_t S, int P,
+                                                  uint64_t* __restrict__ out, const LevelState* st) {
+  if (bm_dead(st)) return;
+  for (uint64_t w = (uint64_t)blockIdx.x * kBT + threadIdx.x; w < S; w += (uint64_t)gridDim.x * kBT) {
+    uint64_t A = 0, C = 0;
+    for (int q = 0; q < P; ++q) {
+      const uint64_t a = recv[2 * S * q + w], c = recv[2 * S * q + S + w];
+      C |= c | (A & a);
+      A |= a;
+    }
+    out[w] = A & ~C;
+  }
+}
+
 // ---- level end: tile totals over the gathered final bits -------------------------------
 // Tile t (2^tb positions, W = 2^(tb-6) words) -> tsum[t] = popcount(g) << 32 | popcount(g & A)
 // over its words (the level's keys placed in the tile, and this rank's share of them); g is
@@ -219,13 +236,21 @@ __device__ __forceinline__ uint64_t rec_index(unsigned i, const unsigned* fo, ui
 }
 
 // Mark: this rank's records of tile t -> local A (>= 1 key) / C (>= 2 keys) in LDS ->
-// the tile's count lanes (byte x = A + C = min(local count, 2)) and its A words (kept
-// for the settle).  Lanes of positions past the level's true size are zeroed here too.
-template <bool kNib>
+// the tile's lanes and its A words (kept for the settle).  Lanes of positions past the
+// level's true size are zeroed here too.  kMode:
+//   kBmBytes / kBmNibbles  count lanes, byte or nibble x = A + C = min(local count, 2),
+//                          summed over the ranks by an RCCL reduce-scatter (u8);
+//   kBmPlanes              the A and C bit planes themselves, 2 bits per position, laid out
+//                          by output slice (slice t = words [t S, (t+1) S): S A words then S C
+//                          words) for an all-to-all and k_bm_merge's associative merge
+//                          (A, C) + (a, c) = (A | a, C | c | (A & a)).
+template <int kMode>
 __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const Rec* __restrict__ bucket,
                                                       const unsigned* __restrict__ tc, uint64_t bucket_cap,
                                                       unsigned tb, const LevelState* st, uint64_t wpad,
-                                                      uint8_t* __restrict__ lanes, uint32_t* __restrict__ A32) {
+                                                      uint8_t* __restrict__ lanes, uint32_t* __restrict__ A32,
+                                                      uint64_t S, uint64_t mS) {
+  constexpr bool kNib = kMode == kBmNibbles;
   extern __shared__ uint32_t bm_lds[];
   __shared__ unsigned s_fo[kResShards + 1];
   if (bm_dead(st) || (st->status & kStStop)) return;
@@ -235,10 +260,20 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const Rec* __re
   uint32_t* sA = bm_lds;
   uint32_t* sC = bm_lds + W32;
   const unsigned tid = threadIdx.x;
-  // zero the lanes of [64 words, 64 wpad): no tile covers them (64 positions: 4 or 2 uint4)
-  constexpr uint64_t kU4 = kNib ? 2 : 4;
-  for (uint64_t q = kU4 * words + (uint64_t)blockIdx.x * kTT + tid; q < kU4 * wpad; q += (uint64_t)gridDim.x * kTT)
-    reinterpret_cast<uint4*>(lanes)[q] = make_uint4(0, 0, 0, 0);
+  // zero the lanes of [64 words, 64 wpad): no tile covers them (64 positions: 4 or 2 uint4,
+  // or one A and one C word)
+  if (kMode == kBmPlanes) {
+    uint64_t* ac = reinterpret_cast<uint64_t*>(lanes);
+    for (uint64_t w = words + (uint64_t)blockIdx.x * kTT + tid; w < wpad; w += (uint64_t)gridDim.x * kTT) {
+      const uint64_t sl = owner_of(w, S, mS), j = w - sl * S;
+      ac[2 * S * sl + j] = 0;
+      ac[2 * S * sl + S + j] = 0;
+    }
+  } else {
+    constexpr uint64_t kU4 = kNib ? 2 : 4;
+    for (uint64_t q = kU4 * words + (uint64_t)blockIdx.x * kTT + tid; q < kU4 * wpad; q += (uint64_t)gridDim.x * kTT)
+      reinterpret_cast<uint4*>(lanes)[q] = make_uint4(0, 0, 0, 0);
+  }
   if (T == 0) return;
   const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
   for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
@@ -271,7 +306,12 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const Rec* __re
     for (unsigned j = tid; j < wend; j += kTT) {
       const uint32_t a = sA[j], c = sC[j];
       A32[(t0 >> 5) + j] = a;
-      if (kNib) {  // 32 lanes in 16 bytes
+      if (kMode == kBmPlanes) {  // u32 half (g32 & 1) of u64 word g32 >> 1, in its slice's planes
+        const uint64_t g32 = (t0 >> 5) + j, w = g32 >> 1, sl = owner_of(w, S, mS), jw = w - sl * S;
+        uint32_t* ac32 = reinterpret_cast<uint32_t*>(lanes);
+        ac32[2 * (2 * S * sl + jw) + (g32 & 1)] = a;
+        ac32[2 * (2 * S * sl + S + jw) + (g32 & 1)] = c;
+      } else if (kNib) {  // 32 lanes in 16 bytes
         uint4* dst = reinterpret_cast<uint4*>(lanes + t0 / 2 + 16ull * j);
         dst[0] = make_uint4(spread8n(a) + spread8n(c), spread8n(a >> 8) + spread8n(c >> 8),
                             spread8n(a >> 16) + spread8n(c >> 16), spread8n(a >> 24) + spread8n(c >> 24));
@@ -544,10 +584,9 @@ size_t bm_tile_lds(unsigned tb, bool settle) {
 }
 
 void bm_set_lds_limits() {
-  (void)hipFuncSetAttribute((const void*)k_bm_tile_mark<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)bm_tile_lds(kBmMaxTb, false));
-  (void)hipFuncSetAttribute((const void*)k_bm_tile_mark<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)bm_tile_lds(kBmMaxTb, false));
+  for (const void* k : {(const void*)k_bm_tile_mark<kBmBytes>, (const void*)k_bm_tile_mark<kBmNibbles>,
+                        (const void*)k_bm_tile_mark<kBmPlanes>})
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_tile_lds(kBmMaxTb, false));
   (void)hipFuncSetAttribute((const void*)k_bm_tile_settle, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)bm_tile_lds(kBmMaxTb, true));
 }
@@ -555,12 +594,17 @@ void bm_set_lds_limits() {
 void launch_bm_range(LevelState* st, int level, hipStream_t s) { k_bm_range<<<1, 64, 0, s>>>(st, level); }
 
 void launch_bm_tile_mark(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
-                         uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A, bool nib,
-                         hipStream_t s) {
+                         uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A, int mode,
+                         uint64_t S, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(256, std::min<uint64_t>(tiles, 1024));
-  auto kern = nib ? k_bm_tile_mark<true> : k_bm_tile_mark<false>;
+  auto kern = mode == kBmPlanes ? k_bm_tile_mark<kBmPlanes> : mode == kBmNibbles ? k_bm_tile_mark<kBmNibbles>
+                                                                                : k_bm_tile_mark<kBmBytes>;
   kern<<<grid, kTT, bm_tile_lds(tb, false), s>>>(level, bucket, tc, bucket_cap, tb, st, wpad, lanes,
-                                                 reinterpret_cast<uint32_t*>(A));
+                                                 reinterpret_cast<uint32_t*>(A), S, level_magic(S));
+}
+
+void launch_bm_merge(const uint64_t* recv, uint64_t S, int P, uint64_t* out, const LevelState* st, hipStream_t s) {
+  k_bm_merge<<<grid_for(S, kBT, 8192), kBT, 0, s>>>(recv, S, P, out, st);
 }
 
 void launch_bm_tile_settle(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,

@@ -1404,8 +1404,9 @@ void ensure_bm_workspace(s3imph_ctx* c, uint64_t N) {
   dalloc(d.bm_a, wpad);
   dalloc(d.bm_g, wpad);
   dalloc(d.bm_dec, S);
-  dalloc(d.bm_lanes, 64 * wpad);
+  dalloc(d.bm_lanes, 64 * wpad);  // count bytes, or the (A, C) planes in 16 B per word
   dalloc(d.bm_slice, 64 * S);
+  dalloc(d.bm_recv, 16 * wpad);   // the planes' all-to-all: P slices of 2 S words
   if (!d.bm_tsum) dalloc(d.bm_tsum, kScatterTiles);
   if (!d.bm_tbase) dalloc(d.bm_tbase, 2 * kScatterTiles);
   d.bm_cap_words = wpad;
@@ -1413,7 +1414,7 @@ void ensure_bm_workspace(s3imph_ctx* c, uint64_t N) {
 
 void free_bm_workspace(DistState& d) {
   dfree(d.bm_a); dfree(d.bm_g); dfree(d.bm_dec);
-  dfree(d.bm_lanes); dfree(d.bm_slice); dfree(d.bm_tsum); dfree(d.bm_tbase);
+  dfree(d.bm_lanes); dfree(d.bm_slice); dfree(d.bm_recv); dfree(d.bm_tsum); dfree(d.bm_tbase);
   dfree(d.bm_out);
   d.bm_cap_words = 0;
   d.bm_cap_out = 0;
@@ -1455,8 +1456,10 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   // size is known without a host round trip; a level outgrowing its bound sets
   // kStBitmapBound and the build reruns on the routed decomposition.
   double nb = (double)N, npred = (double)n_local;
-  // count lanes: a nibble per position while the rank sums cannot carry out of it (2P <= 14)
-  const bool nib = P <= kBmNibRanks;
+  // what crosses xGMI per position: the 2-bit (A, C) planes (default), or count lanes summed
+  // by RCCL — a nibble while the rank sums cannot carry out of it (2P <= 14), else a byte
+  const int lanes = c->bm_counts ? (P <= kBmNibRanks ? kBmNibbles : kBmBytes) : kBmPlanes;
+  std::vector<uint64_t> xoff(P), xbytes(P);
   int L = 0;
   for (;;) {
     const uint64_t wmax = level_words((uint64_t)std::ceil(nb)), S = (wmax + P - 1) / P, wpad = S * (uint64_t)P;
@@ -1476,9 +1479,19 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     const int gsr = (int)std::max<uint64_t>(1, std::min<uint64_t>((np + kSubRound - 1) / kSubRound, 256));
     launch_binned_scatter_res(L, bs, g, gsr, s);
     const unsigned* tc = c->tcnt + (uint64_t)L * kTcntStride;
-    launch_bm_tile_mark(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, nib, s);
-    cm.reduce_scatter_u8(d.bm_lanes, d.bm_slice, (nib ? 32 : 64) * S, s);
-    launch_bm_decide(d.bm_slice, S, d.bm_dec, st, nib, s);
+    launch_bm_tile_mark(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, lanes, S, s);
+    if (lanes == kBmPlanes) {
+      // slice t's planes (2 S words) to rank t; rank q's planes of this rank's slice land at 2 S q
+      for (int t = 0; t < P; ++t) {
+        xoff[t] = 16 * S * (uint64_t)t;
+        xbytes[t] = 16 * S;
+      }
+      cm.alltoallv(d.bm_lanes, xoff.data(), xbytes.data(), d.bm_recv, xoff.data(), xbytes.data(), s);
+      launch_bm_merge(reinterpret_cast<const uint64_t*>(d.bm_recv), S, P, d.bm_dec, st, s);
+    } else {
+      cm.reduce_scatter_u8(d.bm_lanes, d.bm_slice, (lanes == kBmNibbles ? 32 : 64) * S, s);
+      launch_bm_decide(d.bm_slice, S, d.bm_dec, st, lanes == kBmNibbles, s);
+    }
     cm.allgather(d.bm_dec, d.bm_g, 8 * S, s);
     launch_bm_level_end(L, d.bm_g, d.bm_a, tb, tiles, c->bits, d.bm_tsum, d.bm_tbase, st, d.gslot, out_cnt, s);
     launch_bm_tile_settle(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
@@ -2041,6 +2054,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     c->fault_dup = std::getenv("S3IMPH_FAULT_DUP_REC") != nullptr;
     if (const char* m = std::getenv("S3IMPH_P0")) c->p0 = std::atoi(m);
+    if (const char* m = std::getenv("S3IMPH_BM_LANES")) c->bm_counts = std::strcmp(m, "counts") == 0;
     if (const char* m = std::getenv("S3IMPH_SCAT_CFG")) c->scat_cfg = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_SKEW_CFG")) c->skew_cfg = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);

@@ -92,7 +92,7 @@ struct DistState {
   // bitmap decomposition workspace: local A / C marks, count lanes, this rank's summed
   // slice, the gathered final bits, their word prefix and block sums
   uint64_t *bm_a = nullptr, *bm_g = nullptr, *bm_dec = nullptr;
-  uint8_t *bm_lanes = nullptr, *bm_slice = nullptr;
+  uint8_t *bm_lanes = nullptr, *bm_slice = nullptr, *bm_recv = nullptr;
   unsigned long long* bm_tsum = nullptr;   // per-tile totals of a level (kScatterTiles)
   unsigned long long* bm_tbase = nullptr;  // per-tile (rank, slot) bases (2 kScatterTiles)
   uint64_t bm_cap_words = 0;
@@ -224,6 +224,7 @@ struct s3imph_ctx {
   unsigned* p0_tcnt = nullptr;
   unsigned long long* p0_flags = nullptr;
   unsigned* p0_scnt = nullptr;
+  bool bm_counts = false;   // S3IMPH_BM_LANES=counts: the bitmap decomposition sums count lanes (A/B knob)
   bool debug = false;
   bool fault_dup = false;   // S3IMPH_FAULT_DUP_REC: test hook, duplicates a record mid-build (fault_dup_record)
   unsigned long long* tile_prof = nullptr;  // debug: tile phase timestamps

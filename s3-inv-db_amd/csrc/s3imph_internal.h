@@ -314,6 +314,9 @@ void launch_dist_replicate(LevelState* st, int L, uint64_t n_all, uint64_t skip_
 void launch_bm_check(LevelState* st, int level, uint64_t wmax, hipStream_t s);
 // nib: count lanes are nibbles (two positions per byte; P <= kBmNibRanks), else bytes
 constexpr int kBmNibRanks = 7;
+// What crosses xGMI per position and level: a count byte, a count nibble (both summed by an
+// RCCL reduce-scatter), or the 2-bit (A, C) planes (an all-to-all and k_bm_merge; default)
+constexpr int kBmBytes = 0, kBmNibbles = 1, kBmPlanes = 2;
 void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const LevelState* st, bool nib, hipStream_t s);
 // Bitmap levels are scattered into tiles of 2^tb positions, kBmMinTb <= tb <= kBmMaxTb, at
 // most kScatterTiles of them (levels of up to 2^31 positions); the settle kernel keeps 18 B
@@ -327,8 +330,10 @@ void launch_bm_level_end(int level, const uint64_t* g, const uint64_t* A, unsign
 void bm_set_lds_limits();
 void launch_bm_range(LevelState* st, int level, hipStream_t s);
 void launch_bm_tile_mark(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
-                         uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A, bool nib,
-                         hipStream_t s);
+                         uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A, int mode,
+                         uint64_t S, hipStream_t s);
+// the all-to-all's (A, C) plane slices (P of them, 2 S words each) -> this rank's final bits
+void launch_bm_merge(const uint64_t* recv, uint64_t S, int P, uint64_t* out, const LevelState* st, hipStream_t s);
 void launch_bm_tile_settle(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
                            uint64_t tiles, LevelState* st, const uint64_t* g, const uint64_t* A,
                            const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next, uint64_t next_cap,

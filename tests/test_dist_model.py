@@ -18,7 +18,10 @@ dist_attempt_bitmap — the north_star's per-level collision-bitmap reduction):
   every rank keeps its key shard; at level L it computes the count lane
   min(local count, 2) of every global position, the lanes are summed over the ranks
   (RCCL reduce-scatter of u8; here an all-reduce whose slice each rank keeps), the
-  slice owner sets final bit = (sum == 1), the final bits are all-gathered, and every
+  slice owner sets final bit = (sum == 1) — or (mode "planes", the default on the GPU)
+  the 2-bit (A, C) planes go to the slice owners by an all-to-all and are merged with
+  (A, C) + (a, c) = (A | a, C | c | (A & a)), final bit = A & ~C — the final bits are
+  all-gathered, and every
   rank settles its own records (bit set at x: placed at lvl_base + popcount(A[0:x)));
   the next level's global size is n_L - popcount(A_L).  Below the switch the remaining
   records are replicated as above; at the end one all-to-all moves the settled
@@ -180,7 +183,7 @@ def _rank_main(rank, world, port, blob, offs, switch, result_q):
     dist.destroy_process_group()
 
 
-def _bitmap_rank_main(rank, world, port, blob, offs, switch, result_q):
+def _bitmap_rank_main(rank, world, port, blob, offs, switch, result_q, planes=False):
     import torch
     import torch.distributed as dist
     import sys
@@ -204,10 +207,26 @@ def _bitmap_rank_main(rank, world, port, blob, offs, switch, result_q):
         words = (2 * nL + 63) // 64
         S = -(-words // world)
         x = _positions(level, k, words)
-        lanes = np.minimum(np.bincount(x, minlength=64 * S * world), 2).astype(np.int32)
-        t = torch.from_numpy(lanes)
-        dist.all_reduce(t)  # the reduce-scatter's sums; this rank decides its slice only
-        mine = t.numpy()[64 * S * rank:64 * S * (rank + 1)] == 1
+        cnt = np.bincount(x, minlength=64 * S * world)
+        if planes:
+            # the 2-bit (A, C) planes by output slice ([A words | C words] per slice) go to the
+            # slice owners (all-to-all); the owner merges (A, C) + (a, c) = (A|a, C|c|(A&a))
+            A = np.packbits(cnt >= 1, bitorder="little").view(np.uint64).reshape(world, S)
+            C = np.packbits(cnt >= 2, bitorder="little").view(np.uint64).reshape(world, S)
+            send = torch.from_numpy(np.concatenate([A, C], axis=1).reshape(-1).view(np.int64).copy())
+            recv = torch.zeros(2 * S * world, dtype=torch.int64)
+            dist.all_to_all_single(recv, send)
+            rv = recv.numpy().view(np.uint64).reshape(world, 2, S)
+            Am = np.zeros(S, np.uint64)
+            Cm = np.zeros(S, np.uint64)
+            for q in range(world):
+                Cm |= rv[q, 1] | (Am & rv[q, 0])
+                Am |= rv[q, 0]
+            mine = np.unpackbits((Am & ~Cm).view(np.uint8), bitorder="little").astype(bool)
+        else:
+            t = torch.from_numpy(np.minimum(cnt, 2).astype(np.int32))
+            dist.all_reduce(t)  # the reduce-scatter's sums; this rank decides its slice only
+            mine = t.numpy()[64 * S * rank:64 * S * (rank + 1)] == 1
         g = [torch.zeros(64 * S, dtype=torch.uint8) for _ in range(world)]
         dist.all_gather(g, torch.from_numpy(mine.astype(np.uint8)))
         final = np.concatenate([a.numpy() for a in g]).astype(bool)
@@ -276,7 +295,7 @@ def _bitmap_rank_main(rank, world, port, blob, offs, switch, result_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["route", "bitmap"])
+@pytest.mark.parametrize("mode", ["route", "bitmap", "planes"])
 @pytest.mark.parametrize("world,switch", [(2, 5000), (3, 5000), (3, 10 ** 9)])
 def test_position_range_ownership_matches_single_process(world, switch, mode, oracle_lib):
     import torch.multiprocessing as mp
@@ -291,7 +310,8 @@ def test_position_range_ownership_matches_single_process(world, switch, mode, or
     q = ctx.Queue()
     port = _free_port()
     target = _rank_main if mode == "route" else _bitmap_rank_main
-    procs = [ctx.Process(target=target, args=(r, world, port, blob, offs, switch, q)) for r in range(world)]
+    extra = (True,) if mode == "planes" else ()
+    procs = [ctx.Process(target=target, args=(r, world, port, blob, offs, switch, q) + extra) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
