@@ -1,20 +1,26 @@
 #!/bin/bash
-# dup probe, P0 parity subset, C3 bench A/B of S3IMPH_P0
+# dup probe, P0 + bitmap parity subset, C3 bench A/B of S3IMPH_P0, bitmap N=1 lanes A/B, C3 host phases
 OUT=gpurun_out/r4_p0b; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 200 python tools/dup_probe.py > $OUT/probe.log 2>&1; rc=$?
-echo "probe rc $rc" >> $OUT/status
-case $rc in 124|134|137|139) exit $rc;; esac
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-  -k "p0 or big_tiles or c3_100m_bit_exact or c5_one_gpu_share" > $OUT/pytest.log 2>&1; rc=$?
-echo "pytest rc $rc" >> $OUT/status
-case $rc in 124|134|137|139) exit $rc;; esac
+stop() { case $1 in 124|134|137|139) echo "stopped rc $1" >> $OUT/status; exit $1;; esac; }
+timeout -k 10 200 python tools/dup_probe.py > $OUT/probe.log 2>&1; rc=$?; echo "probe rc $rc" >> $OUT/status; stop $rc
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+  -k "p0 or big_tiles or c3_100m_bit_exact or c5_one_gpu_share or bitmap or 64_ranks" > $OUT/pytest.log 2>&1; rc=$?
+echo "pytest rc $rc" >> $OUT/status; stop $rc
 for rep in 1 2; do for v in 1 0; do
-  S3IMPH_P0=$v timeout -k 10 200 python bench.py --no-cpu-baseline --headline-only --no-secondary --config c3 --steps 20 >> $OUT/c3_$v.log 2>&1 || exit $?
+  S3IMPH_P0=$v timeout -k 10 200 python bench.py --no-cpu-baseline --headline-only --no-secondary --config c3 --steps 20 >> $OUT/c3_p0_$v.log 2>&1; rc=$?; stop $rc
 done; done
+for v in planes counts; do
+  S3IMPH_BM_LANES=$v timeout -k 10 200 python bench.py --no-cpu-baseline --headline-only --no-secondary --config c3 --steps 10 --dist --decomp bitmap >> $OUT/c3_bm_$v.log 2>&1; rc=$?; stop $rc
+done
+timeout -k 10 200 python tools/host_phase.py 100000000 64 --debug > $OUT/host_c3.log 2>&1; rc=$?; stop $rc
+for m in 0 1 2; do
+  timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch_$m -o run -- ./tools/ubench_fetch $m \
+    > $OUT/fetch_$m.log 2>&1; rc=$?; stop $rc
+done
 python3 - > $OUT/summary.txt <<PY
 import json, glob
-for f in sorted(glob.glob("$OUT/c*_*.log")):
+for f in sorted(glob.glob("$OUT/c3_*.log")):
     for line in open(f):
         if line.startswith("{"):
             d = json.loads(line)
