@@ -2634,27 +2634,33 @@ __device__ __forceinline__ uint64_t lb_resolve(unsigned long long* flags, uint64
   return excl;
 }
 
-__global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket, uint64_t bucket_cap,
+// k20: R20 records (identity positions: p = pos_base + key index, 12-B stage entries);
+// otherwise Rec records of any level whose tiles are 2^14 positions (16-B stage entries).
+template <bool k20>
+__global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restrict__ bucket_v, uint64_t bucket_cap,
                                                   const unsigned* __restrict__ tcnt, unsigned long long* flags,
                                                   uint64_t* __restrict__ bits, Rec* __restrict__ next,
                                                   uint64_t* __restrict__ fp_out, uint64_t* __restrict__ pos_out,
                                                   LevelState* st, uint64_t pos_base) {
+  using PT = std::conditional_t<k20, uint32_t, uint64_t>;  // key index, or p
   __shared__ uint64_t sf[kP0Stage];
-  __shared__ uint32_t si[kP0Stage];
+  __shared__ PT si[kP0Stage];
   __shared__ uint32_t sA[kP0W32], sC[kP0W32];
   __shared__ unsigned s_wc[kP0T / 64];
   __shared__ unsigned s_cnt[2][kResShards];
   __shared__ unsigned long long s_t[2], s_b0, s_excl;
   __shared__ unsigned s_late;
-  if (!level_active(0, st)) return;
+  if (!level_active(level, st)) return;
   const uint64_t N = st->out_cap;
-  const bool out_on = level_out_on(st, 0);
-  const uint64_t words = st->words[0], magic = st->magic[0];
-  const uint64_t T = st->ntiles[0];
-  const uint64_t w32_level = 2 * words;
-  uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[0]);
-  const uint64_t seed = level_seed(0);
-  const uint64_t lvl_base = st->lvl_base[0];
+  const bool out_on = level_out_on(st, level);
+  const uint64_t words = st->words[level], magic = st->magic[level];
+  const uint64_t T = st->ntiles[level];
+  const LevelRange rg = level_range(st, level, words);
+  const uint64_t w32_level = 2 * rg.rw;
+  uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[level] + rg.plo / 64);
+  const uint64_t seed = level_seed(level);
+  const uint64_t lvl_base = st->lvl_base[level];
+  auto pos_of = [&](PT v) -> uint64_t { return k20 ? pos_base + v : (uint64_t)v; };
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint64_t lt = lanemask_lt();
   const uint64_t cap = bucket_cap / T, shcap = cap / kResShards;
@@ -2675,20 +2681,26 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
     F.n = a;
     return F;
   };
-  // tile t's record j as (k, f, key index)
-  auto rec = [&](uint64_t t, const Fills& F, unsigned j, uint64_t& k_, uint64_t& f_, uint32_t& p_) {
+  // tile t's record j as (k, f, key index or p)
+  auto rec = [&](uint64_t t, const Fills& F, unsigned j, uint64_t& k_, uint64_t& f_, PT& p_) {
     uint32_t o = j;
 #pragma unroll
     for (int x = 1; x < kResShards; ++x)
       if (j >= F.pre[x]) o = (uint32_t)(x * shcap) + (j - F.pre[x]);
-    const R20* q = bucket + t * cap + o;
-    const R20 r = *q;
-    k_ = (uint64_t)r.w[0] | ((uint64_t)r.w[1] << 32);
-    f_ = (uint64_t)r.w[2] | ((uint64_t)r.w[3] << 32);
-    p_ = r.w[4];
+    if constexpr (k20) {
+      const R20 r = static_cast<const R20*>(bucket_v)[t * cap + o];
+      k_ = (uint64_t)r.w[0] | ((uint64_t)r.w[1] << 32);
+      f_ = (uint64_t)r.w[2] | ((uint64_t)r.w[3] << 32);
+      p_ = r.w[4];
+    } else {
+      const Rec* q = static_cast<const Rec*>(bucket_v) + t * cap + o;
+      k_ = q->k;
+      f_ = q->f;
+      p_ = q->p;
+    }
   };
   uint64_t k[kP0R], f[kP0R];
-  uint32_t p[kP0R];
+  PT p[kP0R];
   auto load_regs = [&](uint64_t t, const Fills& F, unsigned me) {
 #pragma unroll
     for (int r = 0; r < kP0R; ++r) {
@@ -2698,7 +2710,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
       if (j < F.n) rec(t, F, j, k[r], f[r], p[r]);
     }
   };
-  if (tid == 0) s_t[0] = atomicAdd(&st->ticket[0], 1ull);
+  if (tid == 0) s_t[0] = atomicAdd(&st->ticket[level], 1ull);
   for (unsigned w = tid; w < kP0W32; w += kP0T) {
     sA[w] = 0;
     sC[w] = 0;
@@ -2719,8 +2731,8 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
     unsigned me = tid;
     asm volatile("" : "+v"(me));
     const bool fits = nk <= (unsigned)kP0R * kP0T;
-    const uint64_t tbase = t << kRegTileMaxBits;
-    if (tid == 0) s_t[nb] = atomicAdd(&st->ticket[0], 1ull);
+    const uint64_t tbase = rg.plo + (t << kRegTileMaxBits);
+    if (tid == 0) s_t[nb] = atomicAdd(&st->ticket[level], 1ull);
     // ---- mark
     unsigned loc2[(kP0R + 1) / 2];
 #define LOC(r) ((loc2[(r) >> 1] >> (((r) & 1) * 16)) & 0xffffu)
@@ -2742,7 +2754,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
       #pragma unroll 1
       for (unsigned j = me; j < nk; j += kP0T) {
         uint64_t jk, jf;
-        uint32_t jp;
+        PT jp;
         rec(t, F, j, jk, jf, jp);
         const unsigned x = (unsigned)(bb_index(seed, jk, words, magic) - tbase);
         const uint32_t bit = 1u << (x & 31);
@@ -2770,7 +2782,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
       lb_publish(flags, t, pop);
       s_late = 0;
     }
-    if (tid == 64) s_b0 = nk > pop ? atomicAdd(&st->n[1], (unsigned long long)(nk - pop)) : 0ull;
+    if (tid == 64) s_b0 = nk > pop ? atomicAdd(&st->n[level + 1], (unsigned long long)(nk - pop)) : 0ull;
     __syncthreads();  // rank prefix, slot reservation
     // ---- classify: settled -> stage[rank]; collided counted per wave
     unsigned wc = 0;
@@ -2806,7 +2818,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
         bool redo = false;
         if (j < nk) {
           uint64_t jk, jf;
-          uint32_t jp;
+          PT jp;
           rec(t, F, j, jk, jf, jp);
           const unsigned x = (unsigned)(bb_index(seed, jk, words, magic) - tbase);
           redo = !((sA[x >> 5] >> (x & 31)) & 1u);
@@ -2828,7 +2840,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
           const unsigned x = LOC(r);
           const bool redo = j < nk && !((sA[x >> 5] >> (x & 31)) & 1u);
           const uint64_t m = __ballot(redo);
-          if (redo) next[o + __popcll(m & lt)] = Rec{k[r], f[r], pos_base + p[r]};
+          if (redo) next[o + __popcll(m & lt)] = Rec{k[r], f[r], pos_of(p[r])};
           o += __popcll(m);
         }
       } else {
@@ -2837,14 +2849,14 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
           const unsigned j = jb + lane;
           bool redo = false;
           uint64_t jk = 0, jf = 0;
-          uint32_t jp = 0;
+          PT jp = 0;
           if (j < nk) {
             rec(t, F, j, jk, jf, jp);
             const unsigned x = (unsigned)(bb_index(seed, jk, words, magic) - tbase);
             redo = !((sA[x >> 5] >> (x & 31)) & 1u);
           }
           const uint64_t m = __ballot(redo);
-          if (redo) next[o + __popcll(m & lt)] = Rec{jk, jf, pos_base + jp};
+          if (redo) next[o + __popcll(m & lt)] = Rec{jk, jf, pos_of(jp)};
           o += __popcll(m);
         }
       }
@@ -2855,7 +2867,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
       if (wave == 0) {
         const uint64_t excl = lb_resolve(flags, t, pop, st);
         if (lane == 0) {
-          if (t == T - 1) st->lvl_base[1] = lvl_base + excl + pop;
+          if (t == T - 1) st->lvl_base[level + 1] = lvl_base + excl + pop;
           s_excl = excl;
         }
       }
@@ -2870,13 +2882,13 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
             const uint32_t wv = sA[x >> 5];
             const uint64_t q = base + sC[x >> 5] + __popc(wv & ((1u << (x & 31)) - 1));
             fp_out[q] = f[r];
-            pos_out[q] = pos_base + p[r];
+            pos_out[q] = pos_of(p[r]);
           }
       } else {
         #pragma unroll 1
         for (unsigned j = me; wr && j < nk; j += kP0T) {
           uint64_t jk, jf;
-          uint32_t jp;
+          PT jp;
           rec(t, F, j, jk, jf, jp);
           const unsigned x = (unsigned)(bb_index(seed, jk, words, magic) - tbase);
           const uint32_t wv = sA[x >> 5];
@@ -2884,7 +2896,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
           if (wv & bit) {
             const uint64_t q = base + sC[x >> 5] + __popc(wv & (bit - 1));
             fp_out[q] = jf;
-            pos_out[q] = pos_base + jp;
+            pos_out[q] = pos_of(jp);
           }
         }
       }
@@ -2899,7 +2911,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
       if (wave == 0) {
         const uint64_t excl = lb_resolve(flags, t, pop, st);
         if (lane == 0) {
-          if (t == T - 1) st->lvl_base[1] = lvl_base + excl + pop;
+          if (t == T - 1) st->lvl_base[level + 1] = lvl_base + excl + pop;
           s_excl = excl;
         }
       }
@@ -2912,7 +2924,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(const R20* __restrict__ bucket
       #pragma unroll 1
       for (unsigned i = me; i < ns; i += kP0T) {
         fp_out[base + i] = sf[i];
-        pos_out[base + i] = pos_base + si[i];
+        pos_out[base + i] = pos_of(si[i]);
       }
     }
     for (unsigned w = tid; w < kP0W32; w += kP0T) {
@@ -3709,6 +3721,18 @@ void launch_binned_scatter(int level, const BinBuffers& b, LevelGeom g, hipStrea
 }
 
 void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_tiles, hipStream_t s, bool reserved) {
+  if (g.tb == kRegMaxBits && reserved && b.pipe_tiles) {
+    // 2^14-position tiles from reservation slots: the persistent, pipelined register tiles
+    // (level 0 with identity positions reads the scatter's R20 records)
+    const unsigned* tc = b.tcnt + (uint64_t)level * kTcntStride;
+    if (level == 0 && !b.dist && !b.pos)
+      k_tile_p0<true><<<256, kP0T, 0, s>>>(0, b.bucket, b.bucket_cap, tc, b.flags, b.bits, b.list[0], b.fp_out,
+                                           b.pos_out, b.st, b.pos_base);
+    else
+      k_tile_p0<false><<<256, kP0T, 0, s>>>(level, b.bucket, b.bucket_cap, tc, b.flags, b.bits, b.list[level & 1],
+                                            b.fp_out, b.pos_out, b.st, b.pos_base);
+    return;
+  }
   if (g.tb <= kRegMaxBits) {
     // records per tile ~2^(tb-1): pick the variant whose NT x R covers it with margin
     // (lighter variants keep several tiles resident per CU)
@@ -3755,7 +3779,8 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
   unsigned* tc = b.tcnt + (uint64_t)level * kTcntStride;
   // level 0 whose tiles go to the split kernel, identity positions: R20 records (the
   // split launch makes the same choice)
-  const bool p20 = l0 && !b.pos && b.split && g.tb > kRegMaxBits && g.tb <= kSplitMaxBits;
+  const bool p20 = l0 && !b.pos && ((b.split && g.tb > kRegMaxBits && g.tb <= kSplitMaxBits) ||
+                                    (b.pipe_tiles && g.tb == kRegMaxBits));
   // LDS count / start / cursor arrays sized to the level's tiles (tmax: the host's bound;
   // a level past it flags kStGeometry and reruns), the freed LDS taken by longer rounds
   // (more records per tile per round: longer runs, fewer reservation atomics per record).
@@ -3839,8 +3864,8 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
 }
 
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
-  k_tile_p0<<<256, kP0T, 0, s>>>(p.bucket, p.bucket_cap, p.tcnt, p.flags, b.bits, b.list[0], b.fp_out, b.pos_out, b.st,
-                                 b.pos_base);
+  k_tile_p0<true><<<256, kP0T, 0, s>>>(0, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.bits, b.list[0], b.fp_out,
+                                       b.pos_out, b.st, b.pos_base);
 }
 
 }  // namespace s3imph

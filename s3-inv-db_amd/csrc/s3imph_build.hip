@@ -284,6 +284,7 @@ BinBuffers make_bufs(s3imph_ctx* c, const uint64_t* pos, uint64_t* fp_out, uint6
   if (!c->split && c->cap_keys > (kMaxTiles << kRegTileMaxBits) / 2) dalloc(c->split, split_scratch_records());
   b.split = c->split;
   b.scat_cfg = c->scat_cfg;
+  b.pipe_tiles = c->p0 != 0;
   b.skew_cfg = c->skew_cfg;
   b.bits = c->bits;
   b.cap_words = c->cap_words;
@@ -1450,6 +1451,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   BinBuffers bs = b;
   bs.dist = false;
   bs.split = nullptr;
+  bs.pipe_tiles = false;  // the bitmap kernels read Rec buckets
   bs.pos = pos;
   bs.pos_base = key_base;
   // Level sizes: the host bounds n_L from above (mean q n + 6 sigma), so every collective's

@@ -219,6 +219,7 @@ struct BinBuffers {
   uint32_t* mid;                        // k_mid_levels scratch (kMidScratchU32)
   Rec* split;                           // k_tile_split scratch (split_scratch_records()), or null
   int scat_cfg = 2;                     // k_scatter_res forms (launch_binned_scatter_res)
+  bool pipe_tiles = false;              // 2^14 reservation tiles on k_tile_p0 (else k_tile_reg)
   int skew_cfg = 2;                     // k_hash_skew block / group shape (launch_hash_skew)
 };
 uint64_t split_scratch_records();  // sub-tile segments of the split big-tile kernel
