@@ -337,17 +337,30 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const Rec* __re
 // so this rank's settled list is in p order whatever order the records arrive in.  The
 // tile keeps g and g & a (16 B per word) and, per group of 4 words, both prefixes (2 B per
 // word): 144 KiB at 2^19 positions.  Collided records go to the next level's list at one
-// atomic per tile plus an LDS cursor.
+// atomic per tile plus an LDS cursor.  A settled key whose p falls in this rank's own output
+// slice [own_lo, own_lo + slice) is written to fp_out / pos_out at once (its list slot stays
+// a hole no one reads); every settled key is counted per output slice in scnt, which is
+// the output all-to-all's send counts (the list's runs by slice, holes included).
 constexpr unsigned kGrp = 4;
+__device__ __forceinline__ void fp_out_own(const OwnSlice& os, uint64_t p, uint64_t f, uint64_t pos, bool& over) {
+  const uint64_t o = p - os.lo;
+  if (p < os.lo || o >= os.cnt) {
+    over = true;
+    return;
+  }
+  os.fp_out[o] = f;
+  os.pos_out[o] = pos;
+}
 __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const Rec* __restrict__ bucket,
                                                         const unsigned* __restrict__ tc, uint64_t bucket_cap,
                                                         unsigned tb, LevelState* st, const uint64_t* __restrict__ g,
                                                         const uint64_t* __restrict__ A,
                                                         const unsigned long long* __restrict__ tbase,
                                                         Rec* __restrict__ out, uint64_t out_cap,
-                                                        Rec* __restrict__ next, uint64_t next_cap) {
+                                                        Rec* __restrict__ next, uint64_t next_cap, OwnSlice os) {
   extern __shared__ uint64_t bm_lds64[];
   __shared__ unsigned long long s_w[kTT / 64];
+  __shared__ unsigned s_sc[kMaxRanks];
   __shared__ unsigned s_fo[kResShards + 1];
   __shared__ unsigned long long s_nb, s_tg, s_ta;
   __shared__ unsigned s_ncur;
@@ -365,6 +378,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const Rec* __
   const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
   constexpr int kGper = 2;  // groups per thread in the tile scan (G <= 2048)
   bool over = false;
+  if (tid < (unsigned)kMaxRanks) s_sc[tid] = 0;  // (the first tile's barriers order it before use)
   for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
     const uint64_t w0 = t * W;
     const unsigned nw = (unsigned)min<uint64_t>(W, words - w0);
@@ -466,11 +480,18 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const Rec* __
             }
           pg += (unsigned)__popcll(v & below);
           pa += (unsigned)__popcll(sga[j] & below);
-          const uint64_t slot = ob + pa;
-          if (slot < out_cap)
-            out[slot] = Rec{pb + pg, r[u].f, r[u].p};
-          else
-            over = true;
+          const uint64_t gp = pb + pg;
+          const unsigned sl = owner_of(gp, os.slice, os.mslice);
+          atomicAdd(&s_sc[sl < (unsigned)os.P ? sl : os.P - 1], 1u);
+          if ((int)sl == os.rank) {
+            fp_out_own(os, gp, r[u].f, r[u].p, over);
+          } else {
+            const uint64_t slot = ob + pa;
+            if (slot < out_cap)
+              out[slot] = Rec{gp, r[u].f, r[u].p};
+            else
+              over = true;
+          }
         } else {
           const uint64_t slot = nb + atomicAdd(&s_ncur, 1u);
           if (slot < next_cap)
@@ -482,6 +503,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const Rec* __
     }
     __syncthreads();  // the tile's LDS state is reused by the next tile
   }
+  if (tid < (unsigned)os.P && s_sc[tid]) atomicAdd(&os.scnt[tid], (unsigned long long)s_sc[tid]);
   if (over) atomicOr(&st->status, kStOverflow);
 }
 
@@ -497,33 +519,6 @@ __global__ void k_bm_range(LevelState* st, int level) {
 // The level's true size against the host's bound (words_L <= wmax), after k_dist_setup.
 __global__ void k_bm_check(LevelState* st, int level, uint64_t wmax) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && st->words[level] > wmax) atomicOr(&st->status, kStBitmapBound);
-}
-
-// This rank's settled list is sorted by p: the run for output slice t ([t slice, (t+1)
-// slice)) is [lower_bound(t slice), lower_bound((t+1) slice)).  One thread per slice
-// boundary; scnt[t] = the run's length, scnt[P] = 0 (no overflow: nothing is copied).
-constexpr int kBmBoundsT = 128;
-__global__ __launch_bounds__(kBmBoundsT) void k_bm_bounds(const Rec* __restrict__ out, const unsigned long long* __restrict__ n_out, uint64_t slice,
-                            int P, unsigned long long* __restrict__ scnt) {
-  __shared__ uint64_t s_b[kMaxRanks + 1];
-  const unsigned t = threadIdx.x;
-  const uint64_t n = *n_out;
-  if (t <= (unsigned)P) {
-    uint64_t lo = 0, hi = n;
-    if (t == (unsigned)P) lo = n;
-    else if (t > 0) {
-      const uint64_t key = (uint64_t)t * slice;
-      while (lo < hi) {
-        const uint64_t mid = (lo + hi) / 2;
-        if (out[mid].k < key) lo = mid + 1;
-        else hi = mid;
-      }
-    }
-    s_b[t] = lo;
-  }
-  __syncthreads();
-  if (t < (unsigned)P) scnt[t] = s_b[t + 1] - s_b[t];
-  if (t == (unsigned)P) scnt[P] = 0;
 }
 
 // Received triples of this rank's output slice [lo, lo + cnt) -> fp_out / pos_out.
@@ -610,18 +605,10 @@ void launch_bm_merge(const uint64_t* recv, uint64_t S, int P, uint64_t* out, con
 void launch_bm_tile_settle(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
                            uint64_t tiles, LevelState* st, const uint64_t* g, const uint64_t* A,
                            const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next, uint64_t next_cap,
-                           hipStream_t s) {
+                           const OwnSlice& os, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1024));
   k_bm_tile_settle<<<grid, kTT, bm_tile_lds(tb, true), s>>>(level, bucket, tc, bucket_cap, tb, st, g, A, tbase, out,
-                                                            out_cap, next, next_cap);
-}
-
-void launch_bm_bounds(const Rec* out, const unsigned long long* n_out, uint64_t slice, int P, unsigned long long* scnt,
-                      hipStream_t s) {
-  // thread t <= P finds boundary t: P + 1 threads, up to kMaxRanks + 1 (a 64-thread launch
-  // left boundary 64, and so the last slice's count, unset at P = 64)
-  static_assert(kMaxRanks + 1 <= kBmBoundsT, "one thread per slice boundary");
-  k_bm_bounds<<<1, kBmBoundsT, 0, s>>>(out, n_out, slice, P, scnt);
+                                                            out_cap, next, next_cap, os);
 }
 
 void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,

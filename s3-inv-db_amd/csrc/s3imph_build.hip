@@ -1444,6 +1444,21 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   Rec* const out = d.bm_out;                   // this rank's settled (p, fp, pos) triples
   unsigned long long* const out_cnt = d.small + 4096;
   HIPCHECK(hipMemsetAsync(out_cnt, 0, 8, s));
+  // this rank's output slice: its settled keys land in fp_out / pos_out during the settle;
+  // d.scnt counts every settled key per slice (the output all-to-all's send counts)
+  const uint64_t slice = (N + P - 1) / P;
+  const uint64_t lo = std::min<uint64_t>((uint64_t)R * slice, N), mine = std::min<uint64_t>(N, lo + slice) - lo;
+  {  // out_cap is the caller's, per rank: agreed before the first level
+    int lrc = S3IMPH_OK;
+    if (mine > out_cap) {
+      *msg = "build MPHF: output capacity " + std::to_string(out_cap) + " < " + std::to_string(mine);
+      lrc = S3IMPH_ERR_INVALID;
+    }
+    const int rc = dist_agree(c, lrc, s, msg);
+    if (rc != S3IMPH_OK) return rc;
+  }
+  const OwnSlice own_slice{lo, mine, slice, level_magic(slice), R, P, fp_out, pos_out, d.scnt};
+  HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
   HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kMaxDistLevels * kTcntStride * sizeof(unsigned), s));
   // The level's records go through the reservation scatter into tiles over the level's
   // whole position range (this rank's records only); the tile kernels then mark and
@@ -1497,7 +1512,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     cm.allgather(d.bm_dec, d.bm_g, 8 * S, s);
     launch_bm_level_end(L, d.bm_g, d.bm_a, tb, tiles, c->bits, d.bm_tsum, d.bm_tbase, st, d.gslot, out_cnt, s);
     launch_bm_tile_settle(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
-                          d.bm_cap_out, c->list[L & 1], d.cap_list, s);
+                          d.bm_cap_out, c->list[L & 1], d.cap_list, own_slice, s);
     ev_mark(c, s, L == 0 ? "level0" : "levels");
     const double nbn = nb * q + 6.0 * std::sqrt(nb) + 64.0;
     npred *= q;
@@ -1611,29 +1626,16 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
            " of " + std::to_string(N) + " keys";
     return S3IMPH_ERR_INTERNAL;
   }
-  // ---- settled triples to the owners of their output slices
-  const uint64_t slice = (N + P - 1) / P;
-  const uint64_t lo = std::min<uint64_t>((uint64_t)R * slice, N), mine = std::min<uint64_t>(N, lo + slice) - lo;
-  {  // out_cap is the caller's, per rank: agreed before the bounds gather
-    int lrc = S3IMPH_OK;
-    if (mine > out_cap) {
-      *msg = "build MPHF: output capacity " + std::to_string(out_cap) + " < " + std::to_string(mine);
-      lrc = S3IMPH_ERR_INVALID;
-    }
-    const int rc = dist_agree(c, lrc, s, msg);
-    if (rc != S3IMPH_OK) return rc;
-  }
-  // this rank's settled list is sorted by p: its run for slice t goes to rank t as it lies
-  // (the own run is placed straight from the list)
-  launch_bm_bounds(out, out_cnt, slice, P, d.scnt, s);
+  // ---- settled triples to the owners of their output slices: this rank's settled list is
+  // sorted by p, so its run for slice t (d.scnt[t] records, counted by the settle) goes to
+  // rank t as it lies; the own run is a hole (those keys were placed by the settle)
   cm.allgather(d.scnt, d.mat, 8ull * (P + 1), s);
   HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
-  uint64_t acc = 0, got = 0, own_off = 0, sent = 0;
+  uint64_t acc = 0, got = 0, sent = 0;
   for (int t = 0; t < P; ++t) {
     const uint64_t cnt_t = M[(uint64_t)R * (P + 1) + t];
-    if (t < R) own_off += cnt_t;
     soff[t] = sent * sizeof(Rec);
     sbytes[t] = t == R ? 0 : cnt_t * sizeof(Rec);
     sent += cnt_t;
@@ -1660,7 +1662,6 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   }
   Rec* recv = c->list[Ls & 1];
   if (P > 1) cm.alltoallv(out, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), s);
-  launch_bm_place(out + own_off, own, lo, mine, fp_out, pos_out, st, s);
   launch_bm_place(recv, got, lo, mine, fp_out, pos_out, st, s);
   launch_bm_tail_copy(c->kh, c->fp, g0, total, lo, mine, fp_out, pos_out, s);
   ev_mark(c, s, "exchange_out");

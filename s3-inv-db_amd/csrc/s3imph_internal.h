@@ -335,13 +335,19 @@ void launch_bm_tile_mark(int level, const Rec* bucket, const unsigned* tc, uint6
                          uint64_t S, hipStream_t s);
 // the all-to-all's (A, C) plane slices (P of them, 2 S words each) -> this rank's final bits
 void launch_bm_merge(const uint64_t* recv, uint64_t S, int P, uint64_t* out, const LevelState* st, hipStream_t s);
+// This rank's output slice [lo, lo + cnt) of the global outputs (slices of `slice` keys,
+// mslice = level_magic(slice)): settled keys with p in it go straight to fp_out / pos_out;
+// scnt[t] (P + 1 counters, zeroed before the first level) counts every settled key of slice t.
+struct OwnSlice {
+  uint64_t lo, cnt, slice, mslice;
+  int rank, P;
+  uint64_t *fp_out, *pos_out;
+  unsigned long long* scnt;
+};
 void launch_bm_tile_settle(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
                            uint64_t tiles, LevelState* st, const uint64_t* g, const uint64_t* A,
                            const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next, uint64_t next_cap,
-                           hipStream_t s);
-// the settled list (sorted by p) -> scnt[t] = its run for output slice t, scnt[P] = 0
-void launch_bm_bounds(const Rec* out, const unsigned long long* n_out, uint64_t slice, int P, unsigned long long* scnt,
-                      hipStream_t s);
+                           const OwnSlice& os, hipStream_t s);
 void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,
                      LevelState* st, hipStream_t s);
 void launch_bm_tail_copy(const uint64_t* sfp, const uint64_t* spos, uint64_t g0, uint64_t total, uint64_t lo,

@@ -63,9 +63,9 @@ def test_thread_per_rank_shared_gpu(s3, oracle_lib, monkeypatch, ranks, kind, av
 
 
 def test_thread_per_rank_64_ranks_bitmap(s3, oracle_lib, monkeypatch):
-    """kMaxRanks = 64 ranks (the API's limit) on the bitmap decomposition: the output
-    exchange's slice bounds need P + 1 = 65 boundaries (k_bm_bounds), the last slice's
-    count included; bit-exact."""
+    """kMaxRanks = 64 ranks (the API's limit) on the bitmap decomposition: 64 output
+    slices counted by the settle (the last slice's count included), the (A, C) plane
+    all-to-all over 64 ranks; bit-exact."""
     monkeypatch.setenv("S3IMPH_DIST_SWITCH", "15000")
     monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
     blob, offs = s3.gen_keys(0, 12, 24, 0, 640_000)

@@ -5,11 +5,11 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 stop() { case $1 in 124|134|137|139) echo "stopped rc $1" >> $OUT/status; exit $1;; esac; }
 timeout -k 10 200 python tools/dup_probe.py > $OUT/probe.log 2>&1; rc=$?; echo "probe rc $rc" >> $OUT/status; stop $rc
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
-  -k "p0 or big_tiles or c3_100m_bit_exact or c5_one_gpu_share or bitmap or 64_ranks" > $OUT/pytest.log 2>&1; rc=$?
+  --durations=10 > $OUT/pytest.log 2>&1; rc=$?
 echo "pytest rc $rc" >> $OUT/status; stop $rc
-for rep in 1 2; do for v in 1 0; do
-  S3IMPH_P0=$v timeout -k 10 200 python bench.py --no-cpu-baseline --headline-only --no-secondary --config c3 --steps 20 >> $OUT/c3_p0_$v.log 2>&1; rc=$?; stop $rc
-done; done
+for rep in 1 2; do for cfg in c3 c2; do for v in 1 0; do
+  S3IMPH_P0=$v timeout -k 10 200 python bench.py --no-cpu-baseline --headline-only --no-secondary --config $cfg --steps 20 >> $OUT/${cfg}_p0_$v.log 2>&1; rc=$?; stop $rc
+done; done; done
 for v in planes counts; do
   S3IMPH_BM_LANES=$v timeout -k 10 200 python bench.py --no-cpu-baseline --headline-only --no-secondary --config c3 --steps 10 --dist --decomp bitmap >> $OUT/c3_bm_$v.log 2>&1; rc=$?; stop $rc
 done
@@ -20,7 +20,7 @@ for m in 0 1 2; do
 done
 python3 - > $OUT/summary.txt <<PY
 import json, glob
-for f in sorted(glob.glob("$OUT/c3_*.log")):
+for f in sorted(glob.glob("$OUT/c[23]_*.log")):
     for line in open(f):
         if line.startswith("{"):
             d = json.loads(line)
