@@ -1018,20 +1018,34 @@ int dist_classify_stop(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offse
     *msg = "build MPHF: can't find minimal perfect hash after " + std::to_string(kMaxLevels) + " levels";
     return S3IMPH_ERR_TOO_MANY_LEVELS;
   }
+  // the leftover records hold the key hash itself, or (left by the single-workgroup tail)
+  // mix64 of it — a bijection, so both forms are counted, each summed over the ranks
   const std::vector<uint64_t> orig = original_key_hashes(c, blob, offsets, n_local, s);
-  std::vector<unsigned long long> cnt(u.size(), 0);
-  for (size_t i = 0; i < u.size(); ++i) {
+  std::vector<uint64_t> mixed(orig.size());
+  for (size_t i = 0; i < orig.size(); ++i) mixed[i] = mix64(orig[i]);
+  std::sort(mixed.begin(), mixed.end());
+  const size_t U = u.size();
+  std::vector<unsigned long long> cnt(2 * U, 0);
+  for (size_t i = 0; i < U; ++i) {
     const auto r = std::equal_range(orig.begin(), orig.end(), u[i]);
+    const auto m = std::equal_range(mixed.begin(), mixed.end(), u[i]);
     cnt[i] = (unsigned long long)(r.second - r.first);
+    cnt[U + i] = (unsigned long long)(m.second - m.first);
   }
-  unsigned long long* ds = d.small + 4000;  // |u| <= 32 P <= 2048 entries each way (below dist_agree's words)
+  unsigned long long* ds = nullptr;  // error path only: a scratch of its own (2 |u| <= 4096 entries each way)
+  dalloc(ds, 4 * U);
+  struct Free {
+    unsigned long long*& p;
+    ~Free() { dfree(p); }
+  } free_ds{ds};
   HIPCHECK(hipMemcpyAsync(ds, cnt.data(), 8 * cnt.size(), hipMemcpyHostToDevice, s));
-  cm.allreduce_u64(ds, ds + 2048, cnt.size(), s);
+  cm.allreduce_u64(ds, ds + 2 * U, cnt.size(), s);
   if (c->debug)
-    for (size_t i = 0; i < u.size(); ++i)
-      std::fprintf(stderr, "[s3imph] rank %d stop level %u: leftover hash %016llx occurs %llu times in %llu local keys\n",
-                   d.rank, nl, (unsigned long long)u[i], cnt[i], (unsigned long long)n_local);
-  HIPCHECK(hipMemcpyAsync(cnt.data(), ds + 2048, 8 * cnt.size(), hipMemcpyDeviceToHost, s));
+    for (size_t i = 0; i < U; ++i)
+      std::fprintf(stderr, "[s3imph] rank %d stop level %u: leftover hash %016llx occurs %llu (raw) / %llu (mixed) "
+                   "times in %llu local keys\n", d.rank, nl, (unsigned long long)u[i], cnt[i], cnt[U + i],
+                   (unsigned long long)n_local);
+  HIPCHECK(hipMemcpyAsync(cnt.data(), ds + 2 * U, 8 * cnt.size(), hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   for (unsigned long long v : cnt)
     if (v >= 2) {
