@@ -24,6 +24,7 @@
 
 #include "s3imph_device.h"
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 #include "s3imph_internal.h"
@@ -35,7 +36,7 @@ namespace {
 constexpr int kCB = 1024;             // count block
 constexpr int kH0T = 256;             // k_hash0_pair: threads (2 keys each per round)
 constexpr int kH0B = 32 << 10;        // ... window bytes per round (4 blocks per CU)
-constexpr int kH0Grid = 4096;         // ... blocks: 4 per resident slot, a contiguous key range each
+constexpr int kH0Grid = kH0GridHost;  // ... blocks: 4 per resident slot, a contiguous key range each
 constexpr int kSB = 1024;             // scatter block
 constexpr int kTailT = 1024;          // tail block
 constexpr unsigned kLenBuckets = 256;  // key-length classes (4 B each) of the level-0 hash sort
@@ -287,14 +288,15 @@ __device__ __forceinline__ void r20_split(const R20& r, uint64_t pos_base, uint6
 // but measured slower (C3 3.02 -> 3.51 ms: register spills, the larger rounds' tail).
 //
 // PT (P0 level 0, s3imph_internal.h): the same in-LDS counting sort, by SUPER-TILE (the
-// record's level-0 position >> 14, divided by tps), and the runs go to the super-tiles'
-// per-XCD-shard slots as R20 records (k, f, key index) — the first of P0's two partition
-// passes rides on the hash, whose HBM share is half idle, instead of a k_scatter_res pass
-// that reads kh / fp back (16 B per key written and read again).
+// record's level-0 position >> 14, divided by tps), and each run is appended to the block's
+// OWN region for that super-tile as R20 records (k, f, key index): no global atomic per
+// round (returning slot reservations stalled every round: hash 2.36 -> 4.15 ms on C3), the
+// region fills are written once at the block's end.  The first of P0's two partition passes
+// rides on the hash, whose HBM share is half idle, instead of a pass that reads kh / fp back.
 struct P0Part {
   R20* sup;
-  uint64_t sup_scap;  // records per (super-tile, shard) slot
-  unsigned* scnt;     // slot fills
+  uint64_t reg_cap;  // records per (hash block, super-tile) region
+  unsigned* pcnt;    // region fills, written at each block's end
   unsigned tps, S;
 };
 template <int NT, int BB, bool PF, bool RT = false, bool PT = false>
@@ -323,6 +325,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   __shared__ unsigned r_cnt[RT || PT ? kMaxRanks : 1], r_start[RT || PT ? kMaxRanks : 1];
   __shared__ uint64_t r_base[RT || PT ? kMaxRanks : 1];
   __shared__ unsigned r_over;
+  __shared__ unsigned p_cur[PT ? kMaxRanks : 1];  // PT: this block's fill of each super-tile region
   if (st->skew) return;  // k_hash_count0 hashes skewed sets (and clears the tile state)
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   static_assert(!RT || G * sizeof(Rec) + G <= sizeof(sw), "the route stage aliases the byte window");
@@ -332,6 +335,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   uint32_t p_mul = 0;
   if (PT) {
     if (tid == 0) r_over = 0;
+    if (tid < kMaxRanks) p_cur[tid] = 0;
     r_words = st->words[0];
     r_magic = st->magic[0];
     p_mul = 0xffffffffu / pt.tps + 1;  // exact for (position >> 14) < 2^18, tps <= 2^14
@@ -363,7 +367,10 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
   uint64_t g = (uint64_t)blockIdx.x * per;
   const uint64_t gend = min(n, g + per);
-  if (g >= gend) return;
+  if (g >= gend) {
+    if (PT && tid < pt.S) pt.pcnt[(uint64_t)blockIdx.x * pt.S + tid] = 0;
+    return;
+  }
   const uint64_t end8 = (offsets[n] + 7) & ~7ull;
   bool zero = false;
   // ---- the round at r0: keys r0 + tid and r0 + NT + tid, its window [wlo, wend) in wr
@@ -592,10 +599,10 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
         }
         r_start[tid] = x - c;
         if (c) {
-          const unsigned slot = tid * kResShards + blockIdx.x % kResShards;
-          const unsigned at = atomicAdd(&pt.scnt[slot], c);
-          if (at + c > pt.sup_scap) r_over = 1;
-          r_base[tid] = (uint64_t)slot * pt.sup_scap + at;
+          const unsigned at = p_cur[tid];
+          if (at + c > pt.reg_cap) r_over = 1;
+          p_cur[tid] = at + c;
+          r_base[tid] = ((uint64_t)blockIdx.x * pt.S + tid) * pt.reg_cap + at;
         }
       }
       __syncthreads();
@@ -639,6 +646,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   if (zero) atomicOr(&st->status, kStKeyZero);
   if (RT && tid == 0 && r_over) atomicOr(&st->status, kStRouteOverflow);
   if (PT && tid == 0 && r_over) atomicOr(&st->status, kStOverflow | kStResOverflow);
+  if (PT && tid < pt.S) pt.pcnt[(uint64_t)blockIdx.x * pt.S + tid] = p_cur[tid];  // wave 0 updated p_cur
 }
 
 // ------------------------------------------- level-0 hash, skewed key lengths --------
@@ -1360,25 +1368,36 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
 // Level 0 of a set with more than kP0MinTiles 2^14-position tiles (C3: 12.2k) takes
 // register-resident tiles too, without the split kernel's 2^14 sub-tile scratch round trip:
 // its positions are cut into S super-tiles of tps tiles each (tps <= kT), the level-0 records
-// (R20: k, f, key index) first land in per-(super-tile, XCD shard) slots of `sup` — written by
-// the level-0 hash itself (k_hash0_pair<..., PT>) or, for skewed / unaligned sets, by a
-// k_scatter_res pass over kh / fp — and this kernel gives each super-tile bps blocks that
+// (R20: k, f, key index) first land in the super-tiles: in per-(hash block, super-tile)
+// regions written by the level-0 hash itself (k_hash0_pair<..., PT>), or, for skewed /
+// unaligned sets, in per-(super-tile, XCD shard) slots written by a k_scatter_res pass over
+// kh / fp — and this kernel gives each super-tile bps blocks that
 // scatter its records into the slots of their 2^14-position tiles: an LDS counting sort by
 // tile inside the super-tile's window, one reservation atomic per (round, tile, XCD shard),
 // runs written whole (k_scatter_res's scheme).  A record reads 20 B and writes 20 B here, and
 // k_tile_p0 reads it once more: the 40 B per record of the split kernel's scratch are gone.
+struct P0In {
+  const R20* sup;
+  uint64_t reg_cap;        // regions: records per (hash block, super-tile) region
+  const unsigned* pcnt;    // ... their fills, [hash block][super-tile]
+  unsigned NB, S;          // hash blocks, super-tiles
+  uint64_t slot_cap;       // slots: records per (super-tile, XCD shard) slot
+  const unsigned* scnt;    // ... their fills
+  bool fused;              // the hash wrote regions (unless it found the set skewed)
+};
 template <int kR, int kT>
-__global__ __launch_bounds__(kSB) void k_scatter_p0(const R20* __restrict__ sup, uint64_t sup_scap,
-                                                    const unsigned* __restrict__ scnt, unsigned bps, unsigned tps,
-                                                    R20* __restrict__ bucket, uint64_t bcap, unsigned* __restrict__ tcnt,
+__global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsigned tps, R20* __restrict__ bucket,
+                                                    uint64_t bcap, unsigned* __restrict__ tcnt,
                                                     unsigned long long* __restrict__ flags, LevelState* st) {
   constexpr int kKPT = kR / kSB;
+  constexpr unsigned kMaxRuns = kH0Grid / 4 + 1;  // bps >= 4 (S <= 64 super-tiles over 256 blocks)
   __shared__ uint64_t stage_raw[(kR * 5 + 1) / 2];
   R20* const stage = reinterpret_cast<R20*>(stage_raw);
   __shared__ unsigned short stile[kR];
   __shared__ unsigned cnt[kT];
   __shared__ unsigned start[kT];
   __shared__ unsigned cur[kT];
+  __shared__ unsigned rp[kMaxRuns + 1];  // regions: the block's runs' exclusive prefix
   __shared__ unsigned s_over;
   if (st->status & kStStop) return;
   const unsigned tid = threadIdx.x;
@@ -1397,19 +1416,46 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(const R20* __restrict__ sup,
     if (tid == 0) atomicOr(&st->status, kStGeometry);
     return;
   }
-  // the super-tile's records: its kResShards slots back to back (index j)
+  // This block's records, index j in [lo, hi): the super-tile's kResShards slots back to back
+  // (a skewed set, partitioned by k_scatter_res), or the runs its part of the hash blocks left
+  // in their regions (prefix rp; record j of run i at region (b0 + i, sidx) + j - rp[i]).
+  const bool regions = in.fused && !st->skew;
   unsigned pre[kResShards + 1];
-  pre[0] = 0;
+  uint64_t lo = 0, hi = 0;
+  unsigned b0 = 0, nr = 0;
+  if (regions) {
+    b0 = (unsigned)((uint64_t)in.NB * part / bps);
+    nr = (unsigned)((uint64_t)in.NB * (part + 1) / bps) - b0;
+    const unsigned c = tid < nr ? in.pcnt[(uint64_t)(b0 + tid) * in.S + sidx] : 0u;
+    uint64_t tot;
+    const uint64_t ex = block_exscan<kSB>(c, &tot);
+    if (tid < nr) rp[tid] = (unsigned)ex;
+    if (tid == 0) rp[nr] = (unsigned)tot;
+    hi = tot;
+    __syncthreads();
+  } else {
+    pre[0] = 0;
 #pragma unroll
-  for (int x = 0; x < kResShards; ++x) pre[x + 1] = pre[x] + scnt[sidx * kResShards + x];
-  const uint64_t m = pre[kResShards];
-  const uint64_t lo = m * part / bps, hi = m * (part + 1) / bps;
-  const R20* sbase = sup + (uint64_t)sidx * kResShards * sup_scap;
+    for (int x = 0; x < kResShards; ++x) pre[x + 1] = pre[x] + in.scnt[sidx * kResShards + x];
+    const uint64_t m = pre[kResShards];
+    lo = m * part / bps;
+    hi = m * (part + 1) / bps;
+  }
+  const R20* sbase = in.sup + (uint64_t)sidx * kResShards * in.slot_cap;
   auto src = [&](uint64_t j) -> const R20& {
+    if (regions) {
+      unsigned a = 0, z = nr;  // the run holding j: rp[a] <= j < rp[a + 1]
+      while (z - a > 1) {
+        const unsigned mid = (a + z) >> 1;
+        if (rp[mid] <= (unsigned)j) a = mid;
+        else z = mid;
+      }
+      return in.sup[((uint64_t)(b0 + a) * in.S + sidx) * in.reg_cap + ((unsigned)j - rp[a])];
+    }
     uint64_t o = j;
 #pragma unroll
     for (int x = 1; x < kResShards; ++x)
-      if (j >= pre[x]) o = (uint64_t)x * sup_scap + (j - pre[x]);
+      if (j >= pre[x]) o = (uint64_t)x * in.slot_cap + (j - pre[x]);
     return sbase[o];
   };
   const uint64_t cap = bcap / T, scap = cap / kResShards;
@@ -1442,7 +1488,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(const R20* __restrict__ sup,
       }
     }
     __syncthreads();
-    constexpr int kTPT = (int)(kT / kSB);
+    constexpr int kTPT = (int)((kT + kSB - 1) / kSB);
     unsigned at[kTPT];
 #pragma unroll
     for (int q = 0; q < kTPT; ++q) {
@@ -3839,14 +3885,22 @@ void launch_p0_partition(const BinBuffers& b, const P0Bufs& p, hipStream_t s, bo
                                                         only_skew ? 1u : 0u);
 }
 
+bool p0_fused(const uint8_t* blob, const P0Bufs& p) {
+  return ((uintptr_t)blob & 15) == 0 && p.S <= (unsigned)kMaxRanks;
+}
+uint64_t p0_region_cap(uint64_t n, unsigned S) {
+  const double per = (double)((n + kH0Grid - 1) / kH0Grid), mean = per / S;
+  return (uint64_t)(mean + 10.0 * std::sqrt(mean) + 32.0);
+}
+
 // P0 level 0's hash and first partition: fused (k_hash0_pair<..., PT>) for an aligned blob
 // of up to kMaxRanks super-tiles, with k_hash_skew + the partition pass standing by for a
 // set the device finds skewed; otherwise kh / fp, then the partition pass.
 void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                     const P0Bufs& p, hipStream_t s) {
-  if (((uintptr_t)blob & 15) == 0 && p.S <= (unsigned)kMaxRanks) {
+  if (p0_fused(blob, p)) {
     unsigned long long* prof = b.tile_prof ? b.tile_prof + (uint64_t)(kMaxLevels - 3) * kMaxTiles * 8 : nullptr;
-    const P0Part pt{p.sup, p.sup_cap / ((uint64_t)p.S * kResShards), p.scnt, p.tps, p.S};
+    const P0Part pt{p.sup, p.reg_cap, p.pcnt, p.tps, p.S};
     k_hash0_pair<kH0T, kH0B, true, false, true><<<kH0Grid, kH0T, 0, s>>>(
         blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, Route0{}, pt);
     launch_hash_skew(blob, offsets, n, b, g, prof, s);
@@ -3857,10 +3911,13 @@ void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, co
   launch_p0_partition(b, p, s, false);
 }
 
-void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
+void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStream_t s) {
   const unsigned bps = std::max(1u, 256u / p.S);
-  k_scatter_p0<5120, 1024><<<p.S * bps, kSB, 0, s>>>(p.sup, p.sup_cap / ((uint64_t)p.S * kResShards), p.scnt, bps,
-                                                     p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st);
+  const P0In in{p.sup, p.reg_cap, p.pcnt, (unsigned)kH0Grid, p.S, p.sup_cap / ((uint64_t)p.S * kResShards), p.scnt, fused};
+  if (p.tps <= 256)
+    k_scatter_p0<5120, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st);
+  else
+    k_scatter_p0<5120, 1024><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st);
 }
 
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {

@@ -105,8 +105,9 @@ void free_workspace(s3imph_ctx* c) {
   dfree(c->block_sums); dfree(c->d_st);
   dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
   dfree(c->tcnt);
-  dfree(c->p0_tcnt); dfree(c->p0_flags); dfree(c->p0_scnt);
+  dfree(c->p0_tcnt); dfree(c->p0_flags); dfree(c->p0_scnt); dfree(c->p0_pcnt); dfree(c->p0_sup);
   c->p0_tiles = 0;
+  c->p0_sup_cap = 0;
   dfree(c->tile_prof);
   dfree(c->hist); dfree(c->hoff); dfree(c->tile_start); dfree(c->scan_sums); dfree(c->flags); dfree(c->sflags);
   if (c->h_st) (void)hipHostFree(c->h_st);
@@ -431,21 +432,31 @@ bool hash_only_knob() {
 }
 
 // P0 geometry and buffers for level 0 of n keys (identity positions): T 2^14-position tiles
-// in S super-tiles of tps; the super-tile slots live in list[1] (unused until level 1's tile
-// pass writes its collided records there), the tile slots in the bucket, both as R20.
+// in S super-tiles of tps (about kP0TargetTps; S <= kMaxRanks), the super-tiles' records in
+// c->p0_sup (sized for the hash's per-block regions and for the slot layout of the pass that
+// stands in for it), the tiles' slots in the bucket, both as R20.
 P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, hipStream_t s) {
   const uint64_t T = tiles_of(level_words(n), kRegTileMaxBits, 0);
   P0Bufs p;
-  p.S = (unsigned)((T + kP0MaxTps - 1) / kP0MaxTps);
+  p.S = (unsigned)std::min<uint64_t>((T + kP0TargetTps - 1) / kP0TargetTps, kMaxRanks);
   p.tps = (unsigned)((T + p.S - 1) / p.S);
+  p.reg_cap = p0_region_cap(n, p.S);
+  const uint64_t need = std::max<uint64_t>((uint64_t)kH0GridHost * p.S * p.reg_cap,
+                                           n + n / 4 + (uint64_t)4096 * p.S * kResShards);
+  if (need > c->p0_sup_cap) {
+    dalloc(c->p0_sup, need);
+    c->p0_sup_cap = need;
+  }
   if (T > c->p0_tiles) {
     dalloc(c->p0_tcnt, T * kResShards);
     dalloc(c->p0_flags, T);
-    if (!c->p0_scnt) dalloc(c->p0_scnt, 256 * kResShards);
     c->p0_tiles = T;
   }
-  p.sup = reinterpret_cast<R20*>(c->list[1]);
-  p.sup_cap = c->cap_keys * sizeof(Rec) / sizeof(R20);
+  if (!c->p0_scnt) dalloc(c->p0_scnt, (uint64_t)kMaxRanks * kResShards);
+  if (!c->p0_pcnt) dalloc(c->p0_pcnt, (uint64_t)kH0GridHost * kMaxRanks);
+  p.sup = c->p0_sup;
+  p.sup_cap = c->p0_sup_cap;
+  p.pcnt = c->p0_pcnt;
   p.scnt = c->p0_scnt;
   p.bucket = reinterpret_cast<R20*>(c->bucket);
   p.bucket_cap = c->bucket_cap * sizeof(Rec) / sizeof(R20);
@@ -460,8 +471,9 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
   const BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
   const double q = 1.0 - std::exp(-0.5);
-  if (!conservative && c->p0 && !pos && n <= kP0MaxKeys && !hash_only_knob() &&
-      tiles_of(level_words(n), kRegTileMaxBits, 0) > kP0MinTiles) {
+  const uint64_t T14 = tiles_of(level_words(n), kRegTileMaxBits, 0);
+  if (!conservative && c->p0 && !pos && n <= kP0MaxKeys && !hash_only_knob() && T14 > kP0MinTiles &&
+      T14 <= (uint64_t)kMaxRanks * kP0MaxTps) {
     // level 0 in 2^14-position register tiles through super-tiles (s3imph_internal.h, P0)
     const P0Bufs p = p0_bufs(c, n, s);
     const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
@@ -469,7 +481,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
     ev_mark(c, s, "init");
     launch_p0_hash(blob, offsets, n, b, g0, p, s);
     ev_mark(c, s, "hash_part0");
-    launch_p0_scatter(b, p, s);
+    launch_p0_scatter(b, p, p0_fused(blob, p), s);
     ev_mark(c, s, "scatter0_p0");
     launch_p0_tile(b, p, s);
     ev_mark(c, s, "tile0_p0");

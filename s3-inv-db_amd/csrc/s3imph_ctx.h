@@ -224,6 +224,9 @@ struct s3imph_ctx {
   unsigned* p0_tcnt = nullptr;
   unsigned long long* p0_flags = nullptr;
   unsigned* p0_scnt = nullptr;
+  unsigned* p0_pcnt = nullptr;  // the fused hash's region fills (kH0GridHost x kMaxRanks)
+  s3imph::R20* p0_sup = nullptr;  // the super-tiles' records
+  uint64_t p0_sup_cap = 0;
   bool bm_counts = false;   // S3IMPH_BM_LANES=counts: the bitmap decomposition sums count lanes (A/B knob)
   bool debug = false;
   bool fault_dup = false;   // S3IMPH_FAULT_DUP_REC: test hook, duplicates a record mid-build (fault_dup_record)

@@ -231,6 +231,7 @@ uint64_t split_scratch_records();  // sub-tile segments of the split big-tile ke
 // shard) slots of `sup`, then to per-(tile, shard) slots of `bucket`, then k_tile_reg.
 constexpr uint64_t kP0MinTiles = 2048;
 constexpr uint64_t kP0MaxTps = 1024;
+constexpr uint64_t kP0TargetTps = 192;  // tiles per super-tile aimed at (S <= kMaxRanks keeps the hash's partition)
 constexpr uint64_t kP0MaxKeys = 1ull << 31;  // bucket slot indices stay below 2^32
 // A level-0 record with an identity position: k (2 dwords), f (2), key index i (p = pos_base + i).
 struct R20 {
@@ -238,8 +239,11 @@ struct R20 {
 };
 struct P0Bufs {
   unsigned S = 0, tps = 0;     // super-tiles, 2^14 tiles per super-tile
-  R20* sup = nullptr;          // super-tile slots (S x kResShards slots of sup_cap / (S kResShards) records)
+  R20* sup = nullptr;          // the super-tiles' records: per-(hash block, super-tile) regions of reg_cap
+                               // (fused hash), or S x kResShards slots of sup_cap / (S kResShards) (pass)
   uint64_t sup_cap = 0;        // R20 records in sup
+  uint64_t reg_cap = 0;
+  unsigned* pcnt = nullptr;    // region fills (kH0Grid x S), written by the hash
   unsigned* scnt = nullptr;    // super-tile slot fills (S x kResShards), zeroed before the build
   R20* bucket = nullptr;       // tile slots (T x kResShards)
   uint64_t bucket_cap = 0;     // R20 records in bucket
@@ -250,7 +254,10 @@ void launch_p0_partition(const BinBuffers& b, const P0Bufs& p, hipStream_t s, bo
 // level 0's hash with the first partition fused in where it can be (else hash, then partition)
 void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                     const P0Bufs& p, hipStream_t s);
-void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
+void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStream_t s);
+bool p0_fused(const uint8_t* blob, const P0Bufs& p);  // the hash partitions (aligned blob, S <= kMaxRanks)
+uint64_t p0_region_cap(uint64_t n, unsigned S);     // records per (hash block, super-tile) region
+constexpr int kH0GridHost = 4096;                    // = k_hash0_pair's grid (kH0Grid)
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
 void binned_set_lds_limits();
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
