@@ -1388,9 +1388,10 @@ struct P0In {
 template <int kR, int kT>
 __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsigned tps, R20* __restrict__ bucket,
                                                     uint64_t bcap, unsigned* __restrict__ tcnt,
-                                                    unsigned long long* __restrict__ flags, LevelState* st) {
+                                                    unsigned long long* __restrict__ flags, LevelState* st,
+                                                    unsigned long long* __restrict__ prof) {
   constexpr int kKPT = kR / kSB;
-  constexpr unsigned kMaxRuns = kH0Grid / 4 + 1;  // bps >= 4 (S <= 64 super-tiles over 256 blocks)
+  constexpr unsigned kMaxRuns = kH0Grid / 8 + 1;  // bps >= 8 (S <= kP0MaxS = 32 super-tiles over 256 blocks)
   __shared__ uint64_t stage_raw[(kR * 5 + 1) / 2];
   R20* const stage = reinterpret_cast<R20*>(stage_raw);
   __shared__ unsigned short stile[kR];
@@ -1442,7 +1443,9 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
     hi = m * (part + 1) / bps;
   }
   const R20* sbase = in.sup + (uint64_t)sidx * kResShards * in.slot_cap;
-  auto src = [&](uint64_t j) -> const R20& {
+  // record j's address (the loads themselves run in straight-line code: a load inside the
+  // search's divergent branches was waited for on the spot, five HBM latencies per round)
+  auto src = [&](uint64_t j) -> const R20* {
     if (regions) {
       unsigned a = 0, z = nr;  // the run holding j: rp[a] <= j < rp[a + 1]
       while (z - a > 1) {
@@ -1450,26 +1453,50 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
         if (rp[mid] <= (unsigned)j) a = mid;
         else z = mid;
       }
-      return in.sup[((uint64_t)(b0 + a) * in.S + sidx) * in.reg_cap + ((unsigned)j - rp[a])];
+      return in.sup + ((uint64_t)(b0 + a) * in.S + sidx) * in.reg_cap + ((unsigned)j - rp[a]);
     }
     uint64_t o = j;
 #pragma unroll
     for (int x = 1; x < kResShards; ++x)
       if (j >= pre[x]) o = (uint64_t)x * in.slot_cap + (j - pre[x]);
-    return sbase[o];
+    return sbase + o;
+  };
+  // records live as (dwords 0-3, dword 4) register pairs: an R20[] copied whole into the stage
+  // stayed a memory array (its f / i words spilled to LDS and scratch, each load waited for)
+  uint4 rq[kKPT];
+  uint32_t rz[kKPT];
+  auto fetch = [&](uint64_t r) {
+    const uint32_t* a[kKPT];
+#pragma unroll
+    for (int u = 0; u < kKPT; ++u) {
+      const uint64_t j = r + (uint64_t)u * kSB + tid;
+      a[u] = (j < hi ? src(j) : in.sup)->w;  // (a past-the-end lane reads record 0; trk skips it)
+    }
+#pragma unroll
+    for (int u = 0; u < kKPT; ++u) {
+      rq[u] = *reinterpret_cast<const uint4*>(a[u]);  // dword-aligned 16-B load
+      rz[u] = a[u][4];
+    }
   };
   const uint64_t cap = bcap / T, scap = cap / kResShards;
   const unsigned shard = blockIdx.x % kResShards;
   const uint64_t seed = level_seed(0);
   uint64_t r0 = lo;
   if (r0 >= hi) return;
-  R20 rr[kKPT];
-#pragma unroll
-  for (int u = 0; u < kKPT; ++u) {
-    const uint64_t j = r0 + (uint64_t)u * kSB + tid;
-    rr[u] = R20{{0, 0, 0, 0, 0}};
-    if (j < hi) rr[u] = src(j);
-  }
+  // debug: phase times summed over the block's rounds, k_scatter_res's row 32 (level 0) layout
+  unsigned long long* tp = prof && blockIdx.x < kMaxTiles ? prof + ((uint64_t)32 * kMaxTiles + blockIdx.x) * 8 : nullptr;
+  unsigned long long t_last = 0, t_first = 0, acc[4] = {0, 0, 0, 0};
+#define P0PROF(i)                                                      \
+  do {                                                                 \
+    if (tp && tid == 0) {                                              \
+      const unsigned long long now_ = wall_clock64();                  \
+      if ((i) == 0) t_first = now_;                                    \
+      else acc[(i) > 0 ? (i) - 1 : 0] += now_ - t_last;                \
+      t_last = now_;                                                   \
+    }                                                                  \
+  } while (0)
+  P0PROF(0);
+  fetch(r0);
   for (unsigned t = tid; t < kT; t += kSB) cnt[t] = 0;
   if (tid == 0) s_over = 0;
   __syncthreads();
@@ -1481,13 +1508,14 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
       const uint64_t j = r0 + (uint64_t)u * kSB + tid;
       trk[u] = 0xffffffffu;
       if (j < hi) {
-        const uint64_t k = (uint64_t)rr[u].w[0] | ((uint64_t)rr[u].w[1] << 32);
+        const uint64_t k = (uint64_t)rq[u].x | ((uint64_t)rq[u].y << 32);
         const uint64_t t = (bb_index(seed, k, words, magic) >> kRegTileMaxBits) - t0;
         if (t < tn) trk[u] = ((unsigned)t << 13) | atomicAdd(&cnt[t], 1u);
         else geo = true;
       }
     }
     __syncthreads();
+    P0PROF(1);
     constexpr int kTPT = (int)((kT + kSB - 1) / kSB);
     unsigned at[kTPT];
 #pragma unroll
@@ -1511,22 +1539,23 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
       }
     }
     __syncthreads();  // start[] complete
+    P0PROF(2);
 #pragma unroll
     for (int u = 0; u < kKPT; ++u) {
       if (trk[u] != 0xffffffffu) {
         const unsigned t = trk[u] >> 13, slot = start[t] + (trk[u] & 8191u);
-        stage[slot] = rr[u];
+        uint32_t* d = stage[slot].w;
+        d[0] = rq[u].x;
+        d[1] = rq[u].y;
+        d[2] = rq[u].z;
+        d[3] = rq[u].w;
+        d[4] = rz[u];
         stile[slot] = (unsigned short)t;
       }
     }
     const unsigned mr = (unsigned)tot;
     r0 += kR;
     const bool more = r0 < hi;
-#pragma unroll
-    for (int u = 0; u < kKPT; ++u) {
-      const uint64_t j = r0 + (uint64_t)u * kSB + tid;
-      if (j < hi) rr[u] = src(j);
-    }
 #pragma unroll
     for (int q = 0; q < kTPT; ++q) {
       const unsigned t = (unsigned)q * kSB + tid;
@@ -1537,16 +1566,30 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
       }
     }
     __syncthreads();
+    P0PROF(3);
     if (s_over) break;
     for (unsigned j = tid; j < mr; j += kSB) {
       const unsigned t = stile[j];
       bucket[cur[t] + (j - start[t])] = stage[j];
     }
+    // The next round's records, in flight over the barriers below.  (Issued before the write
+    // above, they were waited for at once: a 64-bit address write to a VGPR pair that a
+    // pending load still read, s_waitcnt vmcnt(0), in the store's address computation.)
+    if (more) fetch(r0);
+
     __syncthreads();
+    P0PROF(4);
     if (!more) break;
     for (unsigned t = tid; t < tn; t += kSB) cnt[t] = 0;
     __syncthreads();
   }
+  if (tp && tid == 0) {
+    unsigned long long c = t_first;
+    tp[0] = c;
+    for (int i = 0; i < 4; ++i) tp[i + 1] = (c += acc[i]);
+    tp[7] = c;
+  }
+#undef P0PROF
   if (geo) atomicOr(&st->status, kStGeometry);
   if (s_over && tid == 0) atomicOr(&st->status, kStOverflow | kStResOverflow);
 }
@@ -3915,9 +3958,11 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
   const unsigned bps = std::max(1u, 256u / p.S);
   const P0In in{p.sup, p.reg_cap, p.pcnt, (unsigned)kH0Grid, p.S, p.sup_cap / ((uint64_t)p.S * kResShards), p.scnt, fused};
   if (p.tps <= 256)
-    k_scatter_p0<5120, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st);
+    k_scatter_p0<5120, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+  else if (p.tps <= 512)
+    k_scatter_p0<5120, 512><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
   else
-    k_scatter_p0<5120, 1024><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st);
+    k_scatter_p0<5120, 1024><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
 }
 
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {

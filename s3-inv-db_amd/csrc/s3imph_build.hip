@@ -432,13 +432,13 @@ bool hash_only_knob() {
 }
 
 // P0 geometry and buffers for level 0 of n keys (identity positions): T 2^14-position tiles
-// in S super-tiles of tps (about kP0TargetTps; S <= kMaxRanks), the super-tiles' records in
+// in S super-tiles of tps (about kP0TargetTps; S <= kP0MaxS), the super-tiles' records in
 // c->p0_sup (sized for the hash's per-block regions and for the slot layout of the pass that
 // stands in for it), the tiles' slots in the bucket, both as R20.
 P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, hipStream_t s) {
   const uint64_t T = tiles_of(level_words(n), kRegTileMaxBits, 0);
   P0Bufs p;
-  p.S = (unsigned)std::min<uint64_t>((T + kP0TargetTps - 1) / kP0TargetTps, kMaxRanks);
+  p.S = (unsigned)std::min<uint64_t>((T + kP0TargetTps - 1) / kP0TargetTps, kP0MaxS);
   p.tps = (unsigned)((T + p.S - 1) / p.S);
   p.reg_cap = p0_region_cap(n, p.S);
   const uint64_t need = std::max<uint64_t>((uint64_t)kH0GridHost * p.S * p.reg_cap,
@@ -473,7 +473,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   const double q = 1.0 - std::exp(-0.5);
   const uint64_t T14 = tiles_of(level_words(n), kRegTileMaxBits, 0);
   if (!conservative && c->p0 && !pos && n <= kP0MaxKeys && !hash_only_knob() && T14 > kP0MinTiles &&
-      T14 <= (uint64_t)kMaxRanks * kP0MaxTps) {
+      T14 <= kP0MaxS * kP0MaxTps) {
     // level 0 in 2^14-position register tiles through super-tiles (s3imph_internal.h, P0)
     const P0Bufs p = p0_bufs(c, n, s);
     const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);

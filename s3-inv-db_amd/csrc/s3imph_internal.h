@@ -231,7 +231,11 @@ uint64_t split_scratch_records();  // sub-tile segments of the split big-tile ke
 // shard) slots of `sup`, then to per-(tile, shard) slots of `bucket`, then k_tile_reg.
 constexpr uint64_t kP0MinTiles = 2048;
 constexpr uint64_t kP0MaxTps = 1024;
-constexpr uint64_t kP0TargetTps = 192;  // tiles per super-tile aimed at (S <= kMaxRanks keeps the hash's partition)
+constexpr uint64_t kP0TargetTps = 192;  // tiles per super-tile aimed at
+// at most 32 super-tiles: k_scatter_p0 gives each one 256 / S >= 8 blocks, so the records of
+// a tile arrive through all kResShards XCD shards (4 blocks per super-tile filled only 4 of a
+// tile's 8 shard slots: twice their capacity on average, C3 overflowed into the rerun)
+constexpr uint64_t kP0MaxS = 32;
 constexpr uint64_t kP0MaxKeys = 1ull << 31;  // bucket slot indices stay below 2^32
 // A level-0 record with an identity position: k (2 dwords), f (2), key index i (p = pos_base + i).
 struct R20 {
