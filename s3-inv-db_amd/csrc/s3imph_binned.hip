@@ -1385,12 +1385,12 @@ struct P0In {
   const unsigned* scnt;    // ... their fills
   bool fused;              // the hash wrote regions (unless it found the set skewed)
 };
-template <int kR, int kT>
-__global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsigned tps, R20* __restrict__ bucket,
+template <int kR, int kT, int NT = kSB>  // (512 threads, 2560-record rounds, two blocks per CU: slower)
+__global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsigned tps, R20* __restrict__ bucket,
                                                     uint64_t bcap, unsigned* __restrict__ tcnt,
                                                     unsigned long long* __restrict__ flags, LevelState* st,
                                                     unsigned long long* __restrict__ prof) {
-  constexpr int kKPT = kR / kSB;
+  constexpr int kKPT = kR / NT;
   constexpr unsigned kMaxRuns = kH0Grid / 8 + 1;  // bps >= 8 (S <= kP0MaxS = 32 super-tiles over 256 blocks)
   __shared__ uint64_t stage_raw[(kR * 5 + 1) / 2];
   R20* const stage = reinterpret_cast<R20*>(stage_raw);
@@ -1408,7 +1408,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
     st->ntiles[0] = T;
     st->nchunks[0] = 0;
   }
-  for (uint64_t t = (uint64_t)blockIdx.x * kSB + tid; t < T; t += (uint64_t)gridDim.x * kSB) flags[t] = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * NT + tid; t < T; t += (uint64_t)gridDim.x * NT) flags[t] = 0;
   const unsigned sidx = blockIdx.x / bps, part = blockIdx.x % bps;
   const uint64_t t0 = (uint64_t)sidx * tps;
   if (t0 >= T) return;
@@ -1427,9 +1427,13 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
   if (regions) {
     b0 = (unsigned)((uint64_t)in.NB * part / bps);
     nr = (unsigned)((uint64_t)in.NB * (part + 1) / bps) - b0;
+    if (nr > (unsigned)NT || nr > kMaxRuns) {  // (the host keeps bps >= NB / NT)
+      if (tid == 0) atomicOr(&st->status, kStGeometry);
+      return;
+    }
     const unsigned c = tid < nr ? in.pcnt[(uint64_t)(b0 + tid) * in.S + sidx] : 0u;
     uint64_t tot;
-    const uint64_t ex = block_exscan<kSB>(c, &tot);
+    const uint64_t ex = block_exscan<NT>(c, &tot);
     if (tid < nr) rp[tid] = (unsigned)ex;
     if (tid == 0) rp[nr] = (unsigned)tot;
     hi = tot;
@@ -1469,7 +1473,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
     const uint32_t* a[kKPT];
 #pragma unroll
     for (int u = 0; u < kKPT; ++u) {
-      const uint64_t j = r + (uint64_t)u * kSB + tid;
+      const uint64_t j = r + (uint64_t)u * NT + tid;
       a[u] = (j < hi ? src(j) : in.sup)->w;  // (a past-the-end lane reads record 0; trk skips it)
     }
 #pragma unroll
@@ -1497,7 +1501,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
   } while (0)
   P0PROF(0);
   fetch(r0);
-  for (unsigned t = tid; t < kT; t += kSB) cnt[t] = 0;
+  for (unsigned t = tid; t < kT; t += NT) cnt[t] = 0;
   if (tid == 0) s_over = 0;
   __syncthreads();
   bool geo = false;
@@ -1505,7 +1509,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
     unsigned trk[kKPT];  // tile in the window << 13 | rank in the round's run of that tile
 #pragma unroll
     for (int u = 0; u < kKPT; ++u) {
-      const uint64_t j = r0 + (uint64_t)u * kSB + tid;
+      const uint64_t j = r0 + (uint64_t)u * NT + tid;
       trk[u] = 0xffffffffu;
       if (j < hi) {
         const uint64_t k = (uint64_t)rq[u].x | ((uint64_t)rq[u].y << 32);
@@ -1516,11 +1520,11 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
     }
     __syncthreads();
     P0PROF(1);
-    constexpr int kTPT = (int)((kT + kSB - 1) / kSB);
+    constexpr int kTPT = (int)((kT + NT - 1) / NT);
     unsigned at[kTPT];
 #pragma unroll
     for (int q = 0; q < kTPT; ++q) {
-      const unsigned t = (unsigned)q * kSB + tid;
+      const unsigned t = (unsigned)q * NT + tid;
       const unsigned c = t < tn ? cnt[t] : 0u;
       at[q] = 0;
       if (c) at[q] = atomicAdd(&tcnt[(t0 + t) * kResShards + shard], c);
@@ -1530,7 +1534,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
 #pragma unroll
     for (int q = 0; q < kTPT; ++q) sum += tb0 + q < tn ? cnt[tb0 + q] : 0u;
     uint64_t tot;
-    uint64_t ex = block_exscan<kSB>(sum, &tot);
+    uint64_t ex = block_exscan<NT>(sum, &tot);
 #pragma unroll
     for (int q = 0; q < kTPT; ++q) {
       if (tb0 + q < tn) {
@@ -1558,7 +1562,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
     const bool more = r0 < hi;
 #pragma unroll
     for (int q = 0; q < kTPT; ++q) {
-      const unsigned t = (unsigned)q * kSB + tid;
+      const unsigned t = (unsigned)q * NT + tid;
       const unsigned c = t < tn ? cnt[t] : 0u;
       if (c) {
         if (at[q] + c > scap) s_over = 1;
@@ -1568,7 +1572,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
     __syncthreads();
     P0PROF(3);
     if (s_over) break;
-    for (unsigned j = tid; j < mr; j += kSB) {
+    for (unsigned j = tid; j < mr; j += NT) {
       const unsigned t = stile[j];
       bucket[cur[t] + (j - start[t])] = stage[j];
     }
@@ -1580,7 +1584,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_p0(P0In in, unsigned bps, unsig
     __syncthreads();
     P0PROF(4);
     if (!more) break;
-    for (unsigned t = tid; t < tn; t += kSB) cnt[t] = 0;
+    for (unsigned t = tid; t < tn; t += NT) cnt[t] = 0;
     __syncthreads();
   }
   if (tp && tid == 0) {
@@ -3955,8 +3959,8 @@ void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, co
 }
 
 void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStream_t s) {
-  const unsigned bps = std::max(1u, 256u / p.S);
   const P0In in{p.sup, p.reg_cap, p.pcnt, (unsigned)kH0Grid, p.S, p.sup_cap / ((uint64_t)p.S * kResShards), p.scnt, fused};
+  const unsigned bps = std::max(1u, 256u / p.S);
   if (p.tps <= 256)
     k_scatter_p0<5120, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
   else if (p.tps <= 512)

@@ -284,20 +284,29 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const Rec* __re
 #pragma unroll
     for (int k = 0; k <= kResShards; ++k) fo[k] = s_fo[k];
     const uint64_t t0 = t << tb;
-    for (unsigned i0 = 0; i0 < fo[kResShards]; i0 += kTT * kU) {
-      uint64_t kk[kU];
+    const unsigned nrec = fo[kResShards];
+    // the next kTT * kU records load while this batch is marked (loads straight-line, the
+    // index clamped instead of guarded)
+    uint64_t kk[kU], kn[kU];
+    auto ld = [&](unsigned i0, uint64_t (&dst)[kU]) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) dst[u] = bucket[rec_index(min(i0 + u * kTT + tid, nrec - 1), fo, t * cap, scap)].k;
+    };
+    if (nrec) ld(0, kk);
+    for (unsigned i0 = 0; i0 < nrec; i0 += kTT * kU) {
+      const bool nx = i0 + kTT * kU < nrec;
+      if (nx) ld(i0 + kTT * kU, kn);
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const unsigned i = i0 + u * kTT + tid;
-        kk[u] = i < fo[kResShards] ? bucket[rec_index(i, fo, t * cap, scap)].k : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        if (i0 + u * kTT + tid < fo[kResShards]) {
+        if (i0 + u * kTT + tid < nrec) {
           const uint64_t lx = bb_index(seed, kk[u], words, magic) - t0;
           const uint32_t bit = 1u << (lx & 31);
           if (atomicOr(&sA[lx >> 5], bit) & bit) atomicOr(&sC[lx >> 5], bit);
         }
+      }
+      if (nx) {
+#pragma unroll
+        for (int u = 0; u < kU; ++u) kk[u] = kn[u];
       }
     }
     __syncthreads();
@@ -452,16 +461,17 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const Rec* __
 #pragma unroll
     for (int k = 0; k <= kResShards; ++k) fo[k] = s_fo[k];
     const uint64_t t0 = t << tb, pb = base + s_tg, ob = s_ta, nb = s_nb;
-    for (unsigned i0 = 0; i0 < fo[kResShards]; i0 += kTT * kU) {
+    const unsigned nrec = fo[kResShards];
+    for (unsigned i0 = 0; i0 < nrec; i0 += kTT * kU) {
       Rec r[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const unsigned i = i0 + u * kTT + tid;
-        if (i < fo[kResShards]) r[u] = bucket[rec_index(i, fo, t * cap, scap)];
+        if (i < nrec) r[u] = bucket[rec_index(i, fo, t * cap, scap)];
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        if (i0 + u * kTT + tid >= fo[kResShards]) continue;
+        if (i0 + u * kTT + tid >= nrec) continue;
         const uint64_t lx = bb_index(seed, r[u].k, words, magic) - t0;
         const unsigned j = (unsigned)(lx >> 6), b = (unsigned)(lx & 63), grp = j / kGrp;
         const uint64_t below = (1ull << b) - 1ull, v = sg[j];

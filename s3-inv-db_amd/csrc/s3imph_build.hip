@@ -1447,6 +1447,18 @@ void free_bm_workspace(DistState& d) {
   d.bm_cap_out = 0;
 }
 
+// Tile count a bitmap level aims at (A/B knob S3IMPH_BM_TILES).  Fewer, larger tiles suit
+// the reservation scatter (C3 level 0: 3052 tiles of 2^16 take its 4096-tile form, 1.66 ms;
+// 763 of 2^18 the 1024-tile form, 0.99 ms) but not the settle, whose random writes by rank
+// spread over a 4x larger window per tile (1.88 -> 3.64 ms).
+uint64_t bm_target_tiles() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("S3IMPH_BM_TILES");
+    return e ? std::max<uint64_t>(64, std::strtoull(e, nullptr, 10)) : kScatterTiles;
+  }();
+  return v;
+}
+
 int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                         uint64_t n_local, uint64_t key_base, uint64_t N, uint64_t* fp_out, uint64_t* pos_out,
                         uint64_t out_cap, hipStream_t s, s3imph_build_info* info, std::string* msg) {
@@ -1506,9 +1518,9 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   int L = 0;
   for (;;) {
     const uint64_t wmax = level_words((uint64_t)std::ceil(nb)), S = (wmax + P - 1) / P, wpad = S * (uint64_t)P;
-    // tiles of 2^tb positions: the smallest tile leaving at most kScatterTiles tiles
+    // tiles of 2^tb positions: the smallest tile leaving at most bm_target_tiles() tiles
     unsigned tb = kBmMinTb;
-    while (tb < kBmMaxTb && tiles_of(wmax, tb, 0) > kScatterTiles) ++tb;
+    while (tb < kBmMaxTb && tiles_of(wmax, tb, 0) > bm_target_tiles()) ++tb;
     const uint64_t tiles = tiles_of(wmax, tb, 0);
     if (tiles > kScatterTiles) return kDistRetry;  // > 2^30 positions: the routed build (same on every rank)
     if (L > 0) launch_dist_setup(st, L, d.gslot + L, 0, R, P, s);
@@ -1520,7 +1532,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     g.chunk = kTargetChunks;
     g.ts = 0;
     const int gsr = (int)std::max<uint64_t>(1, std::min<uint64_t>((np + kSubRound - 1) / kSubRound, 256));
-    launch_binned_scatter_res(L, bs, g, gsr, s);
+    launch_binned_scatter_res(L, bs, g, gsr, s, 0, 0, tiles);
     const unsigned* tc = c->tcnt + (uint64_t)L * kTcntStride;
     launch_bm_tile_mark(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, lanes, S, s);
     if (lanes == kBmPlanes) {
@@ -1882,7 +1894,8 @@ void staged_d2h(s3imph_ctx* c, const std::vector<D2HJob>& jobs) {
     if (!e.empty()) throw Fail{S3IMPH_ERR_HIP, e};
 }
 
-void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias, int conv) {
+void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias, int conv,
+                 std::atomic<bool>* wide) {
   if (!bytes) return;
   if (!h2d) return staged_d2h(c, {D2HJob{dst, src, bytes, conv}});
   // Pageable H2D through the runtime already runs at the PCIe rate (C2: 400 MB in
@@ -1909,6 +1922,20 @@ void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t b
             const uint64_t* s64 = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(src) + 2 * off);
             uint32_t* d32 = static_cast<uint32_t*>(g.pin[w][b]);
             for (uint64_t i = 0; i < len / 4; ++i) d32[i] = (uint32_t)(s64[i] - bias);
+          } else if (conv == 3) {  // u64 offsets -> u16 key lengths (src holds one more word)
+            const uint64_t* s64 = reinterpret_cast<const uint64_t*>(src) + off / 2;
+            uint16_t* d16 = static_cast<uint16_t*>(g.pin[w][b]);
+            uint64_t over = 0;
+            for (uint64_t i = 0; i < len / 2; ++i) {
+              const uint64_t l = s64[i + 1] - s64[i];
+              over |= l >> 16;
+              d16[i] = (uint16_t)l;
+            }
+            if (over) {
+              wide->store(true);
+              break;
+            }
+            if (wide->load(std::memory_order_relaxed)) break;
           } else if (bias) {
             const uint64_t* s64 = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(src) + off);
             uint64_t* d64 = static_cast<uint64_t*>(g.pin[w][b]);
@@ -1932,6 +1959,15 @@ void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t b
   for (auto& t : th) t.join();
   for (const auto& e : errs)
     if (!e.empty()) throw Fail{S3IMPH_ERR_HIP, e};
+}
+
+// S3IMPH_OFF16=0: offsets cross PCIe as before (u32 / u64), the A/B reference
+bool off16_disabled() {
+  static const bool off = [] {
+    const char* e = std::getenv("S3IMPH_OFF16");
+    return e && std::atoi(e) == 0;
+  }();
+  return off;
 }
 
 // Host-memory build through the device path (used by s3imph_build_host and the builder).
@@ -1963,14 +1999,21 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
     hipStream_t s = c->own_stream;
     HIPCHECK(hipStreamSynchronize(s));  // staging buffers may be in use by the last build
     const auto t0 = clk::now();
-    // offsets cross PCIe as u32 when the blob is under 4 GiB (widened on the device, in
-    // s_fp's space: the build writes s_fp only later on the same stream); their rebasing /
-    // narrowing and pinned copies run on a second thread beside the blob's runtime copy
+    // Offsets cross PCIe as u16 key lengths (2 B per key: C3's 800 MB of u64 offsets become
+    // 200 MB) and are rebuilt on the device by a scan; a key longer than 65535 B sends them
+    // as u32 (blob under 4 GiB, widened on the device) or u64 instead.  Staged in s_fp's
+    // space (the build writes s_fp only later on the same stream); the conversion and pinned
+    // copies run on a second thread beside the blob's runtime copy.
     const bool off32 = nbytes < (1ull << 32);
     uint32_t* tmp32 = reinterpret_cast<uint32_t*>(c->s_fp);
+    uint16_t* tmp16 = reinterpret_cast<uint16_t*>(c->s_fp);
+    uint64_t* sums16 = c->s_fp + (2 * n + 255) / 256 * 32;  // after the lengths, 256-B aligned
+    std::atomic<bool> wide{off16_disabled()};
     Fail off_err{S3IMPH_OK, ""};
     std::thread toff([&]() {
       try {
+        if (!wide.load()) staged_copy(c, true, tmp16, offsets, n * 2, 0, 3, &wide);
+        if (!wide.load()) return;
         if (off32) staged_copy(c, true, tmp32, offsets, (n + 1) * 4, b0, 1);
         else staged_copy(c, true, c->s_offsets, offsets, (n + 1) * 8, b0);
       } catch (const Fail& f) {
@@ -1985,7 +2028,8 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
     }
     toff.join();
     if (off_err.code != S3IMPH_OK) throw off_err;
-    if (off32) launch_widen32(tmp32, c->s_offsets, n + 1, s);
+    if (!wide.load()) launch_len16_offsets(tmp16, n, sums16, c->s_offsets, s);
+    else if (off32) launch_widen32(tmp32, c->s_offsets, n + 1, s);
     if (pos) staged_copy(c, true, c->s_pos, pos, n * 8);
     const auto t1 = clk::now();
     s3imph_build_info info;
@@ -1993,27 +2037,53 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
                           &info, msg);
     if (rc != S3IMPH_OK) return rc;
     const auto t2 = clk::now();
-    // both output arrays in one pass over the pinned workers (identity positions are < n <
-    // 2^32: u32 over PCIe, narrowed into the offsets' space, which is free now)
-    if (!pos) {
-      uint32_t* pos32 = reinterpret_cast<uint32_t*>(c->s_offsets);
-      launch_narrow32(c->s_posout, pos32, n, s);
-      HIPCHECK(hipStreamSynchronize(s));
-      staged_d2h(c, {D2HJob{fp_out, c->s_fp, n * 8, 0}, D2HJob{pos_out, pos32, n * 4, 2}});
-    } else {
-      staged_d2h(c, {D2HJob{fp_out, c->s_fp, n * 8, 0}, D2HJob{pos_out, c->s_posout, n * 8, 0}});
+    // mph.bin (level words D2H into fresh pageable pages: ~9 ms at C3) is marshalled on a
+    // second thread while the output arrays stream back (ctx mutex held by this call)
+    std::string mmsg;
+    int mrc = S3IMPH_OK;
+    clk::time_point t3m;
+    std::thread tm([&]() {
+      try {
+        HIPCHECK(hipSetDevice(c->device));
+        mph->resize(info.mph_bin_len);
+        uint64_t len = 0;
+        mrc = marshal_locked(c, mph->data(), mph->size(), &len, &mmsg);
+      } catch (const Fail& f) {
+        mrc = f.code;
+        mmsg = f.msg;
+      } catch (const std::bad_alloc&) {
+        mrc = S3IMPH_ERR_NOMEM;
+        mmsg = "out of host memory";
+      }
+      t3m = clk::now();
+    });
+    try {
+      // both output arrays in one pass over the pinned workers (identity positions are < n <
+      // 2^32: u32 over PCIe, narrowed into the offsets' space, which is free now)
+      if (!pos) {
+        uint32_t* pos32 = reinterpret_cast<uint32_t*>(c->s_offsets);
+        launch_narrow32(c->s_posout, pos32, n, s);
+        HIPCHECK(hipStreamSynchronize(s));
+        staged_d2h(c, {D2HJob{fp_out, c->s_fp, n * 8, 0}, D2HJob{pos_out, pos32, n * 4, 2}});
+      } else {
+        staged_d2h(c, {D2HJob{fp_out, c->s_fp, n * 8, 0}, D2HJob{pos_out, c->s_posout, n * 8, 0}});
+      }
+    } catch (...) {
+      tm.join();
+      throw;
     }
     const auto t3 = clk::now();
-    mph->resize(info.mph_bin_len);
-    uint64_t len = 0;
-    // ctx mutex already held: marshal inline.
-    rc = marshal_locked(c, mph->data(), mph->size(), &len, msg);
+    tm.join();
+    if (mrc != S3IMPH_OK) *msg = mmsg;
     if (c->debug) {
       auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
-      std::fprintf(stderr, "[s3imph] host build: entry %.2f, h2d %.2f ms, build %.2f ms, d2h %.2f ms, marshal %.2f ms\n",
-                   ms(t0 - te), ms(t1 - t0), ms(t2 - t1), ms(t3 - t2), ms(clk::now() - t3));
+      std::fprintf(stderr,
+                   "[s3imph] host build: entry %.2f, h2d %.2f ms (offsets as %s), build %.2f ms, d2h %.2f ms, "
+                   "marshal ends %.2f ms after the build (beside the d2h), join %.2f ms\n",
+                   ms(t0 - te), ms(t1 - t0), wide.load() ? (off32 ? "u32" : "u64") : "u16 lengths", ms(t2 - t1),
+                   ms(t3 - t2), ms(t3m - t2), ms(clk::now() - t3));
     }
-    return rc;
+    return mrc;
   } catch (const Fail& f) {
     *msg = f.msg;
     return f.code;

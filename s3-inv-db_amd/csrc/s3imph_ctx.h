@@ -268,11 +268,16 @@ int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
 uint64_t dist_out_cap(const s3imph_ctx* c, uint64_t n_global);
 // Chunked host <-> device copy through the ctx's pinned stager (h2d: device dst <- host src;
 // with `bias`, src holds u64 words stored minus bias).
-// conv 1: host u64 -> device u32 (h2d), conv 2: device u32 -> host u64 (d2h); `bytes` are device bytes.
+// conv 1: host u64 -> device u32 (h2d), conv 2: device u32 -> host u64 (d2h), conv 3: host
+// u64 offsets -> device u16 key lengths (h2d; a length past 65535 sets *wide and stops the
+// copy); `bytes` are device bytes.
 void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t bytes, uint64_t bias = 0,
-                 int conv = 0);
+                 int conv = 0, std::atomic<bool>* wide = nullptr);
 void launch_widen32(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);
 void launch_narrow32(const uint64_t* in, uint32_t* out, uint64_t n, hipStream_t s);
+// u16 key lengths -> u64 offsets (n + 1 of them); sums: len16_scratch_words(n) words
+uint64_t len16_scratch_words(uint64_t n);
+void launch_len16_offsets(const uint16_t* len, uint64_t n, uint64_t* sums, uint64_t* out, hipStream_t s);
 // FNV-1a of keys [0, n) into out (the error path's recount of the original key hashes)
 void launch_key_hashes(const uint8_t* blob, const uint64_t* offsets, uint64_t n, uint64_t* out, hipStream_t s);
 int marshal_locked(s3imph_ctx* c, uint8_t* out, uint64_t cap, uint64_t* len, std::string* msg);

@@ -249,6 +249,87 @@ __global__ __launch_bounds__(256) void k_narrow32(const uint64_t* __restrict__ i
     out[i] = (uint32_t)in[i];
 }
 
+// Key lengths (u16, the host's narrowest form of the offsets: 2 B per key over PCIe instead
+// of 4 or 8) back to offsets: offsets[0] = 0, offsets[i + 1] = offsets[i] + len[i].  Three
+// passes over 16384-key blocks: block sums, one-block scan of the sums, block-local scans.
+constexpr int kLsT = 1024, kLsPer = 16;
+constexpr uint64_t kLsBlock = (uint64_t)kLsT * kLsPer;
+__device__ __forceinline__ uint64_t ls_block_exscan(uint64_t v, uint64_t* total) {
+  __shared__ uint64_t s_w[kLsT / 64];
+  const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d);
+    if (lane >= (unsigned)d) x += y;
+  }
+  if (lane == 63) s_w[wave] = x;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kLsT / 64; ++w) {
+    if ((unsigned)w < wave) pre += s_w[w];
+    tot += s_w[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+// a thread's 16 consecutive lengths (two 16-byte loads when the block is whole)
+__device__ __forceinline__ void ls_load(const uint16_t* __restrict__ len, uint64_t n, uint64_t i0, unsigned (&v)[kLsPer]) {
+  if (i0 + kLsPer <= n) {
+    const uint4 a = *reinterpret_cast<const uint4*>(len + i0), b = *reinterpret_cast<const uint4*>(len + i0 + 8);
+    const unsigned w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      v[2 * q] = w[q] & 0xffffu;
+      v[2 * q + 1] = w[q] >> 16;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kLsPer; ++q) v[q] = i0 + q < n ? len[i0 + q] : 0u;
+  }
+}
+__global__ __launch_bounds__(kLsT) void k_len_sums(const uint16_t* __restrict__ len, uint64_t n,
+                                                   uint64_t* __restrict__ sums) {
+  unsigned v[kLsPer];
+  ls_load(len, n, blockIdx.x * kLsBlock + (uint64_t)threadIdx.x * kLsPer, v);
+  uint64_t t = 0;
+#pragma unroll
+  for (int q = 0; q < kLsPer; ++q) t += v[q];
+  uint64_t tot;
+  (void)ls_block_exscan(t, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(kLsT) void k_len_scan_sums(uint64_t* __restrict__ sums, uint64_t nb) {
+  uint64_t carry = 0;
+  for (uint64_t b0 = 0; b0 < nb; b0 += kLsT) {
+    const uint64_t i = b0 + threadIdx.x;
+    const uint64_t v = i < nb ? sums[i] : 0;
+    uint64_t tot;
+    const uint64_t ex = ls_block_exscan(v, &tot);
+    if (i < nb) sums[i] = carry + ex;
+    carry += tot;
+  }
+}
+__global__ __launch_bounds__(kLsT) void k_len_offsets(const uint16_t* __restrict__ len, uint64_t n,
+                                                      const uint64_t* __restrict__ sums, uint64_t* __restrict__ out) {
+  unsigned v[kLsPer];
+  const uint64_t i0 = blockIdx.x * kLsBlock + (uint64_t)threadIdx.x * kLsPer;
+  ls_load(len, n, i0, v);
+  uint64_t t = 0;
+#pragma unroll
+  for (int q = 0; q < kLsPer; ++q) t += v[q];
+  uint64_t tot;
+  uint64_t o = sums[blockIdx.x] + ls_block_exscan(t, &tot);
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
+#pragma unroll
+  for (int q = 0; q < kLsPer; ++q) {
+    o += v[q];
+    if (i0 + q < n) out[i0 + q + 1] = o;
+  }
+}
+
 // FNV-1a hash of every key (mphf.go:349-369), nothing else: the error path's recount of
 // the ORIGINAL key hashes (the level-0 pipeline keeps them only in its own layouts).
 __global__ __launch_bounds__(kBlock) void k_key_hash(const uint8_t* __restrict__ blob,
@@ -297,6 +378,15 @@ void launch_widen32(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s
 }
 void launch_narrow32(const uint64_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
   if (n) k_narrow32<<<(unsigned)std::min<uint64_t>(8192, (n + 255) / 256), 256, 0, s>>>(in, out, n);
+}
+
+uint64_t len16_scratch_words(uint64_t n) { return (n + kLsBlock - 1) / kLsBlock; }
+void launch_len16_offsets(const uint16_t* len, uint64_t n, uint64_t* sums, uint64_t* out, hipStream_t s) {
+  const uint64_t nb = len16_scratch_words(n);
+  if (!nb) return;
+  k_len_sums<<<(unsigned)nb, kLsT, 0, s>>>(len, n, sums);
+  k_len_scan_sums<<<1, kLsT, 0, s>>>(sums, nb);
+  k_len_offsets<<<(unsigned)nb, kLsT, 0, s>>>(len, n, sums, out);
 }
 
 void launch_key_hashes(const uint8_t* blob, const uint64_t* offsets, uint64_t n, uint64_t* out, hipStream_t s) {

@@ -214,6 +214,37 @@ def test_build_host_staged_chunks_offset_blob_custom_pos(s3, oracle_lib):
     assert np.array_equal(gfp, fp) and np.array_equal(gpo, po)
 
 
+def test_build_host_offsets_as_u16_lengths(s3, oracle_lib):
+    """build_host sends the offsets as u16 key lengths (device scan back to offsets): a set
+    whose lengths span several 8 MiB staging chunks (4.2M keys: 8.4 MB of lengths, the
+    scan's last block ragged), a non-zero offsets[0]."""
+    n = 4_200_001
+    blob, offs = s3.gen_keys(0, 5, 40, 0, n)
+    blob = blob[: int(offs[-1])]
+    st, fp, po, mph = oracle_lib.build(blob, offs)
+    assert st == 0
+    shifted = np.concatenate([np.frombuffer(b"0123456", np.uint8), blob])
+    gfp, gpo, gmph = s3.build_host(shifted, offs + np.uint64(7))
+    assert gmph == mph
+    assert np.array_equal(gfp, fp) and np.array_equal(gpo, po)
+
+
+def test_build_host_key_longer_than_u16(s3, oracle_lib):
+    """A key of 65536 B or more cannot travel as a u16 length: build_host falls back to
+    u32 offsets for the whole set, bit-exact."""
+    rng = np.random.default_rng(12)
+    keys = {rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in (65535, 65536, 70000)}
+    while len(keys) < 50000:
+        keys.add(rng.integers(0, 256, int(rng.integers(1, 30)), dtype=np.uint8).tobytes())
+    keys = sorted(keys)
+    blob, offs = O.keys_to_blob(keys)
+    st, fp, po, mph = oracle_lib.build(blob, offs)
+    assert st == 0
+    gfp, gpo, gmph = s3.build_host(blob, offs)
+    assert gmph == mph
+    assert np.array_equal(gfp, fp) and np.array_equal(gpo, po)
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 31, 32, 33, 63, 64, 65, 1000, 4097, 65535, 65536, 65537, 200000])
 def test_sizes_around_boundaries(s3, oracle_lib, ctx, n):
     blob, offs = s3.gen_keys(0, 7, 24, 0, n)

@@ -2,12 +2,17 @@
 
 FETCH_SIZE and WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM):
 FETCH_SIZE reads exactly half the bytes of a wide coalesced streaming read, so the
-corrected read bytes are 2 x FETCH_SIZE for streaming kernels (an upper bound for
-others); WRITE_SIZE is exact for 16-B-per-lane streaming stores.
+corrected read bytes are 2 x FETCH_SIZE for streaming kernels; WRITE_SIZE is exact for
+16-B-per-lane streaming stores.  Calibrated per access shape (`tools/ubench_fetch.hip`,
+`profiles/r4_fetch_cal/`): 64-byte runs read in scrambled order count in full (x 1), so
+k_hash_skew's per-key 64-B chunk reads take READ_FACTOR 1.
 """
 import csv
 import json
 import sys
+
+
+READ_FACTOR = {"k_hash_skew": 1.0}  # default 2.0 (streaming)
 
 
 def kname(full: str) -> str:
@@ -33,10 +38,11 @@ def main():
         dur = (int(f["End_Timestamp"]) - int(f["Start_Timestamp"])) / 1e3
         fk, wk = float(f["Counter_Value"]), float(w["Counter_Value"])
         out.append({"kernel": name, "grid": int(f["Grid_Size"]), "fetch_kib": fk, "write_kib": wk,
-                    "read_bytes_corrected": 2 * fk * 1024, "write_bytes": wk * 1024, "dur_us_profiled": dur})
+                    "read_bytes_corrected": READ_FACTOR.get(name, 2.0) * fk * 1024, "write_bytes": wk * 1024,
+                    "read_factor": READ_FACTOR.get(name, 2.0), "dur_us_profiled": dur})
     for o in out:
         if o["fetch_kib"] + o["write_kib"] > 1024:
-            print(f"{o['kernel']:16s} grid={o['grid']:>8d} read(2xFETCH)={o['read_bytes_corrected']/1e6:8.1f} MB "
+            print(f"{o['kernel']:16s} grid={o['grid']:>8d} read({o['read_factor']:.0f}xFETCH)={o['read_bytes_corrected']/1e6:8.1f} MB "
                   f"write={o['write_bytes']/1e6:8.1f} MB")
     if len(sys.argv) > 3:
         json.dump(out, open(sys.argv[3], "w"), indent=1)
