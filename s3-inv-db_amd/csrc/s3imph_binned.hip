@@ -2803,7 +2803,13 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
       if (j < F.n) rec(t, F, j, k[r], f[r], p[r]);
     }
   };
-  if (tid == 0) s_t[0] = atomicAdd(&st->ticket[level], 1ull);
+  // Tickets run one tile ahead of the prefetch: tile i + 2's is taken beside tile i's look-back
+  // (before any prefetch load of tid 0's wave, so its return does not wait behind them:
+  // vmcnt counts in order).  Here: the first two.
+  if (tid == 0) {
+    s_t[0] = atomicAdd(&st->ticket[level], 1ull);
+    s_t[1] = atomicAdd(&st->ticket[level], 1ull);
+  }
   for (unsigned w = tid; w < kP0W32; w += kP0T) {
     sA[w] = 0;
     sC[w] = 0;
@@ -2825,7 +2831,6 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
     asm volatile("" : "+v"(me));
     const bool fits = nk <= (unsigned)kP0R * kP0T;
     const uint64_t tbase = rg.plo + (t << kRegTileMaxBits);
-    if (tid == 0) s_t[nb] = atomicAdd(&st->ticket[level], 1ull);
     // ---- mark
     unsigned loc2[(kP0R + 1) / 2];
 #define LOC(r) ((loc2[(r) >> 1] >> (((r) & 1) * 16)) & 0xffffu)
@@ -2855,7 +2860,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
         if (old & bit) atomicOr(&sC[x >> 5], bit);
       }
     }
-    __syncthreads();  // A / C complete; the next ticket is in s_t[nb]
+    __syncthreads();  // A / C complete; the next tile's ticket is in s_t[nb] (taken a tile ago)
     const uint64_t tn = s_t[nb];
     if (tid >= kCntT && tn < T) s_cnt[nb][tid - kCntT] = tcnt[tn * kResShards + (tid - kCntT)];
     // ---- finalize: A & ~C -> LDS + global bits; per-word rank prefix into C
@@ -2957,6 +2962,9 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
     // ---- the rare tiles: base first, then the records the stage does not hold
     const bool early = !fits || s_late;
     if (early) {
+      // the tile after tn: its ticket in flight beside the look-back's flag loads
+      unsigned long long tk = 0;
+      if (tid == 0) tk = atomicAdd(&st->ticket[level], 1ull);
       if (wave == 0) {
         const uint64_t excl = lb_resolve(flags, t, pop, st);
         if (lane == 0) {
@@ -2964,6 +2972,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
           s_excl = excl;
         }
       }
+      if (tid == 0) s_t[cb] = tk;
       __syncthreads();
       const uint64_t base = lvl_base + s_excl;
       const bool wr = out_on && base + pop <= N;
@@ -2996,11 +3005,17 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
     }
 #undef LOC
     __syncthreads();  // s_cnt[nb] visible; every register record consumed
-    // ---- prefetch the next tile's records
+    // ---- prefetch the next tile's records (wave 0, which polls the look-back, after it:
+    // its flag loads would otherwise wait behind its own prefetch, in order, and hold the
+    // barrier that every wave then waits at)
     const Fills Fn = fills(s_cnt[nb]);
-    if (tn < T && Fn.n <= (unsigned)kP0R * kP0T) load_regs(tn, Fn, me);
+    const bool pf = tn < T && Fn.n <= (unsigned)kP0R * kP0T;
+    if (pf && (wave != 0 || early)) load_regs(tn, Fn, me);
     // ---- resolve the look-back, write the stage
     if (!early) {
+      // the tile after tn: its ticket in flight beside the look-back's flag loads
+      unsigned long long tk = 0;
+      if (tid == 0) tk = atomicAdd(&st->ticket[level], 1ull);
       if (wave == 0) {
         const uint64_t excl = lb_resolve(flags, t, pop, st);
         if (lane == 0) {
@@ -3008,7 +3023,9 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
           s_excl = excl;
         }
       }
+      if (tid == 0) s_t[cb] = tk;
       __syncthreads();
+      if (pf && wave == 0) load_regs(tn, Fn, me);
     }
     const uint64_t base = lvl_base + s_excl;
     if (base + pop > N && out_on) bad = true;

@@ -339,7 +339,12 @@ unsigned choose_split_ts(uint64_t size, bool exact) {
   const double est = exact ? (double)size : (double)size / 1.1;
   unsigned best = 0;
   double best_cost = 0;
-  for (unsigned ts = 2; ts <= (1u << (kSplitMaxBits - 14)); ++ts) {
+  // A/B knob S3IMPH_TS_MAX: the largest ts tried (smaller sub-tile scratch per workgroup)
+  static const unsigned ts_max = [] {
+    const char* e = std::getenv("S3IMPH_TS_MAX");
+    return e ? std::max(2u, std::min((unsigned)std::atoi(e), 1u << (kSplitMaxBits - 14))) : 1u << (kSplitMaxBits - 14);
+  }();
+  for (unsigned ts = 2; ts <= ts_max; ++ts) {
     const double T = est / (double)((uint64_t)ts << 14);
     if (T > (double)kSplitTargetTiles) continue;
     const double rounds = std::ceil(T / ((exact ? 1.0 : 0.95) * kSplitGridHost));
