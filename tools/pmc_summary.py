@@ -57,11 +57,14 @@ def main():
             first.setdefault(o["kernel"], o)
         ent = tr.setdefault(cfg, {})
         scatter0 = "k_scatter_res" if "k_scatter_res" in first and "k_hscan" not in first else "k_scatter"
-        tile0 = next((o["kernel"] for o in out if o["kernel"] in ("k_tile_reg", "k_tile_split", "k_tile")), "k_tile_reg")
+        tile0 = next((o["kernel"] for o in out if o["kernel"] in ("k_tile_reg", "k_tile_p0", "k_tile_split", "k_tile")), "k_tile_reg")
         # the level-0 hash that did the work (the others are no-op launches for this set's skew)
         hash0 = max((k for k in ("k_hash0_pair", "k_hash_skew", "k_hash_count0") if k in first),
                     key=lambda k: first[k]["read_bytes_corrected"] + first[k]["write_bytes"], default="k_hash0_pair")
-        for stage, kern in (("hash_count0", hash0), ("scatter0", scatter0), ("tile0", tile0)):
+        stages = (("hash_count0", hash0), ("scatter0", scatter0), ("tile0", tile0))
+        if "k_scatter_p0" in first:  # P0 level 0: the fused hash partition, super-tile scatter, tiles
+            stages = (("hash_part0", hash0), ("scatter0_p0", "k_scatter_p0"), ("tile0_p0", "k_tile_p0"))
+        for stage, kern in stages:
             if kern in first:
                 o = first[kern]
                 ent[stage] = {"kernel": kern, "n_gpus": 1,
