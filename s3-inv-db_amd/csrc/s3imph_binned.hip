@@ -3977,7 +3977,10 @@ void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, co
 
 void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStream_t s) {
   const P0In in{p.sup, p.reg_cap, p.pcnt, (unsigned)kH0Grid, p.S, p.sup_cap / ((uint64_t)p.S * kResShards), p.scnt, fused};
-  const unsigned bps = std::max(1u, 256u / p.S);
+  // blocks per super-tile: a multiple of kResShards, so every shard slot of a tile takes the
+  // records of the same number of blocks (9 blocks put 2/9 of a super-tile's records on one
+  // shard: 1.8x the mean fill, past the slot capacity at S = 26)
+  const unsigned bps = std::max(1u, 256u / p.S / kResShards) * kResShards;
   if (p.tps <= 256)
     k_scatter_p0<5120, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
   else if (p.tps <= 512)

@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kBT) void k_bm_tsum(int level, const uint64_t* __re
 // the level) and tbase[2t + 1] (its first slot in this rank's settled list, which runs on
 // from *out_cnt: the list is in (level, position) order, so sorted by p).  The level's
 // total settles the next level's global size and rank base.
-constexpr int kTsPer = (int)(kScatterTiles / kBTopT);
+constexpr int kTsPer = (int)(kBmMaxTiles / kBTopT);
 __global__ __launch_bounds__(kBTopT) void k_bm_tscan(int level, const unsigned long long* __restrict__ tsum,
                                                      unsigned tb, unsigned long long* __restrict__ tbase,
                                                      LevelState* st, unsigned long long* __restrict__ gslot,
@@ -244,8 +244,14 @@ __device__ __forceinline__ uint64_t rec_index(unsigned i, const unsigned* fo, ui
 //                          by output slice (slice t = words [t S, (t+1) S): S A words then S C
 //                          words) for an all-to-all and k_bm_merge's associative merge
 //                          (A, C) + (a, c) = (A | a, C | c | (A & a)).
-template <int kMode>
-__global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const Rec* __restrict__ bucket,
+// a record's k (offset 0 of both record types)
+template <class RT>
+__device__ __forceinline__ uint64_t rec_k(const RT* __restrict__ q) {
+  const uint2 v = *reinterpret_cast<const uint2*>(q);
+  return (uint64_t)v.x | ((uint64_t)v.y << 32);
+}
+template <int kMode, class RT>
+__global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __restrict__ bucket,
                                                       const unsigned* __restrict__ tc, uint64_t bucket_cap,
                                                       unsigned tb, const LevelState* st, uint64_t wpad,
                                                       uint8_t* __restrict__ lanes, uint32_t* __restrict__ A32,
@@ -290,7 +296,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const Rec* __re
     uint64_t kk[kU], kn[kU];
     auto ld = [&](unsigned i0, uint64_t (&dst)[kU]) {
 #pragma unroll
-      for (int u = 0; u < kU; ++u) dst[u] = bucket[rec_index(min(i0 + u * kTT + tid, nrec - 1), fo, t * cap, scap)].k;
+      for (int u = 0; u < kU; ++u) dst[u] = rec_k(bucket + rec_index(min(i0 + u * kTT + tid, nrec - 1), fo, t * cap, scap));
     };
     if (nrec) ld(0, kk);
     for (unsigned i0 = 0; i0 < nrec; i0 += kTT * kU) {
@@ -360,7 +366,8 @@ __device__ __forceinline__ void fp_out_own(const OwnSlice& os, uint64_t p, uint6
   os.fp_out[o] = f;
   os.pos_out[o] = pos;
 }
-__global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const Rec* __restrict__ bucket,
+template <class RT>
+__global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __restrict__ bucket, uint64_t pos_base,
                                                         const unsigned* __restrict__ tc, uint64_t bucket_cap,
                                                         unsigned tb, LevelState* st, const uint64_t* __restrict__ g,
                                                         const uint64_t* __restrict__ A,
@@ -467,7 +474,16 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const Rec* __
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const unsigned i = i0 + u * kTT + tid;
-        if (i < nrec) r[u] = bucket[rec_index(i, fo, t * cap, scap)];
+        if (i < nrec) {
+          const RT* q = bucket + rec_index(i, fo, t * cap, scap);
+          if constexpr (sizeof(RT) == sizeof(Rec)) {
+            r[u] = *reinterpret_cast<const Rec*>(q);
+          } else {  // R20: (k, f, key index), p = pos_base + index
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(q);
+            const uint4 a = *reinterpret_cast<const uint4*>(w);  // dword-aligned 16-B load
+            r[u] = Rec{(uint64_t)a.x | ((uint64_t)a.y << 32), (uint64_t)a.z | ((uint64_t)a.w << 32), pos_base + w[4]};
+          }
+        }
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
@@ -589,36 +605,49 @@ size_t bm_tile_lds(unsigned tb, bool settle) {
 }
 
 void bm_set_lds_limits() {
-  for (const void* k : {(const void*)k_bm_tile_mark<kBmBytes>, (const void*)k_bm_tile_mark<kBmNibbles>,
-                        (const void*)k_bm_tile_mark<kBmPlanes>})
+  for (const void* k : {(const void*)k_bm_tile_mark<kBmBytes, Rec>, (const void*)k_bm_tile_mark<kBmNibbles, Rec>,
+                        (const void*)k_bm_tile_mark<kBmPlanes, Rec>, (const void*)k_bm_tile_mark<kBmBytes, R20>,
+                        (const void*)k_bm_tile_mark<kBmNibbles, R20>, (const void*)k_bm_tile_mark<kBmPlanes, R20>})
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_tile_lds(kBmMaxTb, false));
-  (void)hipFuncSetAttribute((const void*)k_bm_tile_settle, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)bm_tile_lds(kBmMaxTb, true));
+  for (const void* k : {(const void*)k_bm_tile_settle<Rec>, (const void*)k_bm_tile_settle<R20>})
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_tile_lds(kBmMaxTb, true));
 }
 
 void launch_bm_range(LevelState* st, int level, hipStream_t s) { k_bm_range<<<1, 64, 0, s>>>(st, level); }
 
-void launch_bm_tile_mark(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
+void launch_bm_tile_mark(int level, const void* bucket, bool r20, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
                          uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A, int mode,
                          uint64_t S, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(256, std::min<uint64_t>(tiles, 1024));
-  auto kern = mode == kBmPlanes ? k_bm_tile_mark<kBmPlanes> : mode == kBmNibbles ? k_bm_tile_mark<kBmNibbles>
-                                                                                : k_bm_tile_mark<kBmBytes>;
-  kern<<<grid, kTT, bm_tile_lds(tb, false), s>>>(level, bucket, tc, bucket_cap, tb, st, wpad, lanes,
-                                                 reinterpret_cast<uint32_t*>(A), S, level_magic(S));
+  auto go = [&](auto rt) {
+    using RT = decltype(rt);
+    const RT* bk = static_cast<const RT*>(bucket);
+    auto kern = mode == kBmPlanes ? k_bm_tile_mark<kBmPlanes, RT> : mode == kBmNibbles ? k_bm_tile_mark<kBmNibbles, RT>
+                                                                                      : k_bm_tile_mark<kBmBytes, RT>;
+    kern<<<grid, kTT, bm_tile_lds(tb, false), s>>>(level, bk, tc, bucket_cap, tb, st, wpad, lanes,
+                                                   reinterpret_cast<uint32_t*>(A), S, level_magic(S));
+  };
+  if (r20) go(R20{});
+  else go(Rec{});
 }
 
 void launch_bm_merge(const uint64_t* recv, uint64_t S, int P, uint64_t* out, const LevelState* st, hipStream_t s) {
   k_bm_merge<<<grid_for(S, kBT, 8192), kBT, 0, s>>>(recv, S, P, out, st);
 }
 
-void launch_bm_tile_settle(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
-                           uint64_t tiles, LevelState* st, const uint64_t* g, const uint64_t* A,
-                           const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next, uint64_t next_cap,
-                           const OwnSlice& os, hipStream_t s) {
+void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos_base, const unsigned* tc,
+                           uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
+                           const uint64_t* A, const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next,
+                           uint64_t next_cap, const OwnSlice& os, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1024));
-  k_bm_tile_settle<<<grid, kTT, bm_tile_lds(tb, true), s>>>(level, bucket, tc, bucket_cap, tb, st, g, A, tbase, out,
-                                                            out_cap, next, next_cap, os);
+  if (r20)
+    k_bm_tile_settle<R20><<<grid, kTT, bm_tile_lds(tb, true), s>>>(level, static_cast<const R20*>(bucket), pos_base, tc,
+                                                                   bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
+                                                                   next_cap, os);
+  else
+    k_bm_tile_settle<Rec><<<grid, kTT, bm_tile_lds(tb, true), s>>>(level, static_cast<const Rec*>(bucket), pos_base, tc,
+                                                                   bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
+                                                                   next_cap, os);
 }
 
 void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,

@@ -436,12 +436,14 @@ bool hash_only_knob() {
   return on;
 }
 
-// P0 geometry and buffers for level 0 of n keys (identity positions): T 2^14-position tiles
+// P0 geometry and buffers for level 0 of n keys over the positions of n_geom keys (the whole
+// level: n_geom = n, or the global key count of the bitmap decomposition), identity
+// positions: T 2^14-position tiles
 // in S super-tiles of tps (about kP0TargetTps; S <= kP0MaxS), the super-tiles' records in
 // c->p0_sup (sized for the hash's per-block regions and for the slot layout of the pass that
 // stands in for it), the tiles' slots in the bucket, both as R20.
-P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, hipStream_t s) {
-  const uint64_t T = tiles_of(level_words(n), kRegTileMaxBits, 0);
+P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s) {
+  const uint64_t T = tiles_of(level_words(n_geom), kRegTileMaxBits, 0);
   P0Bufs p;
   p.S = (unsigned)std::min<uint64_t>((T + kP0TargetTps - 1) / kP0TargetTps, kP0MaxS);
   p.tps = (unsigned)((T + p.S - 1) / p.S);
@@ -480,7 +482,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   if (!conservative && c->p0 && !pos && n <= kP0MaxKeys && !hash_only_knob() && T14 > kP0MinTiles &&
       T14 <= kP0MaxS * kP0MaxTps) {
     // level 0 in 2^14-position register tiles through super-tiles (s3imph_internal.h, P0)
-    const P0Bufs p = p0_bufs(c, n, s);
+    const P0Bufs p = p0_bufs(c, n, n, s);
     const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
     launch_init_state(c->d_st, n, n, s, offsets);
     ev_mark(c, s, "init");
@@ -1439,8 +1441,8 @@ void ensure_bm_workspace(s3imph_ctx* c, uint64_t N) {
   dalloc(d.bm_lanes, 64 * wpad);  // count bytes, or the (A, C) planes in 16 B per word
   dalloc(d.bm_slice, 64 * S);
   dalloc(d.bm_recv, 16 * wpad);   // the planes' all-to-all: P slices of 2 S words
-  if (!d.bm_tsum) dalloc(d.bm_tsum, kScatterTiles);
-  if (!d.bm_tbase) dalloc(d.bm_tbase, 2 * kScatterTiles);
+  if (!d.bm_tsum) dalloc(d.bm_tsum, kBmMaxTiles);
+  if (!d.bm_tbase) dalloc(d.bm_tbase, 2 * kBmMaxTiles);
   d.bm_cap_words = wpad;
 }
 
@@ -1478,12 +1480,28 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   const double q = 1.0 - std::exp(-0.5);
   launch_init_state(st, n_local, out_cap, s, n_local ? offsets : nullptr);
   launch_dist_setup(st, 0, nullptr, N, R, P, s);
+  launch_bm_range(st, 0, s);  // the whole level before the hash: P0's partition pass reads the range
   ev_mark(c, s, "init");
+  // Level 0 through the P0 super-tiles into 2^14-position tiles when the whole
+  // level's tile count is in P0's range and positions are the identity: the fused hash
+  // partition, the super-tile scatter, then the bitmap tile kernels over R20 slots.
+  const uint64_t T14 = tiles_of(level_words(N), kRegTileMaxBits, 0);
+  const bool p0 = c->p0 && !pos && n_local && n_local <= kP0MaxKeys && !hash_only_knob() && T14 > kP0MinTiles &&
+                  T14 <= kP0MaxS * kP0MaxTps && T14 <= kBmMaxTiles;
+  P0Bufs pb{};
   if (n_local) {
     const LevelGeom gh0 = choose_geom_sz(n_local, 64 * level_words(N), kTargetTiles0, chunks0(n_local), kTileMaxBits);
-    launch_hash0_only(blob, offsets, n_local, b, gh0, level_grids(n_local, 64 * level_words(N), gh0).gc, s);
+    if (p0) {
+      pb = p0_bufs(c, n_local, N, s);
+      launch_p0_hash(blob, offsets, n_local, b, gh0, pb, s);
+    } else {
+      launch_hash0_only(blob, offsets, n_local, b, gh0, level_grids(n_local, 64 * level_words(N), gh0).gc, s);
+    }
   }
-  ev_mark(c, s, "hash_count0");
+  ev_mark(c, s, p0 ? "hash_part0" : "hash_count0");
+  if (c->debug && p0)
+    std::fprintf(stderr, "[s3imph] rank %d bitmap: level 0 through P0 super-tiles (%llu tiles of 2^14)\n", R,
+                 (unsigned long long)T14);
   Rec* const out = d.bm_out;                   // this rank's settled (p, fp, pos) triples
   unsigned long long* const out_cnt = d.small + 4096;
   HIPCHECK(hipMemsetAsync(out_cnt, 0, 8, s));
@@ -1524,10 +1542,13 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   for (;;) {
     const uint64_t wmax = level_words((uint64_t)std::ceil(nb)), S = (wmax + P - 1) / P, wpad = S * (uint64_t)P;
     // tiles of 2^tb positions: the smallest tile leaving at most bm_target_tiles() tiles
+    // (level 0 under P0: its 2^14-position tiles)
+    const bool l0p = L == 0 && p0;
     unsigned tb = kBmMinTb;
-    while (tb < kBmMaxTb && tiles_of(wmax, tb, 0) > bm_target_tiles()) ++tb;
+    while (!l0p && tb < kBmMaxTb && tiles_of(wmax, tb, 0) > bm_target_tiles()) ++tb;
     const uint64_t tiles = tiles_of(wmax, tb, 0);
-    if (tiles > kScatterTiles) return kDistRetry;  // > 2^30 positions: the routed build (same on every rank)
+    // > 2^30 positions: the routed build (same on every rank); P0's level 0 takes up to kBmMaxTiles
+    if (tiles > (l0p ? kBmMaxTiles : kScatterTiles)) return kDistRetry;
     if (L > 0) launch_dist_setup(st, L, d.gslot + L, 0, R, P, s);
     launch_bm_range(st, L, s);
     launch_bm_check(st, L, wmax, s);
@@ -1537,9 +1558,18 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     g.chunk = kTargetChunks;
     g.ts = 0;
     const int gsr = (int)std::max<uint64_t>(1, std::min<uint64_t>((np + kSubRound - 1) / kSubRound, 256));
-    launch_binned_scatter_res(L, bs, g, gsr, s, 0, 0, tiles);
+    const void* bk = c->bucket;
+    uint64_t bcap = c->bucket_cap;
     const unsigned* tc = c->tcnt + (uint64_t)L * kTcntStride;
-    launch_bm_tile_mark(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, lanes, S, s);
+    if (l0p) {
+      if (n_local) launch_p0_scatter(b, pb, p0_fused(blob, pb), s);
+      bk = pb.bucket;
+      bcap = pb.bucket_cap;
+      tc = pb.tcnt;
+    } else {
+      launch_binned_scatter_res(L, bs, g, gsr, s, 0, 0, tiles);
+    }
+    launch_bm_tile_mark(L, bk, l0p, tc, bcap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, lanes, S, s);
     if (lanes == kBmPlanes) {
       // slice t's planes (2 S words) to rank t; rank q's planes of this rank's slice land at 2 S q
       for (int t = 0; t < P; ++t) {
@@ -1554,7 +1584,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     }
     cm.allgather(d.bm_dec, d.bm_g, 8 * S, s);
     launch_bm_level_end(L, d.bm_g, d.bm_a, tb, tiles, c->bits, d.bm_tsum, d.bm_tbase, st, d.gslot, out_cnt, s);
-    launch_bm_tile_settle(L, c->bucket, tc, c->bucket_cap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
+    launch_bm_tile_settle(L, bk, l0p, key_base, tc, bcap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
                           d.bm_cap_out, c->list[L & 1], d.cap_list, own_slice, s);
     ev_mark(c, s, L == 0 ? "level0" : "levels");
     const double nbn = nb * q + 6.0 * std::sqrt(nb) + 64.0;

@@ -334,6 +334,9 @@ void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const Lev
 // most kScatterTiles of them (levels of up to 2^31 positions); the settle kernel keeps 18 B
 // per tile word in LDS: 144 KiB at 2^19 positions.
 constexpr unsigned kBmMinTb = 14, kBmMaxTb = 19;
+// tiles of a bitmap level: kScatterTiles from the reservation scatter, or up to kP0MaxS x
+// kP0MaxTps 2^14-position tiles from the P0 super-tile scatter (level 0)
+constexpr uint64_t kBmMaxTiles = 32768;
 // level end: per-tile totals of the final bits -> tbase[2t] (rank within the level), tbase[2t+1]
 // (first slot in this rank's settled list, continuing *out_cnt, which it then advances)
 void launch_bm_level_end(int level, const uint64_t* g, const uint64_t* A, unsigned tb, uint64_t tiles, uint64_t* bits,
@@ -341,7 +344,9 @@ void launch_bm_level_end(int level, const uint64_t* g, const uint64_t* A, unsign
                          unsigned long long* gslot, unsigned long long* out_cnt, hipStream_t s);
 void bm_set_lds_limits();
 void launch_bm_range(LevelState* st, int level, hipStream_t s);
-void launch_bm_tile_mark(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
+// bucket: Rec slots, or (r20) the P0 super-tile scatter's R20 slots of 2^14-position tiles
+// (level 0 with identity positions p = pos_base + key index)
+void launch_bm_tile_mark(int level, const void* bucket, bool r20, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
                          uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A, int mode,
                          uint64_t S, hipStream_t s);
 // the all-to-all's (A, C) plane slices (P of them, 2 S words each) -> this rank's final bits
@@ -355,10 +360,10 @@ struct OwnSlice {
   uint64_t *fp_out, *pos_out;
   unsigned long long* scnt;
 };
-void launch_bm_tile_settle(int level, const Rec* bucket, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
-                           uint64_t tiles, LevelState* st, const uint64_t* g, const uint64_t* A,
-                           const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next, uint64_t next_cap,
-                           const OwnSlice& os, hipStream_t s);
+void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos_base, const unsigned* tc,
+                           uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
+                           const uint64_t* A, const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next,
+                           uint64_t next_cap, const OwnSlice& os, hipStream_t s);
 void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,
                      LevelState* st, hipStream_t s);
 void launch_bm_tail_copy(const uint64_t* sfp, const uint64_t* spos, uint64_t g0, uint64_t total, uint64_t lo,

@@ -89,6 +89,29 @@ def test_one_gpu_sharded_bitmap_over_rccl(s3, oracle_lib, monkeypatch, switch, n
         assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
 
 
+@pytest.mark.parametrize("ranks,kind,avg,n", [(1, 0, 24, 17_500_000), (2, 0, 24, 20_000_000),
+                                              (3, 1, 0, 18_000_000), (1, 0, 16, 40_000_000)])
+def test_bitmap_level0_through_p0_tiles(s3, oracle_lib, monkeypatch, capfd, ranks, kind, avg, n):
+    """The bitmap decomposition's level 0 through the P0 super-tiles (the whole level's
+    2^14-position tiles > 2048: N > 16.8M keys; 40M: 4883 tiles, more than the reservation
+    scatter's 4096): fused hash partition (skewed lengths:
+    k_hash_skew + the partition pass), super-tile scatter into R20 slots, then the bitmap
+    mark / settle over R20 records.  One rank over RCCL, 2-3 over the host transport;
+    every rank reports the P0 level 0 (S3IMPH_DEBUG); bit-exact (S3IMPH_DIST_STRICT)."""
+    monkeypatch.setenv("S3IMPH_DEBUG", "1")
+    monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", str(2_000_000 + 7 * ranks))  # fresh contexts read S3IMPH_DEBUG
+    blob, offs = s3.gen_keys(kind, 31, avg, 0, n)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    if ranks == 1:
+        g = s3.build_host(blob, offs, num_gpus=1, flags=s3.MULTI_FORCE_SHARDED | s3.MULTI_BITMAP)
+    else:
+        g = s3.build_host(blob, offs, devices=[0] * ranks, flags=s3.MULTI_BITMAP)
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+    err = capfd.readouterr().err
+    assert err.count("level 0 through P0 super-tiles") == ranks, err[-2000:]
+
+
 @pytest.mark.parametrize("ranks", [2, 3])
 def test_thread_per_rank_chunked_level0_exchange(s3, oracle_lib, monkeypatch, capfd, ranks):
     """Shards of >= 8M keys take the chunked level 0 (s3imph_build.hip route0_chunked):

@@ -539,23 +539,27 @@ def test_big_tiles_bit_exact(s3, oracle_lib):
         c.close()
 
 
-@pytest.mark.parametrize("n,unaligned", [(16_800_000, False), (20_000_000, True)])
+@pytest.mark.parametrize("n,unaligned", [(16_800_000, False), (20_000_000, True), (40_000_000, False)])
 def test_p0_level0_bit_exact(s3, oracle_lib, n, unaligned):
     """Level 0 with more than 2048 tiles of 2^14 positions (P0, s3imph_internal.h): the
     records go to super-tile slots, then to their tiles' slots, then the pipelined register
     tiles (k_tile_p0).  Just past the threshold (2051 tiles), and an unaligned blob whose
-    level-0 hash is k_hash_count0 (kh / fp, then the partition pass).  Bit-exact."""
+    level-0 hash is k_hash_count0 (kh / fp, then the partition pass); 12 / 26 super-tiles
+    (blocks per super-tile a multiple of the 8 XCD shards).  Bit-exact, and the build's
+    last attempt is P0's (no conservative rerun: its stage marks are P0's)."""
     c = s3.DeviceBuilder(0)
     try:
         blob, offs = s3.gen_keys(0, 19, 20, 0, n)
         blob = blob[: int(offs[-1])]
         st, fp, po, mph = oracle_lib.build_mt(blob, offs, threads=16)
         assert st == 0
+        c.set_profiling(1)
         if unaligned:
             gfp, gpo, gmph, _ = _device_build(s3, c, np.concatenate([np.frombuffer(b"q", np.uint8), blob]), offs + 1)
         else:
             gfp, gpo, gmph, _ = _device_build(s3, c, blob, offs)
         assert gmph == mph and np.array_equal(gfp, fp) and np.array_equal(gpo, po)
+        assert "scatter0_p0" in c.stage_times(), c.stage_times()
     finally:
         c.close()
 
