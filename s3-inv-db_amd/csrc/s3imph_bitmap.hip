@@ -357,6 +357,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
 // a hole no one reads); every settled key is counted per output slice in scnt, which is
 // the output all-to-all's send counts (the list's runs by slice, holes included).
 constexpr unsigned kGrp = 4;
+constexpr unsigned kBmStage = 5632;  // staged settled keys per 2^14 tile (mean 4969 at one rank: 9.9 sigma)
 __device__ __forceinline__ void fp_out_own(const OwnSlice& os, uint64_t p, uint64_t f, uint64_t pos, bool& over) {
   const uint64_t o = p - os.lo;
   if (p < os.lo || o >= os.cnt) {
@@ -374,6 +375,9 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
                                                         const unsigned long long* __restrict__ tbase,
                                                         Rec* __restrict__ out, uint64_t out_cap,
                                                         Rec* __restrict__ next, uint64_t next_cap, OwnSlice os) {
+  // R20 records come in 2^14-position tiles (P0's level 0): this rank's settled keys of a
+  // tile (<= ~5.2k at one rank) are staged in LDS behind the tile words
+  constexpr bool kStaged = sizeof(RT) != sizeof(Rec);
   extern __shared__ uint64_t bm_lds64[];
   __shared__ unsigned long long s_w[kTT / 64];
   __shared__ unsigned s_sc[kMaxRanks];
@@ -390,6 +394,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
   uint64_t* sga = sg + W;
   unsigned* gpg = reinterpret_cast<unsigned*>(sga + W);  // per group: popcount(g) before it
   unsigned* gpa = gpg + G;                               // ... popcount(g & a)
+  Rec* stg = reinterpret_cast<Rec*>(gpa + G);            // kStaged: kBmStage records (8-B aligned: G even)
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
   constexpr int kGper = 2;  // groups per thread in the tile scan (G <= 2048)
@@ -509,7 +514,9 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
           const uint64_t gp = pb + pg;
           const unsigned sl = owner_of(gp, os.slice, os.mslice);
           atomicAdd(&s_sc[sl < (unsigned)os.P ? sl : os.P - 1], 1u);
-          if ((int)sl == os.rank) {
+          if (kStaged && pa < kBmStage) {  // written out below in pa order
+            stg[pa] = Rec{gp, r[u].f, r[u].p};
+          } else if ((int)sl == os.rank) {
             fp_out_own(os, gp, r[u].f, r[u].p, over);
           } else {
             const uint64_t slot = ob + pa;
@@ -524,6 +531,23 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
             next[slot] = r[u];
           else
             over = true;
+        }
+      }
+    }
+    if constexpr (kStaged) {
+      // this rank's settled keys of the tile in pa order: their p ascend, so own-slice keys
+      // land in runs of fp_out / pos_out (at one rank: the whole tile, one run) and the
+      // others in one run of the settled list, instead of one scattered 8-byte store each
+      __syncthreads();
+      const unsigned ns = (unsigned)min<unsigned long long>(tot & 0xffffffffull, kBmStage);
+      for (unsigned i = tid; i < ns; i += kTT) {
+        const Rec e = stg[i];
+        if ((int)owner_of(e.k, os.slice, os.mslice) == os.rank) {
+          fp_out_own(os, e.k, e.f, e.p, over);
+        } else if (ob + i < out_cap) {
+          out[ob + i] = e;
+        } else {
+          over = true;
         }
       }
     }
@@ -609,8 +633,10 @@ void bm_set_lds_limits() {
                         (const void*)k_bm_tile_mark<kBmPlanes, Rec>, (const void*)k_bm_tile_mark<kBmBytes, R20>,
                         (const void*)k_bm_tile_mark<kBmNibbles, R20>, (const void*)k_bm_tile_mark<kBmPlanes, R20>})
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_tile_lds(kBmMaxTb, false));
-  for (const void* k : {(const void*)k_bm_tile_settle<Rec>, (const void*)k_bm_tile_settle<R20>})
-    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_tile_lds(kBmMaxTb, true));
+  (void)hipFuncSetAttribute((const void*)k_bm_tile_settle<Rec>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)bm_tile_lds(kBmMaxTb, true));
+  (void)hipFuncSetAttribute((const void*)k_bm_tile_settle<R20>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(bm_tile_lds(kBmMinTb, true) + kBmStage * sizeof(Rec)));
 }
 
 void launch_bm_range(LevelState* st, int level, hipStream_t s) { k_bm_range<<<1, 64, 0, s>>>(st, level); }
@@ -641,7 +667,7 @@ void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos
                            uint64_t next_cap, const OwnSlice& os, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1024));
   if (r20)
-    k_bm_tile_settle<R20><<<grid, kTT, bm_tile_lds(tb, true), s>>>(level, static_cast<const R20*>(bucket), pos_base, tc,
+    k_bm_tile_settle<R20><<<grid, kTT, bm_tile_lds(tb, true) + kBmStage * sizeof(Rec), s>>>(level, static_cast<const R20*>(bucket), pos_base, tc,
                                                                    bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
                                                                    next_cap, os);
   else
