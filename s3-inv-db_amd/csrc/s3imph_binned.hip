@@ -589,20 +589,28 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
           ork[h] = atomicAdd(&r_cnt[od[h]], 1u);
         }
       __syncthreads();  // every lane has hashed (the window is free) and counted
+      // 32-bit arithmetic only (offsets within this block's S regions, a uniform base): a
+      // 64-bit result in a VGPR pair made wave 0 wait here for the next round's prefetch
+      const unsigned rcap = (unsigned)pt.reg_cap;
+      unsigned* r_off = reinterpret_cast<unsigned*>(r_base);
       if (tid < 64) {
-        const unsigned c = tid < pt.S ? r_cnt[tid] : 0u;
+        // (the thread index opaque here: its LDS addresses recomputed, not hoisted out of
+        // the round loop and spilled — a scratch reload waits for every load in flight)
+        unsigned me = tid;
+        asm volatile("" : "+v"(me));
+        const unsigned c = me < pt.S ? r_cnt[me] : 0u;
         unsigned x = c;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
           const unsigned y = __shfl_up(x, o);
-          if (tid >= (unsigned)o) x += y;
+          if (me >= (unsigned)o) x += y;
         }
-        r_start[tid] = x - c;
+        r_start[me] = x - c;
         if (c) {
-          const unsigned at = p_cur[tid];
-          if (at + c > pt.reg_cap) r_over = 1;
-          p_cur[tid] = at + c;
-          r_base[tid] = ((uint64_t)blockIdx.x * pt.S + tid) * pt.reg_cap + at;
+          const unsigned at = p_cur[me];
+          if (at + c > rcap) r_over = 1;
+          p_cur[me] = at + c;
+          r_off[me] = me * rcap + at;
         }
       }
       __syncthreads();
@@ -617,9 +625,10 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
         }
       __syncthreads();
       if (!r_over) {
+        R20* const blk = pt.sup + (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x) * pt.S * pt.reg_cap;
         for (unsigned j = tid; j < m; j += NT) {
           const unsigned o = sdst[j];
-          pt.sup[r_base[o] + (j - r_start[o])] = stg[j];
+          blk[r_off[o] + (j - r_start[o])] = stg[j];
         }
       }
     }
