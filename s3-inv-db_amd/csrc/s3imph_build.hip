@@ -436,6 +436,15 @@ bool hash_only_knob() {
   return on;
 }
 
+// Level 0 takes P0 above this many 2^14-position tiles (A/B knob S3IMPH_P0_MIN_TILES)
+uint64_t p0_min_tiles() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("S3IMPH_P0_MIN_TILES");
+    return e ? std::strtoull(e, nullptr, 10) : kP0MinTiles;
+  }();
+  return v;
+}
+
 // P0 geometry and buffers for level 0 of n keys over the positions of n_geom keys (the whole
 // level: n_geom = n, or the global key count of the bitmap decomposition), identity
 // positions: T 2^14-position tiles
@@ -479,7 +488,7 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   const BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
   const double q = 1.0 - std::exp(-0.5);
   const uint64_t T14 = tiles_of(level_words(n), kRegTileMaxBits, 0);
-  if (!conservative && c->p0 && !pos && n <= kP0MaxKeys && !hash_only_knob() && T14 > kP0MinTiles &&
+  if (!conservative && c->p0 && !pos && n <= kP0MaxKeys && !hash_only_knob() && T14 > p0_min_tiles() &&
       T14 <= kP0MaxS * kP0MaxTps) {
     // level 0 in 2^14-position register tiles through super-tiles (s3imph_internal.h, P0)
     const P0Bufs p = p0_bufs(c, n, n, s);
@@ -1486,7 +1495,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   // level's tile count is in P0's range and positions are the identity: the fused hash
   // partition, the super-tile scatter, then the bitmap tile kernels over R20 slots.
   const uint64_t T14 = tiles_of(level_words(N), kRegTileMaxBits, 0);
-  const bool p0 = c->p0 && !pos && n_local && n_local <= kP0MaxKeys && !hash_only_knob() && T14 > kP0MinTiles &&
+  const bool p0 = c->p0 && !pos && n_local && n_local <= kP0MaxKeys && !hash_only_knob() && T14 > p0_min_tiles() &&
                   T14 <= kP0MaxS * kP0MaxTps && T14 <= kBmMaxTiles;
   P0Bufs pb{};
   if (n_local) {
