@@ -705,9 +705,18 @@ __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict
                                                        unsigned long long* __restrict__ flags,
                                                        unsigned long long* __restrict__ sflags, LevelState* st,
                                                        unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt,
-                                                       unsigned long long* __restrict__ prof, int order) {
+                                                       unsigned long long* __restrict__ prof, int order,
+                                                       P0Part pt = P0Part{}) {
   extern __shared__ __align__(16) unsigned char sk_lds[];
+  // pt.sup (P0's level 0): each group's records (R20) go to this block's region of their
+  // super-tile through an LDS cursor per super-tile, instead of kh / fp in key order
+  __shared__ unsigned sk_pcur[kMaxRanks];
   if (!st->skew) return;  // k_hash0_pair hashed this near-uniform set
+  const bool part = pt.sup != nullptr;
+  const uint32_t p_mul = part ? 0xffffffffu / pt.tps + 1 : 0u;
+  const uint64_t p_words = st->words[0], p_magic = st->magic[0];
+  bool p_over = false;
+  if (part && threadIdx.x < kMaxRanks) sk_pcur[threadIdx.x] = 0;  // (the first group's barriers order it)
   const bool interleave = order == 0;
   // prof (S3IMPH_DEBUG): per wave, shader cycles total / hashing / waiting for a chunk's
   // loads / the rest (sort, tickets, barriers, write-back)
@@ -909,11 +918,26 @@ __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict
     }
     const unsigned long long e0t = prof ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();
-    for (unsigned k = tid; k < m; k += kSkT) {
-      const uint64_t a = res_a[k];
-      kh[grp + k] = a;
-      fp[grp + k] = res_b[k];
-      zero |= a == 0;
+    if (part) {
+      for (unsigned k = tid; k < m; k += kSkT) {
+        const uint64_t a = res_a[k];
+        zero |= a == 0;
+        const uint64_t x = bb_index(level_seed(0), a, p_words, p_magic);
+        unsigned od = __umulhi((uint32_t)(x >> kRegTileMaxBits), p_mul);
+        if (od >= pt.S) od = pt.S - 1;  // unreachable: positions < 64 words
+        const unsigned at = atomicAdd(&sk_pcur[od], 1u);
+        if (at < (unsigned)pt.reg_cap)
+          pt.sup[((uint64_t)blockIdx.x * pt.S + od) * pt.reg_cap + at] = r20_make(a, res_b[k], (uint32_t)(grp + k));
+        else
+          p_over = true;
+      }
+    } else {
+      for (unsigned k = tid; k < m; k += kSkT) {
+        const uint64_t a = res_a[k];
+        kh[grp + k] = a;
+        fp[grp + k] = res_b[k];
+        zero |= a == 0;
+      }
     }
     __syncthreads();  // the next group reuses cnt / sidx / res
     if (prof) p_end += __builtin_amdgcn_s_memtime() - e0t;
@@ -931,6 +955,11 @@ __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict
     q[7] = (p_sort << 32) | (p_end & 0xffffffffull);  // group phases: sort | barrier + write-back
   }
   if (zero) atomicOr(&st->status, kStKeyZero);
+  if (part) {
+    __syncthreads();  // every cursor atomic done (the last group's barrier preceded the stores only)
+    if (tid < pt.S) pt.pcnt[(uint64_t)blockIdx.x * pt.S + tid] = min<unsigned>(sk_pcur[tid], (unsigned)pt.reg_cap);
+    if (p_over) atomicOr(&st->status, kStOverflow | kStResOverflow);
+  }
 }
 
 // ------------------------------------------------------------- level L setup ---------
@@ -1390,6 +1419,8 @@ struct P0In {
   uint64_t reg_cap;        // regions: records per (hash block, super-tile) region
   const unsigned* pcnt;    // ... their fills, [hash block][super-tile]
   unsigned NB, S;          // hash blocks, super-tiles
+  unsigned NB_skew;        // a skewed set: k_hash_skew's blocks and region size
+  uint64_t reg_cap_skew;
   uint64_t slot_cap;       // slots: records per (super-tile, XCD shard) slot
   const unsigned* scnt;    // ... their fills
   bool fused;              // the hash wrote regions (unless it found the set skewed)
@@ -1429,13 +1460,16 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
   // This block's records, index j in [lo, hi): the super-tile's kResShards slots back to back
   // (a skewed set, partitioned by k_scatter_res), or the runs its part of the hash blocks left
   // in their regions (prefix rp; record j of run i at region (b0 + i, sidx) + j - rp[i]).
-  const bool regions = in.fused && !st->skew;
+  // regions: the fused partition of either level-0 hash (k_hash_skew's for a skewed set)
+  const bool regions = in.fused;
+  const unsigned NB = st->skew ? in.NB_skew : in.NB;
+  const uint64_t reg_cap = st->skew ? in.reg_cap_skew : in.reg_cap;
   unsigned pre[kResShards + 1];
   uint64_t lo = 0, hi = 0;
   unsigned b0 = 0, nr = 0;
   if (regions) {
-    b0 = (unsigned)((uint64_t)in.NB * part / bps);
-    nr = (unsigned)((uint64_t)in.NB * (part + 1) / bps) - b0;
+    b0 = (unsigned)((uint64_t)NB * part / bps);
+    nr = (unsigned)((uint64_t)NB * (part + 1) / bps) - b0;
     if (nr > (unsigned)NT || nr > kMaxRuns) {  // (the host keeps bps >= NB / NT)
       if (tid == 0) atomicOr(&st->status, kStGeometry);
       return;
@@ -1466,7 +1500,7 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
         if (rp[mid] <= (unsigned)j) a = mid;
         else z = mid;
       }
-      return in.sup + ((uint64_t)(b0 + a) * in.S + sidx) * in.reg_cap + ((unsigned)j - rp[a]);
+      return in.sup + ((uint64_t)(b0 + a) * in.S + sidx) * reg_cap + ((unsigned)j - rp[a]);
     }
     uint64_t o = j;
 #pragma unroll
@@ -3749,7 +3783,7 @@ uint64_t split_scratch_records() { return split_scratch_recs(); }
 // (1.75 ms); S3IMPH_SKEW_ORDER=0 alternates the longest and the shortest batch instead of
 // longest first.
 void launch_hash_skew(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
-                      unsigned long long* prof, hipStream_t s) {
+                      unsigned long long* prof, hipStream_t s, const P0Part& pt = P0Part{}) {
   const int cfg = b.skew_cfg;
   static const int order = [] {  // 1: longest first; 0: alternating longest / shortest
     const char* e = std::getenv("S3IMPH_SKEW_ORDER");
@@ -3757,13 +3791,13 @@ void launch_hash_skew(const uint8_t* blob, const uint64_t* offsets, uint64_t n, 
   }();
   if (cfg == 1)
     k_hash_skew<1024, 4096><<<256, 1024, sk_lds_bytes<1024, 4096>(), s>>>(
-        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order);
+        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order, pt);
   else if (cfg == 2)
     k_hash_skew<768, 5120><<<256, 768, sk_lds_bytes<768, 5120>(), s>>>(
-        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order);
+        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order, pt);
   else
     k_hash_skew<512, 2048><<<512, 512, sk_lds_bytes<512, 2048>(), s>>>(
-        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order);
+        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order, pt);
 }
 
 void binned_set_lds_limits() {
@@ -3961,10 +3995,11 @@ void launch_p0_partition(const BinBuffers& b, const P0Bufs& p, hipStream_t s, bo
 bool p0_fused(const uint8_t* blob, const P0Bufs& p) {
   return ((uintptr_t)blob & 15) == 0 && p.S <= (unsigned)kMaxRanks;
 }
-uint64_t p0_region_cap(uint64_t n, unsigned S) {
-  const double per = (double)((n + kH0Grid - 1) / kH0Grid), mean = per / S;
+uint64_t p0_region_cap(uint64_t n, unsigned S, unsigned blocks) {
+  const double per = (double)((n + blocks - 1) / blocks), mean = per / S;
   return (uint64_t)(mean + 10.0 * std::sqrt(mean) + 32.0);
 }
+unsigned p0_skew_blocks(int skew_cfg) { return skew_cfg == 0 ? 512u : 256u; }  // launch_hash_skew's grid
 
 // P0 level 0's hash and first partition: fused (k_hash0_pair<..., PT>) for an aligned blob
 // of up to kMaxRanks super-tiles, with k_hash_skew + the partition pass standing by for a
@@ -3976,8 +4011,10 @@ void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, co
     const P0Part pt{p.sup, p.reg_cap, p.pcnt, p.tps, p.S};
     k_hash0_pair<kH0T, kH0B, true, false, true><<<kH0Grid, kH0T, 0, s>>>(
         blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, Route0{}, pt);
-    launch_hash_skew(blob, offsets, n, b, g, prof, s);
-    launch_p0_partition(b, p, s, true);
+    // a skewed set: k_hash_skew's groups partition the same way, into regions of its own
+    // (fewer, larger: p0_skew_blocks blocks, reg_cap_skew records each)
+    const P0Part pts{p.sup, p.reg_cap_skew, p.pcnt, p.tps, p.S};
+    launch_hash_skew(blob, offsets, n, b, g, prof, s, pts);
     return;
   }
   launch_binned_count(0, blob, offsets, n, b, g, 256, s, false);
@@ -3985,7 +4022,8 @@ void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, co
 }
 
 void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStream_t s) {
-  const P0In in{p.sup, p.reg_cap, p.pcnt, (unsigned)kH0Grid, p.S, p.sup_cap / ((uint64_t)p.S * kResShards), p.scnt, fused};
+  const P0In in{p.sup, p.reg_cap, p.pcnt, (unsigned)kH0Grid, p.S, p0_skew_blocks(b.skew_cfg), p.reg_cap_skew,
+                p.sup_cap / ((uint64_t)p.S * kResShards), p.scnt, fused};
   // blocks per super-tile: a multiple of kResShards, so every shard slot of a tile takes the
   // records of the same number of blocks (9 blocks put 2/9 of a super-tile's records on one
   // shard: 1.8x the mean fill, past the slot capacity at S = 26)

@@ -456,8 +456,11 @@ P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s) {
   P0Bufs p;
   p.S = (unsigned)std::min<uint64_t>((T + kP0TargetTps - 1) / kP0TargetTps, kP0MaxS);
   p.tps = (unsigned)((T + p.S - 1) / p.S);
-  p.reg_cap = p0_region_cap(n, p.S);
-  const uint64_t need = std::max<uint64_t>((uint64_t)kH0GridHost * p.S * p.reg_cap,
+  p.reg_cap = p0_region_cap(n, p.S, kH0GridHost);
+  const unsigned nbs = p0_skew_blocks(c->skew_cfg);
+  p.reg_cap_skew = p0_region_cap(n, p.S, nbs);
+  const uint64_t need = std::max<uint64_t>(std::max<uint64_t>((uint64_t)kH0GridHost * p.S * p.reg_cap,
+                                                              (uint64_t)nbs * p.S * p.reg_cap_skew),
                                            n + n / 4 + (uint64_t)4096 * p.S * kResShards);
   if (need > c->p0_sup_cap) {
     dalloc(c->p0_sup, need);

@@ -247,6 +247,7 @@ struct P0Bufs {
                                // (fused hash), or S x kResShards slots of sup_cap / (S kResShards) (pass)
   uint64_t sup_cap = 0;        // R20 records in sup
   uint64_t reg_cap = 0;
+  uint64_t reg_cap_skew = 0;   // the same for k_hash_skew's p0_skew_blocks blocks (a skewed set)
   unsigned* pcnt = nullptr;    // region fills (kH0Grid x S), written by the hash
   unsigned* scnt = nullptr;    // super-tile slot fills (S x kResShards), zeroed before the build
   R20* bucket = nullptr;       // tile slots (T x kResShards)
@@ -260,7 +261,8 @@ void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, co
                     const P0Bufs& p, hipStream_t s);
 void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStream_t s);
 bool p0_fused(const uint8_t* blob, const P0Bufs& p);  // the hash partitions (aligned blob, S <= kMaxRanks)
-uint64_t p0_region_cap(uint64_t n, unsigned S);     // records per (hash block, super-tile) region
+uint64_t p0_region_cap(uint64_t n, unsigned S, unsigned blocks);  // records per (hash block, super-tile) region
+unsigned p0_skew_blocks(int skew_cfg);               // k_hash_skew's grid (its fused partition's blocks)
 constexpr int kH0GridHost = 4096;                    // = k_hash0_pair's grid (kH0Grid)
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
 void binned_set_lds_limits();
