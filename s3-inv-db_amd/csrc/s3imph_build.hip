@@ -454,7 +454,11 @@ uint64_t p0_min_tiles() {
 P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s) {
   const uint64_t T = tiles_of(level_words(n_geom), kRegTileMaxBits, 0);
   P0Bufs p;
-  p.S = (unsigned)std::min<uint64_t>((T + kP0TargetTps - 1) / kP0TargetTps, kP0MaxS);
+  static const uint64_t target = [] {  // A/B knob S3IMPH_P0_TPS: tiles per super-tile aimed at
+    const char* e = std::getenv("S3IMPH_P0_TPS");
+    return e ? std::max<uint64_t>(16, std::strtoull(e, nullptr, 10)) : kP0TargetTps;
+  }();
+  p.S = (unsigned)std::min<uint64_t>((T + target - 1) / target, kP0MaxS);
   p.tps = (unsigned)((T + p.S - 1) / p.S);
   p.reg_cap = p0_region_cap(n, p.S, kH0GridHost);
   const unsigned nbs = p0_skew_blocks(c->skew_cfg);
