@@ -258,6 +258,14 @@ __device__ __forceinline__ void r20_split(const R20& r, uint64_t pos_base, uint6
   f = (uint64_t)r.w[2] | ((uint64_t)r.w[3] << 32);
   p = pos_base + r.w[4];
 }
+// A collided record into the next list: Rec, or (o20: the next level's list is R20, see
+// BinBuffers::l20) R20 with the key index p - pos_base.  o20 is a kernel argument: a uniform
+// branch.
+__device__ __forceinline__ void next_put(Rec* next, bool o20, uint64_t i, uint64_t k, uint64_t f, uint64_t p,
+                                         uint64_t pos_base) {
+  if (o20) reinterpret_cast<R20*>(next)[i] = r20_make(k, f, (uint32_t)(p - pos_base));
+  else next[i] = Rec{k, f, p};
+}
 
 // ------------------------------------------------ level-0 hash, LDS-staged ----------
 // FNV-1a + FNV-1 of every key (StreamingMPHFBuilder.Add, mphf_streaming.go:73,80;
@@ -1192,7 +1200,8 @@ constexpr unsigned kSplitSubBitsDev = 14;  // = kSplitSubBits (sub-tile of the s
 // (k = 0) to skip: the multi-GPU build's fixed-size exchange regions (k_route_pad).  A compile-time source keeps the loads
 // straight-line: with run-time selects the compiler waited out every record's loads
 // before issuing the next record's (four round trips per round).
-// kP20 (kSrc 2 only): bucket records are R20 (the split kernel reads them).
+// kP20 (kSrc 2 / 4): bucket records are R20 (the split kernel reads them).  kSrc 4: records
+// from ilist as R20 (a list level with identity positions, BinBuffers::l20).
 template <int kR, int kT, int kSrc, bool kP20 = false>
 __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __restrict__ ilist,
                                                      const uint64_t* __restrict__ ik, const uint64_t* __restrict__ ifp,
@@ -1204,7 +1213,8 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
                                                      uint64_t i_hi, unsigned ts, unsigned gate) {
   constexpr int kKPT = kR / kSB;
   if (gate && !st->skew) return;  // gate: only for a skewed set (the fused P0 hash partitioned the rest)
-  static_assert(!kP20 || kSrc == 2, "20-byte records carry identity positions");
+  static_assert(!kP20 || kSrc == 2 || kSrc == 4, "20-byte records carry identity positions");
+  static_assert(kSrc != 4 || kP20, "an R20 list scatters into R20 slots");
   __shared__ uint64_t stage_raw[kP20 ? (kR * 5 + 1) / 2 : kR * 3];  // kR Rec, or kR R20
   Rec* const stage = reinterpret_cast<Rec*>(stage_raw);
   R20* const stage20 = reinterpret_cast<R20*>(stage_raw);
@@ -1282,7 +1292,12 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   // Level 0 reads the hash kernel's key-order arrays instead of a record list.
   uint64_t rk_[kKPT], rf_[kKPT], rp_[kKPT];
   auto load = [&](uint64_t i, int q) {
-    if constexpr (kSrc == 0 || kSrc == 3) {
+    if constexpr (kSrc == 4) {
+      const R20 r = reinterpret_cast<const R20*>(ilist)[i];
+      rk_[q] = (uint64_t)r.w[0] | ((uint64_t)r.w[1] << 32);
+      rf_[q] = (uint64_t)r.w[2] | ((uint64_t)r.w[3] << 32);
+      rp_[q] = r.w[4];
+    } else if constexpr (kSrc == 0 || kSrc == 3) {
       rk_[q] = ilist[i].k;
       rf_[q] = ilist[i].f;
       rp_[q] = ilist[i].p;
@@ -1352,7 +1367,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
       if (i < n && (kSrc != 3 || rk_[q] != 0)) {
         const unsigned t = trk[q] >> 13, slot = start[t] + (trk[q] & 8191u);
         // identity positions (kSrc 2) are the record's index, recomputed rather than held
-        if constexpr (kP20) stage20[slot] = r20_make(rk_[q], rf_[q], (uint32_t)i);
+        if constexpr (kP20) stage20[slot] = r20_make(rk_[q], rf_[q], (uint32_t)(kSrc == 4 ? rp_[q] : i));
         else stage[slot] = Rec{rk_[q], rf_[q], kSrc == 2 ? pos_base + i : rp_[q]};
         stile[slot] = (unsigned short)t;
       }
@@ -2074,9 +2089,9 @@ constexpr int kSplitT = 1024;
 constexpr int kSplitGrid = kSplitGridHost;  // one workgroup per CU (its LDS takes ~144 KiB)
 __host__ __device__ constexpr uint64_t split_scratch_recs() { return (uint64_t)kSplitGrid * kSplitMaxSub * kSplitSeg; }
 
-// kP20: the bucket holds level 0's R20 records (p = pos_base + i); the scratch segments
-// then hold R20 too.
-template <bool kP20>
+// kP20: the bucket holds R20 records (p = pos_base + i: level 0, or a list level whose list
+// is R20); the scratch segments then hold R20 too.  o20: collided records leave as R20.
+template <bool kP20, bool kO20>
 __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __restrict__ bucket,
                                                         const unsigned* __restrict__ tile_start,
                                                         const unsigned* __restrict__ tcnt, uint64_t bucket_cap,
@@ -2085,6 +2100,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
                                                         uint64_t* __restrict__ pos_out, LevelState* st, unsigned tb,
                                                         Rec* __restrict__ scratch, unsigned long long* __restrict__ prof,
                                                         uint64_t pos_base, unsigned ts) {
+  constexpr bool o20 = kO20;  // (a template argument: as a run-time flag the kernel spilled 7 more VGPRs)
   constexpr int kSU = 3;  // split-phase records per thread per batch (the batch is staged in sfp)
   static_assert((size_t)kSU * kSplitT * sizeof(Rec) <= 2 * kSplitStage * sizeof(uint64_t), "split stage fits sf/sp");
   __shared__ uint32_t sA[1u << (kSplitMaxBits - 5)], sC[1u << (kSplitMaxBits - 5)];
@@ -2363,7 +2379,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
         for (int r = 0; r < kSplitR; ++r) {
           const bool rd = (redo >> r) & 1u;
           const uint64_t mm = __ballot(rd);
-          if (rd) next[o + __popcll(mm & lt)] = Rec{k[r], f[r], p[r]};
+          if (rd) next_put(next, o20, o + __popcll(mm & lt), k[r], f[r], p[r], pos_base);
           o += __popcll(mm);
         }
       } else {
@@ -2403,7 +2419,7 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
             rd = !((sA[loc >> 5] >> (loc & 31)) & 1u);
           }
           const uint64_t mm = __ballot(rd);
-          if (rd) next[o + __popcll(mm & lt)] = Rec{jk, jf, jp};
+          if (rd) next_put(next, o20, o + __popcll(mm & lt), jk, jf, jp, pos_base);
           o += __popcll(mm);
         }
       }
@@ -2772,12 +2788,13 @@ __device__ __forceinline__ uint64_t lb_resolve(unsigned long long* flags, uint64
 
 // k20: R20 records (identity positions: p = pos_base + key index, 12-B stage entries);
 // otherwise Rec records of any level whose tiles are 2^14 positions (16-B stage entries).
+// o20: the collided records leave as R20 (the next level's list is R20, BinBuffers::l20).
 template <bool k20>
 __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restrict__ bucket_v, uint64_t bucket_cap,
                                                   const unsigned* __restrict__ tcnt, unsigned long long* flags,
                                                   uint64_t* __restrict__ bits, Rec* __restrict__ next,
                                                   uint64_t* __restrict__ fp_out, uint64_t* __restrict__ pos_out,
-                                                  LevelState* st, uint64_t pos_base) {
+                                                  LevelState* st, uint64_t pos_base, bool o20) {
   using PT = std::conditional_t<k20, uint32_t, uint64_t>;  // key index, or p
   __shared__ uint64_t sf[kP0Stage];
   __shared__ PT si[kP0Stage];
@@ -2981,7 +2998,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
           const unsigned x = LOC(r);
           const bool redo = j < nk && !((sA[x >> 5] >> (x & 31)) & 1u);
           const uint64_t m = __ballot(redo);
-          if (redo) next[o + __popcll(m & lt)] = Rec{k[r], f[r], pos_of(p[r])};
+          if (redo) next_put(next, o20, o + __popcll(m & lt), k[r], f[r], pos_of(p[r]), pos_base);
           o += __popcll(m);
         }
       } else {
@@ -2997,7 +3014,7 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
             redo = !((sA[x >> 5] >> (x & 31)) & 1u);
           }
           const uint64_t m = __ballot(redo);
-          if (redo) next[o + __popcll(m & lt)] = Rec{jk, jf, pos_of(jp)};
+          if (redo) next_put(next, o20, o + __popcll(m & lt), jk, jf, pos_of(jp), pos_base);
           o += __popcll(m);
         }
       }
@@ -3878,12 +3895,13 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
     // 2^14-position tiles from reservation slots: the persistent, pipelined register tiles
     // (level 0 with identity positions reads the scatter's R20 records)
     const unsigned* tc = b.tcnt + (uint64_t)level * kTcntStride;
-    if (level == 0 && !b.dist && !b.pos)
-      k_tile_p0<true><<<256, kP0T, 0, s>>>(0, b.bucket, b.bucket_cap, tc, b.flags, b.bits, b.list[0], b.fp_out,
-                                           b.pos_out, b.st, b.pos_base);
+    // R20 buckets: level 0 with identity positions, or a level whose list is R20
+    if ((level == 0 && !b.dist && !b.pos) || b.list20(level))
+      k_tile_p0<true><<<256, kP0T, 0, s>>>(level, b.bucket, b.bucket_cap, tc, b.flags, b.bits, b.list[level & 1],
+                                           b.fp_out, b.pos_out, b.st, b.pos_base, b.list20(level + 1));
     else
       k_tile_p0<false><<<256, kP0T, 0, s>>>(level, b.bucket, b.bucket_cap, tc, b.flags, b.bits, b.list[level & 1],
-                                            b.fp_out, b.pos_out, b.st, b.pos_base);
+                                            b.fp_out, b.pos_out, b.st, b.pos_base, b.list20(level + 1));
     return;
   }
   if (g.tb <= kRegMaxBits) {
@@ -3914,8 +3932,11 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
   // and for the 2^17+ tiles of oversized conservative reruns)
   if (b.split && g.tb > kRegMaxBits && g.tb <= kSplitMaxBits) {
     // level 0 through the reservation scatter with identity positions: R20 records
-    const bool p20 = level == 0 && !b.dist && !b.pos && reserved;
-    (p20 ? k_tile_split<true> : k_tile_split<false>)<<<kSplitGrid, kSplitT, 0, s>>>(
+    // (or a list level whose list is R20: the scatter kept them R20)
+    const bool p20 = (level == 0 && !b.dist && !b.pos && reserved) || b.list20(level);
+    const bool o20 = b.list20(level + 1);
+    (p20 ? (o20 ? k_tile_split<true, true> : k_tile_split<true, false>)
+         : (o20 ? k_tile_split<false, true> : k_tile_split<false, false>))<<<kSplitGrid, kSplitT, 0, s>>>(
         level, b.bucket, b.tile_start, tc, b.bucket_cap, b.flags, b.bits, b.list[level & 1], b.fp_out, b.pos_out, b.st,
         g.tb, b.split, b.tile_prof, b.pos_base, reserved ? g.ts : 0u);
     return;
@@ -3949,7 +3970,12 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
   };
   using KFn = decltype(&k_scatter_res<kSubRound, kLdsTiles, 0>);
   KFn kern;
-  if (kt == 1024) {
+  const bool l20 = !l0 && b.list20(level);  // an R20 list (kSrc 4) into R20 slots
+  if (l20) {
+    kern = kt == 1024   ? pick(k_scatter_res<4096, 1024, 4, true>, k_scatter_res<5120, 1024, 4, true>)
+           : kt == 2048 ? pick(k_scatter_res<4096, 2048, 4, true>, k_scatter_res<5120, 2048, 4, true>)
+                        : k_scatter_res<kSubRound, kLdsTiles, 4, true>;
+  } else if (kt == 1024) {
     kern = !l0    ? (b.padded ? pick(k_scatter_res<4096, 1024, 3>, k_scatter_res<5120, 1024, 3>)
                               : pick(k_scatter_res<4096, 1024, 0>, k_scatter_res<5120, 1024, 0>))
            : b.pos ? pick(k_scatter_res<4096, 1024, 1>, k_scatter_res<5120, 1024, 1>)
@@ -4038,7 +4064,7 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
 
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
   k_tile_p0<true><<<256, kP0T, 0, s>>>(0, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.bits, b.list[0], b.fp_out,
-                                       b.pos_out, b.st, b.pos_base);
+                                       b.pos_out, b.st, b.pos_base, b.list20(1));
 }
 
 }  // namespace s3imph

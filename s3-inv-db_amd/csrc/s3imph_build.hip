@@ -180,11 +180,17 @@ int predict_big_levels(uint64_t n) {
 
 // Values that occur more than once among n device records' key hashes (sorted, distinct,
 // at most `cap` of them): the keys a stopped build could not place.
-std::vector<uint64_t> record_dup_values(const Rec* d_list, uint64_t n, size_t cap) {
-  std::vector<Rec> h(n);
-  if (n) HIPCHECK(hipMemcpy(h.data(), d_list, n * sizeof(Rec), hipMemcpyDeviceToHost));
+std::vector<uint64_t> record_dup_values(const Rec* d_list, uint64_t n, size_t cap, bool r20 = false) {
   std::vector<uint64_t> k(n);
-  for (uint64_t i = 0; i < n; ++i) k[i] = h[i].k;
+  if (r20) {  // an R20 list (BinBuffers::l20): k is dwords 0-1
+    std::vector<R20> h(n);
+    if (n) HIPCHECK(hipMemcpy(h.data(), d_list, n * sizeof(R20), hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < n; ++i) k[i] = (uint64_t)h[i].w[0] | ((uint64_t)h[i].w[1] << 32);
+  } else {
+    std::vector<Rec> h(n);
+    if (n) HIPCHECK(hipMemcpy(h.data(), d_list, n * sizeof(Rec), hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < n; ++i) k[i] = h[i].k;
+  }
   std::sort(k.begin(), k.end());
   std::vector<uint64_t> out;
   for (uint64_t i = 1; i < n && out.size() < cap; ++i)
@@ -217,7 +223,7 @@ int classify_stop(s3imph_ctx* c, unsigned flags, const uint8_t* blob, const uint
   const unsigned S = h.stop_level;
   std::vector<uint64_t> left;
   if ((flags & kStTooManyLevels) && S >= 1 && S < (unsigned)kMaxLevels + 2 && h.n[S])
-    left = record_dup_values(c->list[(S - 1) & 1], h.n[S], 1);
+    left = record_dup_values(c->list[(S - 1) & 1], h.n[S], 1, S < 32 && ((c->l20_mask >> S) & 1u));
   const std::vector<uint64_t> orig = original_key_hashes(c, blob, offsets, n, s);
   if (std::adjacent_find(orig.begin(), orig.end()) != orig.end()) {
     *msg = "build MPHF: duplicate FNV-1a key hashes: bbhash cannot place them";
@@ -251,8 +257,10 @@ int map_status(s3imph_ctx* c, unsigned flags, const uint8_t* blob, const uint64_
 // Test hook (S3IMPH_FAULT_DUP_REC, read at context creation): copy record 0 of a list over
 // record 1, as a kernel race that duplicated a record would, so the tests can check that the
 // stop it causes is reported as an internal fault and not as the caller's duplicate keys.
-void fault_dup_record(s3imph_ctx* c, Rec* list, hipStream_t s) {
-  if (c->fault_dup) HIPCHECK(hipMemcpyAsync(list + 1, list, sizeof(Rec), hipMemcpyDeviceToDevice, s));
+void fault_dup_record(s3imph_ctx* c, Rec* list, hipStream_t s, bool r20 = false) {
+  const size_t sz = r20 ? sizeof(R20) : sizeof(Rec);
+  if (c->fault_dup)
+    HIPCHECK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(list) + sz, list, sz, hipMemcpyDeviceToDevice, s));
 }
 
 BinBuffers make_bufs(s3imph_ctx* c, const uint64_t* pos, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s) {
@@ -359,16 +367,27 @@ unsigned choose_split_ts(uint64_t size, bool exact) {
 
 // One list-input level L (records in list[(L-1)&1]): about nb records over `size`
 // positions.  Small levels take the reservation scatter (no count / histogram scan).
-void enqueue_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, uint64_t size, bool conservative,
-                        const LevelGeom* force, hipStream_t s, bool exact_size = false) {
+struct ListPlan {
+  bool res;
+  LevelGeom g;
+};
+ListPlan plan_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, uint64_t size, bool conservative,
+                         const LevelGeom* force, bool exact_size) {
   // reservation slots are bucket_cap / T records per tile: keep them >= 4x the mean fill
   const bool res = !conservative && nb <= c->res_max_keys && res_fits(c, nb, size) && L < kResLevels;
   LevelGeom g = force ? *force
                 : res ? choose_geom_sz(nb, size, kTargetTilesRes, kTargetChunks, kRegTileMaxBits)
                       : choose_geom_sz(nb, size, kTargetTiles, kTargetChunks, kRegTileMaxBits);
   if (res && !force && b.split && g.tb > kRegTileMaxBits && g.tb <= kSplitMaxBits) g.ts = choose_split_ts(size, exact_size);
+  return ListPlan{res, g};
+}
+
+void enqueue_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, uint64_t size, bool conservative,
+                        const LevelGeom* force, hipStream_t s, bool exact_size = false) {
+  const ListPlan pl = plan_list_level(c, b, L, nb, size, conservative, force, exact_size);
+  const LevelGeom g = pl.g;
   const Grids gr = level_grids(nb, size, g);
-  if (res) {
+  if (pl.res) {
     const int gsr = (int)std::min<uint64_t>((nb + kSubRound - 1) / kSubRound, 256);
     launch_binned_scatter_res(L, b, g, std::max(gsr, 1), s, 0, 0, tiles_of((size + 63) / 64, g.tb, b.split ? g.ts : 0));
     launch_binned_tile(L, b, g, gr.gt, s, true);
@@ -380,14 +399,31 @@ void enqueue_list_level(s3imph_ctx* c, const BinBuffers& b, int L, uint64_t nb, 
   }
 }
 
-// Levels L0, L0+1, ... of a whole-level build (every position on this GPU), starting
-// from n0 records in list[(L0-1)&1]: predicted-big levels as full-grid kernels, then
-// the single-workgroup tail.  Returns the last big level launched (L0-1 if none).
-int enqueue_levels_from(s3imph_ctx* c, const BinBuffers& b, int L0, uint64_t n0, const LevelGeom& gcons,
-                        bool conservative, hipStream_t s) {
+// Does a reservation level of geometry g run a tile kernel that reads and writes R20 records
+// (k_tile_p0 on 2^14-position tiles, k_tile_split on 2^15-2^18)?  launch_binned_tile's choice.
+bool r20_tiles(const BinBuffers& b, const LevelGeom& g) {
+  return (g.tb == kRegTileMaxBits && b.pipe_tiles) || (b.split && g.tb > kRegTileMaxBits && g.tb <= kSplitMaxBits);
+}
+
+// The levels enqueue_levels_from runs from L0 (n0 records in list[(L0-1)&1]): predicted-big
+// levels as full-grid kernels (lv, consecutive from L0), then at most one k_mid_levels range.
+struct LevelsPlan {
+  struct Lv {
+    int L;
+    uint64_t nb, size;
+    bool tight;
+    ListPlan pl;
+  };
+  std::vector<Lv> lv;
+  int mid0 = -1, mid1 = -1;
+  int launched;  // the last big level launched (L0 - 1 if none)
+};
+LevelsPlan plan_levels_from(s3imph_ctx* c, const BinBuffers& b, int L0, uint64_t n0, const LevelGeom& gcons,
+                            bool conservative) {
   const double q = 1.0 - std::exp(-0.5);  // fraction of keys that collide at load 1/2
   const int big = conservative ? kMaxLevels - 2 : L0 - 1 + predict_big_levels(n0 / q);
-  int launched = L0 - 1;
+  LevelsPlan P;
+  P.launched = L0 - 1;
   for (int L = L0; L <= big && L < kMaxLevels - 1; ++L) {
     // Level sizes concentrate tightly around n q^L; a level predicted within 1/kTailMargin
     // of the tail's capacity is left to the tail (an unexpectedly large one is caught by
@@ -399,22 +435,63 @@ int enqueue_levels_from(s3imph_ctx* c, const BinBuffers& b, int L0, uint64_t n0,
       int L1 = L;
       while (L1 + 1 <= big && L1 + 1 < kMaxLevels - 1 && pred * std::pow(q, L1 + 1 - L) * kTailMargin >= (double)kTailKeys)
         ++L1;
-      launch_binned_mid(L, L1, b, s);
-      launched = L1;
+      P.mid0 = L;
+      P.mid1 = L1;
+      P.launched = L1;
       break;
     }
-    launched = L;
+    P.launched = L;
     const uint64_t nb = conservative ? n0 : (uint64_t)(pred * 1.1) + 4096;
     // geometry from a tight bound on the level's size (level sizes concentrate: sigma ~ sqrt(n));
     // a level past it flags kStGeometry and the build reruns conservatively
     const bool tight = !conservative && !c->loose_geom;
     const uint64_t nsz = tight ? (uint64_t)(pred * 1.02 + 6.0 * std::sqrt(pred)) + 1024 : nb;
-    enqueue_list_level(c, b, L, nb, 64 * level_words(nsz), conservative, conservative ? &gcons : nullptr, s, tight);
+    const uint64_t size = 64 * level_words(nsz);
+    P.lv.push_back({L, nb, size, tight,
+                    plan_list_level(c, b, L, nb, size, conservative, conservative ? &gcons : nullptr, tight)});
   }
+  return P;
+}
+
+// BinBuffers::l20 for a single-GPU build with identity positions: level L's list is R20 when
+// level L - 1's tile kernel writes R20 (prev_r20 for L0 - 1) and level L is a reservation
+// level on an R20 tile kernel.  Mid and tail levels read Rec lists.
+unsigned plan_l20(const s3imph_ctx* c, const BinBuffers& b, const LevelsPlan& P, bool prev_r20, uint64_t n) {
+  if (!c->l20 || b.pos || b.dist || n >= (1ull << 32)) return 0;
+  unsigned m = 0;
+  bool prev = prev_r20;
+  for (const auto& v : P.lv) {
+    const bool cap = v.pl.res && r20_tiles(b, v.pl.g);
+    if (prev && cap && v.L < 32) m |= 1u << v.L;
+    prev = cap;
+  }
+  return m;
+}
+
+// Levels L0, L0+1, ... of a whole-level build (every position on this GPU), starting
+// from n0 records in list[(L0-1)&1]: predicted-big levels as full-grid kernels, then
+// the single-workgroup tail.  Returns the last big level launched (L0-1 if none).
+int run_levels(s3imph_ctx* c, const BinBuffers& b, const LevelsPlan& P, int L0, hipStream_t s) {
+  for (const auto& v : P.lv) {
+    const LevelGeom g = v.pl.g;
+    enqueue_list_level(c, b, v.L, v.nb, v.size, false, &g, s, v.tight);
+  }
+  if (P.mid0 >= 0) launch_binned_mid(P.mid0, P.mid1, b, s);
   ev_mark(c, s, "levels");
-  launch_binned_tail(L0, launched, b, s);
+  launch_binned_tail(L0, P.launched, b, s);
   ev_mark(c, s, "tail");
-  return launched;
+  return P.launched;
+}
+int enqueue_levels_from(s3imph_ctx* c, const BinBuffers& b, int L0, uint64_t n0, const LevelGeom& gcons,
+                        bool conservative, hipStream_t s) {
+  const LevelsPlan P = plan_levels_from(c, b, L0, n0, gcons, conservative);
+  if (!conservative) return run_levels(c, b, P, L0, s);
+  for (const auto& v : P.lv) enqueue_list_level(c, b, v.L, v.nb, v.size, true, &gcons, s, v.tight);
+  if (P.mid0 >= 0) launch_binned_mid(P.mid0, P.mid1, b, s);
+  ev_mark(c, s, "levels");
+  launch_binned_tail(L0, P.launched, b, s);
+  ev_mark(c, s, "tail");
+  return P.launched;
 }
 
 // Chunks (hash blocks) of the level-0 hash over n keys.  Blocks are scheduled as they
@@ -492,7 +569,8 @@ P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s) {
 
 void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
-  const BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
+  BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
+  c->l20_mask = 0;
   const double q = 1.0 - std::exp(-0.5);
   const uint64_t T14 = tiles_of(level_words(n), kRegTileMaxBits, 0);
   if (!conservative && c->p0 && !pos && n <= kP0MaxKeys && !hash_only_knob() && T14 > p0_min_tiles() &&
@@ -500,6 +578,9 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
     // level 0 in 2^14-position register tiles through super-tiles (s3imph_internal.h, P0)
     const P0Bufs p = p0_bufs(c, n, n, s);
     const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
+    // the list levels' plan first: level 0's tile kernel writes level 1's list as R20 or Rec
+    const LevelsPlan P = plan_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false);
+    b.l20 = c->l20_mask = plan_l20(c, b, P, true, n);
     launch_init_state(c->d_st, n, n, s, offsets);
     ev_mark(c, s, "init");
     launch_p0_hash(blob, offsets, n, b, g0, p, s);
@@ -508,8 +589,8 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
     ev_mark(c, s, "scatter0_p0");
     launch_p0_tile(b, p, s);
     ev_mark(c, s, "tile0_p0");
-    fault_dup_record(c, c->list[0], s);
-    enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
+    fault_dup_record(c, c->list[0], s, b.list20(1));
+    run_levels(c, b, P, 1, s);
     return;
   }
   const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
@@ -526,12 +607,14 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   if (res0) {
     LevelGeom gr0 = g0;  // split-kernel level 0: tiles in whole rounds over the CUs (exact size)
     if (b.split && g0.tb > kRegTileMaxBits && g0.tb <= kSplitMaxBits) gr0.ts = choose_split_ts(64 * level_words(n), true);
+    const LevelsPlan P = plan_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false);
+    b.l20 = c->l20_mask = plan_l20(c, b, P, r20_tiles(b, gr0), n);
     launch_binned_scatter_res(0, b, gr0, 256, s, 0, 0, tiles_of(level_words(n), gr0.tb, b.split ? gr0.ts : 0));
     ev_mark(c, s, "scatter0");
     launch_binned_tile(0, b, gr0, gr.gt, s, true);
     ev_mark(c, s, "tile0");
-    fault_dup_record(c, c->list[0], s);
-    enqueue_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false, s);
+    fault_dup_record(c, c->list[0], s, b.list20(1));
+    run_levels(c, b, P, 1, s);
     return;
   }
   launch_binned_scan(0, b, gr.gs, s);
@@ -2204,6 +2287,7 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
     c->fault_dup = std::getenv("S3IMPH_FAULT_DUP_REC") != nullptr;
     if (const char* m = std::getenv("S3IMPH_P0")) c->p0 = std::atoi(m);
+    if (const char* m = std::getenv("S3IMPH_L20")) c->l20 = std::atoi(m) != 0;
     if (const char* m = std::getenv("S3IMPH_BM_LANES")) c->bm_counts = std::strcmp(m, "counts") == 0;
     if (const char* m = std::getenv("S3IMPH_SCAT_CFG")) c->scat_cfg = std::atoi(m);
     if (const char* m = std::getenv("S3IMPH_SKEW_CFG")) c->skew_cfg = std::atoi(m);

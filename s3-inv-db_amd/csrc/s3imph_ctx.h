@@ -227,6 +227,10 @@ struct s3imph_ctx {
   unsigned* p0_pcnt = nullptr;  // the fused hash's region fills (kH0GridHost x kMaxRanks)
   s3imph::R20* p0_sup = nullptr;  // the super-tiles' records
   uint64_t p0_sup_cap = 0;
+  // R20 list levels (BinBuffers::l20): on unless S3IMPH_L20=0 (A/B knob); l20_mask is the
+  // last build's mask (classify_stop reads its stop level's list in that format)
+  bool l20 = true;
+  unsigned l20_mask = 0;
   bool bm_counts = false;   // S3IMPH_BM_LANES=counts: the bitmap decomposition sums count lanes (A/B knob)
   bool debug = false;
   bool fault_dup = false;   // S3IMPH_FAULT_DUP_REC: test hook, duplicates a record mid-build (fault_dup_record)

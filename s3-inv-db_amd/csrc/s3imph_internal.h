@@ -221,6 +221,12 @@ struct BinBuffers {
   int scat_cfg = 2;                     // k_scatter_res forms (launch_binned_scatter_res)
   bool pipe_tiles = false;              // 2^14 reservation tiles on k_tile_p0 (else k_tile_reg)
   int skew_cfg = 2;                     // k_hash_skew block / group shape (launch_hash_skew)
+  // bit L (L >= 1): level L's input list holds R20 records (k, f, key index; identity
+  // positions) instead of Rec: its producer (k_tile_p0 / k_tile_split of level L - 1) writes
+  // them, its reservation scatter reads them and keeps them R20 in the slots, and its tile
+  // kernel (k_tile_p0 / k_tile_split) reads R20 — 4 bytes less per record on every pass
+  unsigned l20 = 0;
+  bool list20(int L) const { return L >= 1 && L < 32 && ((l20 >> L) & 1u); }
 };
 uint64_t split_scratch_records();  // sub-tile segments of the split big-tile kernel
 

@@ -452,6 +452,26 @@ def test_skew_shapes_bit_exact(s3, oracle_lib, cfg, monkeypatch):
         c.close()
 
 
+@pytest.mark.parametrize("l20", ["0", "1"])
+def test_list_record_formats_bit_exact(s3, oracle_lib, l20, monkeypatch):
+    """List levels on the reservation path carry R20 records (k, f, key index) by default and
+    Rec (k, f, p) with S3IMPH_L20=0: both byte-identical to the oracle on a 6M set whose
+    levels 1-3 are reservation levels on the persistent 2^14-position tiles."""
+    monkeypatch.setenv("S3IMPH_L20", l20)
+    c = s3.DeviceBuilder(0)
+    try:
+        n = 6_000_000
+        blob, offs = s3.gen_keys(0, 31, 40, 0, n)
+        st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)
+        assert st == 0
+        gfp, gpo, gmph, info = _device_build(s3, c, blob, offs)
+        assert gmph == mph
+        assert np.array_equal(gfp, fp)
+        assert np.array_equal(gpo, po)
+    finally:
+        c.close()
+
+
 def test_c2_10m_bit_exact(s3, oracle_lib, ctx):
     """BASELINE config 2: 10M synthetic prefixes, avg 32 B — full bit-exact comparison."""
     n = 10_000_000
