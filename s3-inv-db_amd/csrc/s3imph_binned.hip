@@ -1440,13 +1440,14 @@ struct P0In {
   const unsigned* scnt;    // ... their fills
   bool fused;              // the hash wrote regions (unless it found the set skewed)
 };
+
 template <int kR, int kT, int NT = kSB>  // (512 threads, 2560-record rounds, two blocks per CU: slower)
 __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsigned tps, R20* __restrict__ bucket,
                                                     uint64_t bcap, unsigned* __restrict__ tcnt,
                                                     unsigned long long* __restrict__ flags, LevelState* st,
                                                     unsigned long long* __restrict__ prof) {
   constexpr int kKPT = kR / NT;
-  constexpr unsigned kMaxRuns = kH0Grid / 8 + 1;  // bps >= 8 (S <= kP0MaxS = 32 super-tiles over 256 blocks)
+  constexpr unsigned kMaxRuns = kH0Grid / 8 + 1;  // bps >= 8 (launch_p0_scatter)
   __shared__ uint64_t stage_raw[(kR * 5 + 1) / 2];
   R20* const stage = reinterpret_cast<R20*>(stage_raw);
   __shared__ unsigned short stile[kR];
@@ -4053,6 +4054,20 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
   // blocks per super-tile: a multiple of kResShards, so every shard slot of a tile takes the
   // records of the same number of blocks (9 blocks put 2/9 of a super-tile's records on one
   // shard: 1.8x the mean fill, past the slot capacity at S = 26)
+  if (p.S > kP0OneBlockS) {
+    // more than 32 super-tiles: 8 blocks of 512 threads each (two per CU), 3072-record rounds
+    // (2560 with 1024-tile counters, so two blocks' LDS fit a CU): shorter rounds than the
+    // one-block form's 5120, but as many records per tile and round at S = 64 (tps ~ 191 vs
+    // 382), and one block's count / scan / stage phases run beside the other's loads and stores
+    constexpr unsigned bps = kResShards;
+    if (p.tps <= 256)
+      k_scatter_p0<3072, 256, 512><<<p.S * bps, 512, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+    else if (p.tps <= 512)
+      k_scatter_p0<3072, 512, 512><<<p.S * bps, 512, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+    else
+      k_scatter_p0<2560, 1024, 512><<<p.S * bps, 512, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+    return;
+  }
   const unsigned bps = std::max(1u, 256u / p.S / kResShards) * kResShards;
   if (p.tps <= 256)
     k_scatter_p0<5120, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);

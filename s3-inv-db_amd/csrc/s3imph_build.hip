@@ -522,6 +522,22 @@ uint64_t p0_min_tiles() {
   return v;
 }
 
+// The most super-tiles P0 cuts level 0 into (A/B knob S3IMPH_P0_MAXS, at most kP0MaxS).  32 by
+// default: 64 super-tiles on the two-block scatter measured no faster there (C3 scatter0_p0
+// 1.23 / 1.29 ms either way) and cost the fused hash partition 0.05-0.11 ms (shorter runs per
+// round), so more than 32 are taken only when a level's tiles need them (tps <= kP0MaxTps).
+uint64_t p0_max_s() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("S3IMPH_P0_MAXS");
+    return e ? std::max<uint64_t>(1, std::min<uint64_t>(std::strtoull(e, nullptr, 10), kP0MaxS)) : (uint64_t)kP0OneBlockS;
+  }();
+  return v;
+}
+uint64_t p0_super_tiles(uint64_t T, uint64_t target) {
+  const uint64_t S = std::min<uint64_t>((T + target - 1) / target, p0_max_s());
+  return std::max<uint64_t>(S, (T + kP0MaxTps - 1) / kP0MaxTps);  // <= kP0MaxS under the callers' gate
+}
+
 // P0 geometry and buffers for level 0 of n keys over the positions of n_geom keys (the whole
 // level: n_geom = n, or the global key count of the bitmap decomposition), identity
 // positions: T 2^14-position tiles
@@ -535,7 +551,7 @@ P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s) {
     const char* e = std::getenv("S3IMPH_P0_TPS");
     return e ? std::max<uint64_t>(16, std::strtoull(e, nullptr, 10)) : kP0TargetTps;
   }();
-  p.S = (unsigned)std::min<uint64_t>((T + target - 1) / target, kP0MaxS);
+  p.S = (unsigned)p0_super_tiles(T, target);
   p.tps = (unsigned)((T + p.S - 1) / p.S);
   p.reg_cap = p0_region_cap(n, p.S, kH0GridHost);
   const unsigned nbs = p0_skew_blocks(c->skew_cfg);

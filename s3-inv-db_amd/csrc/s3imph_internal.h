@@ -238,10 +238,13 @@ uint64_t split_scratch_records();  // sub-tile segments of the split big-tile ke
 constexpr uint64_t kP0MinTiles = 2048;
 constexpr uint64_t kP0MaxTps = 1024;
 constexpr uint64_t kP0TargetTps = 192;  // tiles per super-tile aimed at
-// at most 32 super-tiles: k_scatter_p0 gives each one 256 / S >= 8 blocks, so the records of
-// a tile arrive through all kResShards XCD shards (4 blocks per super-tile filled only 4 of a
-// tile's 8 shard slots: twice their capacity on average, C3 overflowed into the rerun)
-constexpr uint64_t kP0MaxS = 32;
+// at most 64 super-tiles.  Up to 32, k_scatter_p0 gives each one 256 / S >= 8 blocks of 1024
+// threads (one per CU); above, 8 blocks of 512 threads (two per CU, one's LDS phases beside
+// the other's memory phases).  Either way the records of a tile arrive through all kResShards
+// XCD shards (4 blocks per super-tile filled only 4 of a tile's 8 shard slots: twice their
+// capacity on average, C3 overflowed into the rerun).  S3IMPH_P0_MAXS lowers the cap (A/B).
+constexpr uint64_t kP0MaxS = 64;
+constexpr unsigned kP0OneBlockS = 32;  // the largest S on one 1024-thread block per CU
 constexpr uint64_t kP0MaxKeys = 1ull << 31;  // bucket slot indices stay below 2^32
 // A level-0 record with an identity position: k (2 dwords), f (2), key index i (p = pos_base + i).
 struct R20 {
@@ -342,8 +345,8 @@ void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const Lev
 // most kScatterTiles of them (levels of up to 2^31 positions); the settle kernel keeps 18 B
 // per tile word in LDS: 144 KiB at 2^19 positions.
 constexpr unsigned kBmMinTb = 14, kBmMaxTb = 19;
-// tiles of a bitmap level: kScatterTiles from the reservation scatter, or up to kP0MaxS x
-// kP0MaxTps 2^14-position tiles from the P0 super-tile scatter (level 0)
+// tiles of a bitmap level: kScatterTiles from the reservation scatter, or up to kBmMaxTiles
+// 2^14-position tiles from the P0 super-tile scatter (level 0)
 constexpr uint64_t kBmMaxTiles = 32768;
 // level end: per-tile totals of the final bits -> tbase[2t] (rank within the level), tbase[2t+1]
 // (first slot in this rank's settled list, continuing *out_cnt, which it then advances)

@@ -638,6 +638,19 @@ def _parity_subprocess(env: dict, cases) -> None:
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
+def test_p0_many_super_tiles_bit_exact(s3, oracle_lib):
+    """More than 32 super-tiles (S3IMPH_P0_TPS=48 S3IMPH_P0_MAXS=64: 45 / 51 of them on 17.5M uniform / 20M
+    skewed keys): the super-tile scatter runs two 512-thread blocks per CU, 8 per super-tile,
+    reading the fused hash's regions and k_hash_skew's; bit-exact."""
+    _parity_subprocess({"S3IMPH_P0_TPS": "48", "S3IMPH_P0_MAXS": "64"}, [(17_500_000, 0, 20), (20_000_000, 1, 0)])
+
+
+def test_p0_super_tile_cap_bit_exact(s3, oracle_lib):
+    """S3IMPH_P0_MAXS=64 (A/B knob; 32 by default): 60M short keys in 39 super-tiles of 188
+    tiles on the two-block-per-CU super-tile scatter instead of 32 of 229: bit-exact."""
+    _parity_subprocess({"S3IMPH_P0_MAXS": "64"}, [(60_000_000, 0, 12)])
+
+
 def test_counted_path_every_level(s3, oracle_lib):
     """With the reservation scatter off (S3IMPH_RES_MAX=0, S3IMPH_RES0=0) every level runs
     count -> histogram scan -> counted scatter -> tile: bit-exact."""
