@@ -26,6 +26,7 @@
 #include "s3imph_internal.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace s3imph {
 
@@ -367,7 +368,10 @@ __device__ __forceinline__ void fp_out_own(const OwnSlice& os, uint64_t p, uint6
   os.fp_out[o] = f;
   os.pos_out[o] = pos;
 }
-template <class RT>
+// kStaged (R20 records in 2^14-position tiles: P0's level 0): this rank's settled keys of a
+// tile (<= ~5.2k at one rank) are staged in LDS behind the tile words.  kO20: the collided
+// records leave as R20 (k, f, p - pos_base), the next bitmap level's list (BinBuffers::l20).
+template <class RT, bool kStaged, bool kO20>
 __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __restrict__ bucket, uint64_t pos_base,
                                                         const unsigned* __restrict__ tc, uint64_t bucket_cap,
                                                         unsigned tb, LevelState* st, const uint64_t* __restrict__ g,
@@ -375,9 +379,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
                                                         const unsigned long long* __restrict__ tbase,
                                                         Rec* __restrict__ out, uint64_t out_cap,
                                                         Rec* __restrict__ next, uint64_t next_cap, OwnSlice os) {
-  // R20 records come in 2^14-position tiles (P0's level 0): this rank's settled keys of a
-  // tile (<= ~5.2k at one rank) are staged in LDS behind the tile words
-  constexpr bool kStaged = sizeof(RT) != sizeof(Rec);
+  static_assert(!kStaged || sizeof(RT) != sizeof(Rec), "staged settles read R20 tiles");
   extern __shared__ uint64_t bm_lds64[];
   __shared__ unsigned long long s_w[kTT / 64];
   __shared__ unsigned s_sc[kMaxRanks];
@@ -527,10 +529,11 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
           }
         } else {
           const uint64_t slot = nb + atomicAdd(&s_ncur, 1u);
-          if (slot < next_cap)
-            next[slot] = r[u];
-          else
-            over = true;
+          if (slot >= next_cap) over = true;
+          else if constexpr (kO20) reinterpret_cast<R20*>(next)[slot] = R20{{(uint32_t)r[u].k, (uint32_t)(r[u].k >> 32),
+                                                                          (uint32_t)r[u].f, (uint32_t)(r[u].f >> 32),
+                                                                          (uint32_t)(r[u].p - pos_base)}};
+          else next[slot] = r[u];
         }
       }
     }
@@ -633,10 +636,12 @@ void bm_set_lds_limits() {
                         (const void*)k_bm_tile_mark<kBmPlanes, Rec>, (const void*)k_bm_tile_mark<kBmBytes, R20>,
                         (const void*)k_bm_tile_mark<kBmNibbles, R20>, (const void*)k_bm_tile_mark<kBmPlanes, R20>})
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_tile_lds(kBmMaxTb, false));
-  (void)hipFuncSetAttribute((const void*)k_bm_tile_settle<Rec>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)bm_tile_lds(kBmMaxTb, true));
-  (void)hipFuncSetAttribute((const void*)k_bm_tile_settle<R20>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(bm_tile_lds(kBmMinTb, true) + kBmStage * sizeof(Rec)));
+  for (const void* k : {(const void*)k_bm_tile_settle<Rec, false, false>, (const void*)k_bm_tile_settle<Rec, false, true>,
+                        (const void*)k_bm_tile_settle<R20, false, false>, (const void*)k_bm_tile_settle<R20, false, true>})
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_tile_lds(kBmMaxTb, true));
+  for (const void* k : {(const void*)k_bm_tile_settle<R20, true, false>, (const void*)k_bm_tile_settle<R20, true, true>})
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(bm_tile_lds(kBmMinTb, true) + kBmStage * sizeof(Rec)));
 }
 
 void launch_bm_range(LevelState* st, int level, hipStream_t s) { k_bm_range<<<1, 64, 0, s>>>(st, level); }
@@ -664,16 +669,22 @@ void launch_bm_merge(const uint64_t* recv, uint64_t S, int P, uint64_t* out, con
 void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos_base, const unsigned* tc,
                            uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
                            const uint64_t* A, const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next,
-                           uint64_t next_cap, const OwnSlice& os, hipStream_t s) {
+                           uint64_t next_cap, bool next20, const OwnSlice& os, hipStream_t s) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1024));
-  if (r20)
-    k_bm_tile_settle<R20><<<grid, kTT, bm_tile_lds(tb, true) + kBmStage * sizeof(Rec), s>>>(level, static_cast<const R20*>(bucket), pos_base, tc,
-                                                                   bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
-                                                                   next_cap, os);
-  else
-    k_bm_tile_settle<Rec><<<grid, kTT, bm_tile_lds(tb, true), s>>>(level, static_cast<const Rec*>(bucket), pos_base, tc,
-                                                                   bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
-                                                                   next_cap, os);
+  auto go = [&](auto rt, auto staged, auto o20) {
+    using RT = decltype(rt);
+    constexpr bool kSt = decltype(staged)::value, kO = decltype(o20)::value;
+    const size_t lds = bm_tile_lds(tb, true) + (kSt ? kBmStage * sizeof(Rec) : 0);
+    k_bm_tile_settle<RT, kSt, kO><<<grid, kTT, lds, s>>>(level, static_cast<const RT*>(bucket), pos_base, tc, bucket_cap,
+                                                          tb, st, g, A, tbase, out, out_cap, next, next_cap, os);
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  // R20 2^14-position tiles stage their settled keys (P0's level 0); R20 list levels' larger
+  // tiles write them directly, as Rec buckets do
+  if (r20 && tb == kBmMinTb) next20 ? go(R20{}, T_{}, T_{}) : go(R20{}, T_{}, F_{});
+  else if (r20) next20 ? go(R20{}, F_{}, T_{}) : go(R20{}, F_{}, F_{});
+  else next20 ? go(Rec{}, F_{}, T_{}) : go(Rec{}, F_{}, F_{});
 }
 
 void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,

@@ -1642,7 +1642,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   BinBuffers bs = b;
   bs.dist = false;
   bs.split = nullptr;
-  bs.pipe_tiles = false;  // the bitmap kernels read Rec buckets
+  bs.pipe_tiles = false;  // the bitmap kernels read Rec buckets (R20 ones on R20 list levels, BinBuffers::l20)
   bs.pos = pos;
   bs.pos_base = key_base;
   // Level sizes: the host bounds n_L from above (mean q n + 6 sigma), so every collective's
@@ -1684,7 +1684,8 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     } else {
       launch_binned_scatter_res(L, bs, g, gsr, s, 0, 0, tiles);
     }
-    launch_bm_tile_mark(L, bk, l0p, tc, bcap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, lanes, S, s);
+    const bool in20 = l0p || bs.list20(L);  // R20 slots: P0's level 0, or a level whose list is R20
+    launch_bm_tile_mark(L, bk, in20, tc, bcap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, lanes, S, s);
     if (lanes == kBmPlanes) {
       // slice t's planes (2 S words) to rank t; rank q's planes of this rank's slice land at 2 S q
       for (int t = 0; t < P; ++t) {
@@ -1699,12 +1700,17 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     }
     cm.allgather(d.bm_dec, d.bm_g, 8 * S, s);
     launch_bm_level_end(L, d.bm_g, d.bm_a, tb, tiles, c->bits, d.bm_tsum, d.bm_tbase, st, d.gslot, out_cnt, s);
-    launch_bm_tile_settle(L, bk, l0p, key_base, tc, bcap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
-                          d.bm_cap_out, c->list[L & 1], d.cap_list, own_slice, s);
-    ev_mark(c, s, L == 0 ? "level0" : "levels");
+    // the next level is a bitmap level too (else the replicated tail, which reads Rec): its
+    // list goes out as R20 with identity positions (BinBuffers::l20)
     const double nbn = nb * q + 6.0 * std::sqrt(nb) + 64.0;
+    const bool more = !(L + 1 >= kMaxDistLevels || nbn <= (double)c->dist_switch);
+    const bool next20 = more && c->l20 && !pos && L + 1 < 32;
+    if (next20) bs.l20 |= 1u << (L + 1);
+    launch_bm_tile_settle(L, bk, in20, key_base, tc, bcap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
+                          d.bm_cap_out, c->list[L & 1], d.cap_list, next20, own_slice, s);
+    ev_mark(c, s, L == 0 ? "level0" : "levels");
     npred *= q;
-    if (L + 1 >= kMaxDistLevels || nbn <= (double)c->dist_switch) break;
+    if (!more) break;
     nb = nbn;
     ++L;
   }

@@ -374,7 +374,7 @@ struct OwnSlice {
 void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos_base, const unsigned* tc,
                            uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
                            const uint64_t* A, const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next,
-                           uint64_t next_cap, const OwnSlice& os, hipStream_t s);
+                           uint64_t next_cap, bool next20, const OwnSlice& os, hipStream_t s);
 void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,
                      LevelState* st, hipStream_t s);
 void launch_bm_tail_copy(const uint64_t* sfp, const uint64_t* spos, uint64_t g0, uint64_t total, uint64_t lo,
