@@ -3973,8 +3973,8 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
   KFn kern;
   const bool l20 = !l0 && b.list20(level);  // an R20 list (kSrc 4) into R20 slots
   if (l20) {
-    kern = kt == 1024   ? pick(k_scatter_res<4096, 1024, 4, true>, k_scatter_res<5120, 1024, 4, true>)
-           : kt == 2048 ? pick(k_scatter_res<4096, 2048, 4, true>, k_scatter_res<5120, 2048, 4, true>)
+    kern = kt == 1024   ? pick(k_scatter_res<4096, 1024, 4, true>, k_scatter_res<6144, 1024, 4, true>)
+           : kt == 2048 ? pick(k_scatter_res<4096, 2048, 4, true>, k_scatter_res<6144, 2048, 4, true>)
                         : k_scatter_res<kSubRound, kLdsTiles, 4, true>;
   } else if (kt == 1024) {
     kern = !l0    ? (b.padded ? pick(k_scatter_res<4096, 1024, 3>, k_scatter_res<5120, 1024, 3>)
