@@ -3980,13 +3980,13 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
     kern = !l0    ? (b.padded ? pick(k_scatter_res<4096, 1024, 3>, k_scatter_res<5120, 1024, 3>)
                               : pick(k_scatter_res<4096, 1024, 0>, k_scatter_res<5120, 1024, 0>))
            : b.pos ? pick(k_scatter_res<4096, 1024, 1>, k_scatter_res<5120, 1024, 1>)
-           : p20   ? pick(k_scatter_res<4096, 1024, 2, true>, k_scatter_res<5120, 1024, 2, true>)
+           : p20   ? pick(k_scatter_res<4096, 1024, 2, true>, k_scatter_res<6144, 1024, 2, true>)
                    : pick(k_scatter_res<4096, 1024, 2>, k_scatter_res<5120, 1024, 2>);
   } else if (kt == 2048) {
     kern = !l0    ? (b.padded ? pick(k_scatter_res<4096, 2048, 3>, k_scatter_res<5120, 2048, 3>)
                               : pick(k_scatter_res<4096, 2048, 0>, k_scatter_res<5120, 2048, 0>))
            : b.pos ? pick(k_scatter_res<4096, 2048, 1>, k_scatter_res<5120, 2048, 1>)
-           : p20   ? pick(k_scatter_res<4096, 2048, 2, true>, k_scatter_res<5120, 2048, 2, true>)
+           : p20   ? pick(k_scatter_res<4096, 2048, 2, true>, k_scatter_res<6144, 2048, 2, true>)
                    : pick(k_scatter_res<4096, 2048, 2>, k_scatter_res<5120, 2048, 2>);
   } else {
     kern = !l0    ? (b.padded ? k_scatter_res<kSubRound, kLdsTiles, 3> : k_scatter_res<kSubRound, kLdsTiles, 0>)
@@ -4070,11 +4070,11 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
   }
   const unsigned bps = std::max(1u, 256u / p.S / kResShards) * kResShards;
   if (p.tps <= 256)
-    k_scatter_p0<5120, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+    k_scatter_p0<6144, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
   else if (p.tps <= 512)
-    k_scatter_p0<5120, 512><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+    k_scatter_p0<6144, 512><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
   else
-    k_scatter_p0<5120, 1024><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+    k_scatter_p0<6144, 1024><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
 }
 
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
