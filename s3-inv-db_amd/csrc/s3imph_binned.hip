@@ -4054,7 +4054,15 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
   // blocks per super-tile: a multiple of kResShards, so every shard slot of a tile takes the
   // records of the same number of blocks (9 blocks put 2/9 of a super-tile's records on one
   // shard: 1.8x the mean fill, past the slot capacity at S = 26)
-  if (p.S > kP0OneBlockS) {
+  // More than 32 super-tiles (C3: 64 of ~191 tiles) take the one-block form too: 8 blocks of
+  // 1024 threads per super-tile, 512 blocks dispatched in two waves over the 256 CUs, 6144-record
+  // rounds of ~32 records per tile (C3 scatter0_p0 1.22 -> 1.09-1.11 ms, the fused partition's
+  // hash +0.09; step -0.05 ms over two same-box A/Bs).  S3IMPH_P0_BIG=0: the two-block form below.
+  static const bool big = [] {
+    const char* e = std::getenv("S3IMPH_P0_BIG");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (p.S > kP0OneBlockS && !big) {
     // more than 32 super-tiles: 8 blocks of 512 threads each (two per CU), 3072-record rounds
     // (2560 with 1024-tile counters, so two blocks' LDS fit a CU): shorter rounds than the
     // one-block form's 5120, but as many records per tile and round at S = 64 (tps ~ 191 vs

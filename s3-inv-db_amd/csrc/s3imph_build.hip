@@ -522,14 +522,14 @@ uint64_t p0_min_tiles() {
   return v;
 }
 
-// The most super-tiles P0 cuts level 0 into (A/B knob S3IMPH_P0_MAXS, at most kP0MaxS).  32 by
-// default: 64 super-tiles on the two-block scatter measured no faster there (C3 scatter0_p0
-// 1.23 / 1.29 ms either way) and cost the fused hash partition 0.05-0.11 ms (shorter runs per
-// round), so more than 32 are taken only when a level's tiles need them (tps <= kP0MaxTps).
+// The most super-tiles P0 cuts level 0 into (A/B knob S3IMPH_P0_MAXS, at most kP0MaxS = 64, the
+// default).  At C3 (12 208 tiles, ~191 per super-tile) 64 beat 32 by 0.05 ms: the super-tile
+// scatter's runs per tile and round double (1.22 -> 1.09-1.11 ms) while the fused partition's
+// shorter region runs cost the hash ~0.09 ms (launch_p0_scatter).
 uint64_t p0_max_s() {
   static const uint64_t v = [] {
     const char* e = std::getenv("S3IMPH_P0_MAXS");
-    return e ? std::max<uint64_t>(1, std::min<uint64_t>(std::strtoull(e, nullptr, 10), kP0MaxS)) : (uint64_t)kP0OneBlockS;
+    return e ? std::max<uint64_t>(1, std::min<uint64_t>(std::strtoull(e, nullptr, 10), kP0MaxS)) : kP0MaxS;
   }();
   return v;
 }

@@ -238,13 +238,13 @@ uint64_t split_scratch_records();  // sub-tile segments of the split big-tile ke
 constexpr uint64_t kP0MinTiles = 2048;
 constexpr uint64_t kP0MaxTps = 1024;
 constexpr uint64_t kP0TargetTps = 192;  // tiles per super-tile aimed at
-// at most 64 super-tiles.  Up to 32, k_scatter_p0 gives each one 256 / S >= 8 blocks of 1024
-// threads (one per CU); above, 8 blocks of 512 threads (two per CU, one's LDS phases beside
-// the other's memory phases).  Either way the records of a tile arrive through all kResShards
-// XCD shards (4 blocks per super-tile filled only 4 of a tile's 8 shard slots: twice their
-// capacity on average, C3 overflowed into the rerun).  S3IMPH_P0_MAXS lowers the cap (A/B).
+// at most 64 super-tiles (C3: 64).  k_scatter_p0 gives each one max(256 / S, 8) blocks of 1024
+// threads, a multiple of 8 (past 32 super-tiles: 512 blocks in two waves over the CUs; with
+// S3IMPH_P0_BIG=0, 8 blocks of 512 threads, two per CU), so the records of a tile arrive through
+// all kResShards XCD shards (4 blocks per super-tile filled only 4 of a tile's 8 shard slots:
+// twice their capacity on average, C3 overflowed into the rerun).  S3IMPH_P0_MAXS lowers the cap.
 constexpr uint64_t kP0MaxS = 64;
-constexpr unsigned kP0OneBlockS = 32;  // the largest S on one 1024-thread block per CU
+constexpr unsigned kP0OneBlockS = 32;  // the most super-tiles the 256 blocks of one wave cover
 constexpr uint64_t kP0MaxKeys = 1ull << 31;  // bucket slot indices stay below 2^32
 // A level-0 record with an identity position: k (2 dwords), f (2), key index i (p = pos_base + i).
 struct R20 {

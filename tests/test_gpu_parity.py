@@ -639,16 +639,16 @@ def _parity_subprocess(env: dict, cases) -> None:
 
 
 def test_p0_many_super_tiles_bit_exact(s3, oracle_lib):
-    """More than 32 super-tiles (S3IMPH_P0_TPS=48 S3IMPH_P0_MAXS=64: 45 / 51 of them on 17.5M uniform / 20M
-    skewed keys): the super-tile scatter runs two 512-thread blocks per CU, 8 per super-tile,
-    reading the fused hash's regions and k_hash_skew's; bit-exact."""
-    _parity_subprocess({"S3IMPH_P0_TPS": "48", "S3IMPH_P0_MAXS": "64"}, [(17_500_000, 0, 20), (20_000_000, 1, 0)])
+    """More than 32 super-tiles on the two-block-per-CU super-tile scatter (S3IMPH_P0_BIG=0,
+    S3IMPH_P0_TPS=48: 45 / 51 super-tiles on 17.5M uniform / 20M skewed keys, 8 blocks of 512
+    threads each), reading the fused hash's regions and k_hash_skew's; bit-exact."""
+    _parity_subprocess({"S3IMPH_P0_TPS": "48", "S3IMPH_P0_BIG": "0"}, [(17_500_000, 0, 20), (20_000_000, 1, 0)])
 
 
 def test_p0_super_tile_cap_bit_exact(s3, oracle_lib):
-    """S3IMPH_P0_MAXS=64 (A/B knob; 32 by default): 60M short keys in 39 super-tiles of 188
-    tiles on the two-block-per-CU super-tile scatter instead of 32 of 229: bit-exact."""
-    _parity_subprocess({"S3IMPH_P0_MAXS": "64"}, [(60_000_000, 0, 12)])
+    """S3IMPH_P0_MAXS=32 (A/B knob; 64 by default): 60M short keys in 32 super-tiles of 229
+    tiles (the one-block scatter's 256-block form) instead of 39 of 188: bit-exact."""
+    _parity_subprocess({"S3IMPH_P0_MAXS": "32"}, [(60_000_000, 0, 12)])
 
 
 def test_counted_path_every_level(s3, oracle_lib):
