@@ -4076,7 +4076,12 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
       k_scatter_p0<2560, 1024, 512><<<p.S * bps, 512, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
     return;
   }
-  const unsigned bps = std::max(1u, 256u / p.S / kResShards) * kResShards;
+  static const unsigned bps_knob = [] {  // A/B knob S3IMPH_P0_BPS: blocks per super-tile (a multiple of 8)
+    const char* e = std::getenv("S3IMPH_P0_BPS");
+    const unsigned v = e ? (unsigned)std::atoi(e) : 0u;
+    return v / kResShards * kResShards;
+  }();
+  const unsigned bps = bps_knob ? bps_knob : std::max(1u, kP0ScatterBlocks / p.S / kResShards) * kResShards;
   if (p.tps <= 256)
     k_scatter_p0<6144, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
   else if (p.tps <= 512)

@@ -237,7 +237,14 @@ uint64_t split_scratch_records();  // sub-tile segments of the split big-tile ke
 // shard) slots of `sup`, then to per-(tile, shard) slots of `bucket`, then k_tile_reg.
 constexpr uint64_t kP0MinTiles = 2048;
 constexpr uint64_t kP0MaxTps = 1024;
-constexpr uint64_t kP0TargetTps = 192;  // tiles per super-tile aimed at
+// tiles per super-tile aimed at: fewer super-tiles give the fused hash partition longer region
+// runs (C3 hash 2.69 -> 2.67 ms at 24 super-tiles vs 64), and the super-tile scatter's blocks
+// (kP0ScatterBlocks in all) still reach ~12 records per tile and round
+constexpr uint64_t kP0TargetTps = 512;
+// the super-tile scatter's blocks: three waves of 1024-thread blocks over the 256 CUs, blocks per
+// super-tile a multiple of the 8 XCD shards (C3: 24 x 32; 6.55-6.57 ms against 6.63-6.67 for
+// 64 x 8 in two same-box sweeps, `gpurun_out` r4_sweep / r4_sweep2)
+constexpr unsigned kP0ScatterBlocks = 768;
 // at most 64 super-tiles (C3: 64).  k_scatter_p0 gives each one max(256 / S, 8) blocks of 1024
 // threads, a multiple of 8 (past 32 super-tiles: 512 blocks in two waves over the CUs; with
 // S3IMPH_P0_BIG=0, 8 blocks of 512 threads, two per CU), so the records of a tile arrive through
