@@ -523,9 +523,8 @@ uint64_t p0_min_tiles() {
 }
 
 // The most super-tiles P0 cuts level 0 into (A/B knob S3IMPH_P0_MAXS, at most kP0MaxS = 64, the
-// default).  At C3 (12 208 tiles, ~191 per super-tile) 64 beat 32 by 0.05 ms: the super-tile
-// scatter's runs per tile and round double (1.22 -> 1.09-1.11 ms) while the fused partition's
-// shorter region runs cost the hash ~0.09 ms (launch_p0_scatter).
+// default).  How many a level takes follows kP0TargetTps (C3: 24); the cap matters for levels of
+// more than 64 x 512 tiles, and for S3IMPH_P0_TPS sweeps.
 uint64_t p0_max_s() {
   static const uint64_t v = [] {
     const char* e = std::getenv("S3IMPH_P0_MAXS");
