@@ -564,8 +564,8 @@ def test_p0_level0_bit_exact(s3, oracle_lib, n, unaligned):
     """Level 0 with more than 2048 tiles of 2^14 positions (P0, s3imph_internal.h): the
     records go to super-tile slots, then to their tiles' slots, then the pipelined register
     tiles (k_tile_p0).  Just past the threshold (2051 tiles), and an unaligned blob whose
-    level-0 hash is k_hash_count0 (kh / fp, then the partition pass); 12 / 26 super-tiles
-    (blocks per super-tile a multiple of the 8 XCD shards).  Bit-exact, and the build's
+    level-0 hash is k_hash_count0 (kh / fp, then the partition pass); 5 / 10 super-tiles
+    (blocks per super-tile a multiple of the 8 XCD shards, ~768 in all).  Bit-exact, and the build's
     last attempt is P0's (no conservative rerun: its stage marks are P0's)."""
     c = s3.DeviceBuilder(0)
     try:
@@ -646,9 +646,9 @@ def test_p0_many_super_tiles_bit_exact(s3, oracle_lib):
 
 
 def test_p0_super_tile_cap_bit_exact(s3, oracle_lib):
-    """S3IMPH_P0_MAXS=32 (A/B knob; 64 by default): 60M short keys in 32 super-tiles of 229
-    tiles (the one-block scatter's 256-block form) instead of 39 of 188: bit-exact."""
-    _parity_subprocess({"S3IMPH_P0_MAXS": "32"}, [(60_000_000, 0, 12)])
+    """S3IMPH_P0_MAXS=8 (A/B knob; 64 by default): 60M short keys in 8 super-tiles of 916 tiles
+    (the super-tile scatter's 1024-tile-counter form) instead of 15 of ~489: bit-exact."""
+    _parity_subprocess({"S3IMPH_P0_MAXS": "8"}, [(60_000_000, 0, 12)])
 
 
 def test_counted_path_every_level(s3, oracle_lib):
