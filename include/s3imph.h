@@ -318,6 +318,17 @@ int s3imph_sha256_file(const char *path, int portable, char hex_out[65], char *e
 int s3imph_gen_keys(int kind, uint64_t seed, uint32_t avg_len, uint64_t lo, uint64_t n,
                     uint8_t *blob, uint64_t *offsets, uint64_t *total_bytes);
 
+/* ------------------------------------------------------------------------
+ * 7. Developer knobs (not on the path; no reference counterpart).
+ *    The library reads its A/B geometry knobs, test-only fallbacks and fault-injection hooks
+ *    (S3IMPH_P0, S3IMPH_L20, S3IMPH_FAULT_DUP_REC, S3IMPH_HASH_ONLY, S3IMPH_DIST_SWITCH, ...;
+ *    DESIGN.md section 5) from the environment ONLY after s3imph_dev_knobs(1), so a stray
+ *    variable in an embedding process cannot change a production build.  The documented user
+ *    settings S3IMPH_DIST_MODE, S3IMPH_PINNED_KEEP and S3IMPH_DEBUG are read regardless.
+ *    Knobs are sampled when a context is created (some on first use): call this first.
+ * ------------------------------------------------------------------------ */
+int s3imph_dev_knobs(int on);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1247,7 +1247,12 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
       st->woff[level + 1] = woff + words;
       st->nlevels = level;
     }
-    if (n <= kGate) return;
+    if (n <= kGate) {
+      // an R20 list (planned before level 0, BinBuffers::l20) for a level that turned out
+      // small enough for the mid / tail kernels, which read Rec: rerun conservatively
+      if (kSrc == 4 && blockIdx.x == 0 && tid == 0) atomicOr(&st->status, kStGeometry);
+      return;
+    }
     if (no_progress(st, level, n)) return;
   }
   const LevelRange rg = level_range(st, level, words);
@@ -3804,7 +3809,7 @@ void launch_hash_skew(const uint8_t* blob, const uint64_t* offsets, uint64_t n, 
                       unsigned long long* prof, hipStream_t s, const P0Part& pt = P0Part{}) {
   const int cfg = b.skew_cfg;
   static const int order = [] {  // 1: longest first; 0: alternating longest / shortest
-    const char* e = std::getenv("S3IMPH_SKEW_ORDER");
+    const char* e = dev_env("S3IMPH_SKEW_ORDER");
     return e ? std::atoi(e) : 1;
   }();
   if (cfg == 1)
@@ -4059,7 +4064,7 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
   // rounds of ~32 records per tile (C3 scatter0_p0 1.22 -> 1.09-1.11 ms, the fused partition's
   // hash +0.09; step -0.05 ms over two same-box A/Bs).  S3IMPH_P0_BIG=0: the two-block form below.
   static const bool big = [] {
-    const char* e = std::getenv("S3IMPH_P0_BIG");
+    const char* e = dev_env("S3IMPH_P0_BIG");
     return !(e && std::atoi(e) == 0);
   }();
   if (p.S > kP0OneBlockS && !big) {
@@ -4077,7 +4082,7 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
     return;
   }
   static const unsigned bps_knob = [] {  // A/B knob S3IMPH_P0_BPS: blocks per super-tile (a multiple of 8)
-    const char* e = std::getenv("S3IMPH_P0_BPS");
+    const char* e = dev_env("S3IMPH_P0_BPS");
     const unsigned v = e ? (unsigned)std::atoi(e) : 0u;
     return v / kResShards * kResShards;
   }();

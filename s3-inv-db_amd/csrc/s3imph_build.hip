@@ -73,6 +73,7 @@ void alloc_common(s3imph_ctx* c, uint64_t n_global) {
 // Single-GPU workspace: ~88 B per key (level-0 list, tile buckets, two next-level lists).
 void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   if (n <= c->cap_keys && c->hist) return;
+  c->cap_keys = 0;  // set again only once every buffer is in place (a NOMEM midway reallocates next time)
   const uint64_t cap = std::max<uint64_t>(n, 1024);
   dalloc(c->kh, cap);
   dalloc(c->fp, cap);
@@ -349,7 +350,7 @@ unsigned choose_split_ts(uint64_t size, bool exact) {
   double best_cost = 0;
   // A/B knob S3IMPH_TS_MAX: the largest ts tried (smaller sub-tile scratch per workgroup)
   static const unsigned ts_max = [] {
-    const char* e = std::getenv("S3IMPH_TS_MAX");
+    const char* e = dev_env("S3IMPH_TS_MAX");
     return e ? std::max(2u, std::min((unsigned)std::atoi(e), 1u << (kSplitMaxBits - 14))) : 1u << (kSplitMaxBits - 14);
   }();
   for (unsigned ts = 2; ts <= ts_max; ++ts) {
@@ -509,14 +510,14 @@ uint64_t chunks0(uint64_t n) {
 // level-0 hash so that kernel can be timed alone, and FAILS with S3IMPH_ERR_INTERNAL — the
 // outputs are not an index, and no caller may mistake the run for a build.
 bool hash_only_knob() {
-  static const bool on = std::getenv("S3IMPH_HASH_ONLY") != nullptr;
+  static const bool on = dev_env("S3IMPH_HASH_ONLY") != nullptr;
   return on;
 }
 
 // Level 0 takes P0 above this many 2^14-position tiles (A/B knob S3IMPH_P0_MIN_TILES)
 uint64_t p0_min_tiles() {
   static const uint64_t v = [] {
-    const char* e = std::getenv("S3IMPH_P0_MIN_TILES");
+    const char* e = dev_env("S3IMPH_P0_MIN_TILES");
     return e ? std::strtoull(e, nullptr, 10) : kP0MinTiles;
   }();
   return v;
@@ -527,7 +528,7 @@ uint64_t p0_min_tiles() {
 // more than 64 x 512 tiles, and for S3IMPH_P0_TPS sweeps.
 uint64_t p0_max_s() {
   static const uint64_t v = [] {
-    const char* e = std::getenv("S3IMPH_P0_MAXS");
+    const char* e = dev_env("S3IMPH_P0_MAXS");
     return e ? std::max<uint64_t>(1, std::min<uint64_t>(std::strtoull(e, nullptr, 10), kP0MaxS)) : kP0MaxS;
   }();
   return v;
@@ -547,7 +548,7 @@ P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s) {
   const uint64_t T = tiles_of(level_words(n_geom), kRegTileMaxBits, 0);
   P0Bufs p;
   static const uint64_t target = [] {  // A/B knob S3IMPH_P0_TPS: tiles per super-tile aimed at
-    const char* e = std::getenv("S3IMPH_P0_TPS");
+    const char* e = dev_env("S3IMPH_P0_TPS");
     return e ? std::max<uint64_t>(16, std::strtoull(e, nullptr, 10)) : kP0TargetTps;
   }();
   p.S = (unsigned)p0_super_tiles(T, target);
@@ -558,11 +559,19 @@ P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s) {
   const uint64_t need = std::max<uint64_t>(std::max<uint64_t>((uint64_t)kH0GridHost * p.S * p.reg_cap,
                                                               (uint64_t)nbs * p.S * p.reg_cap_skew),
                                            n + n / 4 + (uint64_t)4096 * p.S * kResShards);
+  // (a capacity is zeroed before its buffer is replaced and set only once the allocation
+  // succeeded: a NOMEM leaves a null buffer that the next build reallocates, never one that a
+  // smaller build would take as big enough)
   if (need > c->p0_sup_cap) {
+    c->p0_sup_cap = 0;
+    dfree(c->p0_sup);
+    if (dev_env("S3IMPH_FAULT_P0_NOMEM"))  // test hook: this allocation fails (the callers fall back)
+      throw Fail{S3IMPH_ERR_NOMEM, "p0_bufs: injected allocation failure (S3IMPH_FAULT_P0_NOMEM)"};
     dalloc(c->p0_sup, need);
     c->p0_sup_cap = need;
   }
   if (T > c->p0_tiles) {
+    c->p0_tiles = 0;
     dalloc(c->p0_tcnt, T * kResShards);
     dalloc(c->p0_flags, T);
     c->p0_tiles = T;
@@ -582,6 +591,19 @@ P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s) {
   return p;
 }
 
+// p0_bufs, or false when its allocation fails (NOMEM): the caller takes the non-P0 path
+bool p0_try_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s, P0Bufs* out) {
+  try {
+    *out = p0_bufs(c, n, n_geom, s);
+    return true;
+  } catch (const Fail& f) {
+    if (f.code != S3IMPH_ERR_NOMEM) throw;
+    (void)hipGetLastError();  // an out-of-memory hipMalloc is not sticky; clear it
+    if (c->debug) std::fprintf(stderr, "[s3imph] P0 buffers: %s; level 0 without P0\n", f.msg.c_str());
+    return false;
+  }
+}
+
 void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
   BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
@@ -590,23 +612,26 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   const uint64_t T14 = tiles_of(level_words(n), kRegTileMaxBits, 0);
   if (!conservative && c->p0 && !pos && n <= kP0MaxKeys && !hash_only_knob() && T14 > p0_min_tiles() &&
       T14 <= kP0MaxS * kP0MaxTps) {
-    // level 0 in 2^14-position register tiles through super-tiles (s3imph_internal.h, P0)
-    const P0Bufs p = p0_bufs(c, n, n, s);
-    const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
-    // the list levels' plan first: level 0's tile kernel writes level 1's list as R20 or Rec
-    const LevelsPlan P = plan_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false);
-    b.l20 = c->l20_mask = plan_l20(c, b, P, true, n);
-    launch_init_state(c->d_st, n, n, s, offsets);
-    ev_mark(c, s, "init");
-    launch_p0_hash(blob, offsets, n, b, g0, p, s);
-    ev_mark(c, s, "hash_part0");
-    launch_p0_scatter(b, p, p0_fused(blob, p), s);
-    ev_mark(c, s, "scatter0_p0");
-    launch_p0_tile(b, p, s);
-    ev_mark(c, s, "tile0_p0");
-    fault_dup_record(c, c->list[0], s, b.list20(1));
-    run_levels(c, b, P, 1, s);
-    return;
+    // level 0 in 2^14-position register tiles through super-tiles (s3imph_internal.h, P0); its
+    // buffers (~1.2 n x 20 B) may not fit next to the workspace: then the split-kernel path
+    P0Bufs p;
+    if (p0_try_bufs(c, n, n, s, &p)) {
+      const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
+      // the list levels' plan first: level 0's tile kernel writes level 1's list as R20 or Rec
+      const LevelsPlan P = plan_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false);
+      b.l20 = c->l20_mask = plan_l20(c, b, P, true, n);
+      launch_init_state(c->d_st, n, n, s, offsets);
+      ev_mark(c, s, "init");
+      launch_p0_hash(blob, offsets, n, b, g0, p, s);
+      ev_mark(c, s, "hash_part0");
+      launch_p0_scatter(b, p, p0_fused(blob, p), s);
+      ev_mark(c, s, "scatter0_p0");
+      launch_p0_tile(b, p, s);
+      ev_mark(c, s, "tile0_p0");
+      fault_dup_record(c, c->list[0], s, b.list20(1));
+      run_levels(c, b, P, 1, s);
+      return;
+    }
   }
   const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
   launch_init_state(c->d_st, n, n, s, offsets);
@@ -978,6 +1003,8 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
     return;
   // the bucket gets 1.3x the list capacity: reservation slots need headroom over the mean fill
   const uint64_t capb = capl + capl * 3 / 10;
+  d.cap_list = d.cap_send = d.cap_stage_words = 0;  // set again once every buffer is in place
+  c->cap_keys = 0;
   dalloc(c->bucket, capb);
   dalloc(c->list[0], capl);
   dalloc(c->list[1], capl);
@@ -1131,7 +1158,10 @@ int dist_classify_stop(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offse
   const LevelState& hs = *c->h_st;
   const unsigned nl = hs.stop_level ? hs.stop_level : hs.nlevels;
   const uint64_t rem = nl >= 1 && nl < (unsigned)kMaxLevels + 2 ? hs.n[nl] : 0;
-  const std::vector<uint64_t> mine = rem ? record_dup_values(c->list[(nl - 1) & 1], rem, kCand) : std::vector<uint64_t>{};
+  // (a bitmap level's list may be R20: c->l20_mask is the attempt's mask, as for one GPU)
+  const bool r20 = nl < 32 && ((c->l20_mask >> nl) & 1u);
+  const std::vector<uint64_t> mine =
+      rem ? record_dup_values(c->list[(nl - 1) & 1], rem, kCand, r20) : std::vector<uint64_t>{};
   unsigned long long* M = d.h_pinned;
   std::fill(M, M + kCand + 1, 0ull);
   M[0] = mine.size();
@@ -1545,10 +1575,12 @@ void ensure_bm_workspace(s3imph_ctx* c, uint64_t N) {
   const uint64_t P = (uint64_t)d.nranks;
   const uint64_t w0 = level_words(N), S = (w0 + P - 1) / P, wpad = S * P;
   if (d.bm_cap_out < d.cap_list) {  // a rank settles at most the records it holds (<= its list capacity)
+    d.bm_cap_out = 0;
     dalloc(d.bm_out, d.cap_list);
     d.bm_cap_out = d.cap_list;
   }
   if (wpad <= d.bm_cap_words && d.bm_a) return;
+  d.bm_cap_words = 0;  // set again once every buffer is in place
   dalloc(d.bm_a, wpad);
   dalloc(d.bm_g, wpad);
   dalloc(d.bm_dec, S);
@@ -1574,7 +1606,7 @@ void free_bm_workspace(DistState& d) {
 // spread over a 4x larger window per tile (1.88 -> 3.64 ms).
 uint64_t bm_target_tiles() {
   static const uint64_t v = [] {
-    const char* e = std::getenv("S3IMPH_BM_TILES");
+    const char* e = dev_env("S3IMPH_BM_TILES");
     return e ? std::max<uint64_t>(64, std::strtoull(e, nullptr, 10)) : kScatterTiles;
   }();
   return v;
@@ -1590,6 +1622,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   // level 0 beyond kScatterTiles tiles of 2^kBmMaxTb positions (N > ~2^30): the routed build
   if (tiles_of(level_words(N), kBmMaxTb, 0) > kScatterTiles) return kDistRetry;
   ensure_bm_workspace(c, N);
+  c->l20_mask = 0;
   const BinBuffers b = make_bufs(c, nullptr, fp_out, pos_out, s);
   const double q = 1.0 - std::exp(-0.5);
   launch_init_state(st, n_local, out_cap, s, n_local ? offsets : nullptr);
@@ -1705,6 +1738,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     const bool more = !(L + 1 >= kMaxDistLevels || nbn <= (double)c->dist_switch);
     const bool next20 = more && c->l20 && !pos && L + 1 < 32;
     if (next20) bs.l20 |= 1u << (L + 1);
+    c->l20_mask = bs.l20;  // dist_classify_stop reads a stop level's list in this format
     launch_bm_tile_settle(L, bk, in20, key_base, tc, bcap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
                           d.bm_cap_out, c->list[L & 1], d.cap_list, next20, own_slice, s);
     ev_mark(c, s, L == 0 ? "level0" : "levels");
@@ -1926,7 +1960,7 @@ int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
                                             info, msg)
                       : dist_attempt(c, blob, offsets, pos, n_local, key_base, N, fp_out, pos_out, out_cap, s,
                                      attempt > 1, info, msg);
-    if (rc == kDistRetry && attempt == 0 && std::getenv("S3IMPH_DIST_STRICT")) {
+    if (rc == kDistRetry && attempt == 0 && dev_env("S3IMPH_DIST_STRICT")) {
       *msg = "build MPHF: the bitmap decomposition missed its size bounds (S3IMPH_DIST_STRICT: no fallback)";
       return S3IMPH_ERR_INTERNAL;  // tests use this to prove the bitmap path built the index
     }
@@ -2119,7 +2153,7 @@ void staged_copy(s3imph_ctx* c, bool h2d, void* dst, const void* src, uint64_t b
 // S3IMPH_OFF16=0: offsets cross PCIe as before (u32 / u64), the A/B reference
 bool off16_disabled() {
   static const bool off = [] {
-    const char* e = std::getenv("S3IMPH_OFF16");
+    const char* e = dev_env("S3IMPH_OFF16");
     return e && std::atoi(e) == 0;
   }();
   return off;
@@ -2300,19 +2334,19 @@ int s3imph_ctx_create(int device, s3imph_ctx** out, char* err, size_t errlen) {
     HIPCHECK(hipSetDevice(device));
     c = new s3imph_ctx();
     c->device = device;
-    if (const char* m = std::getenv("S3IMPH_RES_MAX")) c->res_max_keys = std::strtoull(m, nullptr, 10);
-    if (const char* m = std::getenv("S3IMPH_RES_FILL")) c->res_fill = std::strtoull(m, nullptr, 10);
-    if (const char* m = std::getenv("S3IMPH_RES0")) c->res0 = std::atoi(m);
-    c->loose_geom = std::getenv("S3IMPH_LOOSE_GEOM") != nullptr;
-    c->route_self = std::getenv("S3IMPH_DIST_ROUTE_SELF") != nullptr;  // A/B knob: list-level geometry from 1.1x bounds
+    if (const char* m = dev_env("S3IMPH_RES_MAX")) c->res_max_keys = std::strtoull(m, nullptr, 10);
+    if (const char* m = dev_env("S3IMPH_RES_FILL")) c->res_fill = std::strtoull(m, nullptr, 10);
+    if (const char* m = dev_env("S3IMPH_RES0")) c->res0 = std::atoi(m);
+    c->loose_geom = dev_env("S3IMPH_LOOSE_GEOM") != nullptr;
+    c->route_self = dev_env("S3IMPH_DIST_ROUTE_SELF") != nullptr;  // A/B knob: list-level geometry from 1.1x bounds
     c->debug = std::getenv("S3IMPH_DEBUG") != nullptr;
-    c->fault_dup = std::getenv("S3IMPH_FAULT_DUP_REC") != nullptr;
-    if (const char* m = std::getenv("S3IMPH_P0")) c->p0 = std::atoi(m);
-    if (const char* m = std::getenv("S3IMPH_L20")) c->l20 = std::atoi(m) != 0;
-    if (const char* m = std::getenv("S3IMPH_BM_LANES")) c->bm_counts = std::strcmp(m, "counts") == 0;
-    if (const char* m = std::getenv("S3IMPH_SCAT_CFG")) c->scat_cfg = std::atoi(m);
-    if (const char* m = std::getenv("S3IMPH_SKEW_CFG")) c->skew_cfg = std::atoi(m);
-    if (const char* m = std::getenv("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);
+    c->fault_dup = dev_env("S3IMPH_FAULT_DUP_REC") != nullptr;
+    if (const char* m = dev_env("S3IMPH_P0")) c->p0 = std::atoi(m);
+    if (const char* m = dev_env("S3IMPH_L20")) c->l20 = std::atoi(m) != 0;
+    if (const char* m = dev_env("S3IMPH_BM_LANES")) c->bm_counts = std::strcmp(m, "counts") == 0;
+    if (const char* m = dev_env("S3IMPH_SCAT_CFG")) c->scat_cfg = std::atoi(m);
+    if (const char* m = dev_env("S3IMPH_SKEW_CFG")) c->skew_cfg = std::atoi(m);
+    if (const char* m = dev_env("S3IMPH_DIST_SWITCH")) c->dist_switch = std::strtoull(m, nullptr, 10);
     if (const char* m = std::getenv("S3IMPH_DIST_MODE")) c->d.mode = std::strcmp(m, "bitmap") == 0 ? kDistBitmap : kDistRoute;
     // A blocking stream: implicitly ordered with the legacy NULL stream, so work a
     // caller queued there (e.g. torch's default stream) completes before ours starts.

@@ -299,6 +299,7 @@ Feed* feed_new(int device, bool use_gpu) {
 }
 
 void feed_free(Feed* f) {
+  if (!f) return;  // only feeds feed_new made are counted (a builder that never stored a key has none)
   delete f;  // its chunks go back to the pool
   if (g_live_feeds.fetch_sub(1) == 1) pool().trim(std::min(pool_keep(), kPoolKeepIdle));
 }

@@ -9,7 +9,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -22,6 +24,12 @@
 #include "s3imph_internal.h"
 
 namespace s3imph {
+
+// Developer knobs (s3imph_dev_knobs, include/s3imph.h section 7): off unless the caller opts in.
+std::atomic<bool> g_dev_knobs{false};
+const char* dev_env(const char* name) {
+  return g_dev_knobs.load(std::memory_order_acquire) ? std::getenv(name) : nullptr;
+}
 
 void set_err(char* err, size_t errlen, const std::string& msg) {
   if (!err || errlen == 0) return;
@@ -387,6 +395,11 @@ struct s3imph_builder {
 };
 
 extern "C" {
+
+int s3imph_dev_knobs(int on) {
+  s3imph::g_dev_knobs.store(on != 0, std::memory_order_release);
+  return S3IMPH_OK;
+}
 
 int s3imph_builder_new(const char* temp_dir, int device, s3imph_builder** out, char* err, size_t errlen) {
   if (!out) return S3IMPH_ERR_INVALID;

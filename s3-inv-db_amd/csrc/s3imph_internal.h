@@ -13,6 +13,11 @@
 
 namespace s3imph {
 
+// A developer knob's value from the environment, or null unless the caller opted in with
+// s3imph_dev_knobs(1) (include/s3imph.h section 7; s3imph_host.cpp).  Every A/B geometry
+// knob, test-only fallback and fault hook goes through this; user settings use getenv.
+const char* dev_env(const char* name);
+
 // Device-resident per-build level bookkeeping.  Written only by kernels (and the
 // init kernel); the host copies it back once, after the build.
 struct LevelState {

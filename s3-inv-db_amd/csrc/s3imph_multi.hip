@@ -177,7 +177,7 @@ std::vector<std::unique_ptr<MultiCtx>> g_retired;  // aborted sets (see build_fr
 
 MultiCtx* multi_ctx(const std::vector<int>& devs, bool host_transport, std::string* msg) {
   uint64_t sw = kDistSwitchKeysDefault;  // contexts read S3IMPH_DIST_SWITCH when made
-  if (const char* e = std::getenv("S3IMPH_DIST_SWITCH")) sw = std::strtoull(e, nullptr, 10);
+  if (const char* e = dev_env("S3IMPH_DIST_SWITCH")) sw = std::strtoull(e, nullptr, 10);
   std::lock_guard<std::mutex> lk(g_multi_mu);
   auto key = std::make_tuple(devs, host_transport, sw);
   auto it = g_multi.find(key);

@@ -65,6 +65,7 @@ EXPORTS = (
     "s3imph_ctx_load_mph_bin", "s3imph_lookup_device", "s3imph_gen_keys",
     "s3imph_finalize_index_host", "s3imph_finalize_index_device",
     "s3imph_write_manifest", "s3imph_verify_manifest", "s3imph_sha256_file",
+    "s3imph_dev_knobs",
 )
 
 
@@ -147,6 +148,7 @@ def _load():
         "s3imph_write_manifest": (i32, [cp, u64, ctypes.c_uint32, cp, sz]),
         "s3imph_verify_manifest": (i32, [cp, cp, sz]),
         "s3imph_sha256_file": (i32, [cp, i32, cp, cp, sz]),
+        "s3imph_dev_knobs": (i32, [i32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -156,6 +158,16 @@ def _load():
 
 
 LIB = _load()
+# Developer knobs (A/B geometry, test fallbacks, fault hooks: include/s3imph.h section 7) are
+# read by the library only after this opt-in; the tests and tools/gpu.sh set S3IMPH_DEV=1.
+if os.environ.get("S3IMPH_DEV") == "1":
+    LIB.s3imph_dev_knobs(1)
+
+
+def dev_knobs(on: bool = True) -> None:
+    """Let the library read its S3IMPH_* developer knobs (tests, A/B runs); not for builds
+    that produce an index."""
+    LIB.s3imph_dev_knobs(1 if on else 0)
 
 
 def status_string(code: int) -> str:

@@ -17,6 +17,11 @@ for p in (os.path.join(ROOT, "s3-inv-db_amd"), os.path.join(ROOT, "oracle"), os.
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# The tests drive the library's developer knobs (S3IMPH_* A/B geometry, fallbacks, fault
+# hooks), which it reads only after the opt-in (include/s3imph.h section 7): set it before
+# s3imph is imported here or in any subprocess a test starts.
+os.environ["S3IMPH_DEV"] = "1"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")

@@ -584,6 +584,52 @@ def test_p0_level0_bit_exact(s3, oracle_lib, n, unaligned):
         c.close()
 
 
+def test_p0_allocation_failure_falls_back_and_recovers(s3, oracle_lib, monkeypatch):
+    """P0's super-tile buffer is replaced when a bigger set needs more.  With the
+    allocation failing (S3IMPH_FAULT_P0_NOMEM frees the old buffer, then fails), the build
+    takes the split-kernel level 0 and is still bit-exact; the next, SMALLER build on the same
+    context must not take the freed buffer as big enough: it reallocates and runs P0 again."""
+    c = s3.DeviceBuilder(0)
+    try:
+        c.set_profiling(1)
+        for n, fault in [(18_000_000, False), (21_000_000, True), (17_500_000, False)]:
+            blob, offs = s3.gen_keys(0, 23, 20, 0, n)
+            blob = blob[: int(offs[-1])]
+            st, fp, po, mph = oracle_lib.build_mt(blob, offs, threads=16)
+            assert st == 0
+            if fault:
+                monkeypatch.setenv("S3IMPH_FAULT_P0_NOMEM", "1")
+            else:
+                monkeypatch.delenv("S3IMPH_FAULT_P0_NOMEM", raising=False)
+            gfp, gpo, gmph, _ = _device_build(s3, c, blob, offs)
+            assert gmph == mph and np.array_equal(gfp, fp) and np.array_equal(gpo, po), (n, fault)
+            assert ("scatter0_p0" in c.stage_times()) == (not fault), (n, fault, c.stage_times())
+    finally:
+        c.close()
+
+
+def test_dev_knobs_ignored_without_opt_in(s3, oracle_lib, monkeypatch):
+    """ADVICE / VERDICT r4: the release library reads no developer knob unless the caller opted
+    in (s3imph_dev_knobs, include/s3imph.h section 7).  Without the opt-in a context made under
+    S3IMPH_FAULT_DUP_REC builds normally (bit-exact); with it the same context setup faults."""
+    monkeypatch.setenv("S3IMPH_FAULT_DUP_REC", "1")
+    blob, offs = s3.gen_keys(0, 5, 32, 0, 200_000)
+    st, fp, po, mph = oracle_lib.build(blob[: offs[-1]], offs)
+    s3.dev_knobs(False)
+    try:
+        c = s3.DeviceBuilder(0)
+        gfp, gpo, gmph, _ = _device_build(s3, c, blob, offs)
+        c.close()
+        assert gmph == mph and np.array_equal(gfp, fp) and np.array_equal(gpo, po)
+    finally:
+        s3.dev_knobs(True)
+    c = s3.DeviceBuilder(0)
+    with pytest.raises(s3.MPHFError) as e:
+        _device_build(s3, c, blob, offs)
+    c.close()
+    assert e.value.status == s3.ERR_INTERNAL
+
+
 def test_p0_off_split_kernel_bit_exact(s3, oracle_lib):
     """S3IMPH_P0=0 (A/B knob): the same big level 0 on the split kernel instead: bit-exact."""
     _parity_subprocess({"S3IMPH_P0": "0"}, [(40_000_000, 0, 12)])

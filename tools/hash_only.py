@@ -5,6 +5,7 @@ import os
 import sys
 
 os.environ["S3IMPH_HASH_ONLY"] = "1"
+os.environ["S3IMPH_DEV"] = "1"  # the library reads developer knobs only after the opt-in
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
