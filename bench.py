@@ -80,9 +80,11 @@ def main() -> None:
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
                     help="N>1 collectives: RCCL over xGMI (default), or host copies over gloo — a rehearsal "
                          "mode that lets several ranks share one GPU (not a measurement)")
-    ap.add_argument("--decomp", default="route", choices=["route", "bitmap"],
-                    help="sharded levels: records routed to position owners (route), or the per-level "
-                         "collision-bitmap count lanes reduce-scattered over RCCL (bitmap)")
+    ap.add_argument("--decomp", default="bitmap", choices=["route", "bitmap"],
+                    help="sharded levels (N > 1 or --dist): the north_star's per-level collision bitmap, "
+                         "(A, C) planes exchanged over RCCL (bitmap, default; timed with no fallback), or "
+                         "records routed to position owners (route); the other is timed beside it "
+                         "(alt_decomposition)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 line beside the C3 headline")
     ap.add_argument("--headline-only", action="store_true",
                     help="skip the lookup / finalize / host_e2e lines (profiling runs)")
@@ -130,7 +132,7 @@ def main() -> None:
             if dist is not None:
                 dist.broadcast_object_list(uid, src=0)
             ctx = s3imph.DistBuilder(local_rank, uid[0], rank, world)
-        ctx.set_mode(s3imph.DIST_BITMAP if args.decomp == "bitmap" else s3imph.DIST_ROUTE)
+        ctx.set_mode(dist_mode(s3imph, args.decomp))
         ctx.reserve(n, plan.n_global)
         out_cap = ctx.out_cap(plan.n_global)
     d_fp = torch.empty(max(out_cap, 1), dtype=torch.int64, device=dev)
@@ -288,14 +290,19 @@ def main() -> None:
         dist.destroy_process_group()
 
 
+def dist_mode(s3imph, decomp: str) -> int:
+    """The context mode of a timed decomposition: the bitmap one with no fallback to routing
+    (a size-bound miss fails the build instead of being timed as the other decomposition)."""
+    return s3imph.DIST_BITMAP | s3imph.DIST_STRICT if decomp == "bitmap" else s3imph.DIST_ROUTE
+
+
 def alt_decomposition(s3imph, ctx, step, args, barrier, dist) -> dict:
     """Time the decomposition bench.py was not asked for (route <-> bitmap) over the same
     shards: min(steps, 5) builds after one warm-up, max over ranks.  The bitmap attempt runs
-    with S3IMPH_DIST_STRICT so a miss of its size bounds is reported, not timed as routing."""
+    with DIST_STRICT so a miss of its size bounds is reported, not timed as routing."""
     import torch
     other = "bitmap" if args.decomp == "route" else "route"
-    ctx.set_mode(s3imph.DIST_BITMAP if other == "bitmap" else s3imph.DIST_ROUTE)
-    os.environ["S3IMPH_DIST_STRICT"] = "1"
+    ctx.set_mode(dist_mode(s3imph, other))
     res = {"decomposition": other}
     dt, err = -1.0, None
     try:
@@ -313,8 +320,7 @@ def alt_decomposition(s3imph, ctx, step, args, barrier, dist) -> dict:
     except s3imph.MPHFError as e:  # a bound miss is a global fact: every rank lands here
         err = str(e)
     finally:
-        del os.environ["S3IMPH_DIST_STRICT"]
-        ctx.set_mode(s3imph.DIST_BITMAP if args.decomp == "bitmap" else s3imph.DIST_ROUTE)
+        ctx.set_mode(dist_mode(s3imph, args.decomp))
     tt = torch.tensor([dt if err is None else -1.0], dtype=torch.float64)
     fl = torch.tensor([0 if err is None else 1], dtype=torch.int64)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -360,22 +366,31 @@ def finalize_rate(ctx, d_blob, d_offs, n: int, reps: int = 5) -> dict:
 
 
 def host_e2e(s3imph, blob, offs, device: int, reps: int = 3) -> dict:
-    """PCIe-inclusive rate of the boundary call the Go caller makes (s3imph_build_host):
-    pageable host blob/offsets in -> H2D -> build -> D2H of mph_fp/mph_pos + mph.bin marshal,
-    into caller-owned output arrays reused across calls (as a pipeline would).
-    Reported beside `value`, never as it (measurement)."""
+    """PCIe-inclusive rate of the boundary call a pipeline makes (s3imph_build_host_into):
+    pageable host blob/offsets in -> offsets (u16 key lengths) H2D -> blob H2D in pieces, the
+    level-0 hash of each piece launched as it lands -> build -> D2H of mph_fp/mph_pos through
+    pinned chunk staging + mph.bin marshalled into a caller buffer, all outputs caller-owned
+    and reused across calls.  `alloc_api_ms`: s3imph_build_host, which returns mph.bin in a
+    fresh malloc'd buffer (Python copies it into bytes).  Reported beside `value`, never as it
+    (DESIGN.md, measurement)."""
     import numpy as np
     n = len(offs) - 1
     out = (np.zeros(n, np.uint64), np.zeros(n, np.uint64))
-    s3imph.build_host(blob, offs, device=device, out=out)  # warm (staging buffers, output pages)
+    mph_buf = np.zeros(s3imph.mph_bin_bound(n), np.uint8)
+    s3imph.build_host_into(blob, offs, out, mph_buf, device=device)  # warm (staging buffers, output pages)
     best = float("inf")
     for _ in range(reps):
         t0 = time.perf_counter()
-        s3imph.build_host(blob, offs, device=device, out=out)
+        s3imph.build_host_into(blob, offs, out, mph_buf, device=device)
         best = min(best, time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    s3imph.build_host(blob, offs, device=device, out=out)
+    alloc_ms = (time.perf_counter() - t0) * 1e3
     return {"keys_per_s": n / best, "ms": best * 1e3, "key_bytes_GBps": int(offs[-1]) / best / 1e9,
-            "note": "pageable host memory: H2D of blob+offsets (runtime path), build, D2H of fp/pos through "
-                    "pinned chunk staging (8 workers), mph.bin marshal; output arrays reused"}
+            "alloc_api_ms": alloc_ms,
+            "note": "pageable host memory: offsets as u16 lengths then the blob H2D in 16 pieces with the "
+                    "level-0 hash of each piece launched as it lands, build, D2H of fp/pos through pinned "
+                    "chunk staging (8 workers), mph.bin into a reused caller buffer; output arrays reused"}
 
 
 def secondary_line(s3imph, device: int, seed: int, steps: int, warmup: int) -> dict:

@@ -105,6 +105,15 @@ int s3imph_build_host(int device, const uint8_t *blob, const uint64_t *offsets, 
                       uint64_t n, uint64_t *fp_out, uint64_t *pos_out, uint8_t **mph_bin,
                       uint64_t *mph_len, char *err, size_t errlen);
 
+/* The same build with mph.bin marshalled into the caller's buffer (mph_cap bytes, at least
+ * s3imph_mph_bin_bound(n); *mph_len gets its size), which a pipeline reuses across calls as it
+ * reuses fp_out / pos_out: no library allocation, no fresh pages to fault in. */
+int s3imph_build_host_into(int device, const uint8_t *blob, const uint64_t *offsets, const uint64_t *pos,
+                           uint64_t n, uint64_t *fp_out, uint64_t *pos_out, uint8_t *mph_out, uint64_t mph_cap,
+                           uint64_t *mph_len, char *err, size_t errlen);
+/* An upper bound on mph.bin's size for n keys (0 for n == 0). */
+uint64_t s3imph_mph_bin_bound(uint64_t n);
+
 void s3imph_free(void *p);
 
 /* Multi-GPU host-memory build for ONE calling process (the reference's caller is one
@@ -217,9 +226,12 @@ int s3imph_ctx_create_dist_host(int device, const s3imph_host_comm *comm, int ra
  *                        all-to-all of the settled (p, fp, pos) at the end.  A level larger
  *                        than its host-side bound reruns the build on ROUTE.
  * Both give byte-identical outputs.  No reference counterpart (bbhash.New runs on one
- * thread, mphf_streaming.go:141). */
+ * thread, mphf_streaming.go:141).  S3IMPH_DIST_STRICT or-ed into BITMAP: no fallback — a
+ * level past its bound fails the build (S3IMPH_ERR_INTERNAL) instead of rerunning on ROUTE
+ * (a benchmark of the bitmap decomposition uses it so it never times the other one). */
 #define S3IMPH_DIST_ROUTE 0
 #define S3IMPH_DIST_BITMAP 1
+#define S3IMPH_DIST_STRICT 0x100
 int s3imph_ctx_set_dist_mode(s3imph_ctx *ctx, int mode);
 
 /* This rank holds keys [key_base, key_base + n_local) of the global set (the

@@ -315,8 +315,13 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
                                                   unsigned long long* __restrict__ sflags, LevelState* st,
                                                   unsigned tb, uint64_t chunk, unsigned* __restrict__ tcnt,
                                                   unsigned long long* __restrict__ prof = nullptr,
-                                                  Route0 rt = Route0{}, P0Part pt = P0Part{}) {
+                                                  Route0 rt = Route0{}, P0Part pt = P0Part{}, unsigned blk0 = 0,
+                                                  unsigned nblk = 0) {
+  // blocks [blk0, blk0 + gridDim.x) of an nblk-block decomposition of the keys (nblk 0: this
+  // grid alone): the host build launches the hash in pieces, each once its keys' bytes have
+  // crossed PCIe (launch_hash_pieces)
   static_assert(!(RT && PT), "route or partition, not both");
+  const unsigned bid = blk0 + blockIdx.x, NBK = nblk ? nblk : gridDim.x;
   unsigned long long pt0 = __builtin_amdgcn_s_memtime(), ph = 0, pw = 0;  // debug phase clock
   const unsigned long long prt0 = __builtin_amdgcn_s_memrealtime();
   constexpr int G = 2 * NT;                    // keys per round
@@ -364,19 +369,21 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
     const uint64_t T = ntiles_of(st->words[0], tb), B = (n + chunk - 1) / chunk;
     const uint64_t nseg = (T * B + kScanSeg - 1) / kScanSeg;
     const uint64_t g0 = (uint64_t)blockIdx.x * NT + tid, gs = (uint64_t)gridDim.x * NT;
-    if (blockIdx.x == 0 && tid == 0) {
+    if (blk0 == 0 && blockIdx.x == 0 && tid == 0) {
       st->ntiles[0] = T;
       st->nchunks[0] = B;
     }
-    for (uint64_t t = g0; t < T; t += gs) flags[t] = 0;
-    for (uint64_t q = g0; q < nseg; q += gs) sflags[q] = 0;
-    for (uint64_t q = g0; q < kTcntWords; q += gs) tcnt[q] = 0;
+    if (blk0 == 0) {  // (the first piece's grid covers them all)
+      for (uint64_t t = g0; t < T; t += gs) flags[t] = 0;
+      for (uint64_t q = g0; q < nseg; q += gs) sflags[q] = 0;
+      for (uint64_t q = g0; q < kTcntWords; q += gs) tcnt[q] = 0;
+    }
   }
-  const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
-  uint64_t g = (uint64_t)blockIdx.x * per;
+  const uint64_t per = (n + NBK - 1) / NBK;
+  uint64_t g = (uint64_t)bid * per;
   const uint64_t gend = min(n, g + per);
   if (g >= gend) {
-    if (PT && tid < pt.S) pt.pcnt[(uint64_t)blockIdx.x * pt.S + tid] = 0;
+    if (PT && tid < pt.S) pt.pcnt[(uint64_t)bid * pt.S + tid] = 0;
     return;
   }
   const uint64_t end8 = (offsets[n] + 7) & ~7ull;
@@ -633,7 +640,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
         }
       __syncthreads();
       if (!r_over) {
-        R20* const blk = pt.sup + (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x) * pt.S * pt.reg_cap;
+        R20* const blk = pt.sup + (uint64_t)__builtin_amdgcn_readfirstlane(bid) * pt.S * pt.reg_cap;
         for (unsigned j = tid; j < m; j += NT) {
           const unsigned o = sdst[j];
           blk[r_off[o] + (j - r_start[o])] = stg[j];
@@ -648,9 +655,9 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
       pw += __builtin_amdgcn_s_memtime() - ptb;
     }
   }
-  if (prof && lane == 0 && (uint64_t)blockIdx.x * NW + wave < 8192) {
+  if (prof && lane == 0 && (uint64_t)bid * NW + wave < 8192) {
     const unsigned long long tot = __builtin_amdgcn_s_memtime() - pt0;
-    unsigned long long* q = prof + ((uint64_t)blockIdx.x * NW + wave) * 8;
+    unsigned long long* q = prof + ((uint64_t)bid * NW + wave) * 8;
     q[0] = tot;
     q[1] = ph;
     q[2] = pw;
@@ -663,7 +670,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   if (zero) atomicOr(&st->status, kStKeyZero);
   if (RT && tid == 0 && r_over) atomicOr(&st->status, kStRouteOverflow);
   if (PT && tid == 0 && r_over) atomicOr(&st->status, kStOverflow | kStResOverflow);
-  if (PT && tid < pt.S) pt.pcnt[(uint64_t)blockIdx.x * pt.S + tid] = p_cur[tid];  // wave 0 updated p_cur
+  if (PT && tid < pt.S) pt.pcnt[(uint64_t)bid * pt.S + tid] = p_cur[tid];  // wave 0 updated p_cur
 }
 
 // ------------------------------------------- level-0 hash, skewed key lengths --------
@@ -1250,7 +1257,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
     if (n <= kGate) {
       // an R20 list (planned before level 0, BinBuffers::l20) for a level that turned out
       // small enough for the mid / tail kernels, which read Rec: rerun conservatively
-      if (kSrc == 4 && blockIdx.x == 0 && tid == 0) atomicOr(&st->status, kStGeometry);
+      if (kSrc == 4 && blockIdx.x == 0 && tid == 0) (atomicOr(&st->status, kStGeometry), atomicCAS(&st->pad0_, 0u, 1u));
       return;
     }
     if (no_progress(st, level, n)) return;
@@ -1261,7 +1268,7 @@ __global__ __launch_bounds__(kSB) void k_scatter_res(int level, const Rec* __res
   // quotient's operand is < 2^18 and ts <= 16)
   const uint32_t ts_mul = ts ? 0xffffffffu / ts + 1 : 0;
   if (T > kT) {
-    if (tid == 0) atomicOr(&st->status, kStGeometry);
+    if (tid == 0) (atomicOr(&st->status, kStGeometry), atomicCAS(&st->pad0_, 0u, 2u));
     return;
   }
   if (blockIdx.x == 0 && tid == 0) {
@@ -1441,21 +1448,27 @@ struct P0In {
   unsigned NB, S;          // hash blocks, super-tiles
   unsigned NB_skew;        // a skewed set: k_hash_skew's blocks and region size
   uint64_t reg_cap_skew;
-  uint64_t slot_cap;       // slots: records per (super-tile, XCD shard) slot
+  uint64_t sup_cap;        // slots: R20 records in sup (the partition pass's bucket capacity)
   const unsigned* scnt;    // ... their fills
   bool fused;              // the hash wrote regions (unless it found the set skewed)
 };
 
-template <int kR, int kT, int NT = kSB>  // (512 threads, 2560-record rounds, two blocks per CU: slower)
+// tb: the tiles' position bits (kRegTileMaxBits for the single-GPU k_tile_p0; the bitmap
+// decomposition scales them with the rank count, P0Bufs::tb <= 16).  kX: each record's
+// position within its tile (u16) also goes to xo at its slot (the bitmap mark reads 2 B per
+// record instead of its 20, and the settle skips bb_index), staged beside the tile.
+template <int kR, int kT, int NT = kSB, bool kX = false>  // (512 threads, 2560-record rounds, two blocks per CU: slower)
 __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsigned tps, R20* __restrict__ bucket,
                                                     uint64_t bcap, unsigned* __restrict__ tcnt,
                                                     unsigned long long* __restrict__ flags, LevelState* st,
-                                                    unsigned long long* __restrict__ prof) {
+                                                    unsigned long long* __restrict__ prof, unsigned tb = kRegTileMaxBits,
+                                                    uint16_t* __restrict__ xo = nullptr, int level = 0) {
   constexpr int kKPT = kR / NT;
   constexpr unsigned kMaxRuns = kH0Grid / 8 + 1;  // bps >= 8 (launch_p0_scatter)
   __shared__ uint64_t stage_raw[(kR * 5 + 1) / 2];
   R20* const stage = reinterpret_cast<R20*>(stage_raw);
-  __shared__ unsigned short stile[kR];
+  __shared__ unsigned short stile[kR];    // slot -> tile in the window
+  __shared__ uint16_t sx[kX ? kR : 1];    // kX: slot -> position in the tile
   __shared__ unsigned cnt[kT];
   __shared__ unsigned start[kT];
   __shared__ unsigned cur[kT];
@@ -1463,11 +1476,12 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
   __shared__ unsigned s_over;
   if (st->status & kStStop) return;
   const unsigned tid = threadIdx.x;
-  const uint64_t words = st->words[0], magic = st->magic[0];
-  const uint64_t T = tiles_of(words, kRegTileMaxBits, 0);
+  // (level > 0: a bitmap list level's records, partitioned into the super-tiles' slots first)
+  const uint64_t words = st->words[level], magic = st->magic[level];
+  const uint64_t T = tiles_of(words, tb, 0);
   if (blockIdx.x == 0 && tid == 0) {
-    st->ntiles[0] = T;
-    st->nchunks[0] = 0;
+    st->ntiles[level] = T;
+    st->nchunks[level] = 0;
   }
   for (uint64_t t = (uint64_t)blockIdx.x * NT + tid; t < T; t += (uint64_t)gridDim.x * NT) flags[t] = 0;
   const unsigned sidx = blockIdx.x / bps, part = blockIdx.x % bps;
@@ -1475,7 +1489,7 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
   if (t0 >= T) return;
   const unsigned tn = (unsigned)min<uint64_t>(tps, T - t0);
   if (tn > (unsigned)kT) {
-    if (tid == 0) atomicOr(&st->status, kStGeometry);
+    if (tid == 0) (atomicOr(&st->status, kStGeometry), atomicCAS(&st->pad0_, 0u, 3u));
     return;
   }
   // This block's records, index j in [lo, hi): the super-tile's kResShards slots back to back
@@ -1492,7 +1506,7 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
     b0 = (unsigned)((uint64_t)NB * part / bps);
     nr = (unsigned)((uint64_t)NB * (part + 1) / bps) - b0;
     if (nr > (unsigned)NT || nr > kMaxRuns) {  // (the host keeps bps >= NB / NT)
-      if (tid == 0) atomicOr(&st->status, kStGeometry);
+      if (tid == 0) (atomicOr(&st->status, kStGeometry), atomicCAS(&st->pad0_, 0u, 4u));
       return;
     }
     const unsigned c = tid < nr ? in.pcnt[(uint64_t)(b0 + tid) * in.S + sidx] : 0u;
@@ -1510,7 +1524,10 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
     lo = m * part / bps;
     hi = m * (part + 1) / bps;
   }
-  const R20* sbase = in.sup + (uint64_t)sidx * kResShards * in.slot_cap;
+  // the partition pass's slot layout (k_scatter_res over ceil(T / tps) super-tiles: cap
+  // = sup_cap / that many per super-tile, cut into kResShards shard slots)
+  const uint64_t sup_each = in.sup_cap / ((T + tps - 1) / tps), slot_cap = sup_each / kResShards;
+  const R20* sbase = in.sup + (uint64_t)sidx * sup_each;
   // record j's address (the loads themselves run in straight-line code: a load inside the
   // search's divergent branches was waited for on the spot, five HBM latencies per round)
   auto src = [&](uint64_t j) -> const R20* {
@@ -1526,7 +1543,7 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
     uint64_t o = j;
 #pragma unroll
     for (int x = 1; x < kResShards; ++x)
-      if (j >= pre[x]) o = (uint64_t)x * in.slot_cap + (j - pre[x]);
+      if (j >= pre[x]) o = (uint64_t)x * slot_cap + (j - pre[x]);
     return sbase + o;
   };
   // records live as (dwords 0-3, dword 4) register pairs: an R20[] copied whole into the stage
@@ -1548,7 +1565,7 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
   };
   const uint64_t cap = bcap / T, scap = cap / kResShards;
   const unsigned shard = blockIdx.x % kResShards;
-  const uint64_t seed = level_seed(0);
+  const uint64_t seed = level_seed(level);
   uint64_t r0 = lo;
   if (r0 >= hi) return;
   // debug: phase times summed over the block's rounds, k_scatter_res's row 32 (level 0) layout
@@ -1571,13 +1588,16 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
   bool geo = false;
   for (;;) {
     unsigned trk[kKPT];  // tile in the window << 13 | rank in the round's run of that tile
+    uint16_t xr[kX ? kKPT : 1];
 #pragma unroll
     for (int u = 0; u < kKPT; ++u) {
       const uint64_t j = r0 + (uint64_t)u * NT + tid;
       trk[u] = 0xffffffffu;
       if (j < hi) {
         const uint64_t k = (uint64_t)rq[u].x | ((uint64_t)rq[u].y << 32);
-        const uint64_t t = (bb_index(seed, k, words, magic) >> kRegTileMaxBits) - t0;
+        const uint64_t x = bb_index(seed, k, words, magic);
+        if constexpr (kX) xr[u] = (uint16_t)(x & ((1u << tb) - 1));
+        const uint64_t t = (x >> tb) - t0;
         if (t < tn) trk[u] = ((unsigned)t << 13) | atomicAdd(&cnt[t], 1u);
         else geo = true;
       }
@@ -1618,6 +1638,7 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
         d[2] = rq[u].z;
         d[3] = rq[u].w;
         d[4] = rz[u];
+        if constexpr (kX) sx[slot] = xr[u];
         stile[slot] = (unsigned short)t;
       }
     }
@@ -1638,7 +1659,9 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
     if (s_over) break;
     for (unsigned j = tid; j < mr; j += NT) {
       const unsigned t = stile[j];
-      bucket[cur[t] + (j - start[t])] = stage[j];
+      const unsigned o = cur[t] + (j - start[t]);
+      bucket[o] = stage[j];
+      if constexpr (kX) xo[o] = sx[j];
     }
     // The next round's records, in flight over the barriers below.  (Issued before the write
     // above, they were waited for at once: a 64-bit address write to a VGPR pair that a
@@ -1658,7 +1681,7 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
     tp[7] = c;
   }
 #undef P0PROF
-  if (geo) atomicOr(&st->status, kStGeometry);
+  if (geo) (atomicOr(&st->status, kStGeometry), atomicCAS(&st->pad0_, 0u, 5u));
   if (s_over && tid == 0) atomicOr(&st->status, kStOverflow | kStResOverflow);
 }
 
@@ -3838,6 +3861,30 @@ void binned_set_lds_limits() {
                             (int)tile_reg_lds_bytes(kRegMaxBits));
 }
 
+// The level-0 pair hash over all kH0Grid blocks: one launch, or (b.feed: the host build's key
+// bytes still crossing PCIe) one launch per piece of the blocks, each after feed->ensure(its
+// keys), so the hash of the arrived keys runs beside the rest of the copy.
+template <bool PT>
+void launch_hash_pieces(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
+                        unsigned long long* prof, const P0Part& pt, hipStream_t s) {
+  auto go = [&](unsigned b0, unsigned nb) {
+    k_hash0_pair<kH0T, kH0B, true, false, PT><<<nb, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
+                                                                 g.tb, g.chunk, b.tcnt, prof, Route0{}, pt, b0,
+                                                                 (unsigned)kH0Grid);
+  };
+  if (!b.feed) {
+    go(0, kH0Grid);
+    return;
+  }
+  const unsigned P = (unsigned)std::max(1, std::min(b.feed->pieces, kH0Grid));
+  const uint64_t per = (n + kH0Grid - 1) / kH0Grid;  // the kernel's key range per block
+  for (unsigned j = 0; j < P; ++j) {
+    const unsigned b0 = (unsigned)((uint64_t)kH0Grid * j / P), b1 = (unsigned)((uint64_t)kH0Grid * (j + 1) / P);
+    b.feed->ensure(std::min<uint64_t>(n, (uint64_t)b1 * per));
+    go(b0, b1 - b0);
+  }
+}
+
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s, bool histogram) {
   if (level == 0 && !b.dist) {
@@ -3847,11 +3894,12 @@ void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets
       // near-uniform lengths: LDS-staged, length-sorted rounds; skewed sets (decided on the
       // device from sampled lengths) fall through to k_hash_count0's length-sorted groups
       unsigned long long* prof = b.tile_prof ? b.tile_prof + (uint64_t)(kMaxLevels - 3) * kMaxTiles * 8 : nullptr;
-      k_hash0_pair<kH0T, kH0B, true><<<kH0Grid, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
-                                                             g.tb, g.chunk, b.tcnt, prof);
+      launch_hash_pieces<false>(blob, offsets, n, b, g, prof, P0Part{}, s);
+      if (b.feed) b.feed->ensure(n);
       launch_hash_skew(blob, offsets, n, b, g, prof, s);
       return;
     }
+    if (b.feed) b.feed->ensure(n);
     k_hash_count0<<<grid_chunks, kCB, 0, s>>>(blob, offsets, n, b.kh, b.fp, histogram ? b.hist : nullptr,
                                                   b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, 3);
   } else {
@@ -4017,10 +4065,19 @@ void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, 
 // The records' first partition, into the super-tiles' slots of p.sup, when the level-0 hash
 // did not write them there (kh / fp from k_hash_count0 or k_hash_skew): k_scatter_res with
 // the super-tiles as its tiles (tile = (position >> 14) / tps, exact by the reciprocal).
+// A bitmap list level's R20 list (level L's input, b.list[(L - 1) & 1]) into the super-tiles'
+// slots: the same pass over the list (k_scatter_res, kSrc 4), which k_scatter_p0 then reads.
+void launch_p0_partition_list(int level, const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
+  k_scatter_res<6144, 1024, 4, true><<<256, kSB, 0, s>>>(level, b.list[(level - 1) & 1], nullptr, nullptr, nullptr,
+                                                         b.pos_base, p.scnt, reinterpret_cast<Rec*>(p.sup), p.sup_cap,
+                                                         p.flags, b.st, kRegTileMaxBits, b.cap_words, nullptr, 0, 0,
+                                                         p.tps_sub(), 0u);
+}
+
 void launch_p0_partition(const BinBuffers& b, const P0Bufs& p, hipStream_t s, bool only_skew) {
   k_scatter_res<5120, 1024, 2, true><<<256, kSB, 0, s>>>(0, nullptr, b.kh, b.fp, nullptr, b.pos_base, p.scnt,
                                                         reinterpret_cast<Rec*>(p.sup), p.sup_cap, p.flags, b.st,
-                                                        kRegTileMaxBits, b.cap_words, nullptr, 0, 0, p.tps,
+                                                        kRegTileMaxBits, b.cap_words, nullptr, 0, 0, p.tps_sub(),
                                                         only_skew ? 1u : 0u);
 }
 
@@ -4040,12 +4097,12 @@ void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, co
                     const P0Bufs& p, hipStream_t s) {
   if (p0_fused(blob, p)) {
     unsigned long long* prof = b.tile_prof ? b.tile_prof + (uint64_t)(kMaxLevels - 3) * kMaxTiles * 8 : nullptr;
-    const P0Part pt{p.sup, p.reg_cap, p.pcnt, p.tps, p.S};
-    k_hash0_pair<kH0T, kH0B, true, false, true><<<kH0Grid, kH0T, 0, s>>>(
-        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, Route0{}, pt);
+    const P0Part pt{p.sup, p.reg_cap, p.pcnt, p.tps_sub(), p.S};
+    launch_hash_pieces<true>(blob, offsets, n, b, g, prof, pt, s);
+    if (b.feed) b.feed->ensure(n);
     // a skewed set: k_hash_skew's groups partition the same way, into regions of its own
     // (fewer, larger: p0_skew_blocks blocks, reg_cap_skew records each)
-    const P0Part pts{p.sup, p.reg_cap_skew, p.pcnt, p.tps, p.S};
+    const P0Part pts{p.sup, p.reg_cap_skew, p.pcnt, p.tps_sub(), p.S};
     launch_hash_skew(blob, offsets, n, b, g, prof, s, pts);
     return;
   }
@@ -4053,9 +4110,13 @@ void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, co
   launch_p0_partition(b, p, s, false);
 }
 
-void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStream_t s) {
+__global__ void k_set_status(LevelState* st, unsigned f) {
+  if (threadIdx.x == 0) atomicOr(&st->status, f);
+}
+
+void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStream_t s, int level) {
   const P0In in{p.sup, p.reg_cap, p.pcnt, (unsigned)kH0Grid, p.S, p0_skew_blocks(b.skew_cfg), p.reg_cap_skew,
-                p.sup_cap / ((uint64_t)p.S * kResShards), p.scnt, fused};
+                p.sup_cap, p.scnt, fused};
   // blocks per super-tile: a multiple of kResShards, so every shard slot of a tile takes the
   // records of the same number of blocks (9 blocks put 2/9 of a super-tile's records on one
   // shard: 1.8x the mean fill, past the slot capacity at S = 26)
@@ -4087,6 +4148,17 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
     return v / kResShards * kResShards;
   }();
   const unsigned bps = bps_knob ? bps_knob : std::max(1u, kP0ScatterBlocks / p.S / kResShards) * kResShards;
+  if (p.x) {
+    // the bitmap decomposition: tiles of 2^p.tb positions, each record's in-tile position to
+    // p.x as well; its levels have at most kBmMaxTiles tiles in <= 64 super-tiles of <= 512
+    if (p.tps > 512) {
+      k_set_status<<<1, 64, 0, s>>>(b.st, kStGeometry);  // unreachable (p0_super_tiles); the build reruns
+      return;
+    }
+    k_scatter_p0<6144, 512, kSB, true><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt,
+                                                                  p.flags, b.st, b.tile_prof, p.tb, p.x, level);
+    return;
+  }
   if (p.tps <= 256)
     k_scatter_p0<6144, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
   else if (p.tps <= 512)

@@ -251,12 +251,14 @@ __device__ __forceinline__ uint64_t rec_k(const RT* __restrict__ q) {
   const uint2 v = *reinterpret_cast<const uint2*>(q);
   return (uint64_t)v.x | ((uint64_t)v.y << 32);
 }
-template <int kMode, class RT>
+// kX: the records' in-tile positions come from xs (u16 per slot, written by the super-tile
+// scatter: 2 B per record read instead of the record's k and its bb_index)
+template <int kMode, class RT, bool kX = false>
 __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __restrict__ bucket,
                                                       const unsigned* __restrict__ tc, uint64_t bucket_cap,
                                                       unsigned tb, const LevelState* st, uint64_t wpad,
                                                       uint8_t* __restrict__ lanes, uint32_t* __restrict__ A32,
-                                                      uint64_t S, uint64_t mS) {
+                                                      uint64_t S, uint64_t mS, const uint16_t* __restrict__ xs = nullptr) {
   constexpr bool kNib = kMode == kBmNibbles;
   extern __shared__ uint32_t bm_lds[];
   __shared__ unsigned s_fo[kResShards + 1];
@@ -297,7 +299,11 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
     uint64_t kk[kU], kn[kU];
     auto ld = [&](unsigned i0, uint64_t (&dst)[kU]) {
 #pragma unroll
-      for (int u = 0; u < kU; ++u) dst[u] = rec_k(bucket + rec_index(min(i0 + u * kTT + tid, nrec - 1), fo, t * cap, scap));
+      for (int u = 0; u < kU; ++u) {
+        const uint64_t ri = rec_index(min(i0 + u * kTT + tid, nrec - 1), fo, t * cap, scap);
+        if constexpr (kX) dst[u] = xs[ri];
+        else dst[u] = rec_k(bucket + ri);
+      }
     };
     if (nrec) ld(0, kk);
     for (unsigned i0 = 0; i0 < nrec; i0 += kTT * kU) {
@@ -306,7 +312,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         if (i0 + u * kTT + tid < nrec) {
-          const uint64_t lx = bb_index(seed, kk[u], words, magic) - t0;
+          const uint64_t lx = kX ? kk[u] : bb_index(seed, kk[u], words, magic) - t0;
           const uint32_t bit = 1u << (lx & 31);
           if (atomicOr(&sA[lx >> 5], bit) & bit) atomicOr(&sC[lx >> 5], bit);
         }
@@ -358,7 +364,15 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
 // a hole no one reads); every settled key is counted per output slice in scnt, which is
 // the output all-to-all's send counts (the list's runs by slice, holes included).
 constexpr unsigned kGrp = 4;
-constexpr unsigned kBmStage = 5632;  // staged settled keys per 2^14 tile (mean 4969 at one rank: 9.9 sigma)
+// staged settled keys per tile: the tiles of a staged level are sized so that a rank holds ~8k
+// records of one (2^14 positions at one rank, 2^(14 + lg P) at P, kBmP0MaxTb at most): mean
+// ~4970 settled, 9.9 sigma below this at one rank (more ranks: the share adds ~1 sigma)
+constexpr unsigned kBmStage = 5632;
+// a staged settled key: its fingerprint, key index (p = pos_base + i) and rank in the tile
+struct BmStaged {
+  uint64_t f;
+  uint32_t i, pg;
+};
 __device__ __forceinline__ void fp_out_own(const OwnSlice& os, uint64_t p, uint64_t f, uint64_t pos, bool& over) {
   const uint64_t o = p - os.lo;
   if (p < os.lo || o >= os.cnt) {
@@ -368,18 +382,21 @@ __device__ __forceinline__ void fp_out_own(const OwnSlice& os, uint64_t p, uint6
   os.fp_out[o] = f;
   os.pos_out[o] = pos;
 }
-// kStaged (R20 records in 2^14-position tiles: P0's level 0): this rank's settled keys of a
-// tile (<= ~5.2k at one rank) are staged in LDS behind the tile words.  kO20: the collided
-// records leave as R20 (k, f, p - pos_base), the next bitmap level's list (BinBuffers::l20).
-template <class RT, bool kStaged, bool kO20>
+// kStaged (R20 records, identity positions, tiles of a rank's ~8k records: 2^14 to
+// 2^kBmP0MaxTb positions): this rank's settled keys of a tile are staged in LDS (16 B each)
+// behind the tile words.  kO20: the collided records leave as R20 (k, f, p - pos_base), the
+// next bitmap level's list (BinBuffers::l20).  kX: positions from xs (the super-tile scatter's).
+template <class RT, bool kStaged, bool kO20, bool kX = false>
 __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __restrict__ bucket, uint64_t pos_base,
                                                         const unsigned* __restrict__ tc, uint64_t bucket_cap,
                                                         unsigned tb, LevelState* st, const uint64_t* __restrict__ g,
                                                         const uint64_t* __restrict__ A,
                                                         const unsigned long long* __restrict__ tbase,
                                                         Rec* __restrict__ out, uint64_t out_cap,
-                                                        Rec* __restrict__ next, uint64_t next_cap, OwnSlice os) {
+                                                        Rec* __restrict__ next, uint64_t next_cap, OwnSlice os,
+                                                        const uint16_t* __restrict__ xs = nullptr) {
   static_assert(!kStaged || sizeof(RT) != sizeof(Rec), "staged settles read R20 tiles");
+  static_assert(!kX || kStaged, "x positions come with P0's R20 tiles");
   extern __shared__ uint64_t bm_lds64[];
   __shared__ unsigned long long s_w[kTT / 64];
   __shared__ unsigned s_sc[kMaxRanks];
@@ -396,7 +413,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
   uint64_t* sga = sg + W;
   unsigned* gpg = reinterpret_cast<unsigned*>(sga + W);  // per group: popcount(g) before it
   unsigned* gpa = gpg + G;                               // ... popcount(g & a)
-  Rec* stg = reinterpret_cast<Rec*>(gpa + G);            // kStaged: kBmStage records (8-B aligned: G even)
+  BmStaged* stg = reinterpret_cast<BmStaged*>(gpa + G);  // kStaged: kBmStage entries (8-B aligned: G even)
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
   constexpr int kGper = 2;  // groups per thread in the tile scan (G <= 2048)
@@ -478,11 +495,14 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
     const unsigned nrec = fo[kResShards];
     for (unsigned i0 = 0; i0 < nrec; i0 += kTT * kU) {
       Rec r[kU];
+      uint16_t rx[kX ? kU : 1];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const unsigned i = i0 + u * kTT + tid;
         if (i < nrec) {
-          const RT* q = bucket + rec_index(i, fo, t * cap, scap);
+          const uint64_t ri = rec_index(i, fo, t * cap, scap);
+          const RT* q = bucket + ri;
+          if constexpr (kX) rx[u] = xs[ri];
           if constexpr (sizeof(RT) == sizeof(Rec)) {
             r[u] = *reinterpret_cast<const Rec*>(q);
           } else {  // R20: (k, f, key index), p = pos_base + index
@@ -495,7 +515,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         if (i0 + u * kTT + tid >= nrec) continue;
-        const uint64_t lx = bb_index(seed, r[u].k, words, magic) - t0;
+        const uint64_t lx = kX ? (uint64_t)rx[u] : bb_index(seed, r[u].k, words, magic) - t0;
         const unsigned j = (unsigned)(lx >> 6), b = (unsigned)(lx & 63), grp = j / kGrp;
         const uint64_t below = (1ull << b) - 1ull, v = sg[j];
         if ((v >> b) & 1ull) {
@@ -517,7 +537,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
           const unsigned sl = owner_of(gp, os.slice, os.mslice);
           atomicAdd(&s_sc[sl < (unsigned)os.P ? sl : os.P - 1], 1u);
           if (kStaged && pa < kBmStage) {  // written out below in pa order
-            stg[pa] = Rec{gp, r[u].f, r[u].p};
+            stg[pa] = BmStaged{r[u].f, (uint32_t)(r[u].p - pos_base), pg};
           } else if ((int)sl == os.rank) {
             fp_out_own(os, gp, r[u].f, r[u].p, over);
           } else {
@@ -544,11 +564,12 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
       __syncthreads();
       const unsigned ns = (unsigned)min<unsigned long long>(tot & 0xffffffffull, kBmStage);
       for (unsigned i = tid; i < ns; i += kTT) {
-        const Rec e = stg[i];
-        if ((int)owner_of(e.k, os.slice, os.mslice) == os.rank) {
-          fp_out_own(os, e.k, e.f, e.p, over);
+        const BmStaged e = stg[i];
+        const uint64_t gp = pb + e.pg, p = pos_base + e.i;
+        if ((int)owner_of(gp, os.slice, os.mslice) == os.rank) {
+          fp_out_own(os, gp, e.f, p, over);
         } else if (ob + i < out_cap) {
-          out[ob + i] = e;
+          out[ob + i] = Rec{gp, e.f, p};
         } else {
           over = true;
         }
@@ -634,32 +655,40 @@ size_t bm_tile_lds(unsigned tb, bool settle) {
 void bm_set_lds_limits() {
   for (const void* k : {(const void*)k_bm_tile_mark<kBmBytes, Rec>, (const void*)k_bm_tile_mark<kBmNibbles, Rec>,
                         (const void*)k_bm_tile_mark<kBmPlanes, Rec>, (const void*)k_bm_tile_mark<kBmBytes, R20>,
-                        (const void*)k_bm_tile_mark<kBmNibbles, R20>, (const void*)k_bm_tile_mark<kBmPlanes, R20>})
+                        (const void*)k_bm_tile_mark<kBmNibbles, R20>, (const void*)k_bm_tile_mark<kBmPlanes, R20>,
+                        (const void*)k_bm_tile_mark<kBmBytes, R20, true>, (const void*)k_bm_tile_mark<kBmNibbles, R20, true>,
+                        (const void*)k_bm_tile_mark<kBmPlanes, R20, true>})
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_tile_lds(kBmMaxTb, false));
   for (const void* k : {(const void*)k_bm_tile_settle<Rec, false, false>, (const void*)k_bm_tile_settle<Rec, false, true>,
                         (const void*)k_bm_tile_settle<R20, false, false>, (const void*)k_bm_tile_settle<R20, false, true>})
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_tile_lds(kBmMaxTb, true));
-  for (const void* k : {(const void*)k_bm_tile_settle<R20, true, false>, (const void*)k_bm_tile_settle<R20, true, true>})
+  static_assert(((size_t)1 << (kBmP0MaxTb - 6)) * 18 + kBmStage * sizeof(BmStaged) <= 160 * 1024, "staged settle LDS");
+  for (const void* k : {(const void*)k_bm_tile_settle<R20, true, false>, (const void*)k_bm_tile_settle<R20, true, true>,
+                        (const void*)k_bm_tile_settle<R20, true, false, true>,
+                        (const void*)k_bm_tile_settle<R20, true, true, true>})
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(bm_tile_lds(kBmMinTb, true) + kBmStage * sizeof(Rec)));
+                              (int)(bm_tile_lds(kBmP0MaxTb, true) + kBmStage * sizeof(BmStaged)));
 }
 
 void launch_bm_range(LevelState* st, int level, hipStream_t s) { k_bm_range<<<1, 64, 0, s>>>(st, level); }
 
 void launch_bm_tile_mark(int level, const void* bucket, bool r20, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
                          uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A, int mode,
-                         uint64_t S, hipStream_t s) {
+                         uint64_t S, hipStream_t s, const uint16_t* xs) {
   const int grid = (int)std::max<uint64_t>(256, std::min<uint64_t>(tiles, 1024));
-  auto go = [&](auto rt) {
+  auto go = [&](auto rt, auto xt) {
     using RT = decltype(rt);
+    constexpr bool kX = decltype(xt)::value;
     const RT* bk = static_cast<const RT*>(bucket);
-    auto kern = mode == kBmPlanes ? k_bm_tile_mark<kBmPlanes, RT> : mode == kBmNibbles ? k_bm_tile_mark<kBmNibbles, RT>
-                                                                                      : k_bm_tile_mark<kBmBytes, RT>;
+    auto kern = mode == kBmPlanes    ? k_bm_tile_mark<kBmPlanes, RT, kX>
+                : mode == kBmNibbles ? k_bm_tile_mark<kBmNibbles, RT, kX>
+                                     : k_bm_tile_mark<kBmBytes, RT, kX>;
     kern<<<grid, kTT, bm_tile_lds(tb, false), s>>>(level, bk, tc, bucket_cap, tb, st, wpad, lanes,
-                                                   reinterpret_cast<uint32_t*>(A), S, level_magic(S));
+                                                   reinterpret_cast<uint32_t*>(A), S, level_magic(S), xs);
   };
-  if (r20) go(R20{});
-  else go(Rec{});
+  if (xs) go(R20{}, std::true_type{});
+  else if (r20) go(R20{}, std::false_type{});
+  else go(Rec{}, std::false_type{});
 }
 
 void launch_bm_merge(const uint64_t* recv, uint64_t S, int P, uint64_t* out, const LevelState* st, hipStream_t s) {
@@ -669,22 +698,27 @@ void launch_bm_merge(const uint64_t* recv, uint64_t S, int P, uint64_t* out, con
 void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos_base, const unsigned* tc,
                            uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
                            const uint64_t* A, const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next,
-                           uint64_t next_cap, bool next20, const OwnSlice& os, hipStream_t s) {
+                           uint64_t next_cap, bool next20, const OwnSlice& os, hipStream_t s, bool staged,
+                           const uint16_t* xs) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1024));
-  auto go = [&](auto rt, auto staged, auto o20) {
+  auto go = [&](auto rt, auto stg, auto o20, auto xt) {
     using RT = decltype(rt);
-    constexpr bool kSt = decltype(staged)::value, kO = decltype(o20)::value;
-    const size_t lds = bm_tile_lds(tb, true) + (kSt ? kBmStage * sizeof(Rec) : 0);
-    k_bm_tile_settle<RT, kSt, kO><<<grid, kTT, lds, s>>>(level, static_cast<const RT*>(bucket), pos_base, tc, bucket_cap,
-                                                          tb, st, g, A, tbase, out, out_cap, next, next_cap, os);
+    constexpr bool kSt = decltype(stg)::value, kO = decltype(o20)::value, kX = decltype(xt)::value;
+    const size_t lds = bm_tile_lds(tb, true) + (kSt ? kBmStage * sizeof(BmStaged) : 0);
+    k_bm_tile_settle<RT, kSt, kO, kX><<<grid, kTT, lds, s>>>(level, static_cast<const RT*>(bucket), pos_base, tc,
+                                                              bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
+                                                              next_cap, os, xs);
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  // R20 2^14-position tiles stage their settled keys (P0's level 0); R20 list levels' larger
-  // tiles write them directly, as Rec buckets do
-  if (r20 && tb == kBmMinTb) next20 ? go(R20{}, T_{}, T_{}) : go(R20{}, T_{}, F_{});
-  else if (r20) next20 ? go(R20{}, F_{}, T_{}) : go(R20{}, F_{}, F_{});
-  else next20 ? go(Rec{}, F_{}, T_{}) : go(Rec{}, F_{}, F_{});
+  // R20 tiles holding ~8k of this rank's records (the caller's `staged`: 2^14 positions per
+  // rank, at most kBmP0MaxTb) stage their settled keys; larger tiles and Rec buckets write
+  // them directly
+  staged = staged && r20 && tb <= kBmP0MaxTb;
+  if (staged && xs) next20 ? go(R20{}, T_{}, T_{}, T_{}) : go(R20{}, T_{}, F_{}, T_{});
+  else if (staged) next20 ? go(R20{}, T_{}, T_{}, F_{}) : go(R20{}, T_{}, F_{}, F_{});
+  else if (r20) next20 ? go(R20{}, F_{}, T_{}, F_{}) : go(R20{}, F_{}, F_{}, F_{});
+  else next20 ? go(Rec{}, F_{}, T_{}, F_{}) : go(Rec{}, F_{}, F_{}, F_{});
 }
 
 void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,

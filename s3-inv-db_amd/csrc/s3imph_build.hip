@@ -106,7 +106,8 @@ void free_workspace(s3imph_ctx* c) {
   dfree(c->block_sums); dfree(c->d_st);
   dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
   dfree(c->tcnt);
-  dfree(c->p0_tcnt); dfree(c->p0_flags); dfree(c->p0_scnt); dfree(c->p0_pcnt); dfree(c->p0_sup);
+  dfree(c->p0_tcnt); dfree(c->p0_flags); dfree(c->p0_scnt); dfree(c->p0_pcnt); dfree(c->p0_sup); dfree(c->p0_x);
+  c->p0_x_cap = 0;
   c->p0_tiles = 0;
   c->p0_sup_cap = 0;
   dfree(c->tile_prof);
@@ -266,6 +267,7 @@ void fault_dup_record(s3imph_ctx* c, Rec* list, hipStream_t s, bool r20 = false)
 
 BinBuffers make_bufs(s3imph_ctx* c, const uint64_t* pos, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s) {
   BinBuffers b{};
+  b.feed = c->feed;
   b.kh = c->kh;
   b.fp = c->fp;
   b.pos = pos;
@@ -544,9 +546,11 @@ uint64_t p0_super_tiles(uint64_t T, uint64_t target) {
 // in S super-tiles of tps (about kP0TargetTps; S <= kP0MaxS), the super-tiles' records in
 // c->p0_sup (sized for the hash's per-block regions and for the slot layout of the pass that
 // stands in for it), the tiles' slots in the bucket, both as R20.
-P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s) {
-  const uint64_t T = tiles_of(level_words(n_geom), kRegTileMaxBits, 0);
+P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s, unsigned tb = kRegTileMaxBits,
+               bool want_x = false) {
+  const uint64_t T = tiles_of(level_words(n_geom), tb, 0);
   P0Bufs p;
+  p.tb = tb;
   static const uint64_t target = [] {  // A/B knob S3IMPH_P0_TPS: tiles per super-tile aimed at
     const char* e = dev_env("S3IMPH_P0_TPS");
     return e ? std::max<uint64_t>(16, std::strtoull(e, nullptr, 10)) : kP0TargetTps;
@@ -584,6 +588,14 @@ P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s) {
   p.scnt = c->p0_scnt;
   p.bucket = reinterpret_cast<R20*>(c->bucket);
   p.bucket_cap = c->bucket_cap * sizeof(Rec) / sizeof(R20);
+  if (want_x) {  // the bitmap decomposition's level 0: each slot's position beside its record
+    if (p.bucket_cap > c->p0_x_cap) {
+      c->p0_x_cap = 0;
+      dalloc(c->p0_x, p.bucket_cap);
+      c->p0_x_cap = p.bucket_cap;
+    }
+    p.x = c->p0_x;
+  }
   p.tcnt = c->p0_tcnt;
   p.flags = c->p0_flags;
   HIPCHECK(hipMemsetAsync(p.tcnt, 0, T * kResShards * sizeof(unsigned), s));
@@ -592,9 +604,10 @@ P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s) {
 }
 
 // p0_bufs, or false when its allocation fails (NOMEM): the caller takes the non-P0 path
-bool p0_try_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s, P0Bufs* out) {
+bool p0_try_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s, P0Bufs* out,
+                 unsigned tb = kRegTileMaxBits, bool want_x = false) {
   try {
-    *out = p0_bufs(c, n, n_geom, s);
+    *out = p0_bufs(c, n, n_geom, s, tb, want_x);
     return true;
   } catch (const Fail& f) {
     if (f.code != S3IMPH_ERR_NOMEM) throw;
@@ -1604,6 +1617,14 @@ void free_bm_workspace(DistState& d) {
 // the reservation scatter (C3 level 0: 3052 tiles of 2^16 take its 4096-tile form, 1.66 ms;
 // 763 of 2^18 the 1024-tile form, 0.99 ms) but not the settle, whose random writes by rank
 // spread over a 4x larger window per tile (1.88 -> 3.64 ms).
+// Tile bits at which a rank holds ~8k records of a bitmap level's tile (2^14 at one rank, as a
+// single GPU's register tile): 14 + floor(lg P), at most kBmP0MaxTb
+unsigned bm_dense_tb(int P) {
+  unsigned tb = kBmMinTb;
+  for (int q = 2; q <= P && tb < kBmP0MaxTb; q *= 2) ++tb;
+  return tb;
+}
+
 uint64_t bm_target_tiles() {
   static const uint64_t v = [] {
     const char* e = dev_env("S3IMPH_BM_TILES");
@@ -1629,17 +1650,26 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   launch_dist_setup(st, 0, nullptr, N, R, P, s);
   launch_bm_range(st, 0, s);  // the whole level before the hash: P0's partition pass reads the range
   ev_mark(c, s, "init");
-  // Level 0 through the P0 super-tiles into 2^14-position tiles when the whole
-  // level's tile count is in P0's range and positions are the identity: the fused hash
-  // partition, the super-tile scatter, then the bitmap tile kernels over R20 slots.
-  const uint64_t T14 = tiles_of(level_words(N), kRegTileMaxBits, 0);
-  const bool p0 = c->p0 && !pos && n_local && n_local <= kP0MaxKeys && !hash_only_knob() && T14 > p0_min_tiles() &&
-                  T14 <= kP0MaxS * kP0MaxTps && T14 <= kBmMaxTiles;
+  // Level 0 through the P0 super-tiles when the whole level's tile count is
+  // in P0's range and positions are the identity: the fused hash partition, the super-tile
+  // scatter (which also writes each slot's position), then the bitmap tile kernels over R20
+  // slots.  Tiles hold 2^tbd positions, tbd = 14 + floor(lg P) (at most kBmP0MaxTb): a rank's
+  // share of a tile stays ~8k records, as one GPU's 2^14 tile, so the settle stages them.
+  // (Tiles are rank-local geometry — only whole words of planes and bits cross ranks — so a
+  // rank may take P0 or not on its own, e.g. one without keys or out of memory.)
+  const unsigned tbd = bm_dense_tb(P);
+  unsigned tb0 = tbd;
+  while (tb0 < kBmP0MaxTb && tiles_of(level_words(N), tb0, 0) > kBmMaxTiles) ++tb0;
+  const uint64_t T0 = tiles_of(level_words(N), tb0, 0);
+  // (the single-GPU threshold, p0_min_tiles, weighs P0 against the split kernel; here the
+  // alternative is a Rec level 0 without staged settles, so P0 takes any level of a tile per CU)
+  bool p0 = c->p0 && !pos && n_local && n_local <= kP0MaxKeys && !hash_only_knob() && T0 >= kBmP0MinTiles &&
+            T0 <= kP0MaxS * kP0MaxTps && T0 <= kBmMaxTiles;
   P0Bufs pb{};
+  if (p0) p0 = p0_try_bufs(c, n_local, N, s, &pb, tb0, true);
   if (n_local) {
     const LevelGeom gh0 = choose_geom_sz(n_local, 64 * level_words(N), kTargetTiles0, chunks0(n_local), kTileMaxBits);
     if (p0) {
-      pb = p0_bufs(c, n_local, N, s);
       launch_p0_hash(blob, offsets, n_local, b, gh0, pb, s);
     } else {
       launch_hash0_only(blob, offsets, n_local, b, gh0, level_grids(n_local, 64 * level_words(N), gh0).gc, s);
@@ -1647,8 +1677,8 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   }
   ev_mark(c, s, p0 ? "hash_part0" : "hash_count0");
   if (c->debug && p0)
-    std::fprintf(stderr, "[s3imph] rank %d bitmap: level 0 through P0 super-tiles (%llu tiles of 2^14)\n", R,
-                 (unsigned long long)T14);
+    std::fprintf(stderr, "[s3imph] rank %d bitmap: level 0 through P0 super-tiles (%llu tiles of 2^%u)\n", R,
+                 (unsigned long long)T0, tb0);
   Rec* const out = d.bm_out;                   // this rank's settled (p, fp, pos) triples
   unsigned long long* const out_cnt = d.small + 4096;
   HIPCHECK(hipMemsetAsync(out_cnt, 0, 8, s));
@@ -1688,18 +1718,25 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   int L = 0;
   for (;;) {
     const uint64_t wmax = level_words((uint64_t)std::ceil(nb)), S = (wmax + P - 1) / P, wpad = S * (uint64_t)P;
-    // tiles of 2^tb positions: the smallest tile leaving at most bm_target_tiles() tiles
-    // (level 0 under P0: its 2^14-position tiles)
+    // tiles of 2^tb positions: from the dense size (a rank's ~8k records), the smallest
+    // leaving at most bm_target_tiles() tiles (level 0 under P0: tb0)
+    const uint64_t np = (uint64_t)(npred * 1.1) + 4096;
+    // an R20 list level with more dense tiles than the reservation scatter takes goes through
+    // the P0 super-tiles too: its list into the super-tiles' slots, then into the dense tiles
+    // (C3 level 1 at one rank: 4.8k tiles of 2^14)
+    P0Bufs pl{};
+    const uint64_t Td = tiles_of(wmax, tbd, 0);
+    const bool lp = L > 0 && c->p0 && bs.list20(L) && Td > bm_target_tiles() && Td <= kBmMaxTiles &&
+                    p0_try_bufs(c, np, (uint64_t)std::ceil(nb), s, &pl, tbd, true);
     const bool l0p = L == 0 && p0;
-    unsigned tb = kBmMinTb;
-    while (!l0p && tb < kBmMaxTb && tiles_of(wmax, tb, 0) > bm_target_tiles()) ++tb;
+    unsigned tb = l0p ? tb0 : tbd;
+    while (!l0p && !lp && tb < kBmMaxTb && tiles_of(wmax, tb, 0) > bm_target_tiles()) ++tb;
     const uint64_t tiles = tiles_of(wmax, tb, 0);
-    // > 2^30 positions: the routed build (same on every rank); P0's level 0 takes up to kBmMaxTiles
-    if (tiles > (l0p ? kBmMaxTiles : kScatterTiles)) return kDistRetry;
+    // > 2^30 positions: the routed build (same on every rank); P0's levels take up to kBmMaxTiles
+    if (tiles > (l0p || lp ? kBmMaxTiles : kScatterTiles)) return kDistRetry;
     if (L > 0) launch_dist_setup(st, L, d.gslot + L, 0, R, P, s);
     launch_bm_range(st, L, s);
     launch_bm_check(st, L, wmax, s);
-    const uint64_t np = (uint64_t)(npred * 1.1) + 4096;
     LevelGeom g{};
     g.tb = tb;
     g.chunk = kTargetChunks;
@@ -1708,16 +1745,28 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     const void* bk = c->bucket;
     uint64_t bcap = c->bucket_cap;
     const unsigned* tc = c->tcnt + (uint64_t)L * kTcntStride;
+    const uint16_t* xs = nullptr;
     if (l0p) {
       if (n_local) launch_p0_scatter(b, pb, p0_fused(blob, pb), s);
       bk = pb.bucket;
       bcap = pb.bucket_cap;
       tc = pb.tcnt;
+      xs = pb.x;
+    } else if (lp) {
+      if (c->debug)
+        std::fprintf(stderr, "[s3imph] rank %d bitmap: level %d through P0 super-tiles (%llu tiles of 2^%u)\n", R, L,
+                     (unsigned long long)tiles, tb);
+      launch_p0_partition_list(L, bs, pl, s);
+      launch_p0_scatter(bs, pl, false, s, L);
+      bk = pl.bucket;
+      bcap = pl.bucket_cap;
+      tc = pl.tcnt;
+      xs = pl.x;
     } else {
       launch_binned_scatter_res(L, bs, g, gsr, s, 0, 0, tiles);
     }
     const bool in20 = l0p || bs.list20(L);  // R20 slots: P0's level 0, or a level whose list is R20
-    launch_bm_tile_mark(L, bk, in20, tc, bcap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, lanes, S, s);
+    launch_bm_tile_mark(L, bk, in20, tc, bcap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, lanes, S, s, xs);
     if (lanes == kBmPlanes) {
       // slice t's planes (2 S words) to rank t; rank q's planes of this rank's slice land at 2 S q
       for (int t = 0; t < P; ++t) {
@@ -1739,9 +1788,19 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     const bool next20 = more && c->l20 && !pos && L + 1 < 32;
     if (next20) bs.l20 |= 1u << (L + 1);
     c->l20_mask = bs.l20;  // dist_classify_stop reads a stop level's list in this format
+    // R20 tiles at the dense size stage their settled keys (each rank's ~8k records a tile)
     launch_bm_tile_settle(L, bk, in20, key_base, tc, bcap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
-                          d.bm_cap_out, c->list[L & 1], d.cap_list, next20, own_slice, s);
+                          d.bm_cap_out, c->list[L & 1], d.cap_list, next20, own_slice, s, tb <= tbd || l0p, xs);
     ev_mark(c, s, L == 0 ? "level0" : "levels");
+    if (c->debug) {  // the level's device status as it ends (a flag's level, for the report)
+      unsigned long long* M = d.h_pinned;
+      HIPCHECK(hipMemcpyAsync(M, &st->status, 4, hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipMemcpyAsync(M + 1, &st->pad0_, 4, hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipStreamSynchronize(s));
+      std::fprintf(stderr, "[s3imph] rank %d bitmap: level %d (tiles 2^%u x %llu%s) status 0x%x site %u\n", R, L, tb,
+                   (unsigned long long)tiles, l0p || lp ? ", P0" : "", (unsigned)(M[0] & 0xffffffffu),
+                   (unsigned)(M[1] & 0xffffffffu));
+    }
     npred *= q;
     if (!more) break;
     nb = nbn;
@@ -1960,7 +2019,7 @@ int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
                                             info, msg)
                       : dist_attempt(c, blob, offsets, pos, n_local, key_base, N, fp_out, pos_out, out_cap, s,
                                      attempt > 1, info, msg);
-    if (rc == kDistRetry && attempt == 0 && dev_env("S3IMPH_DIST_STRICT")) {
+    if (rc == kDistRetry && attempt == 0 && (d.strict || dev_env("S3IMPH_DIST_STRICT"))) {
       *msg = "build MPHF: the bitmap decomposition missed its size bounds (S3IMPH_DIST_STRICT: no fallback)";
       return S3IMPH_ERR_INTERNAL;  // tests use this to prove the bitmap path built the index
     }
@@ -2160,83 +2219,118 @@ bool off16_disabled() {
 }
 
 // Host-memory build through the device path (used by s3imph_build_host and the builder).
+uint64_t mph_bin_bound(uint64_t n) { return 8 * kPartitions + 8 + 8ull * kMaxLevels + 8 * cap_words_for(n); }
+
+// One-shot host build (s3imph_build_host): offsets (as u16 key lengths where they fit) and
+// then the blob cross PCIe, the blob in pieces that the level-0 hash launches wait for one by
+// one (HashFeed), so the hash of arrived keys runs beside the rest of the copy; the build;
+// mph.bin marshalled on a second thread while fp / positions stream back through the pinned
+// workers.  With S3IMPH_DEBUG every phase is timed from entry to return (they sum to it).
 int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
-                    uint64_t n, uint64_t* fp_out, uint64_t* pos_out, std::vector<uint8_t>* mph,
-                    std::string* msg) {
+                    uint64_t n, uint64_t* fp_out, uint64_t* pos_out, MphOut* mph, std::string* msg) {
   using clk = std::chrono::steady_clock;
   const auto te = clk::now();
   s3imph_ctx* c = default_ctx(device, msg);
   if (!c) return S3IMPH_ERR_HIP;
   std::lock_guard<std::mutex> lk(c->mu);
+  struct FeedReset {  // the feed lives on this frame
+    s3imph_ctx* c;
+    ~FeedReset() { c->feed = nullptr; }
+  } feed_reset{c};
   try {
     HIPCHECK(hipSetDevice(c->device));
-    mph->clear();
+    mph->len = 0;
+    if (mph->vec) mph->vec->clear();
     if (n == 0) return S3IMPH_OK;
     const uint64_t b0 = offsets[0], nbytes = offsets[n] - offsets[0];
     const uint64_t bcap = ((nbytes + 7) & ~7ull) + 8;
     if (bcap > c->s_blob_cap) {
+      c->s_blob_cap = 0;
       dalloc(c->s_blob, bcap);
       c->s_blob_cap = bcap;
     }
     if (n > c->s_cap) {
+      c->s_cap = 0;
       dalloc(c->s_offsets, n + 1);
       dalloc(c->s_pos, n);
       dalloc(c->s_fp, n);
       dalloc(c->s_posout, n);
       c->s_cap = n;
     }
+    if (!c->copy_stream) HIPCHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    if (!c->copy_ev) HIPCHECK(hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming));
     hipStream_t s = c->own_stream;
     HIPCHECK(hipStreamSynchronize(s));  // staging buffers may be in use by the last build
     const auto t0 = clk::now();
-    // Offsets cross PCIe as u16 key lengths (2 B per key: C3's 800 MB of u64 offsets become
-    // 200 MB) and are rebuilt on the device by a scan; a key longer than 65535 B sends them
-    // as u32 (blob under 4 GiB, widened on the device) or u64 instead.  Staged in s_fp's
-    // space (the build writes s_fp only later on the same stream); the conversion and pinned
-    // copies run on a second thread beside the blob's runtime copy.
+    // Offsets cross PCIe first, as u16 key lengths (2 B per key: C3's 800 MB of u64 offsets
+    // become 200 MB) rebuilt on the device by a scan; a key longer than 65535 B sends them as
+    // u32 (blob under 4 GiB, widened on the device) or u64 instead.  Staged in s_fp's space
+    // (the build writes s_fp only later on the same stream).
     const bool off32 = nbytes < (1ull << 32);
     uint32_t* tmp32 = reinterpret_cast<uint32_t*>(c->s_fp);
     uint16_t* tmp16 = reinterpret_cast<uint16_t*>(c->s_fp);
     uint64_t* sums16 = c->s_fp + (2 * n + 255) / 256 * 32;  // after the lengths, 256-B aligned
     std::atomic<bool> wide{off16_disabled()};
-    Fail off_err{S3IMPH_OK, ""};
-    std::thread toff([&]() {
-      try {
-        if (!wide.load()) staged_copy(c, true, tmp16, offsets, n * 2, 0, 3, &wide);
-        if (!wide.load()) return;
-        if (off32) staged_copy(c, true, tmp32, offsets, (n + 1) * 4, b0, 1);
-        else staged_copy(c, true, c->s_offsets, offsets, (n + 1) * 8, b0);
-      } catch (const Fail& f) {
-        off_err = f;
-      }
-    });
-    try {
-      staged_copy(c, true, c->s_blob, blob + b0, nbytes);
-    } catch (...) {
-      toff.join();
-      throw;
+    if (!wide.load()) staged_copy(c, true, tmp16, offsets, n * 2, 0, 3, &wide);
+    if (wide.load()) {
+      if (off32) staged_copy(c, true, tmp32, offsets, (n + 1) * 4, b0, 1);
+      else staged_copy(c, true, c->s_offsets, offsets, (n + 1) * 8, b0);
     }
-    toff.join();
-    if (off_err.code != S3IMPH_OK) throw off_err;
     if (!wide.load()) launch_len16_offsets(tmp16, n, sums16, c->s_offsets, s);
     else if (off32) launch_widen32(tmp32, c->s_offsets, n + 1, s);
     if (pos) staged_copy(c, true, c->s_pos, pos, n * 8);
     const auto t1 = clk::now();
+    // The blob, piece by piece as the level-0 hash asks for its keys: a piece is [what is on
+    // the device, the keys' end + 16 B) on the copy stream, and the build stream waits for it
+    uint64_t copied = 0;
+    clk::duration t_copy{};
+    HashFeed feed;
+    feed.ensure = [&](uint64_t k) {
+      const uint64_t want = k >= n ? nbytes : std::min<uint64_t>(nbytes, offsets[k] - b0 + 16);
+      if (want <= copied) return;
+      const auto tc = clk::now();
+      HIPCHECK(hipMemcpyAsync(c->s_blob + copied, blob + b0 + copied, want - copied, hipMemcpyHostToDevice,
+                              c->copy_stream));
+      HIPCHECK(hipEventRecord(c->copy_ev, c->copy_stream));
+      HIPCHECK(hipStreamWaitEvent(s, c->copy_ev, 0));
+      copied = want;
+      t_copy += clk::now() - tc;
+    };
+    c->feed = &feed;
     s3imph_build_info info;
     int rc = build_single(c, c->s_blob, c->s_offsets, pos ? c->s_pos : nullptr, n, c->s_fp, c->s_posout, s,
                           &info, msg);
+    c->feed = nullptr;
+    feed.ensure(n);  // (a path that never hashed: nothing may still be in flight into s_blob)
+    HIPCHECK(hipStreamSynchronize(c->copy_stream));
     if (rc != S3IMPH_OK) return rc;
     const auto t2 = clk::now();
-    // mph.bin (level words D2H into fresh pageable pages: ~9 ms at C3) is marshalled on a
-    // second thread while the output arrays stream back (ctx mutex held by this call)
+    // mph.bin (level words D2H, ~40 MB at C3) is marshalled on a second thread, straight into
+    // its destination, while the output arrays stream back (ctx mutex held by this call)
     std::string mmsg;
     int mrc = S3IMPH_OK;
     clk::time_point t3m;
     std::thread tm([&]() {
       try {
         HIPCHECK(hipSetDevice(c->device));
-        mph->resize(info.mph_bin_len);
+        const uint64_t need = info.mph_bin_len;
+        uint8_t* dst = nullptr;
+        if (mph->vec) {
+          mph->vec->resize(need);
+          dst = mph->vec->data();
+        } else if (mph->alloc) {
+          dst = static_cast<uint8_t*>(std::malloc(need ? need : 1));
+          if (!dst) throw std::bad_alloc();
+          mph->buf = dst;
+        } else {
+          if (mph->cap < need) throw Fail{S3IMPH_ERR_INVALID, "build MPHF: mph.bin buffer of " +
+                                                                   std::to_string(mph->cap) + " B < " +
+                                                                   std::to_string(need) + " B"};
+          dst = mph->buf;
+        }
         uint64_t len = 0;
-        mrc = marshal_locked(c, mph->data(), mph->size(), &len, &mmsg);
+        mrc = marshal_locked(c, dst, need, &len, &mmsg);
+        mph->len = len;
       } catch (const Fail& f) {
         mrc = f.code;
         mmsg = f.msg;
@@ -2263,14 +2357,22 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
     }
     const auto t3 = clk::now();
     tm.join();
-    if (mrc != S3IMPH_OK) *msg = mmsg;
+    if (mrc != S3IMPH_OK) {
+      *msg = mmsg;
+      if (mph->alloc && mph->buf) {
+        std::free(mph->buf);
+        mph->buf = nullptr;
+      }
+    }
     if (c->debug) {
       auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
+      const auto tx = clk::now();
       std::fprintf(stderr,
-                   "[s3imph] host build: entry %.2f, h2d %.2f ms (offsets as %s), build %.2f ms, d2h %.2f ms, "
-                   "marshal ends %.2f ms after the build (beside the d2h), join %.2f ms\n",
+                   "[s3imph] host build: entry %.2f + offsets h2d %.2f (as %s) + blob h2d and build %.2f (blob copy "
+                   "calls %.2f, %d pieces) + d2h %.2f + marshal wait %.2f = %.2f ms (marshal ended %.2f ms after "
+                   "the build)\n",
                    ms(t0 - te), ms(t1 - t0), wide.load() ? (off32 ? "u32" : "u64") : "u16 lengths", ms(t2 - t1),
-                   ms(t3 - t2), ms(t3m - t2), ms(clk::now() - t3));
+                   ms(t_copy), feed.pieces, ms(t3 - t2), ms(tx - t3), ms(tx - te), ms(t3m - t2));
     }
     return mrc;
   } catch (const Fail& f) {
@@ -2280,6 +2382,13 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
     *msg = "out of host memory";
     return S3IMPH_ERR_NOMEM;
   }
+}
+
+int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t n,
+                    uint64_t* fp_out, uint64_t* pos_out, std::vector<uint8_t>* mph, std::string* msg) {
+  MphOut o;
+  o.vec = mph;
+  return build_from_host(device, blob, offsets, pos, n, fp_out, pos_out, &o, msg);
 }
 
 int marshal_locked(s3imph_ctx* c, uint8_t* out, uint64_t cap, uint64_t* len, std::string* msg) {
@@ -2381,6 +2490,8 @@ int s3imph_ctx_destroy(s3imph_ctx* c) {
   for (hipEvent_t e : {c->d.ev_route, c->d.ev_counts, c->d.ev_x})
     if (e) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  if (c->copy_ev) (void)hipEventDestroy(c->copy_ev);
   delete c;
   return S3IMPH_OK;
 }
@@ -2550,9 +2661,11 @@ int s3imph_dist_segments(s3imph_ctx* c, uint64_t* seg, uint64_t cap, uint64_t* c
 }
 
 int s3imph_ctx_set_dist_mode(s3imph_ctx* c, int mode) {
-  if (!c || !c->dist || (mode != S3IMPH_DIST_ROUTE && mode != S3IMPH_DIST_BITMAP)) return S3IMPH_ERR_INVALID;
+  const int m = mode & ~S3IMPH_DIST_STRICT;
+  if (!c || !c->dist || (m != S3IMPH_DIST_ROUTE && m != S3IMPH_DIST_BITMAP)) return S3IMPH_ERR_INVALID;
   std::lock_guard<std::mutex> lk(c->mu);
-  c->d.mode = mode == S3IMPH_DIST_BITMAP ? kDistBitmap : kDistRoute;
+  c->d.mode = m == S3IMPH_DIST_BITMAP ? kDistBitmap : kDistRoute;
+  c->d.strict = (mode & S3IMPH_DIST_STRICT) != 0;
   return S3IMPH_OK;
 }
 
@@ -2688,21 +2801,42 @@ int s3imph_build_host(int device, const uint8_t* blob, const uint64_t* offsets, 
   }
   *mph_bin = nullptr;
   *mph_len = 0;
-  std::vector<uint8_t> mph;
+  MphOut o;
+  o.alloc = true;  // marshalled straight into the returned buffer (no second host copy)
   std::string msg;
-  int rc = build_from_host(device, blob, offsets, pos, n, fp_out, pos_out, &mph, &msg);
+  int rc = build_from_host(device, blob, offsets, pos, n, fp_out, pos_out, &o, &msg);
   if (rc != S3IMPH_OK) {
     set_err(err, errlen, msg);
     return rc;
   }
-  if (!mph.empty()) {
-    *mph_bin = static_cast<uint8_t*>(std::malloc(mph.size()));
-    if (!*mph_bin) return S3IMPH_ERR_NOMEM;
-    std::memcpy(*mph_bin, mph.data(), mph.size());
-    *mph_len = mph.size();
-  }
+  *mph_bin = o.len ? o.buf : nullptr;
+  if (!o.len) std::free(o.buf);
+  *mph_len = o.len;
   return S3IMPH_OK;
 }
+
+int s3imph_build_host_into(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
+                           uint64_t n, uint64_t* fp_out, uint64_t* pos_out, uint8_t* mph_out, uint64_t mph_cap,
+                           uint64_t* mph_len, char* err, size_t errlen) {
+  if (!mph_len || (n && (!blob || !offsets || !fp_out || !pos_out || !mph_out))) {
+    set_err(err, errlen, "invalid argument");
+    return S3IMPH_ERR_INVALID;
+  }
+  *mph_len = 0;
+  MphOut o;
+  o.buf = mph_out;
+  o.cap = mph_cap;
+  std::string msg;
+  int rc = build_from_host(device, blob, offsets, pos, n, fp_out, pos_out, &o, &msg);
+  if (rc != S3IMPH_OK) {
+    set_err(err, errlen, msg);
+    return rc;
+  }
+  *mph_len = o.len;
+  return S3IMPH_OK;
+}
+
+uint64_t s3imph_mph_bin_bound(uint64_t n) { return n ? mph_bin_bound(n) : 0; }
 
 void s3imph_free(void* p) { std::free(p); }
 

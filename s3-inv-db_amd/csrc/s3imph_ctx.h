@@ -99,6 +99,7 @@ struct DistState {
   Rec* bm_out = nullptr;  // this rank's settled (p, fp, pos) triples (the tail's tile kernels own the bucket)
   uint64_t bm_cap_out = 0;
   int mode = kDistRoute;
+  bool strict = false;  // S3IMPH_DIST_STRICT: the bitmap decomposition may not fall back to routing
   // level 0's exchange runs on its own stream, chunk by chunk, beside the next chunk's hash
   hipStream_t xs = nullptr;
   hipEvent_t ev_route = nullptr, ev_counts = nullptr, ev_x = nullptr;
@@ -227,6 +228,8 @@ struct s3imph_ctx {
   unsigned* p0_pcnt = nullptr;  // the fused hash's region fills (kH0GridHost x kMaxRanks)
   s3imph::R20* p0_sup = nullptr;  // the super-tiles' records
   uint64_t p0_sup_cap = 0;
+  uint16_t* p0_x = nullptr;       // bitmap decomposition: in-tile position of each level-0 R20 slot
+  uint64_t p0_x_cap = 0;
   // R20 list levels (BinBuffers::l20): on unless S3IMPH_L20=0 (A/B knob); l20_mask is the
   // last build's mask (classify_stop reads its stop level's list in that format)
   bool l20 = true;
@@ -238,6 +241,9 @@ struct s3imph_ctx {
   bool lds_attr_set = false;
 
   // staging for host-memory builds
+  hipStream_t copy_stream = nullptr;  // the blob's H2D pieces (build_from_host), beside the hash
+  hipEvent_t copy_ev = nullptr;
+  const s3imph::HashFeed* feed = nullptr;  // set for the duration of one host build
   uint8_t* s_blob = nullptr;
   uint64_t s_blob_cap = 0;
   uint64_t *s_offsets = nullptr, *s_pos = nullptr, *s_fp = nullptr, *s_posout = nullptr;

@@ -200,6 +200,16 @@ struct Rec {
   uint64_t k, f, p;
 };
 
+// The host build's key bytes arriving over PCIe (build_from_host): ensure(k) returns once
+// keys [0, k) — and the 16 bytes after them, which the hash's wide loads may touch — are on
+// the device, ordered before anything enqueued on the build stream afterwards.  The level-0
+// hash is then launched in `pieces` launches, each as soon as its keys have arrived, so it
+// runs beside the rest of the copy.
+struct HashFeed {
+  std::function<void(uint64_t)> ensure;
+  int pieces = 16;
+};
+
 struct BinBuffers {
   uint64_t *kh, *fp;                    // level-0 hashes (key order)
   const uint64_t* pos;                  // caller positions (nullable: identity)
@@ -232,6 +242,7 @@ struct BinBuffers {
   // kernel (k_tile_p0 / k_tile_split) reads R20 — 4 bytes less per record on every pass
   unsigned l20 = 0;
   bool list20(int L) const { return L >= 1 && L < 32 && ((l20 >> L) & 1u); }
+  const HashFeed* feed = nullptr;  // level 0's key bytes still arriving (host build), or null
 };
 uint64_t split_scratch_records();  // sub-tile segments of the split big-tile kernel
 
@@ -275,12 +286,21 @@ struct P0Bufs {
   uint64_t bucket_cap = 0;     // R20 records in bucket
   unsigned* tcnt = nullptr;    // tile slot fills (T x kResShards), zeroed before the build
   unsigned long long* flags = nullptr;  // look-back words, one per tile
+  // tile bits: kRegTileMaxBits for k_tile_p0; the bitmap decomposition's level 0 takes 2^tb
+  // positions per tile (up to kBmP0MaxTb), so a rank's share of a tile stays ~8k records
+  unsigned tb = kRegTileMaxBits;
+  uint16_t* x = nullptr;       // bitmap decomposition: each slot's position in its tile (the mark's input)
+  // super-tiles in 2^14-position units (tps tiles of 2^tb): the partition passes cut
+  // (position >> 14) by this, so they need not know tb
+  unsigned tps_sub() const { return tps << (tb - kRegTileMaxBits); }
 };
 void launch_p0_partition(const BinBuffers& b, const P0Bufs& p, hipStream_t s, bool only_skew);
 // level 0's hash with the first partition fused in where it can be (else hash, then partition)
 void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                     const P0Bufs& p, hipStream_t s);
-void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStream_t s);
+// level > 0 (the bitmap decomposition's R20 list levels): after launch_p0_partition_list
+void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStream_t s, int level = 0);
+void launch_p0_partition_list(int level, const BinBuffers& b, const P0Bufs& p, hipStream_t s);
 bool p0_fused(const uint8_t* blob, const P0Bufs& p);  // the hash partitions (aligned blob, S <= kMaxRanks)
 uint64_t p0_region_cap(uint64_t n, unsigned S, unsigned blocks);  // records per (hash block, super-tile) region
 unsigned p0_skew_blocks(int skew_cfg);               // k_hash_skew's grid (its fused partition's blocks)
@@ -357,6 +377,11 @@ void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const Lev
 // most kScatterTiles of them (levels of up to 2^31 positions); the settle kernel keeps 18 B
 // per tile word in LDS: 144 KiB at 2^19 positions.
 constexpr unsigned kBmMinTb = 14, kBmMaxTb = 19;
+// the largest tile whose settle stages its settled keys in LDS and the largest tile of the
+// bitmap level 0 through P0 (2^16 positions: in-tile positions are u16; a rank's ~4k records
+// of a tile at P = 8)
+constexpr unsigned kBmP0MaxTb = 16;
+constexpr uint64_t kBmP0MinTiles = 256;  // the bitmap level 0 takes P0 from this many tiles (one per CU)
 // tiles of a bitmap level: kScatterTiles from the reservation scatter, or up to kBmMaxTiles
 // 2^14-position tiles from the P0 super-tile scatter (level 0)
 constexpr uint64_t kBmMaxTiles = 32768;
@@ -369,9 +394,10 @@ void bm_set_lds_limits();
 void launch_bm_range(LevelState* st, int level, hipStream_t s);
 // bucket: Rec slots, or (r20) the P0 super-tile scatter's R20 slots of 2^14-position tiles
 // (level 0 with identity positions p = pos_base + key index)
+// xs (nullable): each slot's position (P0's level 0, R20 slots)
 void launch_bm_tile_mark(int level, const void* bucket, bool r20, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
                          uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A, int mode,
-                         uint64_t S, hipStream_t s);
+                         uint64_t S, hipStream_t s, const uint16_t* xs = nullptr);
 // the all-to-all's (A, C) plane slices (P of them, 2 S words each) -> this rank's final bits
 void launch_bm_merge(const uint64_t* recv, uint64_t S, int P, uint64_t* out, const LevelState* st, hipStream_t s);
 // This rank's output slice [lo, lo + cnt) of the global outputs (slices of `slice` keys,
@@ -386,15 +412,30 @@ struct OwnSlice {
 void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos_base, const unsigned* tc,
                            uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
                            const uint64_t* A, const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next,
-                           uint64_t next_cap, bool next20, const OwnSlice& os, hipStream_t s);
+                           uint64_t next_cap, bool next20, const OwnSlice& os, hipStream_t s, bool staged = false,
+                           const uint16_t* xs = nullptr);
 void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,
                      LevelState* st, hipStream_t s);
 void launch_bm_tail_copy(const uint64_t* sfp, const uint64_t* spos, uint64_t g0, uint64_t total, uint64_t lo,
                          uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s);
 
 // ---- host-memory builds (s3imph_build.hip, s3imph_multi.hip) -------------------------
+// Where a host build puts mph.bin: a vector (resized to fit), the caller's buffer of cap
+// bytes (reused across calls: no fresh pages), or (alloc) a malloc'd buffer of its exact
+// size that the caller frees (s3imph_build_host's contract).  len is set on success.
+struct MphOut {
+  std::vector<uint8_t>* vec = nullptr;
+  uint8_t* buf = nullptr;
+  uint64_t cap = 0;
+  bool alloc = false;
+  uint64_t len = 0;
+};
+int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t n,
+                    uint64_t* fp_out, uint64_t* pos_out, MphOut* mph, std::string* msg);
 int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t n,
                     uint64_t* fp_out, uint64_t* pos_out, std::vector<uint8_t>* mph, std::string* msg);
+// mph.bin's size bound for n keys (the caller buffer of s3imph_build_host_into)
+uint64_t mph_bin_bound(uint64_t n);
 int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const uint8_t* blob, const uint64_t* offsets,
                           const uint64_t* pos, uint64_t n, uint64_t* fp_out, uint64_t* pos_out,
                           std::vector<uint8_t>* mph, std::string* msg);

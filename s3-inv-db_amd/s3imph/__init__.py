@@ -50,6 +50,7 @@ MULTI_HOST_TRANSPORT = 2  # in-process host-copy collectives instead of RCCL
 MULTI_BITMAP = 4          # the bitmap decomposition of the sharded levels
 DIST_ROUTE = 0            # sharded levels: records routed to their position-range owner
 DIST_BITMAP = 1           # sharded levels: count-lane reduction of the collision bitmap
+DIST_STRICT = 0x100       # or-ed into DIST_BITMAP: no fallback to routing (the build fails instead)
 
 # Every entry point include/s3imph.h declares (checked by tests/test_capi.py).
 EXPORTS = (
@@ -65,7 +66,7 @@ EXPORTS = (
     "s3imph_ctx_load_mph_bin", "s3imph_lookup_device", "s3imph_gen_keys",
     "s3imph_finalize_index_host", "s3imph_finalize_index_device",
     "s3imph_write_manifest", "s3imph_verify_manifest", "s3imph_sha256_file",
-    "s3imph_dev_knobs",
+    "s3imph_dev_knobs", "s3imph_build_host_into", "s3imph_mph_bin_bound",
 )
 
 
@@ -149,6 +150,8 @@ def _load():
         "s3imph_verify_manifest": (i32, [cp, cp, sz]),
         "s3imph_sha256_file": (i32, [cp, i32, cp, cp, sz]),
         "s3imph_dev_knobs": (i32, [i32]),
+        "s3imph_build_host_into": (i32, [i32, vp, vp, vp, u64, vp, vp, vp, u64, P(u64), cp, sz]),
+        "s3imph_mph_bin_bound": (u64, [u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -263,6 +266,35 @@ class StreamingMPHFBuilder:
             self.close()
         except Exception:
             pass
+
+
+def mph_bin_bound(n: int) -> int:
+    """An upper bound on mph.bin's size for n keys (the buffer of build_host_into)."""
+    return int(LIB.s3imph_mph_bin_bound(n))
+
+
+def build_host_into(blob: np.ndarray, offsets: np.ndarray, out: tuple[np.ndarray, np.ndarray],
+                    mph_buf: np.ndarray, pos: np.ndarray | None = None, device: int = 0) -> int:
+    """s3imph_build_host_into: the one-shot host build into caller-owned, reusable outputs —
+    fp / pos arrays (u64, N each) and mph_buf (u8, >= mph_bin_bound(N)); returns mph.bin's
+    length (mph_buf[:len] holds it)."""
+    blob = np.ascontiguousarray(blob, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = len(offsets) - 1
+    if pos is not None:
+        pos = np.ascontiguousarray(pos, np.uint64)
+    fp_out, pos_out = out
+    for a in (fp_out, pos_out):
+        if a.dtype != np.uint64 or len(a) < n or not a.flags.c_contiguous:
+            raise ValueError("out arrays must be contiguous uint64 with at least N entries")
+    if mph_buf.dtype != np.uint8 or not mph_buf.flags.c_contiguous:
+        raise ValueError("mph_buf must be a contiguous uint8 array")
+    ml = ctypes.c_uint64()
+    err = ctypes.create_string_buffer(1024)
+    rc = LIB.s3imph_build_host_into(device, _np_ptr(blob), _np_ptr(offsets), _np_ptr(pos), n, _np_ptr(fp_out),
+                                    _np_ptr(pos_out), _np_ptr(mph_buf), len(mph_buf), ctypes.byref(ml), err, 1024)
+    _check(rc, err)
+    return int(ml.value)
 
 
 def build_host(blob: np.ndarray, offsets: np.ndarray, pos: np.ndarray | None = None, device: int = 0,

@@ -92,9 +92,9 @@ def test_one_gpu_sharded_bitmap_over_rccl(s3, oracle_lib, monkeypatch, switch, n
 @pytest.mark.parametrize("ranks,kind,avg,n", [(1, 0, 24, 17_500_000), (2, 0, 24, 20_000_000),
                                               (3, 1, 0, 18_000_000), (1, 0, 16, 40_000_000)])
 def test_bitmap_level0_through_p0_tiles(s3, oracle_lib, monkeypatch, capfd, ranks, kind, avg, n):
-    """The bitmap decomposition's level 0 through the P0 super-tiles (the whole level's
-    2^14-position tiles > 2048: N > 16.8M keys; 40M: 4883 tiles, more than the reservation
-    scatter's 4096): fused hash partition (skewed lengths:
+    """The bitmap decomposition's level 0 through the P0 super-tiles (tiles of 2^(14 + lg P)
+    positions, a rank's ~8k records each, from 256 of them; 40M at one rank: 4883 tiles, more
+    than the reservation scatter's 4096): fused hash partition (skewed lengths:
     k_hash_skew + the partition pass), super-tile scatter into R20 slots, then the bitmap
     mark / settle over R20 records.  One rank over RCCL, 2-3 over the host transport;
     every rank reports the P0 level 0 (S3IMPH_DEBUG); bit-exact (S3IMPH_DIST_STRICT)."""

@@ -245,6 +245,34 @@ def test_build_host_key_longer_than_u16(s3, oracle_lib):
     assert np.array_equal(gfp, fp) and np.array_equal(gpo, po)
 
 
+def test_build_host_into_reused_buffers_piecewise_hash(s3, oracle_lib):
+    """s3imph_build_host_into: the blob crosses PCIe in pieces and the level-0 hash of each piece
+    is launched as it lands (HashFeed); outputs and mph.bin go to caller buffers reused across
+    calls.  Sets of every level-0 path — P0 (18M keys: the fused partition hash in pieces),
+    the plain pair hash (2M), a skewed set (k_hash_skew after the last piece), a blob at a
+    non-zero offsets[0] with custom positions, a tiny set — each bit-exact vs the oracle, and
+    equal to s3imph_build_host's malloc'd mph.bin."""
+    cap = 18_000_000
+    out = (np.zeros(cap, np.uint64), np.zeros(cap, np.uint64))
+    mph_buf = np.zeros(s3.mph_bin_bound(cap), np.uint8)
+    cases = [(0, 29, 20, 18_000_000, False), (0, 30, 32, 2_000_000, False), (1, 31, 0, 1_500_000, False),
+             (0, 32, 24, 900_000, True), (0, 33, 24, 5, False)]
+    for kind, seed, avg, n, shifted in cases:
+        blob, offs = s3.gen_keys(kind, seed, avg, 0, n)
+        blob = blob[: int(offs[-1])]
+        pos = np.random.default_rng(seed).permutation(n).astype(np.uint64) * np.uint64(3) if shifted else None
+        st, fp, po, mph = oracle_lib.build_mt(blob, offs, pos, threads=16)
+        assert st == 0
+        if shifted:
+            blob = np.concatenate([np.frombuffer(b"xyz", np.uint8), blob])
+            offs = offs + np.uint64(3)
+        ln = s3.build_host_into(blob, offs, out, mph_buf, pos)
+        assert bytes(mph_buf[:ln]) == mph, (kind, n)
+        assert np.array_equal(out[0][:n], fp) and np.array_equal(out[1][:n], po), (kind, n)
+        g = s3.build_host(blob, offs, pos)
+        assert g[2] == mph
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 31, 32, 33, 63, 64, 65, 1000, 4097, 65535, 65536, 65537, 200000])
 def test_sizes_around_boundaries(s3, oracle_lib, ctx, n):
     blob, offs = s3.gen_keys(0, 7, 24, 0, n)

@@ -90,6 +90,46 @@ def test_c3_100m_bit_exact(oracle_lib):
     assert info["big_levels"] >= 5
 
 
+def test_c3_bitmap_one_rank_bit_exact(oracle_lib, monkeypatch, capfd):
+    """The north_star decomposition (per-level collision bitmap) on the bench headline's
+    workload at one rank (RCCL, nranks = 1): level 0 through the P0 super-tiles into 2^14
+    tiles, level 1 (39M records: 4.8k tiles, more than the reservation scatter takes) through
+    its own super-tile pass, the in-tile positions (u16) read by the marks, staged settles;
+    mph.bin, mph_fp and mph_pos byte for byte against the oracle, no fallback
+    (S3IMPH_DIST_STRICT)."""
+    import s3imph
+    monkeypatch.setenv("S3IMPH_DEBUG", "1")
+    monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", str((2 << 20) + 11))  # a fresh context (reads S3IMPH_DEBUG)
+    n = 100_000_000
+    blob, offs = s3imph.gen_keys(0, 42, 64, 0, n)
+    st, fp, po, mph = oracle_lib.build_mt(blob[: int(offs[-1])], offs, threads=16)
+    assert st == 0
+    g = s3imph.build_host(blob, offs, num_gpus=1, flags=s3imph.MULTI_FORCE_SHARDED | s3imph.MULTI_BITMAP)
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+    err = capfd.readouterr().err
+    assert "level 0 through P0 super-tiles" in err and "level 1 through P0 super-tiles" in err, err[-3000:]
+
+
+def test_bitmap_8_ranks_past_p0_single_limit_bit_exact(oracle_lib, monkeypatch, capfd):
+    """the bitmap decomposition at 8 ranks x 40M keys (320M globally, past the
+    268M that P0's 2^14 tiles covered) through the host transport on one GPU: every rank's
+    level 0 goes through P0 with tiles scaled to the rank count (2^16 positions, a rank's
+    ~4k records each); bit-exact against the oracle, no fallback (S3IMPH_DIST_STRICT)."""
+    import s3imph
+    monkeypatch.setenv("S3IMPH_DEBUG", "1")
+    monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", str((2 << 20) + 13))
+    n = 320_000_000
+    blob, offs = s3imph.gen_keys(0, 77, 16, 0, n)
+    st, fp, po, mph = oracle_lib.build_mt(blob[: int(offs[-1])], offs, threads=16)
+    assert st == 0
+    g = s3imph.build_host(blob, offs, devices=[0] * 8, flags=s3imph.MULTI_BITMAP)
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+    err = capfd.readouterr().err
+    assert err.count("level 0 through P0 super-tiles") == 8 and "tiles of 2^16" in err, err[-3000:]
+
+
 def test_c5_one_gpu_share_bit_exact(oracle_lib):
     """One GPU's share of C5 (keys [0, 25M) of the 200M skewed sequence) against the oracle."""
     _bit_exact(oracle_lib, 1, 0, 25_000_000)

@@ -1,6 +1,7 @@
-"""Phase split of the one-shot host-memory build (s3imph_build_host) on C2: H2D, build, D2H
-and marshal times from the library's debug report (--debug: S3IMPH_DEBUG), and the wall time of
-repeated builds.   python tools/host_phase.py [n] [avg] [--debug]"""
+"""Phase split of the one-shot host-memory build (s3imph_build_host_into) on C2 (or [n] [avg]):
+the library's debug report (--debug: S3IMPH_DEBUG) times every phase from entry to return; this
+prints the Python wall of the same calls beside it, so the table sums to the wall.
+    python tools/host_phase.py [n] [avg] [--debug]"""
 import os
 import sys
 import time
@@ -17,7 +18,12 @@ blob, offs = s3imph.gen_keys(0, 42, avg, 0, n)
 blob = blob[: int(offs[-1])].copy()
 import numpy as np  # noqa: E402
 out = (np.zeros(n, np.uint64), np.zeros(n, np.uint64))  # reused, as bench.py's host_e2e
+mph_buf = np.zeros(s3imph.mph_bin_bound(n), np.uint8)
 for i in range(6):
     t = time.perf_counter()
-    s3imph.build_host(blob, offs, out=out)
-    print(f"build_host {i}: {(time.perf_counter() - t) * 1e3:.2f} ms", file=sys.stderr, flush=True)
+    s3imph.build_host_into(blob, offs, out, mph_buf)
+    print(f"build_host_into {i}: {(time.perf_counter() - t) * 1e3:.2f} ms (python wall)", file=sys.stderr, flush=True)
+t = time.perf_counter()
+s3imph.build_host(blob, offs, out=out)
+print(f"build_host (malloc'd mph.bin + bytes copy): {(time.perf_counter() - t) * 1e3:.2f} ms", file=sys.stderr,
+      flush=True)
