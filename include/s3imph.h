@@ -116,6 +116,12 @@ uint64_t s3imph_mph_bin_bound(uint64_t n);
 
 void s3imph_free(void *p);
 
+/* Free the device workspaces the host-memory builds keep between calls (the default context
+ * of every device, the cached per-rank contexts of s3imph_build_host_multi); the next build
+ * allocates again.  Call when no build is running (a pipeline between index builds, or
+ * before handing HBM to something else). */
+int s3imph_release_workspaces(void);
+
 /* Multi-GPU host-memory build for ONE calling process (the reference's caller is one
  * process: indexbuild.go:506-518 -> Build).  num_gpus host threads, one per GPU, each
  * run the sharded rank build of section 4 on a contiguous key shard of about equal key

@@ -373,6 +373,13 @@ struct BmStaged {
   uint64_t f;
   uint32_t i, pg;
 };
+// a settled key bound for another rank's output slice: as Rec {p, f, pos}, or (identity
+// positions) in 16 B — p as an offset in its slice, pos as this rank's key index
+__device__ __forceinline__ void put_out(Rec* out, bool o16, uint64_t i, uint64_t p, uint64_t f, uint64_t pos,
+                                        const OwnSlice& os, unsigned sl, uint64_t pos_base) {
+  if (o16) reinterpret_cast<BmT16*>(out)[i] = BmT16{(uint32_t)(p - (uint64_t)sl * os.slice), (uint32_t)(pos - pos_base), f};
+  else out[i] = Rec{p, f, pos};
+}
 __device__ __forceinline__ void fp_out_own(const OwnSlice& os, uint64_t p, uint64_t f, uint64_t pos, bool& over) {
   const uint64_t o = p - os.lo;
   if (p < os.lo || o >= os.cnt) {
@@ -394,7 +401,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
                                                         const unsigned long long* __restrict__ tbase,
                                                         Rec* __restrict__ out, uint64_t out_cap,
                                                         Rec* __restrict__ next, uint64_t next_cap, OwnSlice os,
-                                                        const uint16_t* __restrict__ xs = nullptr) {
+                                                        const uint16_t* __restrict__ xs, bool o16) {
   static_assert(!kStaged || sizeof(RT) != sizeof(Rec), "staged settles read R20 tiles");
   static_assert(!kX || kStaged, "x positions come with P0's R20 tiles");
   extern __shared__ uint64_t bm_lds64[];
@@ -543,7 +550,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
           } else {
             const uint64_t slot = ob + pa;
             if (slot < out_cap)
-              out[slot] = Rec{gp, r[u].f, r[u].p};
+              put_out(out, o16, slot, gp, r[u].f, r[u].p, os, sl, pos_base);
             else
               over = true;
           }
@@ -566,10 +573,11 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
       for (unsigned i = tid; i < ns; i += kTT) {
         const BmStaged e = stg[i];
         const uint64_t gp = pb + e.pg, p = pos_base + e.i;
-        if ((int)owner_of(gp, os.slice, os.mslice) == os.rank) {
+        const unsigned sl = owner_of(gp, os.slice, os.mslice);
+        if ((int)sl == os.rank) {
           fp_out_own(os, gp, e.f, p, over);
         } else if (ob + i < out_cap) {
-          out[ob + i] = Rec{gp, e.f, p};
+          put_out(out, o16, ob + i, gp, e.f, p, os, sl, pos_base);
         } else {
           over = true;
         }
@@ -595,20 +603,37 @@ __global__ void k_bm_check(LevelState* st, int level, uint64_t wmax) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && st->words[level] > wmax) atomicOr(&st->status, kStBitmapBound);
 }
 
-// Received triples of this rank's output slice [lo, lo + cnt) -> fp_out / pos_out.
-__global__ __launch_bounds__(kBT) void k_bm_place(const Rec* __restrict__ in, uint64_t n, uint64_t lo, uint64_t cnt,
+// Received triples of this rank's output slice [lo, lo + cnt) -> fp_out / pos_out.  k16: 16-B
+// entries (offset in the slice, the sender's key index); tab holds, per sender q, the index of
+// its first entry in `in` (tab[q]) and its key base (tab[P + q]).
+template <bool k16>
+__global__ __launch_bounds__(kBT) void k_bm_place(const void* __restrict__ in_v, uint64_t n, uint64_t lo, uint64_t cnt,
                                                   uint64_t* __restrict__ fp_out, uint64_t* __restrict__ pos_out,
-                                                  LevelState* st) {
+                                                  LevelState* st, const unsigned long long* __restrict__ tab, int P) {
   bool bad = false;
   for (uint64_t i = (uint64_t)blockIdx.x * kBT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBT) {
-    const Rec r = in[i];
-    const uint64_t o = r.k - lo;
-    if (r.k < lo || o >= cnt) {
+    uint64_t p, f, pos;
+    if constexpr (k16) {
+      const BmT16 r = static_cast<const BmT16*>(in_v)[i];
+      int q = 0;  // the sender: the last whose first entry is <= i (P <= 64)
+      for (int x = 1; x < P; ++x)
+        if (tab[x] <= i) q = x;
+      p = lo + r.off;
+      f = r.f;
+      pos = tab[P + q] + r.idx;
+    } else {
+      const Rec r = static_cast<const Rec*>(in_v)[i];
+      p = r.k;
+      f = r.f;
+      pos = r.p;
+    }
+    const uint64_t o = p - lo;
+    if (p < lo || o >= cnt) {
       bad = true;
       continue;
     }
-    fp_out[o] = r.f;
-    pos_out[o] = r.p;
+    fp_out[o] = f;
+    pos_out[o] = pos;
   }
   if (bad) atomicOr(&st->status, kStRank);
 }
@@ -699,7 +724,7 @@ void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos
                            uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
                            const uint64_t* A, const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next,
                            uint64_t next_cap, bool next20, const OwnSlice& os, hipStream_t s, bool staged,
-                           const uint16_t* xs) {
+                           const uint16_t* xs, bool o16) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1024));
   auto go = [&](auto rt, auto stg, auto o20, auto xt) {
     using RT = decltype(rt);
@@ -707,7 +732,7 @@ void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos
     const size_t lds = bm_tile_lds(tb, true) + (kSt ? kBmStage * sizeof(BmStaged) : 0);
     k_bm_tile_settle<RT, kSt, kO, kX><<<grid, kTT, lds, s>>>(level, static_cast<const RT*>(bucket), pos_base, tc,
                                                               bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
-                                                              next_cap, os, xs);
+                                                              next_cap, os, xs, o16);
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
@@ -721,9 +746,11 @@ void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos
   else next20 ? go(Rec{}, F_{}, T_{}, F_{}) : go(Rec{}, F_{}, F_{}, F_{});
 }
 
-void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,
-                     LevelState* st, hipStream_t s) {
-  if (n) k_bm_place<<<grid_for(n, kBT, 8192), kBT, 0, s>>>(in, n, lo, cnt, fp_out, pos_out, st);
+void launch_bm_place(const void* in, bool k16, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out,
+                     uint64_t* pos_out, LevelState* st, const unsigned long long* tab, int P, hipStream_t s) {
+  if (!n) return;
+  if (k16) k_bm_place<true><<<grid_for(n, kBT, 8192), kBT, 0, s>>>(in, n, lo, cnt, fp_out, pos_out, st, tab, P);
+  else k_bm_place<false><<<grid_for(n, kBT, 8192), kBT, 0, s>>>(in, n, lo, cnt, fp_out, pos_out, st, tab, P);
 }
 
 void launch_bm_tail_copy(const uint64_t* sfp, const uint64_t* spos, uint64_t g0, uint64_t total, uint64_t lo,

@@ -90,7 +90,8 @@ void ensure_workspace(s3imph_ctx* c, uint64_t n) {
   dalloc(c->tcnt, (uint64_t)kResLevels * kTcntStride);
   alloc_common(c, cap);
   dalloc(c->bits, c->cap_words);
-  dalloc(c->rank_base, 2 * c->cap_words);  // rank directory: (word, rank) pairs
+  dfree(c->rank_base);  // the Lookup rank directory: made on the first lookup (ensure_rank_dir)
+  c->rank_base_cap = 0;
   c->cap_blocks = (c->cap_words + 2047) / 2048 + 1;
   dalloc(c->block_sums, c->cap_blocks);
   c->cap_keys = cap;
@@ -103,6 +104,8 @@ void free_workspace(s3imph_ctx* c) {
   dfree(c->mid);
   dfree(c->split);
   dfree(c->kh); dfree(c->fp); dfree(c->bits); dfree(c->rank_base);
+  c->rank_base_cap = 0;
+  c->bucket_cap = 0;
   dfree(c->block_sums); dfree(c->d_st);
   dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
   dfree(c->tcnt);
@@ -115,6 +118,7 @@ void free_workspace(s3imph_ctx* c) {
   if (c->h_st) (void)hipHostFree(c->h_st);
   c->h_st = nullptr;
   dfree(c->s_blob); dfree(c->s_offsets); dfree(c->s_pos); dfree(c->s_fp); dfree(c->s_posout);
+  c->s_blob_cap = c->s_cap = c->s_pos_cap = 0;
   for (int w = 0; w < kStageWorkers; ++w) {
     for (int b = 0; b < 2; ++b) {
       if (c->stager.pin[w][b]) (void)hipHostFree(c->stager.pin[w][b]);
@@ -1012,11 +1016,11 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
   const uint64_t caps = capl + 4096ull * P;
   const uint64_t stagew = level_words(std::max<uint64_t>(n_global, 1)) + 2ull * P + 64;
   const uint64_t capw = cap_words_for(std::max<uint64_t>(n_global, 1024)) + stagew;
-  if (capl <= d.cap_list && caps <= d.cap_send && stagew <= d.cap_stage_words && capw <= c->cap_words && c->hist)
-    return;
+  (void)caps;
+  if (capl <= d.cap_list && stagew <= d.cap_stage_words && capw <= c->cap_words && c->hist) return;
   // the bucket gets 1.3x the list capacity: reservation slots need headroom over the mean fill
   const uint64_t capb = capl + capl * 3 / 10;
-  d.cap_list = d.cap_send = d.cap_stage_words = 0;  // set again once every buffer is in place
+  d.cap_list = d.cap_stage_words = 0;  // set again once every buffer is in place
   c->cap_keys = 0;
   dalloc(c->bucket, capb);
   dalloc(c->list[0], capl);
@@ -1034,13 +1038,14 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
   dalloc(c->tcnt, (uint64_t)kResLevels * kTcntStride);
   c->cap_words = capw;
   dalloc(c->bits, capw);
-  dalloc(c->rank_base, 2 * capw);  // rank directory: (word, rank) pairs
+  dfree(c->rank_base);  // the Lookup rank directory: made on the first lookup (ensure_rank_dir)
+  c->rank_base_cap = 0;
   c->cap_blocks = (capw + 2047) / 2048 + 1;
   dalloc(c->block_sums, c->cap_blocks);
-  dalloc(d.send, caps);
+  // d.send (the routed build's send regions, the replicated gather's staging) is made by
+  // the paths that use it (ensure_send): the bitmap decomposition needs only the gather's
   dalloc(d.stage_bits, stagew);
   d.cap_list = capl;
-  d.cap_send = caps;
   d.cap_stage_words = stagew;
 }
 
@@ -1242,6 +1247,14 @@ int dist_attempt(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
   DistState& d = c->d;
   Comm& cm = *d.comm;
   const int P = d.nranks, R = d.rank;
+  {  // the send regions (ensure_dist_workspace leaves them to the routed build)
+    const uint64_t caps = d.cap_list + 4096ull * P;
+    if (caps > d.cap_send) {
+      d.cap_send = 0;
+      dalloc(d.send, caps);
+      d.cap_send = caps;
+    }
+  }
   LevelState* st = c->d_st;
   const BinBuffers b = make_bufs(c, nullptr, fp_out, pos_out, s);
   // Distributed levels keep their input in list[1] and their collided records in list[0]:
@@ -1597,7 +1610,7 @@ void ensure_bm_workspace(s3imph_ctx* c, uint64_t N) {
   dalloc(d.bm_a, wpad);
   dalloc(d.bm_g, wpad);
   dalloc(d.bm_dec, S);
-  dalloc(d.bm_lanes, 64 * wpad);  // count bytes, or the (A, C) planes in 16 B per word
+  dalloc(d.bm_lanes, (c->bm_counts ? 64 : 16) * wpad);  // count bytes (64 per word), or the (A, C) planes (16)
   dalloc(d.bm_slice, 64 * S);
   dalloc(d.bm_recv, 16 * wpad);   // the planes' all-to-all: P slices of 2 S words
   if (!d.bm_tsum) dalloc(d.bm_tsum, kBmMaxTiles);
@@ -1696,6 +1709,10 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     if (rc != S3IMPH_OK) return rc;
   }
   const OwnSlice own_slice{lo, mine, slice, level_magic(slice), R, P, fp_out, pos_out, d.scnt};
+  // with identity positions the settled keys bound for other slices cross as 16-B entries
+  // (offset in the slice, this rank's key index, fp) instead of 24-B (p, fp, pos) records
+  const bool out16 = !pos;
+  const uint64_t es = out16 ? sizeof(BmT16) : sizeof(Rec);
   HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
   HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kMaxDistLevels * kTcntStride * sizeof(unsigned), s));
   // The level's records go through the reservation scatter into tiles over the level's
@@ -1790,7 +1807,8 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     c->l20_mask = bs.l20;  // dist_classify_stop reads a stop level's list in this format
     // R20 tiles at the dense size stage their settled keys (each rank's ~8k records a tile)
     launch_bm_tile_settle(L, bk, in20, key_base, tc, bcap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
-                          d.bm_cap_out, c->list[L & 1], d.cap_list, next20, own_slice, s, tb <= tbd || l0p, xs);
+                          out16 ? d.bm_cap_out * sizeof(Rec) / sizeof(BmT16) : d.bm_cap_out, c->list[L & 1], d.cap_list,
+                          next20, own_slice, s, tb <= tbd || l0p, xs, out16);
     ev_mark(c, s, L == 0 ? "level0" : "levels");
     if (c->debug) {  // the level's device status as it ends (a flag's level, for the report)
       unsigned long long* M = d.h_pinned;
@@ -1915,19 +1933,24 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   // ---- settled triples to the owners of their output slices: this rank's settled list is
   // sorted by p, so its run for slice t (d.scnt[t] records, counted by the settle) goes to
   // rank t as it lies; the own run is a hole (those keys were placed by the settle)
+  launch_set_u64(d.scnt + P, key_base, s);  // (scnt[P] is free here) every rank's key base, for the 16-B entries
   cm.allgather(d.scnt, d.mat, 8ull * (P + 1), s);
   HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
   uint64_t acc = 0, got = 0, sent = 0;
+  unsigned long long* tab_h = d.h_pinned + kSmallWords + 2 * 16;  // sender table (after dist_agree's words)
+  std::vector<unsigned long long> tab(2 * (size_t)P);
   for (int t = 0; t < P; ++t) {
     const uint64_t cnt_t = M[(uint64_t)R * (P + 1) + t];
-    soff[t] = sent * sizeof(Rec);
-    sbytes[t] = t == R ? 0 : cnt_t * sizeof(Rec);
+    soff[t] = sent * es;
+    sbytes[t] = t == R ? 0 : cnt_t * es;
     sent += cnt_t;
     const uint64_t in_t = M[(uint64_t)t * (P + 1) + R];
     roff[t] = acc;
-    rbytes[t] = t == R ? 0 : in_t * sizeof(Rec);
+    rbytes[t] = t == R ? 0 : in_t * es;
+    tab[t] = acc / es;
+    tab[P + t] = M[(uint64_t)t * (P + 1) + P];
     acc += rbytes[t];
     if (t != R) got += in_t;
   }
@@ -1948,7 +1971,13 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   }
   Rec* recv = c->list[Ls & 1];
   if (P > 1) cm.alltoallv(out, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), s);
-  launch_bm_place(recv, got, lo, mine, fp_out, pos_out, st, s);
+  unsigned long long* tab_d = d.small + 6144;  // (d.small: gathers below 4096, out_cnt at 4096)
+  if (got && out16) {
+    HIPCHECK(hipStreamSynchronize(s));  // tab_h is reused by the next build
+    std::copy(tab.begin(), tab.end(), tab_h);
+    HIPCHECK(hipMemcpyAsync(tab_d, tab_h, 16ull * P, hipMemcpyHostToDevice, s));
+  }
+  launch_bm_place(recv, out16, got, lo, mine, fp_out, pos_out, st, tab_d, P, s);
   launch_bm_tail_copy(c->kh, c->fp, g0, total, lo, mine, fp_out, pos_out, s);
   ev_mark(c, s, "exchange_out");
   HIPCHECK(hipMemcpyAsync(M, &st->status, 4, hipMemcpyDeviceToHost, s));
@@ -2219,6 +2248,14 @@ bool off16_disabled() {
 }
 
 // Host-memory build through the device path (used by s3imph_build_host and the builder).
+// the caller positions' staging (host builds with pos != NULL only)
+void ensure_s_pos(s3imph_ctx* c, uint64_t n) {
+  if (n <= c->s_pos_cap && c->s_pos) return;
+  c->s_pos_cap = 0;
+  dalloc(c->s_pos, n);
+  c->s_pos_cap = n;
+}
+
 uint64_t mph_bin_bound(uint64_t n) { return 8 * kPartitions + 8 + 8ull * kMaxLevels + 8 * cap_words_for(n); }
 
 // One-shot host build (s3imph_build_host): offsets (as u16 key lengths where they fit) and
@@ -2252,11 +2289,11 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
     if (n > c->s_cap) {
       c->s_cap = 0;
       dalloc(c->s_offsets, n + 1);
-      dalloc(c->s_pos, n);
       dalloc(c->s_fp, n);
       dalloc(c->s_posout, n);
       c->s_cap = n;
     }
+    if (pos) ensure_s_pos(c, n);
     if (!c->copy_stream) HIPCHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     if (!c->copy_ev) HIPCHECK(hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming));
     hipStream_t s = c->own_stream;
@@ -2734,7 +2771,8 @@ int s3imph_ctx_load_mph_bin(s3imph_ctx* c, const uint8_t* mph_bin, uint64_t len)
     const uint64_t need = std::max<uint64_t>(words.size(), 1);
     if (need > c->cap_words || !c->bits) {
       dalloc(c->bits, need);
-      dalloc(c->rank_base, 2 * need);
+      dfree(c->rank_base);
+      c->rank_base_cap = 0;
       c->cap_blocks = (need + 2047) / 2048 + 1;
       dalloc(c->block_sums, c->cap_blocks);
       c->cap_words = need;
@@ -2778,6 +2816,11 @@ int s3imph_lookup_device(s3imph_ctx* c, const uint8_t* d_blob, const uint64_t* d
       HIPCHECK(hipMemsetAsync(d_result, 0xff, n * 8, s));
     } else {
       if (!c->rank_valid) {  // word-level rank prefix, built on first lookup after a build
+        if (c->rank_base_cap < 2 * c->cap_words) {  // (word, rank) pairs
+          c->rank_base_cap = 0;
+          dalloc(c->rank_base, 2 * c->cap_words);
+          c->rank_base_cap = 2 * c->cap_words;
+        }
         launch_rank_scan(c->bits, c->cap_words, c->rank_base, c->block_sums, c->cap_blocks, c->d_st, s);
         c->rank_valid = true;
       }
@@ -2837,6 +2880,22 @@ int s3imph_build_host_into(int device, const uint8_t* blob, const uint64_t* offs
 }
 
 uint64_t s3imph_mph_bin_bound(uint64_t n) { return n ? mph_bin_bound(n) : 0; }
+
+int s3imph_release_workspaces(void) {
+  release_multi_sets();
+  std::lock_guard<std::mutex> glk(g_default_mu);
+  for (s3imph_ctx* c : g_default) {
+    if (!c) continue;
+    std::lock_guard<std::mutex> lk(c->mu);
+    (void)hipSetDevice(c->device);
+    if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+    free_workspace(c);
+    fin_scratch_free(c);
+    c->have_build = false;
+    c->rank_valid = false;
+  }
+  return S3IMPH_OK;
+}
 
 void s3imph_free(void* p) { std::free(p); }
 

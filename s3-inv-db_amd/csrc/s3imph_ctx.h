@@ -193,6 +193,7 @@ struct s3imph_ctx {
 
   uint64_t cap_keys = 0, cap_words = 0, cap_blocks = 0;
   uint64_t *kh = nullptr, *fp = nullptr, *bits = nullptr, *rank_base = nullptr;
+  uint64_t rank_base_cap = 0;  // words of rank_base (the Lookup directory, made on first lookup)
   unsigned long long* block_sums = nullptr;
   LevelState* d_st = nullptr;
   LevelState* h_st = nullptr;
@@ -248,6 +249,7 @@ struct s3imph_ctx {
   uint64_t s_blob_cap = 0;
   uint64_t *s_offsets = nullptr, *s_pos = nullptr, *s_fp = nullptr, *s_posout = nullptr;
   uint64_t s_cap = 0;
+  uint64_t s_pos_cap = 0;  // s_pos is made only for builds with caller positions
   Stager stager;
 
   bool have_build = false;
@@ -291,6 +293,8 @@ void launch_len16_offsets(const uint16_t* len, uint64_t n, uint64_t* sums, uint6
 // FNV-1a of keys [0, n) into out (the error path's recount of the original key hashes)
 void launch_key_hashes(const uint8_t* blob, const uint64_t* offsets, uint64_t n, uint64_t* out, hipStream_t s);
 int marshal_locked(s3imph_ctx* c, uint8_t* out, uint64_t cap, uint64_t* len, std::string* msg);
+void ensure_s_pos(s3imph_ctx* c, uint64_t n);
+void release_multi_sets();  // s3imph_multi.hip
 // Index finalize arrays (s3imph_finalize.hip): device pass over keys in HBM, and the
 // host-memory form that writes the five files.
 int finalize_device(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint32_t* depths, uint64_t n,

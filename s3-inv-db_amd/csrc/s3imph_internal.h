@@ -413,9 +413,16 @@ void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos
                            uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
                            const uint64_t* A, const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next,
                            uint64_t next_cap, bool next20, const OwnSlice& os, hipStream_t s, bool staged = false,
-                           const uint16_t* xs = nullptr);
-void launch_bm_place(const Rec* in, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out,
-                     LevelState* st, hipStream_t s);
+                           const uint16_t* xs = nullptr, bool o16 = false);
+// a settled key crossing to its output slice's owner with identity positions (16 B instead
+// of a 24-B Rec): p - the slice's first p, the sending rank's key index, the fingerprint
+struct BmT16 {
+  uint32_t off, idx;
+  uint64_t f;
+};
+// k16: `in` holds BmT16 entries, tab the senders' first entries (P) and key bases (P)
+void launch_bm_place(const void* in, bool k16, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out,
+                     uint64_t* pos_out, LevelState* st, const unsigned long long* tab, int P, hipStream_t s);
 void launch_bm_tail_copy(const uint64_t* sfp, const uint64_t* spos, uint64_t g0, uint64_t total, uint64_t lo,
                          uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s);
 

@@ -35,6 +35,13 @@ namespace {
 // leave their barrier with an error instead of waiting forever.
 struct ThreadHub {
   int P = 1;
+  // serial (S3IMPH_HOST_SERIAL, a measurement mode): the ranks' device work never overlaps —
+  // a rank holds `token` from the end of one collective to the point the next one has synced
+  // its stream, so each kernel of a rank runs alone on the shared GPU and its trace duration
+  // is that rank's device time (the P = 8 geometry on one GPU)
+  bool serial = false;
+  std::mutex token;
+  std::vector<char> held;
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0;
@@ -43,7 +50,17 @@ struct ThreadHub {
   std::vector<std::vector<uint8_t>> slot;  // per rank
   std::vector<std::vector<uint64_t>> soff, sbytes;
 
-  explicit ThreadHub(int p) : P(p), slot(p), soff(p), sbytes(p) {}
+  explicit ThreadHub(int p) : P(p), held(p, 0), slot(p), soff(p), sbytes(p) {}
+  void seg_begin(int r) {  // this rank's device work starts
+    if (!serial || held[r]) return;
+    token.lock();
+    held[r] = 1;
+  }
+  void seg_end(int r) {  // ... and has completed (its stream synchronised)
+    if (!serial || !held[r]) return;
+    held[r] = 0;
+    token.unlock();
+  }
   void reset() {
     std::lock_guard<std::mutex> lk(mu);
     arrived = 0;
@@ -82,16 +99,19 @@ struct ThreadComm final : Comm {
     mine.resize(bytes + 1);
     d2h(mine.data(), d_send, bytes, s);
     HIPCHECK(hipStreamSynchronize(s));
+    hub->seg_end(rank);
     hub->barrier();
     for (int r = 0; r < nranks; ++r) h2d(static_cast<uint8_t*>(d_recv) + (uint64_t)r * bytes, hub->slot[r].data(), bytes, s);
     HIPCHECK(hipStreamSynchronize(s));
     hub->barrier();  // every rank has read the slots before they are reused
+    hub->seg_begin(rank);
   }
   void reduce_scatter_u8(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
     auto& mine = hub->slot[rank];
     mine.resize(bytes * nranks + 1);
     d2h(mine.data(), d_send, bytes * nranks, s);
     HIPCHECK(hipStreamSynchronize(s));
+    hub->seg_end(rank);
     hub->barrier();
     std::vector<uint8_t> sum(bytes + 1, 0);
     for (int r = 0; r < nranks; ++r) {
@@ -101,6 +121,7 @@ struct ThreadComm final : Comm {
     h2d(d_recv, sum.data(), bytes, s);
     HIPCHECK(hipStreamSynchronize(s));
     hub->barrier();
+    hub->seg_begin(rank);
   }
   void allreduce_u64(const unsigned long long* d_in, unsigned long long* d_out, uint64_t count,
                      hipStream_t s) override {
@@ -109,6 +130,7 @@ struct ThreadComm final : Comm {
     mine.resize(bytes + 1);
     d2h(mine.data(), d_in, bytes, s);
     HIPCHECK(hipStreamSynchronize(s));
+    hub->seg_end(rank);
     hub->barrier();
     std::vector<unsigned long long> sum(count, 0);
     for (int r = 0; r < nranks; ++r)
@@ -120,6 +142,7 @@ struct ThreadComm final : Comm {
     h2d(d_out, sum.data(), bytes, s);
     HIPCHECK(hipStreamSynchronize(s));
     hub->barrier();
+    hub->seg_begin(rank);
   }
   void alltoallv(const void* d_send, const uint64_t* soff, const uint64_t* sbytes, void* d_recv,
                  const uint64_t* roff, const uint64_t* rbytes, hipStream_t s) override {
@@ -138,6 +161,7 @@ struct ThreadComm final : Comm {
     for (int q = 0; q < nranks; ++q)
       d2h(mine.data() + po[q], static_cast<const uint8_t*>(d_send) + soff[q], sbytes[q], s);
     HIPCHECK(hipStreamSynchronize(s));
+    hub->seg_end(rank);
     hub->barrier();
     for (int q = 0; q < nranks; ++q) {
       if (hub->sbytes[q][rank] != rbytes[q]) throw Fail{S3IMPH_ERR_INTERNAL, "alltoallv: size mismatch"};
@@ -145,6 +169,7 @@ struct ThreadComm final : Comm {
     }
     HIPCHECK(hipStreamSynchronize(s));
     hub->barrier();
+    hub->seg_begin(rank);
   }
 };
 
@@ -158,6 +183,7 @@ struct MultiCtx {
   std::mutex mu;
   std::mutex abort_mu;
   bool aborted = false;  // a rank failed alone: the transport was torn down, the set is dropped
+  bool released = false;  // its contexts were freed (release_sets): a caller takes a fresh set
   // Unblock every rank: the host hub wakes its barrier waiters with an error; RCCL
   // communicators are aborted (their pending kernels exit, so peers blocked in a stream
   // sync return) and cannot be reused.
@@ -175,12 +201,47 @@ std::mutex g_multi_mu;
 std::map<std::tuple<std::vector<int>, bool, uint64_t>, std::unique_ptr<MultiCtx>> g_multi;
 std::vector<std::unique_ptr<MultiCtx>> g_retired;  // aborted sets (see build_from_host_multi)
 
+// Free the contexts (workspaces, communicators) of sets already taken out of g_multi, once no
+// build holds them; the emptied sets stay allocated (g_retired) for callers that still hold a
+// pointer and will see `released`.
+void release_sets(std::vector<std::unique_ptr<MultiCtx>> sets) {
+  for (auto& mc : sets) {
+    {
+      std::lock_guard<std::mutex> lk(mc->mu);
+      for (s3imph_ctx* c : mc->ctx) s3imph_ctx_destroy(c);
+      mc->ctx.clear();
+      mc->released = true;
+    }
+    std::lock_guard<std::mutex> glk(g_multi_mu);
+    g_retired.push_back(std::move(mc));
+  }
+}
+
+// The cached set for (devs, transport, S3IMPH_DIST_SWITCH); another cached set over the same
+// devices (a different switch: tests) is released first, so sets never pile up in HBM.
 MultiCtx* multi_ctx(const std::vector<int>& devs, bool host_transport, std::string* msg) {
   uint64_t sw = kDistSwitchKeysDefault;  // contexts read S3IMPH_DIST_SWITCH when made
   if (const char* e = dev_env("S3IMPH_DIST_SWITCH")) sw = std::strtoull(e, nullptr, 10);
-  std::lock_guard<std::mutex> lk(g_multi_mu);
   auto key = std::make_tuple(devs, host_transport, sw);
-  auto it = g_multi.find(key);
+  {
+    std::vector<std::unique_ptr<MultiCtx>> stale;
+    {
+      std::lock_guard<std::mutex> lk(g_multi_mu);
+      auto it = g_multi.find(key);
+      if (it != g_multi.end()) return it->second.get();
+      for (auto jt = g_multi.begin(); jt != g_multi.end();) {
+        if (std::get<0>(jt->first) == devs && std::get<1>(jt->first) == host_transport) {
+          stale.push_back(std::move(jt->second));
+          jt = g_multi.erase(jt);
+        } else {
+          ++jt;
+        }
+      }
+    }
+    release_sets(std::move(stale));
+  }
+  std::lock_guard<std::mutex> lk(g_multi_mu);
+  auto it = g_multi.find(key);  // (another caller may have made it meanwhile)
   if (it != g_multi.end()) return it->second.get();
   auto mc = std::make_unique<MultiCtx>();
   mc->devs = devs;
@@ -246,17 +307,19 @@ int rank_build(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
   const uint64_t cap = dist_out_cap(c, n);
   const uint64_t bcap = ((nbytes + 7) & ~7ull) + 8;
   if (bcap > c->s_blob_cap) {
+    c->s_blob_cap = 0;
     dalloc(c->s_blob, bcap);
     c->s_blob_cap = bcap;
   }
   const uint64_t need = std::max(cap, nl + 1);
   if (need > c->s_cap) {  // s_cap keys: s_offsets holds s_cap + 1 words (as build_from_host's)
+    c->s_cap = 0;
     dalloc(c->s_offsets, need + 1);
-    dalloc(c->s_pos, need);
     dalloc(c->s_fp, need);
     dalloc(c->s_posout, need);
     c->s_cap = need;
   }
+  if (pos) ensure_s_pos(c, need);
   hipStream_t s = c->own_stream;
   HIPCHECK(hipStreamSynchronize(s));
   staged_copy(c, true, c->s_blob, blob + b0, nbytes);
@@ -318,14 +381,23 @@ int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const ui
   mph->clear();
   if (n == 0) return S3IMPH_OK;
   try {
-    MultiCtx* mc = multi_ctx(devs, repeated || (flags & S3IMPH_MULTI_HOST_TRANSPORT), msg);
-    if (!mc) return S3IMPH_ERR_RCCL;
-    std::lock_guard<std::mutex> lk(mc->mu);
+    MultiCtx* mc = nullptr;
+    std::unique_lock<std::mutex> lk;
+    for (;;) {  // a set released between the lookup and its lock: take a fresh one
+      mc = multi_ctx(devs, repeated || (flags & S3IMPH_MULTI_HOST_TRANSPORT), msg);
+      if (!mc) return S3IMPH_ERR_RCCL;
+      lk = std::unique_lock<std::mutex>(mc->mu);
+      if (!mc->released) break;
+      lk.unlock();
+    }
     if (mc->aborted) {
       *msg = "build MPHF: the multi-GPU set was torn down by a failed build; call again";
       return S3IMPH_ERR_RCCL;
     }
-    if (mc->hub) mc->hub->reset();
+    if (mc->hub) {
+      mc->hub->reset();
+      mc->hub->serial = dev_env("S3IMPH_HOST_SERIAL") != nullptr;
+    }
     {
       const char* em = std::getenv("S3IMPH_DIST_MODE");
       const bool bitmap = (flags & S3IMPH_MULTI_BITMAP) || (em && std::strcmp(em, "bitmap") == 0);
@@ -342,6 +414,7 @@ int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const ui
     std::vector<std::string> msgs(P);
     auto work = [&](int r) {
       try {
+        if (mc->hub) mc->hub->seg_begin(r);
         rcs[r] = rank_build(mc->ctx[r], blob, offsets, pos, n, cuts[r], cuts[r + 1], fp_out, pos_out, mph, &msgs[r]);
       } catch (const Fail& f) {
         rcs[r] = f.code;
@@ -350,6 +423,7 @@ int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const ui
         rcs[r] = S3IMPH_ERR_NOMEM;
         msgs[r] = "out of host memory";
       }
+      if (mc->hub) mc->hub->seg_end(r);
       // Key-set failures (duplicate or zero key hashes, too many levels) are decided from
       // all-reduced counts, so every rank returns them at the same point.  Anything else
       // (HIP / RCCL errors, allocation failures, internal checks) may leave the peers inside
@@ -392,6 +466,17 @@ int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const ui
     *msg = f.msg;
     return f.code;
   }
+}
+
+// every cached multi-GPU set (s3imph_release_workspaces)
+void release_multi_sets() {
+  std::vector<std::unique_ptr<MultiCtx>> all;
+  {
+    std::lock_guard<std::mutex> lk(g_multi_mu);
+    for (auto& kv : g_multi) all.push_back(std::move(kv.second));
+    g_multi.clear();
+  }
+  release_sets(std::move(all));
 }
 
 }  // namespace s3imph

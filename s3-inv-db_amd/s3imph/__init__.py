@@ -66,7 +66,7 @@ EXPORTS = (
     "s3imph_ctx_load_mph_bin", "s3imph_lookup_device", "s3imph_gen_keys",
     "s3imph_finalize_index_host", "s3imph_finalize_index_device",
     "s3imph_write_manifest", "s3imph_verify_manifest", "s3imph_sha256_file",
-    "s3imph_dev_knobs", "s3imph_build_host_into", "s3imph_mph_bin_bound",
+    "s3imph_dev_knobs", "s3imph_build_host_into", "s3imph_mph_bin_bound", "s3imph_release_workspaces",
 )
 
 
@@ -152,6 +152,7 @@ def _load():
         "s3imph_dev_knobs": (i32, [i32]),
         "s3imph_build_host_into": (i32, [i32, vp, vp, vp, u64, vp, vp, vp, u64, P(u64), cp, sz]),
         "s3imph_mph_bin_bound": (u64, [u64]),
+        "s3imph_release_workspaces": (i32, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -266,6 +267,11 @@ class StreamingMPHFBuilder:
             self.close()
         except Exception:
             pass
+
+
+def release_workspaces() -> None:
+    """Free the device workspaces cached by the host-memory builds (s3imph_release_workspaces)."""
+    _check(LIB.s3imph_release_workspaces(), None, "release_workspaces")
 
 
 def mph_bin_bound(n: int) -> int:

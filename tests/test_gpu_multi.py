@@ -62,6 +62,37 @@ def test_thread_per_rank_shared_gpu(s3, oracle_lib, monkeypatch, ranks, kind, av
     assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
 
 
+@pytest.mark.parametrize("bitmap", [False, True])
+def test_thread_per_rank_serialised_device_work(s3, oracle_lib, monkeypatch, bitmap):
+    """S3IMPH_HOST_SERIAL (the measurement mode of tools/p8_geometry.py): the host transport
+    hands the GPU to one rank at a time between collectives; 4 ranks, both decompositions,
+    bit-exact, twice (the token is released at the end of every build)."""
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", "15001")
+    monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
+    monkeypatch.setenv("S3IMPH_HOST_SERIAL", "1")
+    blob, offs = s3.gen_keys(0, 14, 24, 0, 1_200_000)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    for _ in range(2):
+        g = s3.build_host(blob, offs, devices=[0] * 4, flags=s3.MULTI_BITMAP if bitmap else 0)
+        assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+
+
+def test_release_workspaces_then_build_again(s3, oracle_lib, monkeypatch):
+    """s3imph_release_workspaces frees the cached default contexts and multi-GPU sets; the next
+    builds (single, 3 ranks, and a Lookup-free rebuild on the same default context) allocate
+    again and stay bit-exact."""
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", "15002")
+    blob, offs = s3.gen_keys(0, 15, 24, 0, 700_000)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    for devices in (None, [0, 0, 0]):
+        g = s3.build_host(blob, offs, devices=devices, flags=s3.MULTI_BITMAP if devices else 0)
+        assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+        s3.release_workspaces()
+        g = s3.build_host(blob, offs, devices=devices, flags=s3.MULTI_BITMAP if devices else 0)
+        assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+    s3.release_workspaces()
+
+
 def test_thread_per_rank_64_ranks_bitmap(s3, oracle_lib, monkeypatch):
     """kMaxRanks = 64 ranks (the API's limit) on the bitmap decomposition: 64 output
     slices counted by the settle (the last slice's count included), the (A, C) plane

@@ -36,6 +36,16 @@ def _dev(a: np.ndarray):
     return torch.from_numpy(a).to("cuda")
 
 
+@pytest.fixture(autouse=True)
+def _release_cached_workspaces():
+    """These builds take most of the HBM: free what earlier host builds keep cached (the default
+    contexts, the multi-GPU sets of up to 8 ranks) before and after each."""
+    import s3imph
+    s3imph.release_workspaces()
+    yield
+    s3imph.release_workspaces()
+
+
 def _properties(n, d_blob, d_offs, min_big_levels):
     """Size-independent checks of one full build: mph_pos is a permutation of [0, N), and
     every member looks itself up (VerifyMPHF, mphf.go:372-393)."""
