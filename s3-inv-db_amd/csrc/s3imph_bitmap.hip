@@ -149,6 +149,11 @@ __global__ __launch_bounds__(kBTopT) void k_bm_tscan(int level, const unsigned l
                                                      unsigned long long* __restrict__ out_cnt) {
   __shared__ unsigned long long s_w[kBTopT / 64];
   __shared__ unsigned long long s_base;
+  // the tile totals pass through LDS in 4096-entry rounds: each round's global loads are
+  // coalesced (a thread's kTsPer consecutive entries straight from HBM touched a line per
+  // lane and load: 40 us for C3's 12k tiles)
+  constexpr int kRound = 4096;
+  __shared__ unsigned long long s_t[kRound];
   if (bm_dead(st) || (st->status & kStStop)) return;
   const uint64_t words = st->words[level];
   const uint64_t W = 1ull << (tb - 6);
@@ -156,12 +161,24 @@ __global__ __launch_bounds__(kBTopT) void k_bm_tscan(int level, const unsigned l
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   if (tid == 0) s_base = *out_cnt;
   unsigned long long v[kTsPer], sum = 0;
+  static_assert(kTsPer * kBTopT % kRound == 0 && kRound % kTsPer == 0, "tscan rounds");
 #pragma unroll
-  for (int q = 0; q < kTsPer; ++q) {
-    const uint64_t i = (uint64_t)tid * kTsPer + q;
-    v[q] = i < T ? tsum[i] : 0ull;
-    sum += v[q];
+  for (int r = 0; r < kTsPer * kBTopT / kRound; ++r) {
+    for (int j = (int)tid; j < kRound; j += kBTopT) {
+      const uint64_t i = (uint64_t)r * kRound + j;
+      s_t[j] = i < T ? tsum[i] : 0ull;
+    }
+    __syncthreads();
+    // threads [r * kRound / kTsPer, (r + 1) * kRound / kTsPer) own this round's entries
+    const unsigned own0 = (unsigned)(r * kRound / kTsPer);
+    if (tid >= own0 && tid < own0 + kRound / kTsPer) {
+#pragma unroll
+      for (int q = 0; q < kTsPer; ++q) v[q] = s_t[(tid - own0) * kTsPer + q];
+    }
+    __syncthreads();
   }
+#pragma unroll
+  for (int q = 0; q < kTsPer; ++q) sum += v[q];
   unsigned long long x = sum;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -380,6 +397,27 @@ __device__ __forceinline__ void put_out(Rec* out, bool o16, uint64_t i, uint64_t
   if (o16) reinterpret_cast<BmT16*>(out)[i] = BmT16{(uint32_t)(p - (uint64_t)sl * os.slice), (uint32_t)(pos - pos_base), f};
   else out[i] = Rec{p, f, pos};
 }
+// a slot from an LDS cursor for each active lane, one atomic per wave (lane order)
+__device__ __forceinline__ unsigned wave_slot(unsigned* cur) {
+  const uint64_t act = __ballot(1);
+  unsigned b = 0;
+  if ((lanemask_lt() & act) == 0) b = atomicAdd(cur, (unsigned)__popcll(act));
+  b = __shfl(b, __builtin_ffsll((long long)act) - 1);
+  return b + (unsigned)__popcll(act & lanemask_lt());
+}
+// one settled key of output slice sl counted in the block's LDS counters: the active lanes of a
+// wave mostly share one slice (at one rank all of them; in p order, runs), so one atomic per
+// wave then (a same-address LDS atomic per key serialised the whole wave)
+__device__ __forceinline__ void count_slice(unsigned* s_sc, unsigned sl, int P) {
+  if (sl >= (unsigned)P) sl = P - 1;
+  const unsigned s0 = __builtin_amdgcn_readfirstlane(sl);
+  const uint64_t act = __ballot(1), same = __ballot(sl == s0);
+  if (same == act) {
+    if ((lanemask_lt() & act) == 0) atomicAdd(&s_sc[s0], (unsigned)__popcll(act));
+  } else {
+    atomicAdd(&s_sc[sl], 1u);
+  }
+}
 __device__ __forceinline__ void fp_out_own(const OwnSlice& os, uint64_t p, uint64_t f, uint64_t pos, bool& over) {
   const uint64_t o = p - os.lo;
   if (p < os.lo || o >= os.cnt) {
@@ -542,8 +580,9 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
           pa += (unsigned)__popcll(sga[j] & below);
           const uint64_t gp = pb + pg;
           const unsigned sl = owner_of(gp, os.slice, os.mslice);
-          atomicAdd(&s_sc[sl < (unsigned)os.P ? sl : os.P - 1], 1u);
-          if (kStaged && pa < kBmStage) {  // written out below in pa order
+          const bool staged = kStaged && pa < kBmStage;  // (staged keys are counted at their write-out)
+          if (!staged) count_slice(s_sc, sl, os.P);
+          if (staged) {  // written out below in pa order
             stg[pa] = BmStaged{r[u].f, (uint32_t)(r[u].p - pos_base), pg};
           } else if ((int)sl == os.rank) {
             fp_out_own(os, gp, r[u].f, r[u].p, over);
@@ -555,7 +594,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
               over = true;
           }
         } else {
-          const uint64_t slot = nb + atomicAdd(&s_ncur, 1u);
+          const uint64_t slot = nb + wave_slot(&s_ncur);
           if (slot >= next_cap) over = true;
           else if constexpr (kO20) reinterpret_cast<R20*>(next)[slot] = R20{{(uint32_t)r[u].k, (uint32_t)(r[u].k >> 32),
                                                                           (uint32_t)r[u].f, (uint32_t)(r[u].f >> 32),
@@ -574,6 +613,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
         const BmStaged e = stg[i];
         const uint64_t gp = pb + e.pg, p = pos_base + e.i;
         const unsigned sl = owner_of(gp, os.slice, os.mslice);
+        count_slice(s_sc, sl, os.P);
         if ((int)sl == os.rank) {
           fp_out_own(os, gp, e.f, p, over);
         } else if (ob + i < out_cap) {
@@ -603,38 +643,85 @@ __global__ void k_bm_check(LevelState* st, int level, uint64_t wmax) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && st->words[level] > wmax) atomicOr(&st->status, kStBitmapBound);
 }
 
-// Received triples of this rank's output slice [lo, lo + cnt) -> fp_out / pos_out.  k16: 16-B
-// entries (offset in the slice, the sender's key index); tab holds, per sender q, the index of
-// its first entry in `in` (tab[q]) and its key base (tab[P + q]).
+// ---- the output slices' assembly at P > 1: a P-way merge through LDS windows ---------------
+// Every rank's settled list is sorted by p, so its run for this rank's slice (received, or its
+// own run in place) is sorted by slice offset.  Window w covers slice offsets [w Wn, (w+1) Wn):
+// its entries of run q are bnd[q][w] .. bnd[q][w+1] (k_bm_place_bounds: a binary search per
+// (run, window)); k_bm_place_merge drops them into LDS by offset and writes the window's
+// fp_out / pos_out as whole lines — one scattered 8-byte store per key (the first form: a line per
+// store at P = 8, 3.5 ms for C3's 100M keys per rank) becomes two coalesced passes.
+constexpr unsigned kPlaceWin = 2048;  // slice offsets per window (32 KB of LDS for fp + pos)
+struct PlaceRun {
+  const void* base;   // the run's first entry
+  uint64_t n;         // entries
+  uint64_t key_base;  // the sending rank's key base (16-B entries)
+};
 template <bool k16>
-__global__ __launch_bounds__(kBT) void k_bm_place(const void* __restrict__ in_v, uint64_t n, uint64_t lo, uint64_t cnt,
-                                                  uint64_t* __restrict__ fp_out, uint64_t* __restrict__ pos_out,
-                                                  LevelState* st, const unsigned long long* __restrict__ tab, int P) {
-  bool bad = false;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBT) {
-    uint64_t p, f, pos;
-    if constexpr (k16) {
-      const BmT16 r = static_cast<const BmT16*>(in_v)[i];
-      int q = 0;  // the sender: the last whose first entry is <= i (P <= 64)
-      for (int x = 1; x < P; ++x)
-        if (tab[x] <= i) q = x;
-      p = lo + r.off;
-      f = r.f;
-      pos = tab[P + q] + r.idx;
-    } else {
-      const Rec r = static_cast<const Rec*>(in_v)[i];
-      p = r.k;
-      f = r.f;
-      pos = r.p;
-    }
-    const uint64_t o = p - lo;
-    if (p < lo || o >= cnt) {
-      bad = true;
-      continue;
-    }
-    fp_out[o] = f;
-    pos_out[o] = pos;
+__device__ __forceinline__ uint64_t run_off(const void* base, uint64_t i, uint64_t lo) {
+  if constexpr (k16) return static_cast<const BmT16*>(base)[i].off;
+  else return static_cast<const Rec*>(base)[i].k - lo;
+}
+template <bool k16>
+__global__ __launch_bounds__(kBT) void k_bm_place_bounds(const PlaceRun* __restrict__ runs, int P, uint64_t lo,
+                                                         uint64_t nwin, uint32_t* __restrict__ bnd) {
+  const uint64_t gid = (uint64_t)blockIdx.x * kBT + threadIdx.x;
+  if (gid >= (uint64_t)P * (nwin + 1)) return;
+  const int q = (int)(gid / (nwin + 1));
+  const uint64_t w = gid % (nwin + 1), key = w * kPlaceWin;
+  const PlaceRun r = runs[q];
+  uint64_t a = 0, b = r.n;  // first entry with offset >= key
+  while (a < b) {
+    const uint64_t m = (a + b) >> 1;
+    if (run_off<k16>(r.base, m, lo) < key) a = m + 1;
+    else b = m;
   }
+  bnd[gid] = (uint32_t)a;
+}
+template <bool k16>
+__global__ __launch_bounds__(kBT) void k_bm_place_merge(const PlaceRun* __restrict__ runs, int P, uint64_t lo,
+                                                        uint64_t limit, uint64_t nwin,
+                                                        const uint32_t* __restrict__ bnd,
+                                                        uint64_t* __restrict__ fp_out, uint64_t* __restrict__ pos_out,
+                                                        LevelState* st) {
+  __shared__ uint64_t sf[kPlaceWin], sp[kPlaceWin];
+  const uint64_t w = blockIdx.x, w0 = w * kPlaceWin;
+  if (w >= nwin) return;
+  const unsigned wn = (unsigned)min<uint64_t>(kPlaceWin, limit - w0);
+  bool bad = false;
+  uint64_t have = 0;  // the window's entries over the runs: exactly one per offset, or a fault
+  for (int q = 0; q < P; ++q) {
+    const PlaceRun r = runs[q];
+    const uint32_t i0 = bnd[(uint64_t)q * (nwin + 1) + w], i1 = bnd[(uint64_t)q * (nwin + 1) + w + 1];
+    have += i1 - i0;
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += kBT) {
+      uint64_t off, f, pos;
+      if constexpr (k16) {
+        const BmT16 e = static_cast<const BmT16*>(r.base)[i];
+        off = e.off;
+        f = e.f;
+        pos = r.key_base + e.idx;
+      } else {
+        const Rec e = static_cast<const Rec*>(r.base)[i];
+        off = e.k - lo;
+        f = e.f;
+        pos = e.p;
+      }
+      const uint64_t j = off - w0;
+      if (j >= wn) {
+        bad = true;
+        continue;
+      }
+      sf[j] = f;
+      sp[j] = pos;
+    }
+  }
+  __syncthreads();
+  if (have != wn) bad = true;
+  else
+    for (unsigned j = threadIdx.x; j < wn; j += kBT) {
+      fp_out[w0 + j] = sf[j];
+      pos_out[w0 + j] = sp[j];
+    }
   if (bad) atomicOr(&st->status, kStRank);
 }
 
@@ -746,12 +833,24 @@ void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos
   else next20 ? go(Rec{}, F_{}, T_{}, F_{}) : go(Rec{}, F_{}, F_{}, F_{});
 }
 
-void launch_bm_place(const void* in, bool k16, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out,
-                     uint64_t* pos_out, LevelState* st, const unsigned long long* tab, int P, hipStream_t s) {
-  if (!n) return;
-  if (k16) k_bm_place<true><<<grid_for(n, kBT, 8192), kBT, 0, s>>>(in, n, lo, cnt, fp_out, pos_out, st, tab, P);
-  else k_bm_place<false><<<grid_for(n, kBT, 8192), kBT, 0, s>>>(in, n, lo, cnt, fp_out, pos_out, st, tab, P);
+
+// runs: P device PlaceRun entries (this rank's own run included); limit: slice offsets the
+// merge fills (below the replicated tail); bnd: P x (nwin + 1) u32 scratch
+void launch_bm_place_merge(const void* runs, bool k16, int P, uint64_t lo, uint64_t limit, uint32_t* bnd,
+                           uint64_t* fp_out, uint64_t* pos_out, LevelState* st, hipStream_t s) {
+  if (!limit) return;
+  const uint64_t nwin = (limit + kPlaceWin - 1) / kPlaceWin;
+  const PlaceRun* r = static_cast<const PlaceRun*>(runs);
+  const int gb = grid_for((uint64_t)P * (nwin + 1), kBT, 1 << 20);
+  if (k16) {
+    k_bm_place_bounds<true><<<gb, kBT, 0, s>>>(r, P, lo, nwin, bnd);
+    k_bm_place_merge<true><<<(int)nwin, kBT, 0, s>>>(r, P, lo, limit, nwin, bnd, fp_out, pos_out, st);
+  } else {
+    k_bm_place_bounds<false><<<gb, kBT, 0, s>>>(r, P, lo, nwin, bnd);
+    k_bm_place_merge<false><<<(int)nwin, kBT, 0, s>>>(r, P, lo, limit, nwin, bnd, fp_out, pos_out, st);
+  }
 }
+uint64_t bm_place_bound_words(int P, uint64_t limit) { return (uint64_t)P * ((limit + kPlaceWin - 1) / kPlaceWin + 1); }
 
 void launch_bm_tail_copy(const uint64_t* sfp, const uint64_t* spos, uint64_t g0, uint64_t total, uint64_t lo,
                          uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s) {

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
 #include <new>
 #include <string>
@@ -1622,6 +1623,8 @@ void free_bm_workspace(DistState& d) {
   dfree(d.bm_a); dfree(d.bm_g); dfree(d.bm_dec);
   dfree(d.bm_lanes); dfree(d.bm_slice); dfree(d.bm_recv); dfree(d.bm_tsum); dfree(d.bm_tbase);
   dfree(d.bm_out);
+  dfree(d.bm_bnd);
+  d.bm_bnd_cap = 0;
   d.bm_cap_words = 0;
   d.bm_cap_out = 0;
 }
@@ -1708,7 +1711,9 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     const int rc = dist_agree(c, lrc, s, msg);
     if (rc != S3IMPH_OK) return rc;
   }
-  const OwnSlice own_slice{lo, mine, slice, level_magic(slice), R, P, fp_out, pos_out, d.scnt};
+  // (one rank writes its settled keys straight to fp_out / pos_out; at P > 1 they join the settled
+  // list, and the slices are assembled by the P-way merge below)
+  const OwnSlice own_slice{lo, mine, slice, level_magic(slice), P == 1 ? R : -1, P, fp_out, pos_out, d.scnt};
   // with identity positions the settled keys bound for other slices cross as 16-B entries
   // (offset in the slice, this rank's key index, fp) instead of 24-B (p, fp, pos) records
   const bool out16 = !pos;
@@ -1751,9 +1756,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     const uint64_t tiles = tiles_of(wmax, tb, 0);
     // > 2^30 positions: the routed build (same on every rank); P0's levels take up to kBmMaxTiles
     if (tiles > (l0p || lp ? kBmMaxTiles : kScatterTiles)) return kDistRetry;
-    if (L > 0) launch_dist_setup(st, L, d.gslot + L, 0, R, P, s);
-    launch_bm_range(st, L, s);
-    launch_bm_check(st, L, wmax, s);
+    launch_bm_level_begin(st, L, L > 0, d.gslot + L, R, P, wmax, s);
     LevelGeom g{};
     g.tb = tb;
     g.chunk = kTargetChunks;
@@ -1939,8 +1942,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   HIPCHECK(hipStreamSynchronize(s));
   std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
   uint64_t acc = 0, got = 0, sent = 0;
-  unsigned long long* tab_h = d.h_pinned + kSmallWords + 2 * 16;  // sender table (after dist_agree's words)
-  std::vector<unsigned long long> tab(2 * (size_t)P);
+  std::vector<unsigned long long> tab(2 * (size_t)P);  // per sender: first received entry, key base
   for (int t = 0; t < P; ++t) {
     const uint64_t cnt_t = M[(uint64_t)R * (P + 1) + t];
     soff[t] = sent * es;
@@ -1971,13 +1973,29 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   }
   Rec* recv = c->list[Ls & 1];
   if (P > 1) cm.alltoallv(out, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), s);
-  unsigned long long* tab_d = d.small + 6144;  // (d.small: gathers below 4096, out_cnt at 4096)
-  if (got && out16) {
-    HIPCHECK(hipStreamSynchronize(s));  // tab_h is reused by the next build
-    std::copy(tab.begin(), tab.end(), tab_h);
-    HIPCHECK(hipMemcpyAsync(tab_d, tab_h, 16ull * P, hipMemcpyHostToDevice, s));
+  if (P > 1) {
+    // the slice below the replicated tail from the P p-sorted runs: the received ones and this
+    // rank's own run, in place in its settled list
+    const uint64_t limit = g0 > lo ? std::min<uint64_t>(mine, g0 - lo) : 0;
+    const uint64_t bw = bm_place_bound_words(P, limit);
+    if (bw > d.bm_bnd_cap) {
+      d.bm_bnd_cap = 0;
+      dalloc(d.bm_bnd, bw);
+      d.bm_bnd_cap = bw;
+    }
+    unsigned long long* run_h = d.h_pinned + kSmallWords + 2 * 16;  // (after dist_agree's words; 3 P <= 192)
+    unsigned long long* run_d = d.small + 6144;                     // (d.small: gathers below 4096, out_cnt at 4096)
+    HIPCHECK(hipStreamSynchronize(s));  // run_h is reused by the next build
+    for (int sq = 0; sq < P; ++sq) {  // run sq: sender sq's entries for this slice
+      const uint8_t* rb = sq == R ? reinterpret_cast<const uint8_t*>(out) + soff[R]
+                                  : reinterpret_cast<const uint8_t*>(recv) + roff[sq];
+      run_h[3 * sq] = (unsigned long long)(uintptr_t)rb;
+      run_h[3 * sq + 1] = sq == R ? own : M[(uint64_t)sq * (P + 1) + R];
+      run_h[3 * sq + 2] = tab[P + sq];
+    }
+    HIPCHECK(hipMemcpyAsync(run_d, run_h, 24ull * P, hipMemcpyHostToDevice, s));
+    launch_bm_place_merge(run_d, out16, P, lo, limit, d.bm_bnd, fp_out, pos_out, st, s);
   }
-  launch_bm_place(recv, out16, got, lo, mine, fp_out, pos_out, st, tab_d, P, s);
   launch_bm_tail_copy(c->kh, c->fp, g0, total, lo, mine, fp_out, pos_out, s);
   ev_mark(c, s, "exchange_out");
   HIPCHECK(hipMemcpyAsync(M, &st->status, 4, hipMemcpyDeviceToHost, s));
@@ -2295,10 +2313,50 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
     }
     if (pos) ensure_s_pos(c, n);
     if (!c->copy_stream) HIPCHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-    if (!c->copy_ev) HIPCHECK(hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming));
+    for (auto& e : c->copy_evs)
+      if (!e) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     hipStream_t s = c->own_stream;
     HIPCHECK(hipStreamSynchronize(s));  // staging buffers may be in use by the last build
     const auto t0 = clk::now();
+    // The blob crosses in pieces (one for a blob under 256 MiB; at most kCopyPieces) on the copy
+    // stream, from a thread of its own that starts at once, beside the offsets' conversion and
+    // copy below; the level-0 hash launches wait for the piece holding their keys (HashFeed).
+    const int pieces = (int)std::min<uint64_t>(kCopyPieces, std::max<uint64_t>(1, nbytes >> 28));
+    std::vector<uint64_t> piece_hi(pieces);
+    for (int j = 0; j < pieces; ++j) piece_hi[j] = j + 1 == pieces ? nbytes : (nbytes * (j + 1) / pieces + 15) & ~15ull;
+    std::mutex pmu;
+    std::condition_variable pcv;
+    int pdone = 0;
+    Fail copy_err{S3IMPH_OK, ""};
+    clk::time_point t_copied{};
+    std::thread tcopy([&]() {
+      try {
+        HIPCHECK(hipSetDevice(c->device));
+        uint64_t lo = 0;
+        for (int j = 0; j < pieces; ++j) {
+          HIPCHECK(hipMemcpyAsync(c->s_blob + lo, blob + b0 + lo, piece_hi[j] - lo, hipMemcpyHostToDevice,
+                                  c->copy_stream));
+          HIPCHECK(hipEventRecord(c->copy_evs[j], c->copy_stream));
+          lo = piece_hi[j];
+          std::lock_guard<std::mutex> g(pmu);
+          pdone = j + 1;
+          pcv.notify_all();
+        }
+        HIPCHECK(hipStreamSynchronize(c->copy_stream));
+      } catch (const Fail& f) {
+        std::lock_guard<std::mutex> g(pmu);
+        copy_err = f;
+        pdone = pieces;
+        pcv.notify_all();
+      }
+      t_copied = clk::now();
+    });
+    struct Join {
+      std::thread& t;
+      ~Join() {
+        if (t.joinable()) t.join();
+      }
+    } join_copy{tcopy};
     // Offsets cross PCIe first, as u16 key lengths (2 B per key: C3's 800 MB of u64 offsets
     // become 200 MB) rebuilt on the device by a scan; a key longer than 65535 B sends them as
     // u32 (blob under 4 GiB, widened on the device) or u64 instead.  Staged in s_fp's space
@@ -2317,29 +2375,41 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
     else if (off32) launch_widen32(tmp32, c->s_offsets, n + 1, s);
     if (pos) staged_copy(c, true, c->s_pos, pos, n * 8);
     const auto t1 = clk::now();
-    // The blob, piece by piece as the level-0 hash asks for its keys: a piece is [what is on
-    // the device, the keys' end + 16 B) on the copy stream, and the build stream waits for it
-    uint64_t copied = 0;
-    clk::duration t_copy{};
+    // ensure(k): the build stream waits for the piece that holds keys [0, k) and the 16 bytes
+    // after them (a piece the copy thread has enqueued; its event marks it landed)
+    int waited = 0;
+    clk::duration t_wait{};
     HashFeed feed;
+    feed.pieces = pieces;  // one hash launch per blob piece
     feed.ensure = [&](uint64_t k) {
       const uint64_t want = k >= n ? nbytes : std::min<uint64_t>(nbytes, offsets[k] - b0 + 16);
-      if (want <= copied) return;
-      const auto tc = clk::now();
-      HIPCHECK(hipMemcpyAsync(c->s_blob + copied, blob + b0 + copied, want - copied, hipMemcpyHostToDevice,
-                              c->copy_stream));
-      HIPCHECK(hipEventRecord(c->copy_ev, c->copy_stream));
-      HIPCHECK(hipStreamWaitEvent(s, c->copy_ev, 0));
-      copied = want;
-      t_copy += clk::now() - tc;
+      int j = 0;  // the piece whose end covers want
+      while (j < pieces - 1 && piece_hi[j] < want) ++j;
+      if (j < waited) return;  // waited for already (the hash of a rerun asks again)
+      const auto tw = clk::now();
+      {
+        std::unique_lock<std::mutex> g(pmu);
+        pcv.wait(g, [&] { return pdone > j; });
+        if (copy_err.code != S3IMPH_OK) throw copy_err;
+      }
+      HIPCHECK(hipStreamWaitEvent(s, c->copy_evs[j], 0));
+      waited = j + 1;
+      t_wait += clk::now() - tw;
     };
-    c->feed = &feed;
+    if (pieces == 1) {  // a blob of one piece: the build starts once it has landed (no event wait)
+      const auto tw = clk::now();
+      tcopy.join();
+      if (copy_err.code != S3IMPH_OK) throw copy_err;
+      t_wait += clk::now() - tw;
+    } else {
+      c->feed = &feed;
+    }
     s3imph_build_info info;
     int rc = build_single(c, c->s_blob, c->s_offsets, pos ? c->s_pos : nullptr, n, c->s_fp, c->s_posout, s,
                           &info, msg);
     c->feed = nullptr;
-    feed.ensure(n);  // (a path that never hashed: nothing may still be in flight into s_blob)
-    HIPCHECK(hipStreamSynchronize(c->copy_stream));
+    if (tcopy.joinable()) tcopy.join();  // (a path that never hashed: nothing may still be in flight into s_blob)
+    if (copy_err.code != S3IMPH_OK) throw copy_err;
     if (rc != S3IMPH_OK) return rc;
     const auto t2 = clk::now();
     // mph.bin (level words D2H, ~40 MB at C3) is marshalled on a second thread, straight into
@@ -2405,11 +2475,11 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
       auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
       const auto tx = clk::now();
       std::fprintf(stderr,
-                   "[s3imph] host build: entry %.2f + offsets h2d %.2f (as %s) + blob h2d and build %.2f (blob copy "
-                   "calls %.2f, %d pieces) + d2h %.2f + marshal wait %.2f = %.2f ms (marshal ended %.2f ms after "
-                   "the build)\n",
+                   "[s3imph] host build: entry %.2f + offsets h2d %.2f (as %s; the blob copy beside it) + build %.2f "
+                   "(hash launches waited %.2f for blob pieces; blob copied %.2f ms after the start, %d pieces) + "
+                   "d2h %.2f + marshal wait %.2f = %.2f ms (marshal ended %.2f ms after the build)\n",
                    ms(t0 - te), ms(t1 - t0), wide.load() ? (off32 ? "u32" : "u64") : "u16 lengths", ms(t2 - t1),
-                   ms(t_copy), feed.pieces, ms(t3 - t2), ms(tx - t3), ms(tx - te), ms(t3m - t2));
+                   ms(t_wait), ms(t_copied - t0), pieces, ms(t3 - t2), ms(tx - t3), ms(tx - te), ms(t3m - t2));
     }
     return mrc;
   } catch (const Fail& f) {
@@ -2528,7 +2598,8 @@ int s3imph_ctx_destroy(s3imph_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-  if (c->copy_ev) (void)hipEventDestroy(c->copy_ev);
+  for (hipEvent_t e : c->copy_evs)
+    if (e) (void)hipEventDestroy(e);
   delete c;
   return S3IMPH_OK;
 }

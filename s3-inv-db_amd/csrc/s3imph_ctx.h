@@ -98,6 +98,8 @@ struct DistState {
   uint64_t bm_cap_words = 0;
   Rec* bm_out = nullptr;  // this rank's settled (p, fp, pos) triples (the tail's tile kernels own the bucket)
   uint64_t bm_cap_out = 0;
+  uint32_t* bm_bnd = nullptr;  // the output merge's window bounds (launch_bm_place_merge)
+  uint64_t bm_bnd_cap = 0;
   int mode = kDistRoute;
   bool strict = false;  // S3IMPH_DIST_STRICT: the bitmap decomposition may not fall back to routing
   // level 0's exchange runs on its own stream, chunk by chunk, beside the next chunk's hash
@@ -163,6 +165,7 @@ struct RcclComm final : Comm {
 // data through pinned memory, so the CPU copies of one worker overlap the DMA of the
 // others and the PCIe link runs at its pinned rate.
 constexpr int kStageWorkers = 8;
+constexpr int kCopyPieces = 16;  // the host build's blob H2D pieces (at most; 256 MiB or more each)
 constexpr uint64_t kStageChunk = 8ull << 20;
 
 struct Stager {
@@ -243,7 +246,7 @@ struct s3imph_ctx {
 
   // staging for host-memory builds
   hipStream_t copy_stream = nullptr;  // the blob's H2D pieces (build_from_host), beside the hash
-  hipEvent_t copy_ev = nullptr;
+  hipEvent_t copy_evs[s3imph::kCopyPieces] = {};
   const s3imph::HashFeed* feed = nullptr;  // set for the duration of one host build
   uint8_t* s_blob = nullptr;
   uint64_t s_blob_cap = 0;

@@ -135,9 +135,8 @@ __global__ __launch_bounds__(kRT) void k_route(int level, const uint64_t* __rest
 
 // Size distributed level L on the device from its global key count (*gcount, the
 // all-reduced redo counts of level L-1, or n for level 0) and this rank's word range.
-__global__ void k_dist_setup(LevelState* st, int L, const unsigned long long* gcount, uint64_t n_value, int rank,
-                             int P) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ void dist_setup(LevelState* st, int L, const unsigned long long* gcount, uint64_t n_value, int rank,
+                           int P) {
   const uint64_t n = gcount ? *gcount : n_value;
   const uint64_t w = level_words(n);
   const uint64_t S = (w + P - 1) / P;
@@ -155,6 +154,21 @@ __global__ void k_dist_setup(LevelState* st, int L, const unsigned long long* gc
   st->nlevels = L + 1;
   st->n[L + 1] = 0;                     // this level's collided records (tile atomics)
   st->lvl_base[L + 1] = st->lvl_base[L];  // overwritten by the last tile, if any
+}
+__global__ void k_dist_setup(LevelState* st, int L, const unsigned long long* gcount, uint64_t n_value, int rank,
+                             int P) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  dist_setup(st, L, gcount, n_value, rank, P);
+}
+// A bitmap level's start in one launch: its setup (setup: from the gathered count), the whole
+// level's range (k_bm_range), and its size against the host's bound wmax (k_bm_check)
+__global__ void k_bm_level_begin(LevelState* st, int L, bool setup, const unsigned long long* gcount, int rank, int P,
+                                 uint64_t wmax) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (setup) dist_setup(st, L, gcount, 0, rank, P);
+  st->wlo[L] = 0;
+  st->rw[L] = st->words[L];
+  if (st->words[L] > wmax) atomicOr(&st->status, kStBitmapBound);
 }
 
 __global__ void k_set_u64(unsigned long long* p, uint64_t v) {
@@ -232,6 +246,11 @@ void launch_dist_setup(LevelState* st, int L, const unsigned long long* gcount, 
 }
 
 void launch_set_u64(unsigned long long* p, uint64_t v, hipStream_t s) { k_set_u64<<<1, 64, 0, s>>>(p, v); }
+
+void launch_bm_level_begin(LevelState* st, int L, bool setup, const unsigned long long* gcount, int rank, int P,
+                           uint64_t wmax, hipStream_t s) {
+  k_bm_level_begin<<<1, 64, 0, s>>>(st, L, setup, gcount, rank, P, wmax);
+}
 
 void launch_dist_replicate(LevelState* st, int L, uint64_t n_all, uint64_t skip_from, hipStream_t s) {
   k_dist_replicate<<<1, 64, 0, s>>>(st, L, n_all, skip_from);

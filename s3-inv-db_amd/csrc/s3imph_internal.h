@@ -367,6 +367,9 @@ void launch_dist_replicate(LevelState* st, int L, uint64_t n_all, uint64_t skip_
 
 // ---- the bitmap decomposition of the multi-GPU build (s3imph_bitmap.hip) --------------
 void launch_bm_check(LevelState* st, int level, uint64_t wmax, hipStream_t s);
+// k_dist_setup (setup: from *gcount), k_bm_range and k_bm_check of level L in one launch
+void launch_bm_level_begin(LevelState* st, int L, bool setup, const unsigned long long* gcount, int rank, int P,
+                           uint64_t wmax, hipStream_t s);
 // nib: count lanes are nibbles (two positions per byte; P <= kBmNibRanks), else bytes
 constexpr int kBmNibRanks = 7;
 // What crosses xGMI per position and level: a count byte, a count nibble (both summed by an
@@ -420,9 +423,13 @@ struct BmT16 {
   uint32_t off, idx;
   uint64_t f;
 };
-// k16: `in` holds BmT16 entries, tab the senders' first entries (P) and key bases (P)
-void launch_bm_place(const void* in, bool k16, uint64_t n, uint64_t lo, uint64_t cnt, uint64_t* fp_out,
-                     uint64_t* pos_out, LevelState* st, const unsigned long long* tab, int P, hipStream_t s);
+
+// P > 1: the slice's settled keys from the P p-sorted runs (runs: device array of P
+// {base, n, key_base}) merged through LDS windows below slice offset `limit`; bnd: scratch of
+// bm_place_bound_words(P, limit) u32
+void launch_bm_place_merge(const void* runs, bool k16, int P, uint64_t lo, uint64_t limit, uint32_t* bnd,
+                           uint64_t* fp_out, uint64_t* pos_out, LevelState* st, hipStream_t s);
+uint64_t bm_place_bound_words(int P, uint64_t limit);
 void launch_bm_tail_copy(const uint64_t* sfp, const uint64_t* spos, uint64_t g0, uint64_t total, uint64_t lo,
                          uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s);
 

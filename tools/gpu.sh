@@ -20,6 +20,10 @@
 #   bash tools/gpu.sh TAG lib REPS CFG            old / new library A/B (abx/libs3imph_{old,new}.so,
 #                                                 alternating) -> lib_summary.txt
 #   bash tools/gpu.sh TAG host NAME [args]        tools/host_phase.py (host-memory build phases) -> NAME.log
+#   bash tools/gpu.sh TAG p8 NAME [P K AVG BUILDS]
+#                                                 tools/p8_geometry.py under rocprofv3 --kernel-trace: the
+#                                                 P-rank bitmap build on this one GPU, ranks serialised; per-
+#                                                 rank kernel sums -> NAME_ranks.txt
 #   bash tools/gpu.sh TAG multi NAME NPROC [bench args]
 #                                                 bench.py's N > 1 path under torchrun, ranks sharing
 #                                                 this one GPU through the host transport -> NAME.log
@@ -102,6 +106,13 @@ case $STEP in
     NAME=$1; shift
     timeout -k 10 300 python tools/host_phase.py "$@" > "$OUT/$NAME.log" 2>&1
     rc=$?; echo "host $NAME rc $rc" >> "$OUT/status"; exit $rc ;;
+  p8)
+    NAME=$1; shift
+    timeout -k 10 1000 rocprofv3 --kernel-trace --output-format csv -d "$OUT/$NAME" -o run -- \
+      python3 tools/p8_geometry.py "$@" > "$OUT/$NAME.log" 2>&1
+    rc=$?; stop $rc
+    python3 tools/rank_kernel_sums.py "$OUT/$NAME/run_kernel_trace.csv" > "$OUT/${NAME}_ranks.txt"
+    echo "p8 $NAME rc $rc" >> "$OUT/status"; exit $rc ;;
   multi)
     NAME=$1; NP=$2; shift 2
     timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$NP" --master-addr 127.0.0.1 \
