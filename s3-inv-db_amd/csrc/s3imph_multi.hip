@@ -49,8 +49,12 @@ struct ThreadHub {
   bool aborted = false;
   std::vector<std::vector<uint8_t>> slot;  // per rank
   std::vector<std::vector<uint64_t>> soff, sbytes;
+  // every rank on one device: the gathers and all-to-alls copy device to device, each rank
+  // from its peers' published send buffers (dptr), instead of through host memory
+  bool same_dev = false;
+  std::vector<const uint8_t*> dptr;
 
-  explicit ThreadHub(int p) : P(p), held(p, 0), slot(p), soff(p), sbytes(p) {}
+  explicit ThreadHub(int p) : P(p), held(p, 0), slot(p), soff(p), sbytes(p), dptr(p, nullptr) {}
   void seg_begin(int r) {  // this rank's device work starts
     if (!serial || held[r]) return;
     token.lock();
@@ -94,7 +98,21 @@ struct ThreadComm final : Comm {
   void h2d(void* d, const void* h, uint64_t bytes, hipStream_t s) {
     if (bytes) HIPCHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
   }
+  void d2d(void* d, const void* src, uint64_t bytes, hipStream_t s) {
+    if (bytes) HIPCHECK(hipMemcpyAsync(d, src, bytes, hipMemcpyDeviceToDevice, s));
+  }
   void allgather(const void* d_send, void* d_recv, uint64_t bytes, hipStream_t s) override {
+    if (hub->same_dev) {
+      hub->dptr[rank] = static_cast<const uint8_t*>(d_send);
+      HIPCHECK(hipStreamSynchronize(s));  // the send buffer is complete
+      hub->seg_end(rank);
+      hub->barrier();
+      for (int r = 0; r < nranks; ++r) d2d(static_cast<uint8_t*>(d_recv) + (uint64_t)r * bytes, hub->dptr[r], bytes, s);
+      HIPCHECK(hipStreamSynchronize(s));
+      hub->barrier();  // every rank has read the peers' buffers before they change
+      hub->seg_begin(rank);
+      return;
+    }
     auto& mine = hub->slot[rank];
     mine.resize(bytes + 1);
     d2h(mine.data(), d_send, bytes, s);
@@ -146,6 +164,22 @@ struct ThreadComm final : Comm {
   }
   void alltoallv(const void* d_send, const uint64_t* soff, const uint64_t* sbytes, void* d_recv,
                  const uint64_t* roff, const uint64_t* rbytes, hipStream_t s) override {
+    if (hub->same_dev) {
+      hub->dptr[rank] = static_cast<const uint8_t*>(d_send);
+      hub->soff[rank].assign(soff, soff + nranks);
+      hub->sbytes[rank].assign(sbytes, sbytes + nranks);
+      HIPCHECK(hipStreamSynchronize(s));
+      hub->seg_end(rank);
+      hub->barrier();
+      for (int q = 0; q < nranks; ++q) {
+        if (hub->sbytes[q][rank] != rbytes[q]) throw Fail{S3IMPH_ERR_INTERNAL, "alltoallv: size mismatch"};
+        d2d(static_cast<uint8_t*>(d_recv) + roff[q], hub->dptr[q] + hub->soff[q][rank], rbytes[q], s);
+      }
+      HIPCHECK(hipStreamSynchronize(s));
+      hub->barrier();
+      hub->seg_begin(rank);
+      return;
+    }
     // this rank's send regions, packed back to back in its slot
     auto& mine = hub->slot[rank];
     auto& po = hub->soff[rank];
@@ -250,6 +284,7 @@ MultiCtx* multi_ctx(const std::vector<int>& devs, bool host_transport, std::stri
   std::vector<Comm*> comms(P, nullptr);
   if (host_transport) {
     mc->hub = std::make_unique<ThreadHub>(P);
+    mc->hub->same_dev = std::all_of(devs.begin(), devs.end(), [&](int d) { return d == devs[0]; });
     for (int r = 0; r < P; ++r) {
       ThreadComm* tc = new ThreadComm();
       tc->hub = mc->hub.get();
