@@ -26,6 +26,7 @@
 #include "s3imph_internal.h"
 
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
 
 namespace s3imph {
@@ -112,29 +113,36 @@ __global__ __launch_bounds__(kBT) void k_bm_tsum(int level, const uint64_t* __re
                                                  const uint64_t* __restrict__ A, unsigned tb,
                                                  uint64_t* __restrict__ bits, unsigned long long* __restrict__ tsum,
                                                  const LevelState* st) {
-  __shared__ unsigned long long s_w[kBT / 64];
   if (bm_dead(st) || (st->status & kStStop)) return;
   const uint64_t words = st->words[level], woff = st->woff[level];
   const uint64_t W = 1ull << (tb - 6);
   const uint64_t T = (words + W - 1) / W;
-  for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
+  const unsigned lane = lane_id();
+  // a wave per tile, 16-byte loads (W >= 256 words: whole word pairs; the level's last tile
+  // may end on an odd word)
+  const uint4* g2 = reinterpret_cast<const uint4*>(g);
+  const uint4* A2 = reinterpret_cast<const uint4*>(A);
+  for (uint64_t t = (uint64_t)blockIdx.x * (kBT / 64) + (threadIdx.x >> 6); t < T; t += (uint64_t)gridDim.x * (kBT / 64)) {
     const uint64_t w0 = t * W, w1 = min<uint64_t>(words, w0 + W);
+    const uint64_t p1 = w1 >> 1;  // whole pairs below w1
     unsigned long long s = 0;
-    for (uint64_t w = w0 + threadIdx.x; w < w1; w += kBT) {
-      const uint64_t v = g[w];
-      s += ((unsigned long long)__popcll(v) << 32) | (unsigned)__popcll(v & A[w]);
-      bits[woff + w] = v;
+#pragma unroll 2
+    for (uint64_t p = (w0 >> 1) + lane; p < p1; p += 64) {
+      const uint4 v = g2[p], a = A2[p];
+      const uint64_t v0 = (uint64_t)v.x | ((uint64_t)v.y << 32), v1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
+      const uint64_t a0 = (uint64_t)a.x | ((uint64_t)a.y << 32), a1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
+      s += ((unsigned long long)(__popcll(v0) + __popcll(v1)) << 32) | (unsigned)(__popcll(v0 & a0) + __popcll(v1 & a1));
+      bits[woff + 2 * p] = v0;
+      bits[woff + 2 * p + 1] = v1;
+    }
+    if ((w1 & 1) && lane == 0) {
+      const uint64_t v = g[w1 - 1];
+      s += ((unsigned long long)__popcll(v) << 32) | (unsigned)__popcll(v & A[w1 - 1]);
+      bits[woff + w1 - 1] = v;
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
-    if (lane_id() == 0) s_w[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned long long tt = 0;
-      for (int k = 0; k < kBT / 64; ++k) tt += s_w[k];
-      tsum[t] = tt;
-    }
-    __syncthreads();
+    if (lane == 0) tsum[t] = s;
   }
 }
 
@@ -381,10 +389,17 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
 // a hole no one reads); every settled key is counted per output slice in scnt, which is
 // the output all-to-all's send counts (the list's runs by slice, holes included).
 constexpr unsigned kGrp = 4;
-// staged settled keys per tile: the tiles of a staged level are sized so that a rank holds ~8k
-// records of one (2^14 positions at one rank, 2^(14 + lg P) at P, kBmP0MaxTb at most): mean
-// ~4970 settled, 9.9 sigma below this at one rank (more ranks: the share adds ~1 sigma)
+// staged settled keys per tile, at most: the tiles of a staged level are sized so that a rank
+// holds ~8k records of one (2^14 positions at one rank, 2^(14 + lg P) at P, kBmP0MaxTb at
+// most): mean ~4970 settled, 9.9 sigma below this at one rank.  A launch stages
+// bm_stage_entries(tb, P) (P = 8 at 2^16: 4k records, 3072 entries — the settle then fits two
+// blocks per CU); a key past the stage is written directly.
 constexpr unsigned kBmStage = 5632;
+unsigned bm_stage_entries(unsigned tb, int P) {
+  const double m = std::ldexp(1.0, (int)tb - 1) / std::max(1, P) * 0.6066;  // e^-1/2 of the rank's records
+  const unsigned e = (unsigned)(m + 10.0 * std::sqrt(m) + 256.0 + 255.0) & ~255u;
+  return std::min(kBmStage, std::max(256u, e));
+}
 // a staged settled key: its fingerprint, key index (p = pos_base + i) and rank in the tile
 struct BmStaged {
   uint64_t f;
@@ -439,7 +454,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
                                                         const unsigned long long* __restrict__ tbase,
                                                         Rec* __restrict__ out, uint64_t out_cap,
                                                         Rec* __restrict__ next, uint64_t next_cap, OwnSlice os,
-                                                        const uint16_t* __restrict__ xs, bool o16) {
+                                                        const uint16_t* __restrict__ xs, bool o16, unsigned stage) {
   static_assert(!kStaged || sizeof(RT) != sizeof(Rec), "staged settles read R20 tiles");
   static_assert(!kX || kStaged, "x positions come with P0's R20 tiles");
   extern __shared__ uint64_t bm_lds64[];
@@ -458,7 +473,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
   uint64_t* sga = sg + W;
   unsigned* gpg = reinterpret_cast<unsigned*>(sga + W);  // per group: popcount(g) before it
   unsigned* gpa = gpg + G;                               // ... popcount(g & a)
-  BmStaged* stg = reinterpret_cast<BmStaged*>(gpa + G);  // kStaged: kBmStage entries (8-B aligned: G even)
+  BmStaged* stg = reinterpret_cast<BmStaged*>(gpa + G);  // kStaged: `stage` entries (8-B aligned: G even)
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
   constexpr int kGper = 2;  // groups per thread in the tile scan (G <= 2048)
@@ -541,20 +556,20 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
     for (unsigned i0 = 0; i0 < nrec; i0 += kTT * kU) {
       Rec r[kU];
       uint16_t rx[kX ? kU : 1];
+      // the batch's loads straight-line, all in flight together (the index clamped instead of
+      // guarded: a guarded load per record waited for the previous one)
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const unsigned i = i0 + u * kTT + tid;
-        if (i < nrec) {
-          const uint64_t ri = rec_index(i, fo, t * cap, scap);
-          const RT* q = bucket + ri;
-          if constexpr (kX) rx[u] = xs[ri];
-          if constexpr (sizeof(RT) == sizeof(Rec)) {
-            r[u] = *reinterpret_cast<const Rec*>(q);
-          } else {  // R20: (k, f, key index), p = pos_base + index
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(q);
-            const uint4 a = *reinterpret_cast<const uint4*>(w);  // dword-aligned 16-B load
-            r[u] = Rec{(uint64_t)a.x | ((uint64_t)a.y << 32), (uint64_t)a.z | ((uint64_t)a.w << 32), pos_base + w[4]};
-          }
+        const unsigned i = min(i0 + u * kTT + tid, nrec - 1);
+        const uint64_t ri = rec_index(i, fo, t * cap, scap);
+        const RT* q = bucket + ri;
+        if constexpr (kX) rx[u] = xs[ri];
+        if constexpr (sizeof(RT) == sizeof(Rec)) {
+          r[u] = *reinterpret_cast<const Rec*>(q);
+        } else {  // R20: (k, f, key index), p = pos_base + index
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(q);
+          const uint4 a = *reinterpret_cast<const uint4*>(w);  // dword-aligned 16-B load
+          r[u] = Rec{(uint64_t)a.x | ((uint64_t)a.y << 32), (uint64_t)a.z | ((uint64_t)a.w << 32), pos_base + w[4]};
         }
       }
 #pragma unroll
@@ -580,7 +595,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
           pa += (unsigned)__popcll(sga[j] & below);
           const uint64_t gp = pb + pg;
           const unsigned sl = owner_of(gp, os.slice, os.mslice);
-          const bool staged = kStaged && pa < kBmStage;  // (staged keys are counted at their write-out)
+          const bool staged = kStaged && pa < stage;  // (staged keys are counted at their write-out)
           if (!staged) count_slice(s_sc, sl, os.P);
           if (staged) {  // written out below in pa order
             stg[pa] = BmStaged{r[u].f, (uint32_t)(r[u].p - pos_base), pg};
@@ -608,7 +623,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
       // land in runs of fp_out / pos_out (at one rank: the whole tile, one run) and the
       // others in one run of the settled list, instead of one scattered 8-byte store each
       __syncthreads();
-      const unsigned ns = (unsigned)min<unsigned long long>(tot & 0xffffffffull, kBmStage);
+      const unsigned ns = (unsigned)min<unsigned long long>(tot & 0xffffffffull, stage);
       for (unsigned i = tid; i < ns; i += kTT) {
         const BmStaged e = stg[i];
         const uint64_t gp = pb + e.pg, p = pos_base + e.i;
@@ -684,45 +699,90 @@ __global__ __launch_bounds__(kBT) void k_bm_place_merge(const PlaceRun* __restri
                                                         uint64_t* __restrict__ fp_out, uint64_t* __restrict__ pos_out,
                                                         LevelState* st) {
   __shared__ uint64_t sf[kPlaceWin], sp[kPlaceWin];
+  __shared__ uint32_t s_i0[kMaxRanks], s_pre[kMaxRanks + 1];
+  __shared__ const void* s_rb[kMaxRanks];  // the runs' bases and key bases, in LDS: an entry's
+  __shared__ uint64_t s_kb[kMaxRanks];     // address waits on no global load but its own
   const uint64_t w = blockIdx.x, w0 = w * kPlaceWin;
   if (w >= nwin) return;
-  const unsigned wn = (unsigned)min<uint64_t>(kPlaceWin, limit - w0);
-  bool bad = false;
-  uint64_t have = 0;  // the window's entries over the runs: exactly one per offset, or a fault
-  for (int q = 0; q < P; ++q) {
-    const PlaceRun r = runs[q];
-    const uint32_t i0 = bnd[(uint64_t)q * (nwin + 1) + w], i1 = bnd[(uint64_t)q * (nwin + 1) + w + 1];
-    have += i1 - i0;
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += kBT) {
-      uint64_t off, f, pos;
-      if constexpr (k16) {
-        const BmT16 e = static_cast<const BmT16*>(r.base)[i];
-        off = e.off;
-        f = e.f;
-        pos = r.key_base + e.idx;
-      } else {
-        const Rec e = static_cast<const Rec*>(r.base)[i];
-        off = e.k - lo;
-        f = e.f;
-        pos = e.p;
-      }
-      const uint64_t j = off - w0;
-      if (j >= wn) {
-        bad = true;
-        continue;
-      }
-      sf[j] = f;
-      sp[j] = pos;
+  const unsigned wn = (unsigned)min<uint64_t>(kPlaceWin, limit - w0), tid = threadIdx.x;
+  // the window's entries over the runs, flattened: run q's part is [s_pre[q], s_pre[q + 1])
+  if (tid < 64) {
+    uint32_t i0 = 0, c = 0;
+    if (tid < (unsigned)P) {
+      i0 = bnd[(uint64_t)tid * (nwin + 1) + w];
+      c = bnd[(uint64_t)tid * (nwin + 1) + w + 1] - i0;
     }
+    uint32_t x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if (tid >= (unsigned)d) x += y;
+    }
+    if (tid < (unsigned)P) {
+      s_i0[tid] = i0;
+      s_pre[tid] = x - c;
+      s_rb[tid] = runs[tid].base;
+      s_kb[tid] = runs[tid].key_base;
+    }
+    if (tid == (unsigned)P - 1) s_pre[P] = x;
   }
   __syncthreads();
-  if (have != wn) bad = true;
-  else
-    for (unsigned j = threadIdx.x; j < wn; j += kBT) {
-      fp_out[w0 + j] = sf[j];
-      pos_out[w0 + j] = sp[j];
+  const uint32_t have = s_pre[P];  // exactly one entry per offset, or a fault
+  bool bad = have != wn;
+  if (!bad) {
+    // kPlaceWin / kBT entries per thread, their loads all in flight before the LDS drops: the
+    // addresses first (LDS only; a thread past the window's entries re-reads the last one),
+    // then straight-line loads through global (not flat) pointers, so no load waits on
+    // another's LDS counter or branch
+    constexpr int kE = (int)(kPlaceWin / kBT);
+    using G64 = const __attribute__((address_space(1))) unsigned long long;
+    uintptr_t ad[kE];
+    uint64_t off[kE], f[kE], pos[kE], kb[kE];
+    bool v[kE];
+    int q = 0;  // (j ascends with e: the run index only advances)
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      const uint32_t j0 = tid + (uint32_t)e * kBT, j = min(j0, have - 1);
+      v[e] = j0 < have;
+      while (q + 1 < P && s_pre[q + 1] <= j) ++q;
+      const uint64_t i = s_i0[q] + (j - s_pre[q]);
+      ad[e] = reinterpret_cast<uintptr_t>(s_rb[q]) + i * (k16 ? sizeof(BmT16) : sizeof(Rec));
+      kb[e] = s_kb[q];
     }
-  if (bad) atomicOr(&st->status, kStRank);
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      G64* x = reinterpret_cast<G64*>(ad[e]);
+      if constexpr (k16) {  // BmT16: off | idx << 32, f
+        const uint64_t a = x[0];
+        f[e] = x[1];
+        off[e] = (uint32_t)a;
+        pos[e] = kb[e] + (a >> 32);
+      } else {  // Rec: k, f, p
+        off[e] = x[0] - lo;
+        f[e] = x[1];
+        pos[e] = x[2];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < kE; ++e)
+      if (v[e]) {
+        const uint64_t j = off[e] - w0;
+        if (j >= wn) bad = true;
+        else {
+          sf[j] = f[e];
+          sp[j] = pos[e];
+        }
+      }
+  }
+  // (a window short of entries, or one off its window, leaves slots unwritten: flagged)
+  if (__syncthreads_or(bad)) {
+    if (tid == 0) atomicOr(&st->status, kStRank);
+    return;
+  }
+  for (unsigned j = tid; j < wn; j += kBT) {
+    fp_out[w0 + j] = sf[j];
+    pos_out[w0 + j] = sp[j];
+  }
 }
 
 // The replicated tail's outputs (global p in [g0, g0 + total), scratch index p - g0) that
@@ -755,7 +815,8 @@ void launch_bm_decide(const uint8_t* slice, uint64_t S, uint64_t* out, const Lev
 void launch_bm_level_end(int level, const uint64_t* g, const uint64_t* A, unsigned tb, uint64_t tiles, uint64_t* bits,
                          unsigned long long* tsum, unsigned long long* tbase, LevelState* st,
                          unsigned long long* gslot, unsigned long long* out_cnt, hipStream_t s) {
-  k_bm_tsum<<<(int)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4096)), kBT, 0, s>>>(level, g, A, tb, bits, tsum, st);
+  k_bm_tsum<<<(int)std::max<uint64_t>(1, std::min<uint64_t>((tiles + kBT / 64 - 1) / (kBT / 64), 4096)), kBT, 0, s>>>(
+      level, g, A, tb, bits, tsum, st);
   k_bm_tscan<<<1, kBTopT, 0, s>>>(level, tsum, tb, tbase, st, gslot, out_cnt);
 }
 
@@ -816,10 +877,11 @@ void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos
   auto go = [&](auto rt, auto stg, auto o20, auto xt) {
     using RT = decltype(rt);
     constexpr bool kSt = decltype(stg)::value, kO = decltype(o20)::value, kX = decltype(xt)::value;
-    const size_t lds = bm_tile_lds(tb, true) + (kSt ? kBmStage * sizeof(BmStaged) : 0);
+    const unsigned stage = kSt ? bm_stage_entries(tb, os.P) : 0u;
+    const size_t lds = bm_tile_lds(tb, true) + stage * sizeof(BmStaged);
     k_bm_tile_settle<RT, kSt, kO, kX><<<grid, kTT, lds, s>>>(level, static_cast<const RT*>(bucket), pos_base, tc,
                                                               bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
-                                                              next_cap, os, xs, o16);
+                                                              next_cap, os, xs, o16, stage);
   };
   using T_ = std::true_type;
   using F_ = std::false_type;

@@ -1787,7 +1787,12 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     }
     const bool in20 = l0p || bs.list20(L);  // R20 slots: P0's level 0, or a level whose list is R20
     launch_bm_tile_mark(L, bk, in20, tc, bcap, tb, tiles, st, wpad, d.bm_lanes, d.bm_a, lanes, S, s, xs);
-    if (lanes == kBmPlanes) {
+    const bool solo = lanes == kBmPlanes && P == 1;
+    if (solo) {
+      // one rank: its planes are the level's, merged straight into the final bits (no
+      // self-copies through the collectives)
+      launch_bm_merge(reinterpret_cast<const uint64_t*>(d.bm_lanes), S, 1, d.bm_g, st, s);
+    } else if (lanes == kBmPlanes) {
       // slice t's planes (2 S words) to rank t; rank q's planes of this rank's slice land at 2 S q
       for (int t = 0; t < P; ++t) {
         xoff[t] = 16 * S * (uint64_t)t;
@@ -1799,7 +1804,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
       cm.reduce_scatter_u8(d.bm_lanes, d.bm_slice, (lanes == kBmNibbles ? 32 : 64) * S, s);
       launch_bm_decide(d.bm_slice, S, d.bm_dec, st, lanes == kBmNibbles, s);
     }
-    cm.allgather(d.bm_dec, d.bm_g, 8 * S, s);
+    if (!solo) cm.allgather(d.bm_dec, d.bm_g, 8 * S, s);
     launch_bm_level_end(L, d.bm_g, d.bm_a, tb, tiles, c->bits, d.bm_tsum, d.bm_tbase, st, d.gslot, out_cnt, s);
     // the next level is a bitmap level too (else the replicated tail, which reads Rec): its
     // list goes out as R20 with identity positions (BinBuffers::l20)
