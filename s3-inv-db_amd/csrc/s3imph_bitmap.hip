@@ -169,9 +169,11 @@ __global__ __launch_bounds__(kBTopT) void k_bm_tscan(int level, const unsigned l
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   if (tid == 0) s_base = *out_cnt;
   unsigned long long v[kTsPer], sum = 0;
-  static_assert(kTsPer * kBTopT % kRound == 0 && kRound % kTsPer == 0, "tscan rounds");
 #pragma unroll
-  for (int r = 0; r < kTsPer * kBTopT / kRound; ++r) {
+  for (int q = 0; q < kTsPer; ++q) v[q] = 0;
+  static_assert(kTsPer * kBTopT % kRound == 0 && kRound % kTsPer == 0, "tscan rounds");
+  const int nr = (int)((T + kRound - 1) / kRound);  // rounds holding tiles (the rest are zeros)
+  for (int r = 0; r < nr; ++r) {
     for (int j = (int)tid; j < kRound; j += kBTopT) {
       const uint64_t i = (uint64_t)r * kRound + j;
       s_t[j] = i < T ? tsum[i] : 0ull;

@@ -168,6 +168,12 @@ void ev_collect(s3imph_ctx* c) {
   for (int i = 1; i < c->ev_used; ++i) {
     float ms = 0;
     HIPCHECK(hipEventElapsedTime(&ms, c->events[i - 1], c->events[i]));
+    // a stage marked more than once (a bitmap build's "levels", once per level) sums
+    const auto at = std::find(c->stage_names.begin(), c->stage_names.end(), c->ev_names[i]);
+    if (at != c->stage_names.end()) {
+      c->stage_ms[at - c->stage_names.begin()] += ms;
+      continue;
+    }
     c->stage_ms.push_back(ms);
     c->stage_names.push_back(c->ev_names[i]);
   }
@@ -980,6 +986,7 @@ void ensure_dist_small(s3imph_ctx* c) {
 // of d.small and the 256 spare words of the pinned stage.
 int dist_agree(s3imph_ctx* c, int rc, hipStream_t s, std::string* msg) {
   DistState& d = c->d;
+  if (d.nranks == 1) return rc;  // nothing to agree on (and no stream drain)
   constexpr int kCodes = 16;
   unsigned long long* h = d.h_pinned + kSmallWords;
   unsigned long long* dv = d.small + kSmallWords - 2 * kCodes;
@@ -1836,11 +1843,17 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   // ---- gather every rank's remaining records; all ranks finish the build identically,
   // the tail's outputs (global p in [N - total, N)) into scratch (kh / fp are free now)
   unsigned long long* M = d.h_pinned;
-  HIPCHECK(hipMemcpyAsync(d.small, &st->n[Ls], 8, hipMemcpyDeviceToDevice, s));
-  HIPCHECK(hipMemcpyAsync(d.small + 1, &st->status, 4, hipMemcpyDeviceToDevice, s));
-  HIPCHECK(hipMemsetAsync(reinterpret_cast<uint8_t*>(d.small + 1) + 4, 0, 4, s));
-  cm.allgather(d.small, d.small + 64, 16, s);
-  HIPCHECK(hipMemcpyAsync(M, d.small + 64, 16ull * P, hipMemcpyDeviceToHost, s));
+  if (P > 1) {
+    HIPCHECK(hipMemcpyAsync(d.small, &st->n[Ls], 8, hipMemcpyDeviceToDevice, s));
+    HIPCHECK(hipMemcpyAsync(d.small + 1, &st->status, 4, hipMemcpyDeviceToDevice, s));
+    HIPCHECK(hipMemsetAsync(reinterpret_cast<uint8_t*>(d.small + 1) + 4, 0, 4, s));
+    cm.allgather(d.small, d.small + 64, 16, s);
+    HIPCHECK(hipMemcpyAsync(M, d.small + 64, 16ull * P, hipMemcpyDeviceToHost, s));
+  } else {  // one rank: its own count and flags (no self-gather)
+    M[1] = 0;
+    HIPCHECK(hipMemcpyAsync(M, &st->n[Ls], 8, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipMemcpyAsync(M + 1, &st->status, 4, hipMemcpyDeviceToHost, s));
+  }
   HIPCHECK(hipStreamSynchronize(s));
   uint64_t total = 0, maxc = 0;
   unsigned flags = 0;
@@ -1870,8 +1883,8 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     const int rc = dist_agree(c, lrc, s, msg);
     if (rc != S3IMPH_OK) return rc;
   }
-  Rec* rl = c->list[(Ls - 1) & 1];
-  if (total) {
+  Rec* rl = c->list[(Ls - 1) & 1];  // (the last bitmap level's collided records: one rank's are all)
+  if (total && P > 1) {
     if ((uint64_t)P * maxc > d.cap_send) {
       dalloc(d.send, (uint64_t)P * maxc);
       d.cap_send = (uint64_t)P * maxc;
@@ -1896,18 +1909,21 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipMemcpyAsync(c->h_st, st, sizeof(LevelState), hipMemcpyDeviceToHost, s));
   HIPCHECK(hipMemcpyAsync(M, out_cnt, 8, hipMemcpyDeviceToHost, s));
+  if (P == 1) HIPCHECK(hipMemcpyAsync(M + 8, d.scnt, 8, hipMemcpyDeviceToHost, s));  // the exchange's counts
   HIPCHECK(hipStreamSynchronize(s));
-  const uint64_t n_out = M[0];
+  const uint64_t n_out = M[0], own1 = P == 1 ? M[8] : 0;
   // ---- every rank's flags, tail result and settled count
   {
     const LevelState& hs = *c->h_st;
     M[0] = hs.status;
     M[1] = hs.rank_total;
     M[2] = n_out;
-    HIPCHECK(hipMemcpyAsync(d.small, M, 24, hipMemcpyHostToDevice, s));
-    cm.allgather(d.small, d.small + 64, 24, s);
-    HIPCHECK(hipMemcpyAsync(M, d.small + 64, 24ull * P, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
+    if (P > 1) {
+      HIPCHECK(hipMemcpyAsync(d.small, M, 24, hipMemcpyHostToDevice, s));
+      cm.allgather(d.small, d.small + 64, 24, s);
+      HIPCHECK(hipMemcpyAsync(M, d.small + 64, 24ull * P, hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipStreamSynchronize(s));
+    }
   }
   uint64_t settled = 0;
   flags = 0;
@@ -1941,10 +1957,15 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   // ---- settled triples to the owners of their output slices: this rank's settled list is
   // sorted by p, so its run for slice t (d.scnt[t] records, counted by the settle) goes to
   // rank t as it lies; the own run is a hole (those keys were placed by the settle)
-  launch_set_u64(d.scnt + P, key_base, s);  // (scnt[P] is free here) every rank's key base, for the 16-B entries
-  cm.allgather(d.scnt, d.mat, 8ull * (P + 1), s);
-  HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, s));
-  HIPCHECK(hipStreamSynchronize(s));
+  if (P > 1) {
+    launch_set_u64(d.scnt + P, key_base, s);  // (scnt[P] is free here) every rank's key base, for the 16-B entries
+    cm.allgather(d.scnt, d.mat, 8ull * (P + 1), s);
+    HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+  } else {  // (read with the tail's state above)
+    M[0] = own1;
+    M[1] = key_base;
+  }
   std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
   uint64_t acc = 0, got = 0, sent = 0;
   std::vector<unsigned long long> tab(2 * (size_t)P);  // per sender: first received entry, key base
@@ -2476,7 +2497,8 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
         mph->buf = nullptr;
       }
     }
-    if (c->debug) {
+    static const bool phases = dev_env("S3IMPH_HOST_PHASES") != nullptr;  // the phase line without debug builds
+    if (c->debug || phases) {
       auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
       const auto tx = clk::now();
       std::fprintf(stderr,

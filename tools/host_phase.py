@@ -1,7 +1,8 @@
 """Phase split of the one-shot host-memory build (s3imph_build_host_into) on C2 (or [n] [avg]):
-the library's debug report (--debug: S3IMPH_DEBUG) times every phase from entry to return; this
-prints the Python wall of the same calls beside it, so the table sums to the wall.
-    python tools/host_phase.py [n] [avg] [--debug]"""
+the library's phase line times every phase from entry to return (--phases: the line alone,
+S3IMPH_HOST_PHASES, a developer knob; --debug: S3IMPH_DEBUG, with the kernels' profiling as well, which
+slows the build); this prints the Python wall of the same calls beside it, so the table sums to the wall.
+    python tools/host_phase.py [n] [avg] [--phases | --debug]"""
 import os
 import sys
 import time
@@ -9,6 +10,10 @@ import time
 if "--debug" in sys.argv:
     sys.argv.remove("--debug")
     os.environ["S3IMPH_DEBUG"] = "1"
+if "--phases" in sys.argv:
+    sys.argv.remove("--phases")
+    os.environ["S3IMPH_DEV"] = "1"
+    os.environ["S3IMPH_HOST_PHASES"] = "1"
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "s3-inv-db_amd"))
 import s3imph  # noqa: E402
 
