@@ -1496,9 +1496,10 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
   // (a skewed set, partitioned by k_scatter_res), or the runs its part of the hash blocks left
   // in their regions (prefix rp; record j of run i at region (b0 + i, sidx) + j - rp[i]).
   // regions: the fused partition of either level-0 hash (k_hash_skew's for a skewed set)
-  const bool regions = in.fused;
-  const unsigned NB = st->skew ? in.NB_skew : in.NB;
-  const uint64_t reg_cap = st->skew ? in.reg_cap_skew : in.reg_cap;
+  // (a list level's regions come from the previous level's settle, whatever the key lengths)
+  const bool regions = in.fused, skw = st->skew && level == 0;
+  const unsigned NB = skw ? in.NB_skew : in.NB;
+  const uint64_t reg_cap = skw ? in.reg_cap_skew : in.reg_cap;
   unsigned pre[kResShards + 1];
   uint64_t lo = 0, hi = 0;
   unsigned b0 = 0, nr = 0;
@@ -4115,8 +4116,8 @@ __global__ void k_set_status(LevelState* st, unsigned f) {
 }
 
 void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStream_t s, int level) {
-  const P0In in{p.sup, p.reg_cap, p.pcnt, (unsigned)kH0Grid, p.S, p0_skew_blocks(b.skew_cfg), p.reg_cap_skew,
-                p.sup_cap, p.scnt, fused};
+  const P0In in{p.sup, p.reg_cap, p.pcnt, p.nb ? p.nb : (unsigned)kH0Grid, p.S, p0_skew_blocks(b.skew_cfg),
+                p.reg_cap_skew, p.sup_cap, p.scnt, fused};
   // blocks per super-tile: a multiple of kResShards, so every shard slot of a tile takes the
   // records of the same number of blocks (9 blocks put 2/9 of a super-tile's records on one
   // shard: 1.8x the mean fill, past the slot capacity at S = 26)

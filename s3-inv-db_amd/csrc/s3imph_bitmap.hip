@@ -448,7 +448,9 @@ __device__ __forceinline__ void fp_out_own(const OwnSlice& os, uint64_t p, uint6
 // 2^kBmP0MaxTb positions): this rank's settled keys of a tile are staged in LDS (16 B each)
 // behind the tile words.  kO20: the collided records leave as R20 (k, f, p - pos_base), the
 // next bitmap level's list (BinBuffers::l20).  kX: positions from xs (the super-tile scatter's).
-template <class RT, bool kStaged, bool kO20, bool kX = false>
+// kPN: the collided records go to the next level's super-tile regions (NextPart) instead of
+// its list.
+template <class RT, bool kStaged, bool kO20, bool kX = false, bool kPN = false>
 __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __restrict__ bucket, uint64_t pos_base,
                                                         const unsigned* __restrict__ tc, uint64_t bucket_cap,
                                                         unsigned tb, LevelState* st, const uint64_t* __restrict__ g,
@@ -456,20 +458,35 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
                                                         const unsigned long long* __restrict__ tbase,
                                                         Rec* __restrict__ out, uint64_t out_cap,
                                                         Rec* __restrict__ next, uint64_t next_cap, OwnSlice os,
-                                                        const uint16_t* __restrict__ xs, bool o16, unsigned stage) {
+                                                        const uint16_t* __restrict__ xs, bool o16, unsigned stage,
+                                                        NextPart pn) {
   static_assert(!kStaged || sizeof(RT) != sizeof(Rec), "staged settles read R20 tiles");
   static_assert(!kX || kStaged, "x positions come with P0's R20 tiles");
+  static_assert(!kPN || kO20, "the next level's regions hold R20 records");
   extern __shared__ uint64_t bm_lds64[];
   __shared__ unsigned long long s_w[kTT / 64];
   __shared__ unsigned s_sc[kMaxRanks];
   __shared__ unsigned s_fo[kResShards + 1];
   __shared__ unsigned long long s_nb, s_tg, s_ta;
   __shared__ unsigned s_ncur;
-  if (bm_dead(st) || (st->status & kStStop)) return;
+  __shared__ unsigned p_cur[kPN ? kMaxRanks : 1];  // kPN: this block's fill of each next-level region
+  // kPN: a block that settles nothing still publishes empty regions (the next level's scatter
+  // reads every block's fills)
+  auto no_regions = [&]() {
+    if constexpr (kPN)
+      for (unsigned q = threadIdx.x; q < pn.S; q += kTT) pn.pcnt[(uint64_t)blockIdx.x * pn.S + q] = 0;
+  };
+  if (bm_dead(st) || (st->status & kStStop)) {
+    no_regions();
+    return;
+  }
   const uint64_t words = st->words[level], magic = st->magic[level], seed = level_seed(level);
   const uint64_t base = st->lvl_base[level];
   const uint64_t T = (64 * words + (1ull << tb) - 1) >> tb;
-  if (T == 0) return;
+  if (T == 0) {
+    no_regions();
+    return;
+  }
   const unsigned W = 1u << (tb - 6), G = W / kGrp;  // words, groups of a tile
   uint64_t* sg = bm_lds64;
   uint64_t* sga = sg + W;
@@ -479,8 +496,20 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
   constexpr int kGper = 2;  // groups per thread in the tile scan (G <= 2048)
-  bool over = false;
+  bool over = false, rover = false;
   if (tid < (unsigned)kMaxRanks) s_sc[tid] = 0;  // (the first tile's barriers order it before use)
+  // kPN: level L + 1's geometry, from its global size (this level's tile scan wrote it)
+  uint64_t w1 = 0, m1 = 0, seed1 = 0;
+  uint32_t pmul = 0;
+  unsigned rcap = 0;
+  if constexpr (kPN) {
+    if (tid < (unsigned)kMaxRanks) p_cur[tid] = 0;
+    w1 = level_words(*pn.gnext);
+    m1 = level_magic(w1);
+    seed1 = level_seed(level + 1);
+    pmul = 0xffffffffu / pn.tps_sub + 1;  // exact for (position >> 14) < 2^18 (as the hash's partition)
+    rcap = (unsigned)pn.reg_cap;
+  }
   for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
     const uint64_t w0 = t * W;
     const unsigned nw = (unsigned)min<uint64_t>(W, words - w0);
@@ -610,6 +639,17 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
             else
               over = true;
           }
+        } else if constexpr (kPN) {  // into this block's region of its level-(L+1) super-tile
+          const uint64_t x1 = bb_index(seed1, r[u].k, w1, m1);
+          unsigned sp = __umulhi((uint32_t)(x1 >> kRegTileMaxBits), pmul);
+          if (sp >= pn.S) sp = pn.S - 1;  // unreachable: positions < 64 w1
+          const unsigned at = atomicAdd(&p_cur[sp], 1u);
+          if (at < rcap)
+            pn.sup[((uint64_t)blockIdx.x * pn.S + sp) * rcap + at] =
+                R20{{(uint32_t)r[u].k, (uint32_t)(r[u].k >> 32), (uint32_t)r[u].f, (uint32_t)(r[u].f >> 32),
+                     (uint32_t)(r[u].p - pos_base)}};
+          else
+            rover = true;
         } else {
           const uint64_t slot = nb + wave_slot(&s_ncur);
           if (slot >= next_cap) over = true;
@@ -644,6 +684,10 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
   }
   if (tid < (unsigned)os.P && s_sc[tid]) atomicAdd(&os.scnt[tid], (unsigned long long)s_sc[tid]);
   if (over) atomicOr(&st->status, kStOverflow);
+  if constexpr (kPN) {  // (the tile loop ended on a barrier: every append is in p_cur)
+    for (unsigned q = tid; q < pn.S; q += kTT) pn.pcnt[(uint64_t)blockIdx.x * pn.S + q] = min(p_cur[q], rcap);
+    if (rover) atomicOr(&st->status, kStResOverflow);  // a region overflowed: the build reruns
+  }
 }
 
 // Bitmap levels cover the level's whole position range on every rank (the routed build's
@@ -653,6 +697,10 @@ __global__ void k_bm_range(LevelState* st, int level) {
     st->wlo[level] = 0;
     st->rw[level] = st->words[level];
   }
+}
+
+__global__ void k_bm_flag(LevelState* st, unsigned f) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) atomicOr(&st->status, f);
 }
 
 // The level's true size against the host's bound (words_L <= wmax), after k_dist_setup.
@@ -840,10 +888,14 @@ void bm_set_lds_limits() {
   static_assert(((size_t)1 << (kBmP0MaxTb - 6)) * 18 + kBmStage * sizeof(BmStaged) <= 160 * 1024, "staged settle LDS");
   for (const void* k : {(const void*)k_bm_tile_settle<R20, true, false>, (const void*)k_bm_tile_settle<R20, true, true>,
                         (const void*)k_bm_tile_settle<R20, true, false, true>,
-                        (const void*)k_bm_tile_settle<R20, true, true, true>})
+                        (const void*)k_bm_tile_settle<R20, true, true, true>,
+                        (const void*)k_bm_tile_settle<R20, true, true, false, true>,
+                        (const void*)k_bm_tile_settle<R20, true, true, true, true>})
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)(bm_tile_lds(kBmP0MaxTb, true) + kBmStage * sizeof(BmStaged)));
 }
+
+void launch_bm_flag(LevelState* st, unsigned flags, hipStream_t s) { k_bm_flag<<<1, 64, 0, s>>>(st, flags); }
 
 void launch_bm_range(LevelState* st, int level, hipStream_t s) { k_bm_range<<<1, 64, 0, s>>>(st, level); }
 
@@ -870,31 +922,41 @@ void launch_bm_merge(const uint64_t* recv, uint64_t S, int P, uint64_t* out, con
   k_bm_merge<<<grid_for(S, kBT, 8192), kBT, 0, s>>>(recv, S, P, out, st);
 }
 
+unsigned bm_settle_grid(uint64_t tiles) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1024)); }
+
 void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos_base, const unsigned* tc,
                            uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
                            const uint64_t* A, const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next,
                            uint64_t next_cap, bool next20, const OwnSlice& os, hipStream_t s, bool staged,
-                           const uint16_t* xs, bool o16) {
-  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1024));
-  auto go = [&](auto rt, auto stg, auto o20, auto xt) {
+                           const uint16_t* xs, bool o16, const NextPart* np) {
+  const int grid = (int)bm_settle_grid(tiles);
+  const NextPart pn = np ? *np : NextPart{};
+  auto go = [&](auto rt, auto stg, auto o20, auto xt, auto pt) {
     using RT = decltype(rt);
-    constexpr bool kSt = decltype(stg)::value, kO = decltype(o20)::value, kX = decltype(xt)::value;
+    constexpr bool kSt = decltype(stg)::value, kO = decltype(o20)::value, kX = decltype(xt)::value,
+                   kP = decltype(pt)::value;
     const unsigned stage = kSt ? bm_stage_entries(tb, os.P) : 0u;
     const size_t lds = bm_tile_lds(tb, true) + stage * sizeof(BmStaged);
-    k_bm_tile_settle<RT, kSt, kO, kX><<<grid, kTT, lds, s>>>(level, static_cast<const RT*>(bucket), pos_base, tc,
-                                                              bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
-                                                              next_cap, os, xs, o16, stage);
+    k_bm_tile_settle<RT, kSt, kO, kX, kP><<<grid, kTT, lds, s>>>(level, static_cast<const RT*>(bucket), pos_base, tc,
+                                                                  bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
+                                                                  next_cap, os, xs, o16, stage, pn);
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
   // R20 tiles holding ~8k of this rank's records (the caller's `staged`: 2^14 positions per
   // rank, at most kBmP0MaxTb) stage their settled keys; larger tiles and Rec buckets write
-  // them directly
+  // them directly.  np (staged R20 levels whose next level is an R20 super-tile level): the
+  // collided records into that level's regions.
   staged = staged && r20 && tb <= kBmP0MaxTb;
-  if (staged && xs) next20 ? go(R20{}, T_{}, T_{}, T_{}) : go(R20{}, T_{}, F_{}, T_{});
-  else if (staged) next20 ? go(R20{}, T_{}, T_{}, F_{}) : go(R20{}, T_{}, F_{}, F_{});
-  else if (r20) next20 ? go(R20{}, F_{}, T_{}, F_{}) : go(R20{}, F_{}, F_{}, F_{});
-  else next20 ? go(Rec{}, F_{}, T_{}, F_{}) : go(Rec{}, F_{}, F_{}, F_{});
+  if (np && !(staged && next20)) {  // (the host never asks for it) the next level would read no regions: rerun
+    k_bm_flag<<<1, 64, 0, s>>>(st, kStGeometry);
+    return;
+  }
+  if (np) xs ? go(R20{}, T_{}, T_{}, T_{}, T_{}) : go(R20{}, T_{}, T_{}, F_{}, T_{});
+  else if (staged && xs) next20 ? go(R20{}, T_{}, T_{}, T_{}, F_{}) : go(R20{}, T_{}, F_{}, T_{}, F_{});
+  else if (staged) next20 ? go(R20{}, T_{}, T_{}, F_{}, F_{}) : go(R20{}, T_{}, F_{}, F_{}, F_{});
+  else if (r20) next20 ? go(R20{}, F_{}, T_{}, F_{}, F_{}) : go(R20{}, F_{}, F_{}, F_{}, F_{});
+  else next20 ? go(Rec{}, F_{}, T_{}, F_{}, F_{}) : go(Rec{}, F_{}, F_{}, F_{}, F_{});
 }
 
 

@@ -557,8 +557,9 @@ uint64_t p0_super_tiles(uint64_t T, uint64_t target) {
 // in S super-tiles of tps (about kP0TargetTps; S <= kP0MaxS), the super-tiles' records in
 // c->p0_sup (sized for the hash's per-block regions and for the slot layout of the pass that
 // stands in for it), the tiles' slots in the bucket, both as R20.
-P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s, unsigned tb = kRegTileMaxBits,
-               bool want_x = false) {
+// The geometry alone (no allocation, no memset): what p0_bufs takes for the same arguments,
+// and the R20 records c->p0_sup must hold for it
+P0Bufs p0_geom(const s3imph_ctx* c, uint64_t n, uint64_t n_geom, unsigned tb, uint64_t* need) {
   const uint64_t T = tiles_of(level_words(n_geom), tb, 0);
   P0Bufs p;
   p.tb = tb;
@@ -571,9 +572,17 @@ P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s, unsign
   p.reg_cap = p0_region_cap(n, p.S, kH0GridHost);
   const unsigned nbs = p0_skew_blocks(c->skew_cfg);
   p.reg_cap_skew = p0_region_cap(n, p.S, nbs);
-  const uint64_t need = std::max<uint64_t>(std::max<uint64_t>((uint64_t)kH0GridHost * p.S * p.reg_cap,
-                                                              (uint64_t)nbs * p.S * p.reg_cap_skew),
-                                           n + n / 4 + (uint64_t)4096 * p.S * kResShards);
+  *need = std::max<uint64_t>(std::max<uint64_t>((uint64_t)kH0GridHost * p.S * p.reg_cap,
+                                                (uint64_t)nbs * p.S * p.reg_cap_skew),
+                             n + n / 4 + (uint64_t)4096 * p.S * kResShards);
+  return p;
+}
+
+P0Bufs p0_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s, unsigned tb = kRegTileMaxBits,
+               bool want_x = false) {
+  const uint64_t T = tiles_of(level_words(n_geom), tb, 0);
+  uint64_t need = 0;
+  P0Bufs p = p0_geom(c, n, n_geom, tb, &need);
   // (a capacity is zeroed before its buffer is replaced and set only once the allocation
   // succeeded: a NOMEM leaves a null buffer that the next build reallocates, never one that a
   // smaller build would take as big enough)
@@ -1642,6 +1651,16 @@ void free_bm_workspace(DistState& d) {
 // spread over a 4x larger window per tile (1.88 -> 3.64 ms).
 // Tile bits at which a rank holds ~8k records of a bitmap level's tile (2^14 at one rank, as a
 // single GPU's register tile): 14 + floor(lg P), at most kBmP0MaxTb
+// The bitmap settle partitioning the next level's records into its super-tile regions
+// (NextPart; A/B knob S3IMPH_BM_FEED=0: the partition pass over the list instead)
+bool bm_feed_next() {
+  static const bool v = [] {
+    const char* e = dev_env("S3IMPH_BM_FEED");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+
 unsigned bm_dense_tb(int P) {
   unsigned tb = kBmMinTb;
   for (int q = 2; q <= P && tb < kBmP0MaxTb; q *= 2) ++tb;
@@ -1745,6 +1764,11 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   const int lanes = c->bm_counts ? (P <= kBmNibRanks ? kBmNibbles : kBmBytes) : kBmPlanes;
   std::vector<uint64_t> xoff(P), xbytes(P);
   int L = 0;
+  // this level's records were partitioned into its super-tiles' regions by the previous level's
+  // settle (NextPart): fed_nb settle blocks' regions of fed_rc records
+  bool fed = false;
+  uint64_t fed_rc = 0;
+  unsigned fed_nb = 0;
   for (;;) {
     const uint64_t wmax = level_words((uint64_t)std::ceil(nb)), S = (wmax + P - 1) / P, wpad = S * (uint64_t)P;
     // tiles of 2^tb positions: from the dense size (a rank's ~8k records), the smallest
@@ -1781,15 +1805,24 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
       xs = pb.x;
     } else if (lp) {
       if (c->debug)
-        std::fprintf(stderr, "[s3imph] rank %d bitmap: level %d through P0 super-tiles (%llu tiles of 2^%u)\n", R, L,
-                     (unsigned long long)tiles, tb);
-      launch_p0_partition_list(L, bs, pl, s);
-      launch_p0_scatter(bs, pl, false, s, L);
+        std::fprintf(stderr, "[s3imph] rank %d bitmap: level %d through P0 super-tiles (%llu tiles of 2^%u%s)\n", R, L,
+                     (unsigned long long)tiles, tb, fed ? ", partitioned by the previous settle" : "");
+      if (fed) {  // the regions are in place: straight to the tiles
+        pl.reg_cap = fed_rc;
+        pl.nb = fed_nb;
+        launch_p0_scatter(bs, pl, true, s, L);
+      } else {
+        launch_p0_partition_list(L, bs, pl, s);
+        launch_p0_scatter(bs, pl, false, s, L);
+      }
       bk = pl.bucket;
       bcap = pl.bucket_cap;
       tc = pl.tcnt;
       xs = pl.x;
     } else {
+      // (a level fed by regions always takes P0 with the geometry its feeder used; a failed
+      // allocation here leaves its records in those regions: the build reruns)
+      if (fed) launch_bm_flag(st, kStResOverflow, s);
       launch_binned_scatter_res(L, bs, g, gsr, s, 0, 0, tiles);
     }
     const bool in20 = l0p || bs.list20(L);  // R20 slots: P0's level 0, or a level whose list is R20
@@ -1821,9 +1854,35 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     if (next20) bs.l20 |= 1u << (L + 1);
     c->l20_mask = bs.l20;  // dist_classify_stop reads a stop level's list in this format
     // R20 tiles at the dense size stage their settled keys (each rank's ~8k records a tile)
+    const bool staged = tb <= tbd || l0p;
+    // the next level through the P0 super-tiles: its records go from this settle straight into
+    // its super-tiles' regions (level L + 1's exact size is known now: the tile scan wrote it),
+    // when its geometry is known to fit the buffers it will take (no reallocation under them)
+    NextPart npart{};
+    bool feed = false;
+    uint64_t rc1 = 0;
+    unsigned nb1 = 0;
+    if (more && next20 && staged && in20 && c->p0 && bm_feed_next()) {
+      const uint64_t ng1 = (uint64_t)std::ceil(nbn), Td1 = tiles_of(level_words(ng1), tbd, 0);
+      if (Td1 > bm_target_tiles() && Td1 <= kBmMaxTiles) {
+        const uint64_t np1 = (uint64_t)(npred * q * 1.1) + 4096;
+        uint64_t need1 = 0;
+        const P0Bufs g1 = p0_geom(c, np1, ng1, tbd, &need1);
+        nb1 = bm_settle_grid(tiles);
+        rc1 = p0_region_cap(np1, g1.S, nb1);
+        if (g1.S <= (unsigned)kMaxRanks && c->p0_sup && c->p0_pcnt &&
+            std::max<uint64_t>(need1, (uint64_t)nb1 * g1.S * rc1) <= c->p0_sup_cap) {
+          npart = NextPart{c->p0_sup, rc1, c->p0_pcnt, g1.tps_sub(), g1.S, d.gslot + L + 1};
+          feed = true;
+        }
+      }
+    }
     launch_bm_tile_settle(L, bk, in20, key_base, tc, bcap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
                           out16 ? d.bm_cap_out * sizeof(Rec) / sizeof(BmT16) : d.bm_cap_out, c->list[L & 1], d.cap_list,
-                          next20, own_slice, s, tb <= tbd || l0p, xs, out16);
+                          next20, own_slice, s, staged, xs, out16, feed ? &npart : nullptr);
+    fed = feed;
+    fed_rc = rc1;
+    fed_nb = nb1;
     ev_mark(c, s, L == 0 ? "level0" : "levels");
     if (c->debug) {  // the level's device status as it ends (a flag's level, for the report)
       unsigned long long* M = d.h_pinned;

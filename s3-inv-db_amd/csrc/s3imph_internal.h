@@ -290,6 +290,8 @@ struct P0Bufs {
   // positions per tile (up to kBmP0MaxTb), so a rank's share of a tile stays ~8k records
   unsigned tb = kRegTileMaxBits;
   uint16_t* x = nullptr;       // bitmap decomposition: each slot's position in its tile (the mark's input)
+  unsigned nb = 0;             // the regions' producer blocks (0: the level-0 hash's grid; a bitmap
+                               // list level fed by the previous settle: its grid, NextPart)
   // super-tiles in 2^14-position units (tps tiles of 2^tb): the partition passes cut
   // (position >> 14) by this, so they need not know tb
   unsigned tps_sub() const { return tps << (tb - kRegTileMaxBits); }
@@ -412,11 +414,25 @@ struct OwnSlice {
   uint64_t *fp_out, *pos_out;
   unsigned long long* scnt;
 };
+// A bitmap level's settle partitioning its collided records straight into the NEXT level's
+// super-tile regions, as the level-0 hash does for level 0 (the next level then skips
+// launch_p0_partition_list): R20 records in per-(settle block, super-tile) regions of reg_cap,
+// fills to pcnt[block][S].  The next level's exact size is known by then: gnext, its global key
+// count, is written by this level's tile scan, which runs before the settle.
+struct NextPart {
+  R20* sup = nullptr;
+  uint64_t reg_cap = 0;
+  unsigned* pcnt = nullptr;
+  unsigned tps_sub = 0, S = 0;  // super-tiles in 2^14-position units (P0Bufs::tps_sub), their count
+  const unsigned long long* gnext = nullptr;
+};
+unsigned bm_settle_grid(uint64_t tiles);  // the settle's blocks (the regions' producers)
+void launch_bm_flag(LevelState* st, unsigned flags, hipStream_t s);  // or device status flags
 void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos_base, const unsigned* tc,
                            uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
                            const uint64_t* A, const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next,
                            uint64_t next_cap, bool next20, const OwnSlice& os, hipStream_t s, bool staged = false,
-                           const uint16_t* xs = nullptr, bool o16 = false);
+                           const uint16_t* xs = nullptr, bool o16 = false, const NextPart* np = nullptr);
 // a settled key crossing to its output slice's owner with identity positions (16 B instead
 // of a 24-B Rec): p - the slice's first p, the sending rank's key index, the fingerprint
 struct BmT16 {
