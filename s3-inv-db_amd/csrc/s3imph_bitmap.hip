@@ -312,9 +312,23 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
   }
   if (T == 0) return;
   const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
+  // a tile's slot fills come in one tile ahead (lanes 0-7 of wave 0), during the previous
+  // tile's writes: a tile starts without a round trip of its own
+  const unsigned lane = lane_id();
+  unsigned nfill = 0;
+  if (tid < (unsigned)kResShards && blockIdx.x < T) nfill = tc[(uint64_t)blockIdx.x * kResShards + tid];
   for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
     for (unsigned j = tid; j < W32; j += kTT) sA[j] = sC[j] = 0;
-    if (tid == 0) shard_prefix(tc, t, s_fo);
+    if (tid < 64) {
+      unsigned xf = tid < (unsigned)kResShards ? nfill : 0u;  // inclusive prefix over lanes 0-7
+#pragma unroll
+      for (int d = 1; d < kResShards; d <<= 1) {
+        const unsigned y = __shfl_up(xf, d);
+        if (lane >= (unsigned)d) xf += y;
+      }
+      if (tid < (unsigned)kResShards) s_fo[tid] = xf - nfill;
+      if (tid == (unsigned)kResShards - 1) s_fo[kResShards] = xf;
+    }
     __syncthreads();
     unsigned fo[kResShards + 1];
 #pragma unroll
@@ -350,28 +364,42 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
       }
     }
     __syncthreads();
-    // the tile's lanes and A words (positions below 64 words only)
+    {  // the next tile's fills, in flight over this tile's writes
+      const uint64_t tn = t + gridDim.x;
+      if (tid < (unsigned)kResShards && tn < T) nfill = tc[tn * kResShards + tid];
+    }
+    // the tile's lanes and A words (positions below 64 words only); planes and A as whole u64
+    // words (t0 is a multiple of 2^14: a pair of u32 words is one u64 word of its slice)
     const uint64_t wend = min<uint64_t>((uint64_t)W32, (64 * words - t0 + 31) / 32);
-    for (unsigned j = tid; j < wend; j += kTT) {
-      const uint32_t a = sA[j], c = sC[j];
-      A32[(t0 >> 5) + j] = a;
-      if (kMode == kBmPlanes) {  // u32 half (g32 & 1) of u64 word g32 >> 1, in its slice's planes
-        const uint64_t g32 = (t0 >> 5) + j, w = g32 >> 1, sl = owner_of(w, S, mS), jw = w - sl * S;
-        uint32_t* ac32 = reinterpret_cast<uint32_t*>(lanes);
-        ac32[2 * (2 * S * sl + jw) + (g32 & 1)] = a;
-        ac32[2 * (2 * S * sl + S + jw) + (g32 & 1)] = c;
-      } else if (kNib) {  // 32 lanes in 16 bytes
-        uint4* dst = reinterpret_cast<uint4*>(lanes + t0 / 2 + 16ull * j);
-        dst[0] = make_uint4(spread8n(a) + spread8n(c), spread8n(a >> 8) + spread8n(c >> 8),
-                            spread8n(a >> 16) + spread8n(c >> 16), spread8n(a >> 24) + spread8n(c >> 24));
-      } else {
-        uint4* dst = reinterpret_cast<uint4*>(lanes + t0 + 32ull * j);
+    if (kMode == kBmPlanes) {
+      uint64_t* ac = reinterpret_cast<uint64_t*>(lanes);
+      uint64_t* A64 = reinterpret_cast<uint64_t*>(A32);
+      for (unsigned jp = tid; 2 * jp < wend; jp += kTT) {
+        const unsigned j = 2 * jp;
+        const uint64_t a = (uint64_t)sA[j] | ((uint64_t)(j + 1 < wend ? sA[j + 1] : 0u) << 32);
+        const uint64_t c = (uint64_t)sC[j] | ((uint64_t)(j + 1 < wend ? sC[j + 1] : 0u) << 32);
+        const uint64_t w = (t0 >> 6) + jp, sl = owner_of(w, S, mS), jw = w - sl * S;
+        A64[w] = a;
+        ac[2 * S * sl + jw] = a;
+        ac[2 * S * sl + S + jw] = c;
+      }
+    } else {
+      for (unsigned j = tid; j < wend; j += kTT) {
+        const uint32_t a = sA[j], c = sC[j];
+        A32[(t0 >> 5) + j] = a;
+        if (kNib) {  // 32 lanes in 16 bytes
+          uint4* dst = reinterpret_cast<uint4*>(lanes + t0 / 2 + 16ull * j);
+          dst[0] = make_uint4(spread8n(a) + spread8n(c), spread8n(a >> 8) + spread8n(c >> 8),
+                              spread8n(a >> 16) + spread8n(c >> 16), spread8n(a >> 24) + spread8n(c >> 24));
+        } else {
+          uint4* dst = reinterpret_cast<uint4*>(lanes + t0 + 32ull * j);
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {  // bytes 16q .. 16q + 15 of this word's 32 lanes
-          const uint32_t as = a >> (16 * q), cs = c >> (16 * q);
-          dst[q] = make_uint4(spread4(as & 15u) + spread4(cs & 15u), spread4((as >> 4) & 15u) + spread4((cs >> 4) & 15u),
-                              spread4((as >> 8) & 15u) + spread4((cs >> 8) & 15u),
-                              spread4((as >> 12) & 15u) + spread4((cs >> 12) & 15u));
+          for (int q = 0; q < 2; ++q) {  // bytes 16q .. 16q + 15 of this word's 32 lanes
+            const uint32_t as = a >> (16 * q), cs = c >> (16 * q);
+            dst[q] = make_uint4(spread4(as & 15u) + spread4(cs & 15u), spread4((as >> 4) & 15u) + spread4((cs >> 4) & 15u),
+                                spread4((as >> 8) & 15u) + spread4((cs >> 8) & 15u),
+                                spread4((as >> 12) & 15u) + spread4((cs >> 12) & 15u));
+          }
         }
       }
     }
@@ -510,9 +538,18 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
     pmul = 0xffffffffu / pn.tps_sub + 1;  // exact for (position >> 14) < 2^18 (as the hash's partition)
     rcap = (unsigned)pn.reg_cap;
   }
+  unsigned long long coll = 0;  // kPN: this block's collided records (one atomic at the end)
   for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
     const uint64_t w0 = t * W;
     const unsigned nw = (unsigned)min<uint64_t>(W, words - w0);
+    // the tile's slot fills (lanes 0-7 of wave 0) and its two bases (lanes 8-9), requested
+    // before its bit words so that both round trips overlap
+    unsigned mfill = 0;
+    unsigned long long mbase = 0;
+    if (wave == 0) {
+      if (lane < (unsigned)kResShards) mfill = tc[t * kResShards + lane];
+      else if (lane < (unsigned)kResShards + 2) mbase = tbase[2 * t + (lane - kResShards)];
+    }
     unsigned long long c[kGper], sum = 0;
 #pragma unroll
     for (int q = 0; q < kGper; ++q) {
@@ -570,13 +607,26 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
       }
       ex += c[q];
     }
-    if (tid == 0) {
-      shard_prefix(tc, t, s_fo);
-      const unsigned nrec = s_fo[kResShards], placed = (unsigned)tot;
-      s_nb = nrec > placed ? atomicAdd(&st->n[level + 1], (unsigned long long)(nrec - placed)) : 0ull;
-      s_ncur = 0;
-      s_tg = tbase[2 * t];
-      s_ta = tbase[2 * t + 1];
+    if (wave == 0) {
+      unsigned xf = lane < (unsigned)kResShards ? mfill : 0u;  // inclusive prefix over lanes 0-7
+#pragma unroll
+      for (int d = 1; d < kResShards; d <<= 1) {
+        const unsigned y = __shfl_up(xf, d);
+        if (lane >= (unsigned)d) xf += y;
+      }
+      if (lane < (unsigned)kResShards) s_fo[lane] = xf - mfill;
+      if (lane == (unsigned)kResShards - 1) s_fo[kResShards] = xf;
+      if (lane == (unsigned)kResShards) s_tg = mbase;
+      if (lane == (unsigned)kResShards + 1) s_ta = mbase;
+      const unsigned nrec = __shfl(xf, kResShards - 1), placed = (unsigned)tot;
+      if (lane == 0) {
+        if constexpr (kPN) {
+          coll += nrec > placed ? nrec - placed : 0u;
+        } else {
+          s_nb = nrec > placed ? atomicAdd(&st->n[level + 1], (unsigned long long)(nrec - placed)) : 0ull;
+        }
+        s_ncur = 0;
+      }
     }
     __syncthreads();
     unsigned fo[kResShards + 1];
@@ -685,6 +735,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
   if (tid < (unsigned)os.P && s_sc[tid]) atomicAdd(&os.scnt[tid], (unsigned long long)s_sc[tid]);
   if (over) atomicOr(&st->status, kStOverflow);
   if constexpr (kPN) {  // (the tile loop ended on a barrier: every append is in p_cur)
+    if (tid == 0 && coll) atomicAdd(&st->n[level + 1], coll);  // this rank's records of level L + 1
     for (unsigned q = tid; q < pn.S; q += kTT) pn.pcnt[(uint64_t)blockIdx.x * pn.S + q] = min(p_cur[q], rcap);
     if (rover) atomicOr(&st->status, kStResOverflow);  // a region overflowed: the build reruns
   }
