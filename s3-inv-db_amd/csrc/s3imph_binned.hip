@@ -629,22 +629,13 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
         }
       }
       __syncthreads();
-      R20* stg = reinterpret_cast<R20*>(sw);
-      unsigned char* sdst = reinterpret_cast<unsigned char*>(stg + G);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        if (rv[h]) {
-          const unsigned slot = r_start[od[h]] + ork[h];
-          stg[slot] = r20_make(ra[h], rb[h], (uint32_t)(r0 + rj[h]));
-          sdst[slot] = (unsigned char)od[h];
-        }
-      __syncthreads();
+      // each record straight to its slot of the round's run in its region (the run is one
+      // contiguous range, written whole by the block within the round)
       if (!r_over) {
         R20* const blk = pt.sup + (uint64_t)__builtin_amdgcn_readfirstlane(bid) * pt.S * pt.reg_cap;
-        for (unsigned j = tid; j < m; j += NT) {
-          const unsigned o = sdst[j];
-          blk[r_off[o] + (j - r_start[o])] = stg[j];
-        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (rv[h]) blk[r_off[od[h]] + ork[h]] = r20_make(ra[h], rb[h], (uint32_t)(r0 + rj[h]));
       }
     }
     unsigned long long ptb = prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -922,31 +913,34 @@ __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
-      // results by key in LDS, written back in key order with coalesced stores (each lane's
-      // own 8-byte stores cost more: they count against vmcnt, which every step waits on,
-      // 1.64 -> 2.11 ms on C5 even with 8192-key groups in the freed LDS)
       if (cur.valid) {
-        res_a[cur.k] = (uint64_t)alo | ((uint64_t)ahi << 32);
-        res_b[cur.k] = (uint64_t)blo | ((uint64_t)bhi << 32);
+        const uint64_t a = (uint64_t)alo | ((uint64_t)ahi << 32), f = (uint64_t)blo | ((uint64_t)bhi << 32);
+        if (part) {
+          // the key's record to its super-tile region right after its last chunk, while the
+          // next batch's first chunk is in flight (at the group's end, after its barrier, this
+          // phase ran with no hashing beside it)
+          zero |= a == 0;
+          const uint64_t x = bb_index(level_seed(0), a, p_words, p_magic);
+          unsigned od = __umulhi((uint32_t)(x >> kRegTileMaxBits), p_mul);
+          if (od >= pt.S) od = pt.S - 1;  // unreachable: positions < 64 words
+          const unsigned at = atomicAdd(&sk_pcur[od], 1u);
+          if (at < (unsigned)pt.reg_cap)
+            pt.sup[((uint64_t)blockIdx.x * pt.S + od) * pt.reg_cap + at] = r20_make(a, f, (uint32_t)(grp + cur.k));
+          else
+            p_over = true;
+        } else {
+          // results by key in LDS, written back in key order with coalesced stores (each
+          // lane's own 8-byte stores cost more: they count against vmcnt, which every step
+          // waits on, 1.64 -> 2.11 ms on C5 even with 8192-key groups in the freed LDS)
+          res_a[cur.k] = a;
+          res_b[cur.k] = f;
+        }
       }
       cur = nxt;
     }
     const unsigned long long e0t = prof ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();
-    if (part) {
-      for (unsigned k = tid; k < m; k += kSkT) {
-        const uint64_t a = res_a[k];
-        zero |= a == 0;
-        const uint64_t x = bb_index(level_seed(0), a, p_words, p_magic);
-        unsigned od = __umulhi((uint32_t)(x >> kRegTileMaxBits), p_mul);
-        if (od >= pt.S) od = pt.S - 1;  // unreachable: positions < 64 words
-        const unsigned at = atomicAdd(&sk_pcur[od], 1u);
-        if (at < (unsigned)pt.reg_cap)
-          pt.sup[((uint64_t)blockIdx.x * pt.S + od) * pt.reg_cap + at] = r20_make(a, res_b[k], (uint32_t)(grp + k));
-        else
-          p_over = true;
-      }
-    } else {
+    if (!part) {
       for (unsigned k = tid; k < m; k += kSkT) {
         const uint64_t a = res_a[k];
         kh[grp + k] = a;
