@@ -2226,11 +2226,22 @@ struct D2HJob {
   uint64_t bytes;  // device bytes
   int conv;        // 0 copy, 2 widen u32 -> u64
 };
+// D2H chunk bytes (<= kStageChunk; A/B knob S3IMPH_D2H_CHUNK in MiB)
+uint64_t d2h_chunk() {
+  static const uint64_t v = [] {
+    const char* e = dev_env("S3IMPH_D2H_CHUNK");
+    const uint64_t m = e ? std::strtoull(e, nullptr, 10) : 0;
+    return m ? std::min<uint64_t>(m << 20, kStageChunk) : kStageChunk;
+  }();
+  return v;
+}
+
 void staged_d2h(s3imph_ctx* c, const std::vector<D2HJob>& jobs) {
   stager_init(c);
   Stager& g = c->stager;
+  const uint64_t chunk = d2h_chunk();
   std::vector<uint64_t> first(jobs.size() + 1, 0);  // first global chunk of each job
-  for (size_t j = 0; j < jobs.size(); ++j) first[j + 1] = first[j] + (jobs[j].bytes + kStageChunk - 1) / kStageChunk;
+  for (size_t j = 0; j < jobs.size(); ++j) first[j + 1] = first[j] + (jobs[j].bytes + chunk - 1) / chunk;
   const uint64_t nch = first.back();
   if (!nch) return;
   const int nw = (int)std::min<uint64_t>(kStageWorkers, nch);
@@ -2241,7 +2252,7 @@ void staged_d2h(s3imph_ctx* c, const std::vector<D2HJob>& jobs) {
       auto job = [&](uint64_t ch) { return (size_t)(std::upper_bound(first.begin(), first.end(), ch) - first.begin() - 1); };
       auto issue = [&](uint64_t ch, int buf) {
         const D2HJob& J = jobs[job(ch)];
-        const uint64_t off = (ch - first[job(ch)]) * kStageChunk, len = std::min(kStageChunk, J.bytes - off);
+        const uint64_t off = (ch - first[job(ch)]) * chunk, len = std::min(chunk, J.bytes - off);
         HIPCHECK(hipMemcpyAsync(g.pin[w][buf], static_cast<const uint8_t*>(J.src) + off, len, hipMemcpyDeviceToHost,
                                 g.st[w]));
         HIPCHECK(hipEventRecord(g.ev[w][buf], g.st[w]));
@@ -2252,7 +2263,7 @@ void staged_d2h(s3imph_ctx* c, const std::vector<D2HJob>& jobs) {
         if (ch + nw < nch) issue(ch + nw, b ^ 1);
         HIPCHECK(hipEventSynchronize(g.ev[w][b]));
         const D2HJob& J = jobs[job(ch)];
-        const uint64_t off = (ch - first[job(ch)]) * kStageChunk, len = std::min(kStageChunk, J.bytes - off);
+        const uint64_t off = (ch - first[job(ch)]) * chunk, len = std::min(chunk, J.bytes - off);
         if (J.conv == 2) {
           const uint32_t* s32 = static_cast<const uint32_t*>(g.pin[w][b]);
           uint64_t* d64 = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(J.dst) + 2 * off);

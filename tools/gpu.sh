@@ -20,6 +20,8 @@
 #   bash tools/gpu.sh TAG lib REPS CFG            old / new library A/B (abx/libs3imph_{old,new}.so,
 #                                                 alternating) -> lib_summary.txt
 #   bash tools/gpu.sh TAG host NAME [args]        tools/host_phase.py (host-memory build phases) -> NAME.log
+#   bash tools/gpu.sh TAG hostab REPS N AVG "ENV_A" "ENV_B" ...
+#                                                 env-knob A/B of the same, alternating -> hostab.log
 #   bash tools/gpu.sh TAG p8 NAME [P K AVG BUILDS]
 #                                                 tools/p8_geometry.py under rocprofv3 --kernel-trace: the
 #                                                 P-rank bitmap build on this one GPU, ranks serialised; per-
@@ -102,6 +104,18 @@ case $STEP in
     done
     cp abx/libs3imph_new.so $L
     python3 tools/ab_summary.py "$OUT" "lib_${CFG}" old new > "$OUT/lib_${CFG}_summary.txt" ;;
+  hostab)
+    # env-knob A/B of the host-memory build (tools/host_phase.py --phases), alternating
+    REPS=$1; N=$2; AVG=$3; shift 3
+    for rep in $(seq "$REPS"); do
+      i=0
+      for e in "$@"; do
+        i=$((i+1)); envs="S3IMPH_DEV=1"; [ "$e" != "-" ] && envs="$envs $e"
+        echo "== v$i ($e) rep $rep" >> "$OUT/hostab.log"
+        env $envs timeout -k 10 200 python tools/host_phase.py "$N" "$AVG" --phases >> "$OUT/hostab.log" 2>&1
+        rc=$?; echo "hostab v$i ($e) rep $rep rc $rc" >> "$OUT/status"; stop $rc
+      done
+    done ;;
   host)
     NAME=$1; shift
     timeout -k 10 300 python tools/host_phase.py "$@" > "$OUT/$NAME.log" 2>&1
