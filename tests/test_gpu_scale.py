@@ -119,6 +119,26 @@ def test_c3_bitmap_one_rank_bit_exact(oracle_lib, monkeypatch, capfd):
     assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
     err = capfd.readouterr().err
     assert "level 0 through P0 super-tiles" in err and "level 1 through P0 super-tiles" in err, err[-3000:]
+    assert "partitioned by the previous settle" in err, err[-3000:]  # level 0's settle fed level 1's regions
+
+
+def test_bitmap_2_ranks_settle_fed_level1_bit_exact(oracle_lib, monkeypatch, capfd):
+    """Two ranks x 88M keys (176M globally: level 1's 69M records take 4.2k tiles of 2^15, past the
+    reservation scatter's 4096) through the host transport: each rank's level-0 settle
+    partitions its collided records into level 1's super-tile regions (NextPart), level 1 goes
+    straight to the super-tile scatter; bit-exact against the oracle (S3IMPH_DIST_STRICT)."""
+    import s3imph
+    monkeypatch.setenv("S3IMPH_DEBUG", "1")
+    monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", str((2 << 20) + 17))
+    n = 176_000_000
+    blob, offs = s3imph.gen_keys(0, 91, 16, 0, n)
+    st, fp, po, mph = oracle_lib.build_mt(blob[: int(offs[-1])], offs, threads=16)
+    assert st == 0
+    g = s3imph.build_host(blob, offs, devices=[0] * 2, flags=s3imph.MULTI_BITMAP)
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+    err = capfd.readouterr().err
+    assert err.count("partitioned by the previous settle") == 2, err[-3000:]
 
 
 def test_bitmap_8_ranks_past_p0_single_limit_bit_exact(oracle_lib, monkeypatch, capfd):
