@@ -246,7 +246,7 @@ def main() -> None:
                 traffic = ent["hbm_bytes_per_launch"]
         except (OSError, ValueError):
             pass
-        try:  # the whole build's counter bytes (tools/gpu_pmc_all.sh), one GPU
+        try:  # the whole build's counter bytes (tools/gpu.sh pmc), one GPU
             with open(args.traffic) as f:
                 pl = json.load(f).get(args.config, {}).get("_pipeline")
             if pl and pl.get("n_gpus", 1) == world and not use_dist:

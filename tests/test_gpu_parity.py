@@ -673,7 +673,7 @@ def test_big_tiles_counted_path(s3, oracle_lib):
 def test_repeated_builds_identical(s3, oracle_lib, ctx, kind, avg):
     """Schedule-dependent races show up as a build that differs from the others: 12
     device builds of one 10M-key set (level 0 and levels 1..7 on the reservation path)
-    each equal the oracle's outputs byte for byte (tools/flake_probe.py runs more)."""
+    each equal the oracle's outputs byte for byte."""
     import torch
     n = 10_000_000
     blob, offs = s3.gen_keys(kind, 3, avg, 0, n)
