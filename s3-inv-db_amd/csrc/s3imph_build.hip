@@ -2417,7 +2417,12 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
     // The blob crosses in pieces (one for a blob under 256 MiB; at most kCopyPieces) on the copy
     // stream, from a thread of its own that starts at once, beside the offsets' conversion and
     // copy below; the level-0 hash launches wait for the piece holding their keys (HashFeed).
-    const int pieces = (int)std::min<uint64_t>(kCopyPieces, std::max<uint64_t>(1, nbytes >> 28));
+    static const unsigned piece_bits = [] {  // A/B knob S3IMPH_PIECE_BITS: log2 of the smallest piece
+      const char* e = dev_env("S3IMPH_PIECE_BITS");
+      const unsigned v = e ? (unsigned)std::atoi(e) : 28u;
+      return std::min(34u, std::max(20u, v));
+    }();
+    const int pieces = (int)std::min<uint64_t>(kCopyPieces, std::max<uint64_t>(1, nbytes >> piece_bits));
     std::vector<uint64_t> piece_hi(pieces);
     for (int j = 0; j < pieces; ++j) piece_hi[j] = j + 1 == pieces ? nbytes : (nbytes * (j + 1) / pieces + 15) & ~15ull;
     std::mutex pmu;
