@@ -2236,6 +2236,35 @@ uint64_t d2h_chunk() {
   return v;
 }
 
+// The copy-out of a landed chunk into the caller's (pageable) array with non-temporal stores:
+// the destination is written once and not read back here, so its lines need not be read for
+// ownership first (regular stores read every destination line in: half the copy's memory
+// traffic).  A/B knob S3IMPH_D2H_NT=0: memcpy and a plain widening loop.
+bool d2h_nt() {
+  static const bool v = [] {
+    const char* e = dev_env("S3IMPH_D2H_NT");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+void copy_out_nt(uint8_t* dst, const uint8_t* src, uint64_t len) {
+  uint64_t h = (8 - ((uintptr_t)dst & 7)) & 7;  // bytes up to an 8-aligned destination
+  if (h > len) h = len;
+  std::memcpy(dst, src, h);
+  uint64_t* d = reinterpret_cast<uint64_t*>(dst + h);
+  const uint8_t* s8 = src + h;
+  const uint64_t nw = (len - h) / 8;
+  for (uint64_t i = 0; i < nw; ++i) {
+    uint64_t v;
+    std::memcpy(&v, s8 + 8 * i, 8);
+    __builtin_nontemporal_store(v, d + i);
+  }
+  std::memcpy(dst + h + 8 * nw, s8 + 8 * nw, len - h - 8 * nw);
+}
+void widen_out_nt(uint64_t* d64, const uint32_t* s32, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) __builtin_nontemporal_store((uint64_t)s32[i], d64 + i);
+}
+
 void staged_d2h(s3imph_ctx* c, const std::vector<D2HJob>& jobs) {
   stager_init(c);
   Stager& g = c->stager;
@@ -2264,14 +2293,20 @@ void staged_d2h(s3imph_ctx* c, const std::vector<D2HJob>& jobs) {
         HIPCHECK(hipEventSynchronize(g.ev[w][b]));
         const D2HJob& J = jobs[job(ch)];
         const uint64_t off = (ch - first[job(ch)]) * chunk, len = std::min(chunk, J.bytes - off);
+        const bool nt = d2h_nt();
         if (J.conv == 2) {
           const uint32_t* s32 = static_cast<const uint32_t*>(g.pin[w][b]);
           uint64_t* d64 = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(J.dst) + 2 * off);
-          for (uint64_t i = 0; i < len / 4; ++i) d64[i] = s32[i];
+          if (nt) widen_out_nt(d64, s32, len / 4);
+          else
+            for (uint64_t i = 0; i < len / 4; ++i) d64[i] = s32[i];
+        } else if (nt) {
+          copy_out_nt(static_cast<uint8_t*>(J.dst) + off, static_cast<const uint8_t*>(g.pin[w][b]), len);
         } else {
           std::memcpy(static_cast<uint8_t*>(J.dst) + off, g.pin[w][b], len);
         }
       }
+      __atomic_thread_fence(__ATOMIC_SEQ_CST);  // the non-temporal stores drained before the join
       HIPCHECK(hipStreamSynchronize(g.st[w]));
     } catch (const Fail& f) {
       errs[w] = f.msg.empty() ? "staged copy failed" : f.msg;
