@@ -230,6 +230,9 @@ __global__ __launch_bounds__(kBTopT) void k_bm_tscan(int level, const unsigned l
 // Both read a tile's records as one flattened index range over its shards, kU records
 // per thread in flight.
 constexpr int kTT = 1024;
+// the mark: a tile per 256-thread block, eight blocks per CU (tiles in flight per CU, not
+// threads per tile, hide its per-tile round trips and barriers)
+constexpr int kMT = 256;
 constexpr int kU = 4;
 
 __device__ __forceinline__ uint32_t spread4(uint32_t v) {  // 4 bits -> 4 bytes (bit j -> byte j)
@@ -281,7 +284,7 @@ __device__ __forceinline__ uint64_t rec_k(const RT* __restrict__ q) {
 // kX: the records' in-tile positions come from xs (u16 per slot, written by the super-tile
 // scatter: 2 B per record read instead of the record's k and its bb_index)
 template <int kMode, class RT, bool kX = false>
-__global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __restrict__ bucket,
+__global__ __launch_bounds__(kMT) void k_bm_tile_mark(int level, const RT* __restrict__ bucket,
                                                       const unsigned* __restrict__ tc, uint64_t bucket_cap,
                                                       unsigned tb, const LevelState* st, uint64_t wpad,
                                                       uint8_t* __restrict__ lanes, uint32_t* __restrict__ A32,
@@ -300,14 +303,14 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
   // or one A and one C word)
   if (kMode == kBmPlanes) {
     uint64_t* ac = reinterpret_cast<uint64_t*>(lanes);
-    for (uint64_t w = words + (uint64_t)blockIdx.x * kTT + tid; w < wpad; w += (uint64_t)gridDim.x * kTT) {
+    for (uint64_t w = words + (uint64_t)blockIdx.x * kMT + tid; w < wpad; w += (uint64_t)gridDim.x * kMT) {
       const uint64_t sl = owner_of(w, S, mS), j = w - sl * S;
       ac[2 * S * sl + j] = 0;
       ac[2 * S * sl + S + j] = 0;
     }
   } else {
     constexpr uint64_t kU4 = kNib ? 2 : 4;
-    for (uint64_t q = kU4 * words + (uint64_t)blockIdx.x * kTT + tid; q < kU4 * wpad; q += (uint64_t)gridDim.x * kTT)
+    for (uint64_t q = kU4 * words + (uint64_t)blockIdx.x * kMT + tid; q < kU4 * wpad; q += (uint64_t)gridDim.x * kMT)
       reinterpret_cast<uint4*>(lanes)[q] = make_uint4(0, 0, 0, 0);
   }
   if (T == 0) return;
@@ -318,7 +321,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
   unsigned nfill = 0;
   if (tid < (unsigned)kResShards && blockIdx.x < T) nfill = tc[(uint64_t)blockIdx.x * kResShards + tid];
   for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
-    for (unsigned j = tid; j < W32; j += kTT) sA[j] = sC[j] = 0;
+    for (unsigned j = tid; j < W32; j += kMT) sA[j] = sC[j] = 0;
     if (tid < 64) {
       unsigned xf = tid < (unsigned)kResShards ? nfill : 0u;  // inclusive prefix over lanes 0-7
 #pragma unroll
@@ -335,24 +338,24 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
     for (int k = 0; k <= kResShards; ++k) fo[k] = s_fo[k];
     const uint64_t t0 = t << tb;
     const unsigned nrec = fo[kResShards];
-    // the next kTT * kU records load while this batch is marked (loads straight-line, the
+    // the next kMT * kU records load while this batch is marked (loads straight-line, the
     // index clamped instead of guarded)
     uint64_t kk[kU], kn[kU];
     auto ld = [&](unsigned i0, uint64_t (&dst)[kU]) {
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const uint64_t ri = rec_index(min(i0 + u * kTT + tid, nrec - 1), fo, t * cap, scap);
+        const uint64_t ri = rec_index(min(i0 + u * kMT + tid, nrec - 1), fo, t * cap, scap);
         if constexpr (kX) dst[u] = xs[ri];
         else dst[u] = rec_k(bucket + ri);
       }
     };
     if (nrec) ld(0, kk);
-    for (unsigned i0 = 0; i0 < nrec; i0 += kTT * kU) {
-      const bool nx = i0 + kTT * kU < nrec;
-      if (nx) ld(i0 + kTT * kU, kn);
+    for (unsigned i0 = 0; i0 < nrec; i0 += kMT * kU) {
+      const bool nx = i0 + kMT * kU < nrec;
+      if (nx) ld(i0 + kMT * kU, kn);
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        if (i0 + u * kTT + tid < nrec) {
+        if (i0 + u * kMT + tid < nrec) {
           const uint64_t lx = kX ? kk[u] : bb_index(seed, kk[u], words, magic) - t0;
           const uint32_t bit = 1u << (lx & 31);
           if (atomicOr(&sA[lx >> 5], bit) & bit) atomicOr(&sC[lx >> 5], bit);
@@ -374,7 +377,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
     if (kMode == kBmPlanes) {
       uint64_t* ac = reinterpret_cast<uint64_t*>(lanes);
       uint64_t* A64 = reinterpret_cast<uint64_t*>(A32);
-      for (unsigned jp = tid; 2 * jp < wend; jp += kTT) {
+      for (unsigned jp = tid; 2 * jp < wend; jp += kMT) {
         const unsigned j = 2 * jp;
         const uint64_t a = (uint64_t)sA[j] | ((uint64_t)(j + 1 < wend ? sA[j + 1] : 0u) << 32);
         const uint64_t c = (uint64_t)sC[j] | ((uint64_t)(j + 1 < wend ? sC[j + 1] : 0u) << 32);
@@ -384,7 +387,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_mark(int level, const RT* __res
         ac[2 * S * sl + S + jw] = c;
       }
     } else {
-      for (unsigned j = tid; j < wend; j += kTT) {
+      for (unsigned j = tid; j < wend; j += kMT) {
         const uint32_t a = sA[j], c = sC[j];
         A32[(t0 >> 5) + j] = a;
         if (kNib) {  // 32 lanes in 16 bytes
@@ -953,7 +956,7 @@ void launch_bm_range(LevelState* st, int level, hipStream_t s) { k_bm_range<<<1,
 void launch_bm_tile_mark(int level, const void* bucket, bool r20, const unsigned* tc, uint64_t bucket_cap, unsigned tb,
                          uint64_t tiles, const LevelState* st, uint64_t wpad, uint8_t* lanes, uint64_t* A, int mode,
                          uint64_t S, hipStream_t s, const uint16_t* xs) {
-  const int grid = (int)std::max<uint64_t>(256, std::min<uint64_t>(tiles, 1024));
+  const int grid = (int)std::max<uint64_t>(256, std::min<uint64_t>(tiles, 4096));
   auto go = [&](auto rt, auto xt) {
     using RT = decltype(rt);
     constexpr bool kX = decltype(xt)::value;
@@ -961,7 +964,7 @@ void launch_bm_tile_mark(int level, const void* bucket, bool r20, const unsigned
     auto kern = mode == kBmPlanes    ? k_bm_tile_mark<kBmPlanes, RT, kX>
                 : mode == kBmNibbles ? k_bm_tile_mark<kBmNibbles, RT, kX>
                                      : k_bm_tile_mark<kBmBytes, RT, kX>;
-    kern<<<grid, kTT, bm_tile_lds(tb, false), s>>>(level, bk, tc, bucket_cap, tb, st, wpad, lanes,
+    kern<<<grid, kMT, bm_tile_lds(tb, false), s>>>(level, bk, tc, bucket_cap, tb, st, wpad, lanes,
                                                    reinterpret_cast<uint32_t*>(A), S, level_magic(S), xs);
   };
   if (xs) go(R20{}, std::true_type{});
