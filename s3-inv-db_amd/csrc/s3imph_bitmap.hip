@@ -481,8 +481,8 @@ __device__ __forceinline__ void fp_out_own(const OwnSlice& os, uint64_t p, uint6
 // next bitmap level's list (BinBuffers::l20).  kX: positions from xs (the super-tile scatter's).
 // kPN: the collided records go to the next level's super-tile regions (NextPart) instead of
 // its list.
-template <class RT, bool kStaged, bool kO20, bool kX = false, bool kPN = false>
-__global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __restrict__ bucket, uint64_t pos_base,
+template <class RT, bool kStaged, bool kO20, bool kX = false, bool kPN = false, int NT = kTT>
+__global__ __launch_bounds__(NT) void k_bm_tile_settle(int level, const RT* __restrict__ bucket, uint64_t pos_base,
                                                         const unsigned* __restrict__ tc, uint64_t bucket_cap,
                                                         unsigned tb, LevelState* st, const uint64_t* __restrict__ g,
                                                         const uint64_t* __restrict__ A,
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
   static_assert(!kX || kStaged, "x positions come with P0's R20 tiles");
   static_assert(!kPN || kO20, "the next level's regions hold R20 records");
   extern __shared__ uint64_t bm_lds64[];
-  __shared__ unsigned long long s_w[kTT / 64];
+  __shared__ unsigned long long s_w[NT / 64];
   __shared__ unsigned s_sc[kMaxRanks];
   __shared__ unsigned s_fo[kResShards + 1];
   __shared__ unsigned long long s_nb, s_tg, s_ta;
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
   // reads every block's fills)
   auto no_regions = [&]() {
     if constexpr (kPN)
-      for (unsigned q = threadIdx.x; q < pn.S; q += kTT) pn.pcnt[(uint64_t)blockIdx.x * pn.S + q] = 0;
+      for (unsigned q = threadIdx.x; q < pn.S; q += NT) pn.pcnt[(uint64_t)blockIdx.x * pn.S + q] = 0;
   };
   if (bm_dead(st) || (st->status & kStStop)) {
     no_regions();
@@ -526,7 +526,12 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
   BmStaged* stg = reinterpret_cast<BmStaged*>(gpa + G);  // kStaged: `stage` entries (8-B aligned: G even)
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
-  constexpr int kGper = 2;  // groups per thread in the tile scan (G <= 2048)
+  constexpr int kGper = 2;  // groups per thread in the tile scan (G <= 2 NT)
+  if (G > (unsigned)(NT * kGper)) {  // (the host takes NT = 512 for tiles of at most 2^16 positions)
+    if (tid == 0) atomicOr(&st->status, kStGeometry);
+    no_regions();
+    return;
+  }
   bool over = false, rover = false;
   if (tid < (unsigned)kMaxRanks) s_sc[tid] = 0;  // (the first tile's barriers order it before use)
   // kPN: level L + 1's geometry, from its global size (this level's tile scan wrote it)
@@ -596,7 +601,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
     __syncthreads();
     unsigned long long pre = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < kTT / 64; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
       if ((unsigned)w < wave) pre += s_w[w];
       tot += s_w[w];
     }
@@ -637,14 +642,14 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
     for (int k = 0; k <= kResShards; ++k) fo[k] = s_fo[k];
     const uint64_t t0 = t << tb, pb = base + s_tg, ob = s_ta, nb = s_nb;
     const unsigned nrec = fo[kResShards];
-    for (unsigned i0 = 0; i0 < nrec; i0 += kTT * kU) {
+    for (unsigned i0 = 0; i0 < nrec; i0 += NT * kU) {
       Rec r[kU];
       uint16_t rx[kX ? kU : 1];
       // the batch's loads straight-line, all in flight together (the index clamped instead of
       // guarded: a guarded load per record waited for the previous one)
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const unsigned i = min(i0 + u * kTT + tid, nrec - 1);
+        const unsigned i = min(i0 + u * NT + tid, nrec - 1);
         const uint64_t ri = rec_index(i, fo, t * cap, scap);
         const RT* q = bucket + ri;
         if constexpr (kX) rx[u] = xs[ri];
@@ -658,7 +663,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        if (i0 + u * kTT + tid >= nrec) continue;
+        if (i0 + u * NT + tid >= nrec) continue;
         const uint64_t lx = kX ? (uint64_t)rx[u] : bb_index(seed, r[u].k, words, magic) - t0;
         const unsigned j = (unsigned)(lx >> 6), b = (unsigned)(lx & 63), grp = j / kGrp;
         const uint64_t below = (1ull << b) - 1ull, v = sg[j];
@@ -719,7 +724,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
       // others in one run of the settled list, instead of one scattered 8-byte store each
       __syncthreads();
       const unsigned ns = (unsigned)min<unsigned long long>(tot & 0xffffffffull, stage);
-      for (unsigned i = tid; i < ns; i += kTT) {
+      for (unsigned i = tid; i < ns; i += NT) {
         const BmStaged e = stg[i];
         const uint64_t gp = pb + e.pg, p = pos_base + e.i;
         const unsigned sl = owner_of(gp, os.slice, os.mslice);
@@ -739,7 +744,7 @@ __global__ __launch_bounds__(kTT) void k_bm_tile_settle(int level, const RT* __r
   if (over) atomicOr(&st->status, kStOverflow);
   if constexpr (kPN) {  // (the tile loop ended on a barrier: every append is in p_cur)
     if (tid == 0 && coll) atomicAdd(&st->n[level + 1], coll);  // this rank's records of level L + 1
-    for (unsigned q = tid; q < pn.S; q += kTT) pn.pcnt[(uint64_t)blockIdx.x * pn.S + q] = min(p_cur[q], rcap);
+    for (unsigned q = tid; q < pn.S; q += NT) pn.pcnt[(uint64_t)blockIdx.x * pn.S + q] = min(p_cur[q], rcap);
     if (rover) atomicOr(&st->status, kStResOverflow);  // a region overflowed: the build reruns
   }
 }
@@ -944,7 +949,13 @@ void bm_set_lds_limits() {
                         (const void*)k_bm_tile_settle<R20, true, false, true>,
                         (const void*)k_bm_tile_settle<R20, true, true, true>,
                         (const void*)k_bm_tile_settle<R20, true, true, false, true>,
-                        (const void*)k_bm_tile_settle<R20, true, true, true, true>})
+                        (const void*)k_bm_tile_settle<R20, true, true, true, true>,
+                        (const void*)k_bm_tile_settle<R20, true, false, false, false, 512>,
+                        (const void*)k_bm_tile_settle<R20, true, true, false, false, 512>,
+                        (const void*)k_bm_tile_settle<R20, true, false, true, false, 512>,
+                        (const void*)k_bm_tile_settle<R20, true, true, true, false, 512>,
+                        (const void*)k_bm_tile_settle<R20, true, true, false, true, 512>,
+                        (const void*)k_bm_tile_settle<R20, true, true, true, true, 512>})
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)(bm_tile_lds(kBmP0MaxTb, true) + kBmStage * sizeof(BmStaged)));
 }
@@ -976,14 +987,29 @@ void launch_bm_merge(const uint64_t* recv, uint64_t S, int P, uint64_t* out, con
   k_bm_merge<<<grid_for(S, kBT, 8192), kBT, 0, s>>>(recv, S, P, out, st);
 }
 
-unsigned bm_settle_grid(uint64_t tiles) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 1024)); }
+// The settle's block: 512 threads (two blocks, two tiles in flight per CU) where the tile's
+// LDS (bit words and the stage) leaves room for two blocks, else 1024
+int bm_settle_threads(unsigned tb, int P, bool staged) {
+  if (!staged || tb > kBmP0MaxTb) return kTT;
+  const size_t lds = bm_tile_lds(tb, true) + bm_stage_entries(tb, P) * sizeof(BmStaged);
+  return lds <= 80 * 1024 ? 512 : kTT;
+}
+unsigned bm_settle_grid(uint64_t tiles, int threads) {
+  return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, threads == kTT ? 1024 : 2048));
+}
 
 void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos_base, const unsigned* tc,
                            uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
                            const uint64_t* A, const unsigned long long* tbase, Rec* out, uint64_t out_cap, Rec* next,
                            uint64_t next_cap, bool next20, const OwnSlice& os, hipStream_t s, bool staged,
                            const uint16_t* xs, bool o16, const NextPart* np) {
-  const int grid = (int)bm_settle_grid(tiles);
+  // R20 tiles holding ~8k of this rank's records (the caller's `staged`: 2^14 positions per
+  // rank, at most kBmP0MaxTb) stage their settled keys; larger tiles and Rec buckets write
+  // them directly.  np (staged R20 levels whose next level is an R20 super-tile level): the
+  // collided records into that level's regions.
+  staged = staged && r20 && tb <= kBmP0MaxTb;
+  const int nt = bm_settle_threads(tb, os.P, staged);
+  const int grid = (int)bm_settle_grid(tiles, nt);
   const NextPart pn = np ? *np : NextPart{};
   auto go = [&](auto rt, auto stg, auto o20, auto xt, auto pt) {
     using RT = decltype(rt);
@@ -991,17 +1017,21 @@ void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos
                    kP = decltype(pt)::value;
     const unsigned stage = kSt ? bm_stage_entries(tb, os.P) : 0u;
     const size_t lds = bm_tile_lds(tb, true) + stage * sizeof(BmStaged);
+    if constexpr (kSt) {
+      if (nt == 512) {
+        k_bm_tile_settle<RT, kSt, kO, kX, kP, 512><<<grid, 512, lds, s>>>(level, static_cast<const RT*>(bucket),
+                                                                           pos_base, tc, bucket_cap, tb, st, g, A, tbase,
+                                                                           out, out_cap, next, next_cap, os, xs, o16,
+                                                                           stage, pn);
+        return;
+      }
+    }
     k_bm_tile_settle<RT, kSt, kO, kX, kP><<<grid, kTT, lds, s>>>(level, static_cast<const RT*>(bucket), pos_base, tc,
-                                                                  bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
-                                                                  next_cap, os, xs, o16, stage, pn);
+                                                                    bucket_cap, tb, st, g, A, tbase, out, out_cap, next,
+                                                                    next_cap, os, xs, o16, stage, pn);
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  // R20 tiles holding ~8k of this rank's records (the caller's `staged`: 2^14 positions per
-  // rank, at most kBmP0MaxTb) stage their settled keys; larger tiles and Rec buckets write
-  // them directly.  np (staged R20 levels whose next level is an R20 super-tile level): the
-  // collided records into that level's regions.
-  staged = staged && r20 && tb <= kBmP0MaxTb;
   if (np && !(staged && next20)) {  // (the host never asks for it) the next level would read no regions: rerun
     k_bm_flag<<<1, 64, 0, s>>>(st, kStGeometry);
     return;

@@ -1868,7 +1868,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
         const uint64_t np1 = (uint64_t)(npred * q * 1.1) + 4096;
         uint64_t need1 = 0;
         const P0Bufs g1 = p0_geom(c, np1, ng1, tbd, &need1);
-        nb1 = bm_settle_grid(tiles);
+        nb1 = bm_settle_grid(tiles, bm_settle_threads(tb, P, true));
         rc1 = p0_region_cap(np1, g1.S, nb1);
         if (g1.S <= (unsigned)kMaxRanks && c->p0_sup && c->p0_pcnt &&
             std::max<uint64_t>(need1, (uint64_t)nb1 * g1.S * rc1) <= c->p0_sup_cap) {

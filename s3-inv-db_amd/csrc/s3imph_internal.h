@@ -426,7 +426,8 @@ struct NextPart {
   unsigned tps_sub = 0, S = 0;  // super-tiles in 2^14-position units (P0Bufs::tps_sub), their count
   const unsigned long long* gnext = nullptr;
 };
-unsigned bm_settle_grid(uint64_t tiles);  // the settle's blocks (the regions' producers)
+int bm_settle_threads(unsigned tb, int P, bool staged);  // the settle's block size
+unsigned bm_settle_grid(uint64_t tiles, int threads);     // ... and its blocks (the regions' producers)
 void launch_bm_flag(LevelState* st, unsigned flags, hipStream_t s);  // or device status flags
 void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos_base, const unsigned* tc,
                            uint64_t bucket_cap, unsigned tb, uint64_t tiles, LevelState* st, const uint64_t* g,
