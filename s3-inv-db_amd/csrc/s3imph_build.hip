@@ -1662,9 +1662,13 @@ bool bm_feed_next() {
 }
 
 unsigned bm_dense_tb(int P) {
-  unsigned tb = kBmMinTb;
+  static const unsigned base = [] {  // A/B knob S3IMPH_BM_DENSE: the tile bits at one rank (14)
+    const char* e = dev_env("S3IMPH_BM_DENSE");
+    return e ? (unsigned)std::max(13, std::min(16, std::atoi(e))) : kBmMinTb;
+  }();
+  unsigned tb = base;
   for (int q = 2; q <= P && tb < kBmP0MaxTb; q *= 2) ++tb;
-  return tb;
+  return std::max(tb, kBmMinTb);
 }
 
 uint64_t bm_target_tiles() {
