@@ -429,9 +429,14 @@ constexpr unsigned kGrp = 4;
 // blocks per CU); a key past the stage is written directly.
 constexpr unsigned kBmStage = 5632;
 unsigned bm_stage_entries(unsigned tb, int P) {
+  static const unsigned cap = [] {  // A/B knob S3IMPH_BM_STAGE_MAX: fewer entries (the rest written directly)
+    const char* e = dev_env("S3IMPH_BM_STAGE_MAX");
+    const unsigned v = e ? (unsigned)std::atoi(e) : kBmStage;
+    return std::max(256u, std::min(kBmStage, v));
+  }();
   const double m = std::ldexp(1.0, (int)tb - 1) / std::max(1, P) * 0.6066;  // e^-1/2 of the rank's records
   const unsigned e = (unsigned)(m + 10.0 * std::sqrt(m) + 256.0 + 255.0) & ~255u;
-  return std::min(kBmStage, std::max(256u, e));
+  return std::min(cap, std::max(256u, e));
 }
 // a staged settled key: its fingerprint, key index (p = pos_base + i) and rank in the tile
 struct BmStaged {
