@@ -6,9 +6,30 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "bbhash_spec.h"
 
 namespace s3imph {
+
+// Integer min / max.  HIP's mixed-type overloads (unsigned long against unsigned long long,
+// a 64-bit value against an int literal) promote both operands to double: v_cvt_f64 /
+// v_min_f64 / v_trunc in the ISA, and inexact past 2^53.  Inside namespace s3imph these
+// hide them; mixed signedness does not compile (say which conversion is meant).
+template <class A, class B>
+__host__ __device__ __forceinline__ typename std::common_type<A, B>::type min(A a, B b) {
+  static_assert(std::is_integral<A>::value && std::is_integral<B>::value, "integer min");
+  static_assert(std::is_signed<A>::value == std::is_signed<B>::value, "min of mixed signedness");
+  using T = typename std::common_type<A, B>::type;
+  return (T)a < (T)b ? (T)a : (T)b;
+}
+template <class A, class B>
+__host__ __device__ __forceinline__ typename std::common_type<A, B>::type max(A a, B b) {
+  static_assert(std::is_integral<A>::value && std::is_integral<B>::value, "integer max");
+  static_assert(std::is_signed<A>::value == std::is_signed<B>::value, "max of mixed signedness");
+  using T = typename std::common_type<A, B>::type;
+  return (T)a < (T)b ? (T)b : (T)a;
+}
 
 static __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
