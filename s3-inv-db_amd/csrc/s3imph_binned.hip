@@ -249,6 +249,31 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
   if (zero) atomicOr(&st->status, kStKeyZero);
 }
 
+// Key bytes are read once, in whole 16-B units of consecutive lanes: the level-0 hash loads
+// them with the non-temporal hint (S3IMPH_NT_LOADS, default on), so the 6.4 GB byte stream
+// leaves L2 first and the block's region write runs stay in it until completed (C3 hash
+// 2.73 -> 2.55 ms, step 6.65 -> 6.49 ms, profiles/r5_hash/nt_loads_ab_r5ae.txt).  Measured
+// and dropped: the hint on the 20-B record loads of the scatters and tile kernels (15-30 %
+// slower, nt_loads_all_ab_r5ad.txt: a record's 16-B and 4-B loads, and neighbouring records,
+// share lines the hint marked for eviction) and on k_hash_skew's 64-B chunk loads
+// (S3IMPH_NT_SKEW, C5 hash 1.63 -> 2.34 ms: a chunk is half a line that neighbouring keys'
+// chunks share).
+#ifndef S3IMPH_NT_LOADS
+#define S3IMPH_NT_LOADS 1
+#endif
+#ifndef S3IMPH_NT_SKEW
+#define S3IMPH_NT_SKEW 0
+#endif
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_stream16(const void* p) {
+#if S3IMPH_NT_LOADS
+  const u32x4v v = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+
 // R20 (s3imph_internal.h): a level-0 record with an identity position, in five dwords.
 __device__ __forceinline__ R20 r20_make(uint64_t k, uint64_t f, uint32_t i) {
   return R20{{(uint32_t)k, (uint32_t)(k >> 32), (uint32_t)f, (uint32_t)(f >> 32), i}};
@@ -409,7 +434,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
       wr[k] = make_uint4(0, 0, 0, 0);
       if (a < wend) {
         if (a + 16 <= end8) {
-          wr[k] = *reinterpret_cast<const uint4*>(blob + a);
+          wr[k] = ld_stream16(blob + a);
         } else {  // the blob's last 8 readable bytes
           const uint2 hh = *reinterpret_cast<const uint2*>(blob + a);
           wr[k].x = hh.x;
@@ -864,7 +889,11 @@ __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict
         const uint32_t a = x.lb[t] + step * kSkC + 16u * u;
         const bool in = a < x.le[t], full = (uint64_t)a + 16 <= end8r;
         uint4 v = make_uint4(0, 0, 0, 0);
+#if S3IMPH_NT_SKEW
+        if (in && full) v = ld_stream16(gblob + a);
+#else
         if (in && full) v = *reinterpret_cast<const uint4*>(gblob + a);
+#endif
         if (in && !full) {
           const uint64_t h = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(gblob + a));
           v = make_uint4((uint32_t)h, (uint32_t)(h >> 32), 0u, 0u);
