@@ -254,8 +254,8 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
 // leaves L2 first and the block's region write runs stay in it until completed (C3 hash
 // 2.73 -> 2.55 ms, step 6.65 -> 6.49 ms, profiles/r5_hash/nt_loads_ab_r5ae.txt).  Measured
 // and dropped: the hint on the 20-B record loads of the scatters and tile kernels (15-30 %
-// slower, nt_loads_all_ab_r5ad.txt: a record's 16-B and 4-B loads, and neighbouring records,
-// share lines the hint marked for eviction) and on k_hash_skew's 64-B chunk loads
+// slower, nt_loads_all_ab_r5ad.txt; in k_scatter_p0 alone, with the 4-B load first, still
+// 1.09 -> 1.37 ms, nt_rec_scatter_ab_r5af.txt) and on k_hash_skew's 64-B chunk loads
 // (S3IMPH_NT_SKEW, C5 hash 1.63 -> 2.34 ms: a chunk is half a line that neighbouring keys'
 // chunks share).
 #ifndef S3IMPH_NT_LOADS
