@@ -24,6 +24,7 @@
 
 #include "s3imph_device.h"
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 
@@ -3173,13 +3174,17 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
 //             written to the (owner, sender) segment of an exchange area (kMidSeg records);
 //   own       the owner gathers its segments into its registers, marks A / C for its
 //             words in LDS, writes the level's bits A & ~C and its words' rank prefix,
-//             publishes its settled total;
-//   settle    rank = level base + totals of the owners before it + in-slice rank: settled
-//             (f, p) are staged by rank in LDS and written as one contiguous run; collided
-//             records stay in registers for the next level and are also appended to the
-//             next list (one reservation per workgroup), where the tail finds them;
-// with a grid barrier after the route and own phases (the settle needs none: the next
-// level's key count is derived from the totals).  Every decision derives from the same
+//             publishes its settled and collided counts in one tagged word;
+//   settle    once every owner's word is in (an all-gather polled by one wave, no fence):
+//             rank = level base + settled counts of the owners before it + in-slice rank:
+//             settled (f, p) are staged by rank in LDS and written as one contiguous run;
+//             collided records stay in registers for the next level and are also written to
+//             the next list at the collided count of the owners before it (no atomic), where
+//             the tail finds them;
+// with a grid barrier after the route phase only (round 5: the second barrier and the
+// next-list reservation atomic became the all-gather, C2 levels 0.296 -> 0.287 ms,
+// profiles/r5_levels/mid_gather_ab_r5ah.txt; the next level's key count is derived from the
+// counts).  Every decision derives from the same
 // level state, so all workgroups take the same branches; an overflow (a segment or an owner
 // past its capacity, predicted not to happen) is flagged and the build reruns on the
 // conservative path.  Level bookkeeping mirrors k_scatter_res + k_tile_reg (words, woff,
@@ -3217,7 +3222,7 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
                                                       uint64_t cap_words, uint64_t* __restrict__ fp_out,
                                                       uint64_t* __restrict__ pos_out, LevelState* st,
                                                       uint32_t* mid, Rec* __restrict__ xb,
-                                                      unsigned long long* __restrict__ prof) {
+                                                      unsigned long long* __restrict__ prof, unsigned seq) {
   // debug (prof != null): phase stamps of the first and last workgroup, 8 per level
   unsigned long long* tp =
       prof && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)
@@ -3232,6 +3237,7 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
   __shared__ uint64_t sf[kMidStage], sp[kMidStage];
   __shared__ unsigned s_cnt[kMidG], s_spre[kMidG + 1];
   __shared__ unsigned long long s_pre[kMidG + 1];
+  __shared__ unsigned s_cpre[kMidG + 1];  // collided records of the owners before
   __shared__ unsigned s_wc[kMidT / 64];
   __shared__ unsigned long long s_wbase[kMidT / 64];
   __shared__ int s_go, s_ok;
@@ -3394,25 +3400,63 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
       uint64_t total;
       const uint64_t ex = block_exscan<kMidT>((uint64_t)__popc(v), &total);
       if (w0 + w < w1) sP[w] = (uint32_t)ex;
-      if (tid == 0) tot[g] = total;
+      // this owner's settled and collided counts (< 2^14 each), tagged with the launch and
+      // level, in ONE word: the all-gather below needs no fence, only the word itself
+      if (tid == 0) {
+        const unsigned held = min(m, (unsigned)kMidR * kMidT);
+        const unsigned long long wv = ((unsigned long long)((seq << 6) | (unsigned)li) << 32) |
+                                      ((unsigned long long)(held - (unsigned)total) << 16) | total;
+        __hip_atomic_store(&tot[g], wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     MPROF(li, 3);
-    target += G;
-    if (!grid_sync(bar, target, st, &s_ok)) break;
-    MPROF(li, 4);
-    // ---- settle: staged outputs, collided records kept and appended to the next list
+    // All-gather of the owners' counts instead of a second grid barrier: wave 0 polls the G
+    // tagged words (one per lane) until every one carries this level's tag.  No data crosses
+    // workgroups in the settle except these counts (ranks, outputs and the next list's runs
+    // are placed from them), and a sender overwrites an owner's exchange segments only after
+    // the next level's first barrier, which follows every owner's reads here.
     if (wave == 0) {
-      const unsigned long long v = lane < G ? tot[lane] : 0ull;
-      unsigned long long xs = v;
+      const unsigned tagv = (seq << 6) | (unsigned)li;
+      unsigned long long v = 0;
+      unsigned spins = 0;
+      int okv = 1;
+      for (;;) {
+        v = lane < G ? __hip_atomic_load(&tot[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : ((unsigned long long)tagv << 32);
+        if (__all((unsigned)(v >> 32) == tagv)) break;
+        if (++spins > (1u << 22)) {  // bounded, as grid_sync
+          if (lane == 0) atomicOr(&st->status, kStTailOverflow);
+          okv = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const unsigned long long sv = lane < G ? (v & 0xffffu) : 0ull;
+      const unsigned cv = lane < G ? (unsigned)((v >> 16) & 0xffffu) : 0u;
+      unsigned long long xs = sv;
+      unsigned xc2 = cv;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const unsigned long long y = __shfl_up(xs, d);
-        if (lane >= (unsigned)d) xs += y;
+        const unsigned y2 = __shfl_up(xc2, d);
+        if (lane >= (unsigned)d) {
+          xs += y;
+          xc2 += y2;
+        }
       }
-      if (lane < G) s_pre[lane] = xs - v;
-      if (lane == G - 1) s_pre[G] = xs;
+      if (lane < G) {
+        s_pre[lane] = xs - sv;
+        s_cpre[lane] = xc2 - cv;
+      }
+      if (lane == G - 1) {
+        s_pre[G] = xs;
+        s_cpre[G] = xc2;
+      }
+      if (lane == 0) s_ok = okv;
     }
     __syncthreads();
+    if (!s_ok) break;
+    MPROF(li, 4);
     const uint64_t lvl_base = st->lvl_base[L];
     if (g == 0 && tid == 0) st->lvl_base[L + 1] = lvl_base + s_pre[G];
     const bool out_on = level_out_on(st, L);
@@ -3446,9 +3490,9 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
     if (lane == 0) s_wc[wave] = wc;
     __syncthreads();
     if (tid == 0) {
-      unsigned long long c = 0;
-      for (int w = 0; w < kMidT / 64; ++w) c += s_wc[w];
-      unsigned long long b0 = c ? atomicAdd(&st->n[L + 1], c) : 0ull;
+      // the next list's runs in owner order: no returning atomic, and the same order every run
+      unsigned long long b0 = s_cpre[g];
+      if (g == 0) st->n[L + 1] = s_cpre[G];
       for (int w = 0; w < kMidT / 64; ++w) {
         s_wbase[w] = b0;
         b0 += s_wc[w];
@@ -4075,9 +4119,16 @@ void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int 
                             b.cap_words, b.tile_prof, i_lo, i_hi, b.split ? g.ts : 0u, 0u);
 }
 
+// A per-launch tag for k_mid_levels' all-gather words (26 bits: a word left by a launch 2^26
+// launches ago in the same scratch could alias)
+static unsigned mid_seq() {
+  static std::atomic<unsigned> q{0};
+  return (q.fetch_add(1, std::memory_order_relaxed) + 1) & ((1u << 26) - 1);
+}
+
 void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s) {
   k_mid_levels<<<kMidG, kMidT, 0, s>>>(L0, L1, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out, b.pos_out, b.st,
-                                       b.mid, reinterpret_cast<Rec*>(b.mid + kMidXb), b.tile_prof);
+                                       b.mid, reinterpret_cast<Rec*>(b.mid + kMidXb), b.tile_prof, mid_seq());
 }
 
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s) {
