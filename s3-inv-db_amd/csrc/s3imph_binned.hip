@@ -250,45 +250,7 @@ __global__ __launch_bounds__(kCB, 8) void k_hash_count0(const uint8_t* __restric
   if (zero) atomicOr(&st->status, kStKeyZero);
 }
 
-// Key bytes are read once, in whole 16-B units of consecutive lanes: the level-0 hash loads
-// them with the non-temporal hint (S3IMPH_NT_LOADS, default on), so the 6.4 GB byte stream
-// leaves L2 first and the block's region write runs stay in it until completed (C3 hash
-// 2.73 -> 2.55 ms, step 6.65 -> 6.49 ms, profiles/r5_hash/nt_loads_ab_r5ae.txt).  Measured
-// and dropped: the hint on the 20-B record loads of the scatters and tile kernels (15-30 %
-// slower, nt_loads_all_ab_r5ad.txt; in k_scatter_p0 alone, with the 4-B load first, still
-// 1.09 -> 1.37 ms, nt_rec_scatter_ab_r5af.txt) and on k_hash_skew's 64-B chunk loads
-// (S3IMPH_NT_SKEW, C5 hash 1.63 -> 2.34 ms: a chunk is half a line that neighbouring keys'
-// chunks share).
-#ifndef S3IMPH_NT_LOADS
-#define S3IMPH_NT_LOADS 1
-#endif
-#ifndef S3IMPH_NT_SKEW
-#define S3IMPH_NT_SKEW 0
-#endif
-// Stores of whole runs that this build does not read back soon: the tile kernels' staged
-// fp_out / pos_out runs and the unfused hash's key-order kh / fp, with the non-temporal hint
-// (S3IMPH_NT_OUT, default on: C2 0.777 -> 0.765 ms, C3 6.45 -> 6.43 ms,
-// profiles/r5_levels/nt_out_ab_r5ai.txt).
-#ifndef S3IMPH_NT_OUT
-#define S3IMPH_NT_OUT 1
-#endif
-template <class T>
-__device__ __forceinline__ void st_stream(T* p, T v) {
-#if S3IMPH_NT_OUT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 ld_stream16(const void* p) {
-#if S3IMPH_NT_LOADS
-  const u32x4v v = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p));
-  return make_uint4(v.x, v.y, v.z, v.w);
-#else
-  return *reinterpret_cast<const uint4*>(p);
-#endif
-}
+// Streamed loads and stores (ld_stream16, st_stream): s3imph_device.h.
 
 // R20 (s3imph_internal.h): a level-0 record with an identity position, in five dwords.
 __device__ __forceinline__ R20 r20_make(uint64_t k, uint64_t f, uint32_t i) {
