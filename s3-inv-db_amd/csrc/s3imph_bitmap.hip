@@ -29,10 +29,6 @@
 #include <cmath>
 #include <type_traits>
 
-#ifndef S3IMPH_NT_BM
-#define S3IMPH_NT_BM 0
-#endif
-
 namespace s3imph {
 
 namespace {
@@ -451,14 +447,7 @@ struct BmStaged {
 // positions) in 16 B — p as an offset in its slice, pos as this rank's key index
 __device__ __forceinline__ void put_out(Rec* out, bool o16, uint64_t i, uint64_t p, uint64_t f, uint64_t pos,
                                         const OwnSlice& os, unsigned sl, uint64_t pos_base) {
-#if S3IMPH_NT_BM
-  if (o16) {
-    const u32x4v v = {(uint32_t)(p - (uint64_t)sl * os.slice), (uint32_t)(pos - pos_base), (uint32_t)f, (uint32_t)(f >> 32)};
-    __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(reinterpret_cast<BmT16*>(out) + i));
-  }
-#else
   if (o16) reinterpret_cast<BmT16*>(out)[i] = BmT16{(uint32_t)(p - (uint64_t)sl * os.slice), (uint32_t)(pos - pos_base), f};
-#endif
   else out[i] = Rec{p, f, pos};
 }
 // a slot from an LDS cursor for each active lane, one atomic per wave (lane order)
@@ -905,13 +894,8 @@ __global__ __launch_bounds__(kBT) void k_bm_place_merge(const PlaceRun* __restri
     return;
   }
   for (unsigned j = tid; j < wn; j += kBT) {
-#if S3IMPH_NT_BM
-    st_stream(fp_out + w0 + j, sf[j]);
-    st_stream(pos_out + w0 + j, sp[j]);
-#else
     fp_out[w0 + j] = sf[j];
     pos_out[w0 + j] = sp[j];
-#endif
   }
 }
 
