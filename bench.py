@@ -98,8 +98,9 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.transport == "host":
-        local_rank = local_rank % max(torch.cuda.device_count(), 1)
+    # (ranks past the device count share devices: the host transport's tests, and the RCCL
+    # fallback's check on a one-GPU box; a node with a GPU per rank is unchanged)
+    local_rank = local_rank % max(torch.cuda.device_count(), 1)
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 needs torchrun --nproc-per-node N (one process per GPU)")
@@ -120,18 +121,37 @@ def main() -> None:
     d_blob = torch.from_numpy(blob).to(dev)
     d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
     use_dist = world > 1 or args.dist
+    transport_note = None
     if not use_dist:
         ctx = s3imph.DeviceBuilder(local_rank)
         ctx.reserve(n)
         out_cap = n
     else:
-        if args.transport == "host":
-            ctx = s3imph.DistBuilder(local_rank, None, rank, world, host_comm=True)
-        else:
+        ctx = None
+        if args.transport == "rccl":
             uid = [s3imph.dist_unique_id() if rank == 0 else None]
             if dist is not None:
                 dist.broadcast_object_list(uid, src=0)
-            ctx = s3imph.DistBuilder(local_rank, uid[0], rank, world)
+            # RCCL has not run with nranks > 1 on this project's one-GPU boxes: if the
+            # communicator cannot be made on any rank, every rank takes the host transport
+            # instead (labelled in config.transport) rather than ending without a line
+            ok = 1
+            try:
+                ctx = s3imph.DistBuilder(local_rank, uid[0], rank, world)
+            except Exception as e:  # noqa: BLE001 - reported, then the fallback
+                ok, transport_note = 0, f"host (RCCL communicator failed on rank {rank}: {e})"
+                print(f"[bench] rank {rank}: {transport_note}", file=sys.stderr)
+            if dist is not None:
+                t = torch.tensor([ok], dtype=torch.int64)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                ok = int(t.item())
+            if not ok:
+                ctx = None
+                args.transport = "host"
+                if transport_note is None:
+                    transport_note = "host (RCCL communicator failed on another rank)"
+        if ctx is None:
+            ctx = s3imph.DistBuilder(local_rank, None, rank, world, host_comm=True)
         ctx.set_mode(dist_mode(s3imph, args.decomp))
         ctx.reserve(n, plan.n_global)
         out_cap = ctx.out_cap(plan.n_global)
@@ -219,7 +239,7 @@ def main() -> None:
         "dtype": "u64",
         "data": "synthetic (deterministic splitmix64 prefixes, byte-sorted, distinct)",
         "config": {"workload": cfg["workload"], "config": args.config, "keys": n_global,
-                   "transport": args.transport if world > 1 else None,
+                   "transport": (transport_note or args.transport) if world > 1 else None,
                    "decomposition": args.decomp if use_dist else None,
                    "key_bytes": key_bytes, "parallelism": f"shard{world}" if use_dist else "single",
                    "gamma": 2.0, "levels": info.get("num_levels")},
