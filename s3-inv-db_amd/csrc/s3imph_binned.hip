@@ -2157,8 +2157,6 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
   uint32_t* g32 = reinterpret_cast<uint32_t*>(bits + st->woff[level] + rg.plo / 64);
   const uint64_t seed = level_seed(level);
   const uint64_t lvl_base = st->lvl_base[level];
-  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  const uint64_t lt = lanemask_lt();
   Rec* seg = scratch + (uint64_t)blockIdx.x * kSplitMaxSub * kSplitSeg;  // this workgroup's sub-tile segments
   R20* seg20 = reinterpret_cast<R20*>(scratch) + (uint64_t)blockIdx.x * kSplitMaxSub * kSplitSeg;
   // record j of a bucket / scratch array as (k, f, p)
@@ -2174,6 +2172,12 @@ __global__ __launch_bounds__(kSplitT) void k_tile_split(int level, const Rec* __
   };
   bool bad = false;
   for (;;) {
+    // the thread index, opaque per tile: its derived addresses are recomputed each tile
+    // instead of hoisted, spilled and reloaded from scratch on each tile's critical path
+    unsigned tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const unsigned lane = tid & 63u, wave = tid >> 6;
+    const uint64_t lt = lane ? ~0ull >> (64 - lane) : 0ull;
     if (tid == 0) s_t = atomicAdd(&st->ticket[level], 1ull);
     for (unsigned w = tid; w < tpw; w += kSplitT) {
       sA[w] = 0;
@@ -3218,13 +3222,12 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
   __shared__ unsigned s_wc[kMidT / 64];
   __shared__ unsigned long long s_wbase[kMidT / 64];
   __shared__ int s_go, s_ok;
-  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+
   const unsigned g = blockIdx.x, G = gridDim.x;
   unsigned* bar = &st->mid_bar;  // zeroed by k_init_state: one mid launch per build attempt
   unsigned* xc = mid + kMidXc;  // [owner][sender] segment counts
   unsigned long long* tot = reinterpret_cast<unsigned long long*>(mid + kMidTot);
   const uint64_t N = st->out_cap;
-  const uint64_t lt = lanemask_lt();
   unsigned target = 0;
   bool bad = false;
   uint64_t k[kMidR], f[kMidR], pp[kMidR];
@@ -3234,6 +3237,13 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
   // next-list atomics and no decision reads state another workgroup may still be writing
   uint64_t n_loc = 0, n_prev = 0;
   for (int L = L0; L <= L1; ++L) {
+    // The thread index, opaque per level: addresses derived from it are recomputed each
+    // level instead of hoisted out of the loop, where they spilled to scratch and every
+    // level waited for their reloads on its critical path
+    unsigned tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const unsigned lane = tid & 63u, wave = tid >> 6;
+    const uint64_t lt = lane ? ~0ull >> (64 - lane) : 0ull;
     // ---- level setup: the same values in every workgroup, workgroup 0 publishes
     if (tid == 0) {
       const int p = L - 1;
