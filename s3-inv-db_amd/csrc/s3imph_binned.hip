@@ -30,6 +30,7 @@
 
 #include "s3imph_internal.h"
 
+
 namespace s3imph {
 
 namespace {
@@ -395,6 +396,12 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   uint64_t kb0[2], kb1[2], wlo = 0, wend = 0;
   bool kin[2];
   uint4 wr[KW];
+  // the window as whole 16-byte chunks [0, nfull) below end8 & ~15, plus, in the blob's last
+  // round only, the 8 bytes at end8 - 8 (chunk nfull) when end8 = 8 mod 16: per chunk a 32-bit
+  // compare against a uniform count instead of two 64-bit address compares (119 VGPRs instead
+  // of 128, C3 6.495 -> 6.460 ms, profiles/r5_hash/window_u32_ab_r5ar.txt)
+  unsigned nfull = 0;
+  bool tail8 = false;
   auto prefetch = [&](uint64_t r0) {
     const uint64_t last = min(gend, r0 + G);
 #pragma unroll
@@ -406,19 +413,17 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
     }
     wlo = uniform64(offsets[r0] & ~15ull);
     wend = uniform64(min((offsets[last] + 15) & ~15ull, wlo + (uint64_t)BB));
+    {
+      const uint64_t e16 = min(wend, end8 & ~15ull);
+      nfull = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(e16 > wlo ? (e16 - wlo) >> 4 : 0));
+      tail8 = (end8 & 8) && end8 - 8 >= wlo && end8 - 8 < wend;
+    }
+    const uint8_t* wb = blob + wlo;
 #pragma unroll
     for (int k = 0; k < KW; ++k) {
-      const uint64_t a = wlo + 16ull * (tid + (unsigned)k * NT);
+      const unsigned c = tid + (unsigned)k * NT;
       wr[k] = make_uint4(0, 0, 0, 0);
-      if (a < wend) {
-        if (a + 16 <= end8) {
-          wr[k] = ld_stream16(blob + a);
-        } else {  // the blob's last 8 readable bytes
-          const uint2 hh = *reinterpret_cast<const uint2*>(blob + a);
-          wr[k].x = hh.x;
-          wr[k].y = hh.y;
-        }
-      }
+      if (c < nfull) wr[k] = ld_stream16(wb + 16u * c);
     }
   };
   if (PF) prefetch(g);
@@ -427,10 +432,14 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
 #pragma unroll
     for (int k = 0; k < KW; ++k) {
       const unsigned c = tid + (unsigned)k * NT;
-      if (wlo + 16ull * c < wend) {
+      if (c < nfull) {
         sw[2 * c] = (uint64_t)wr[k].x | ((uint64_t)wr[k].y << 32);
         sw[2 * c + 1] = (uint64_t)wr[k].z | ((uint64_t)wr[k].w << 32);
       }
+    }
+    if (tail8 && tid == 0) {  // once per blob: the last 8 readable bytes (a blocking load)
+      sw[2 * nfull] = *reinterpret_cast<const uint64_t*>(blob + (end8 - 8));
+      sw[2 * nfull + 1] = 0;
     }
     for (unsigned b = tid; b < kLB; b += NT) lcnt[b] = 0;
     if ((RT || PT) && tid < kMaxRanks) r_cnt[tid] = 0;
