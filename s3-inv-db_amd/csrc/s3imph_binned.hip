@@ -610,7 +610,9 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
 #pragma unroll
       for (int h = 0; h < 2; ++h)
         if (rv[h]) {
-          const uint64_t x = bb_index(level_seed(0), ra[h], r_words, r_magic);
+          uint64_t x;  // (r_words: uniform; P0 levels have >= 2^19 words, the general form is a guard)
+          if (r_words >= (1ull << 19)) x = bb_index_big(level_seed(0), ra[h], r_words, r_magic);
+          else x = bb_index(level_seed(0), ra[h], r_words, r_magic);
           od[h] = __umulhi((uint32_t)(x >> kRegTileMaxBits), p_mul);
           if (od[h] >= pt.S) od[h] = pt.S - 1;  // unreachable: positions < 64 words
           ork[h] = atomicAdd(&r_cnt[od[h]], 1u);

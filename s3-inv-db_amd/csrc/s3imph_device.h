@@ -96,6 +96,26 @@ static __device__ __forceinline__ uint64_t bb_index(uint64_t seed, uint64_t key,
   return (r << 6) | (h & 63);
 }
 
+// bb_index for a level of at least 2^19 words (level_magic < 2^45, P0's level 0): the same
+// Barrett quotient, its high half built from three 32x32 products whose 64-bit sum cannot
+// overflow (q < 2^58), and qe * words from qe < 2^39 and words < 2^32 (the compiler's
+// general 64x64 forms spent ~10 more VALU per key, half of them moves).
+static __device__ __forceinline__ uint64_t bb_index_big(uint64_t seed, uint64_t key, uint64_t words,
+                                                      uint64_t magic) {
+  const uint64_t h = key_mix(seed, key);
+  const uint64_t q = h >> 6;
+  const uint32_t ql = (uint32_t)q, qh = (uint32_t)(q >> 32);
+  const uint32_t ml = (uint32_t)magic, mh = (uint32_t)(magic >> 32);
+  uint64_t sum = (uint64_t)qh * ml + __umulhi(ql, ml);
+  sum += (uint64_t)ql * mh;
+  const uint64_t qe = (uint64_t)qh * mh + (sum >> 32);
+  const uint32_t wl = (uint32_t)words;
+  const uint64_t prod = (uint64_t)(uint32_t)qe * wl + ((uint64_t)((uint32_t)(qe >> 32) * wl) << 32);
+  uint64_t r = q - prod;
+  if (r >= words) r -= words;
+  return (r << 6) | (h & 63);
+}
+
 // bb_index with the level-independent half of key_mix already applied (mk = mix64(key)),
 // for code that revisits the same key at several levels.
 static __device__ __forceinline__ uint64_t bb_index_mk(uint64_t seed, uint64_t mk, uint64_t words,
