@@ -938,7 +938,9 @@ __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict
           // next batch's first chunk is in flight (at the group's end, after its barrier, this
           // phase ran with no hashing beside it)
           zero |= a == 0;
-          const uint64_t x = bb_index(level_seed(0), a, p_words, p_magic);
+          uint64_t x;  // (as k_hash0_pair's partition)
+          if (p_words >= (1ull << 19)) x = bb_index_big(level_seed(0), a, p_words, p_magic);
+          else x = bb_index(level_seed(0), a, p_words, p_magic);
           unsigned od = __umulhi((uint32_t)(x >> kRegTileMaxBits), p_mul);
           if (od >= pt.S) od = pt.S - 1;  // unreachable: positions < 64 words
           const unsigned at = atomicAdd(&sk_pcur[od], 1u);
