@@ -333,7 +333,9 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   constexpr unsigned kLB = 256;                // length classes of the sort
   constexpr int NW = NT / 64;
   __shared__ uint64_t sw[BB / 8 + 2];          // the round's window (+ 16 B: a lane may read one word past)
-  __shared__ unsigned soff[G], slen[G];        // sorted slot -> key's window offset, length
+  // sorted slot -> key's window offset (< BB) | length (<= BB) << 16: one LDS word per key
+  static_assert(BB <= 32768, "offset and length in 16 bits each");
+  __shared__ unsigned sol[G];
   __shared__ unsigned short sidx[G];           // sorted slot -> key index in the round
   __shared__ unsigned lcnt[kLB];
   __shared__ unsigned s_cnt[NW];
@@ -496,8 +498,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
       if (fits[h]) {
         const unsigned slot = lcnt[cls[h]] + rk[h];
         sidx[slot] = (unsigned short)(tid + (unsigned)h * NT);
-        soff[slot] = (unsigned)(t_b0[h] - rw);
-        slen[slot] = (unsigned)(t_b1[h] - t_b0[h]);
+        sol[slot] = (unsigned)(t_b0[h] - rw) | ((unsigned)(t_b1[h] - t_b0[h]) << 16);
       }
     __syncthreads();
     const uint64_t r0 = g;
@@ -531,7 +532,8 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
         if (h == 0 ? tid < (m + 1) / 2 : tid < m / 2) {
           uint64_t a, b;
           const unsigned j = sidx[slot];
-          fnv_window(reinterpret_cast<const uint32_t*>(sw), soff[slot], slen[slot], a, b);
+          const unsigned ol = sol[slot];
+          fnv_window(reinterpret_cast<const uint32_t*>(sw), ol & 0xffffu, ol >> 16, a, b);
           ra[h] = a;
           rb[h] = b;
           rj[h] = j;
