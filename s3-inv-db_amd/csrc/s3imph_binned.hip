@@ -4227,13 +4227,18 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
   const unsigned bps = bps_knob ? bps_knob : std::max(1u, kP0ScatterBlocks / p.S / kResShards) * kResShards;
   if (p.x) {
     // the bitmap decomposition: tiles of 2^p.tb positions, each record's in-tile position to
-    // p.x as well; its levels have at most kBmMaxTiles tiles in <= 64 super-tiles of <= 512
-    if (p.tps > 512) {
+    // p.x as well; its levels have at most kBmMaxTiles tiles in <= 64 super-tiles of <= 1024
+    // (super-tiles of 513-1024 tiles: 5120-record rounds, ~137 KB of LDS)
+    if (p.tps > 1024) {
       k_set_status<<<1, 64, 0, s>>>(b.st, kStGeometry);  // unreachable (p0_super_tiles); the build reruns
       return;
     }
-    k_scatter_p0<6144, 512, kSB, true><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt,
-                                                                  p.flags, b.st, b.tile_prof, p.tb, p.x, level);
+    if (p.tps > 512)
+      k_scatter_p0<5120, 1024, kSB, true><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt,
+                                                                     p.flags, b.st, b.tile_prof, p.tb, p.x, level);
+    else
+      k_scatter_p0<6144, 512, kSB, true><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt,
+                                                                    p.flags, b.st, b.tile_prof, p.tb, p.x, level);
     return;
   }
   if (p.tps <= 256)
