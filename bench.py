@@ -9,12 +9,16 @@ I/O (/root/reference/pkg/format/mphf_streaming.go:122-213).
   python bench.py [--gpus N --steps K --warmup W --config c3]
   N > 1: torchrun --nproc-per-node N bench.py --gpus N ...  (one process per GPU;
          RCCL communicator owned by libs3imph; torch.distributed/gloo only for the
-         rendezvous, barriers and the max-over-ranks time).
+         rendezvous, barriers and the max-over-ranks time).  `python bench.py --gpus N`
+         without torchrun starts that same torchrun itself (before anything touches a
+         GPU) and exits with its status; rank 0's JSON line is the output.
 
 Workload: BASELINE.json configs[2] (C3), the largest single-GPU configuration:
 100M synthetic prefixes per GPU, avg key 64 B (weak scaling: N GPUs build one MPHF over
-N x 100M keys).  At N = 1 a C2 line (configs[1], 10M keys, avg 32 B) rides beside it
-as `secondary` (never `value`).
+N x 100M keys).  At N = 1 lines ride beside it (never `value`): C2 (configs[1], 10M keys,
+avg 32 B) as `secondary.c2`, the C5 share of one GPU (25M keys, 1-1024 B) as
+`secondary.c5`, and C3 through the north_star's per-level collision-bitmap decomposition
+at one rank as `bitmap_n1`.
 """
 from __future__ import annotations
 
@@ -90,20 +94,39 @@ def main() -> None:
                     help="skip the lookup / finalize / host_e2e lines (profiling runs)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC summary (HBM bytes per launch) to attach as roofline.traffic")
+    ap.add_argument("--probe-launch", action="store_true",
+                    help="(tests) each rank prints its rank / world as JSON and exits before any GPU call")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # One command for N GPUs: start one process per GPU through torchrun and relay its
+        # status.  Nothing above this line has touched a GPU (torch is not even imported),
+        # and the ranks are child processes, not an exec of this one.
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.probe_launch:
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "gpus": args.gpus}), flush=True)
+        return
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch one process per GPU")
 
     import numpy as np
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # (ranks past the device count share devices: the host transport's tests, and the RCCL
-    # fallback's check on a one-GPU box; a node with a GPU per rank is unchanged)
-    local_rank = local_rank % max(torch.cuda.device_count(), 1)
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 needs torchrun --nproc-per-node N (one process per GPU)")
+    # Ranks past the device count (a one-GPU box) must share devices; RCCL refuses two ranks
+    # on one device, so such a run takes the host transport and is a rehearsal of the N > 1
+    # path, never a measurement (its `value` is null).  torch.cuda.device_count() does not
+    # initialise the GPU on this image.
+    n_dev = max(torch.cuda.device_count(), 1)
+    shared = world > n_dev
+    transport_note = None
+    if shared:
+        local_rank = local_rank % n_dev
+        if args.transport == "rccl":
+            args.transport = "host"
+            transport_note = f"host (rehearsal: {world} ranks on {n_dev} GPU(s); RCCL needs a GPU per rank)"
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -121,7 +144,7 @@ def main() -> None:
     d_blob = torch.from_numpy(blob).to(dev)
     d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
     use_dist = world > 1 or args.dist
-    transport_note = None
+    fallback = None  # set when the timed build is not the one asked for (reported, never silent)
     if not use_dist:
         ctx = s3imph.DeviceBuilder(local_rank)
         ctx.reserve(n)
@@ -129,27 +152,10 @@ def main() -> None:
     else:
         ctx = None
         if args.transport == "rccl":
-            uid = [s3imph.dist_unique_id() if rank == 0 else None]
-            if dist is not None:
-                dist.broadcast_object_list(uid, src=0)
-            # RCCL has not run with nranks > 1 on this project's one-GPU boxes: if the
-            # communicator cannot be made on any rank, every rank takes the host transport
-            # instead (labelled in config.transport) rather than ending without a line
-            ok = 1
-            try:
-                ctx = s3imph.DistBuilder(local_rank, uid[0], rank, world)
-            except Exception as e:  # noqa: BLE001 - reported, then the fallback
-                ok, transport_note = 0, f"host (RCCL communicator failed on rank {rank}: {e})"
-                print(f"[bench] rank {rank}: {transport_note}", file=sys.stderr)
-            if dist is not None:
-                t = torch.tensor([ok], dtype=torch.int64)
-                dist.all_reduce(t, op=dist.ReduceOp.MIN)
-                ok = int(t.item())
-            if not ok:
-                ctx = None
+            ctx, fallback = make_rccl_ctx(s3imph, torch, dist, local_rank, rank, world)
+            if ctx is None:
                 args.transport = "host"
-                if transport_note is None:
-                    transport_note = "host (RCCL communicator failed on another rank)"
+                transport_note = fallback
         if ctx is None:
             ctx = s3imph.DistBuilder(local_rank, None, rank, world, host_comm=True)
         ctx.set_mode(dist_mode(s3imph, args.decomp))
@@ -166,6 +172,24 @@ def main() -> None:
         def step():
             return ctx.build_shard(d_blob, d_offs, n, plan.lo, d_fp, d_po, out_cap)[2]
 
+    bitmap_error = None
+    if use_dist and args.decomp == "bitmap":
+        # A strict bitmap build fails (on every rank: dist_agree) when a level misses its
+        # size bounds.  Then the routed decomposition — same bytes out — is timed instead,
+        # and the line says so (config.decomposition, bitmap_error).
+        try:
+            step()
+        except s3imph.MPHFError as e:
+            bitmap_error = str(e)
+        fl = torch.tensor([0 if bitmap_error is None else 1], dtype=torch.int64)
+        if dist is not None:
+            dist.all_reduce(fl)
+        if int(fl.item()):
+            print(f"[bench] rank {rank}: bitmap decomposition failed ({bitmap_error or 'on another rank'}); "
+                  f"timing the routed decomposition", file=sys.stderr)
+            args.decomp = "route"
+            bitmap_error = bitmap_error or "failed on another rank"
+            ctx.set_mode(dist_mode(s3imph, "route"))
     for _ in range(args.warmup):
         step()
     # Timed region: two HIP events per build, around the level-0 hash (the dominant kernel),
@@ -227,7 +251,9 @@ def main() -> None:
     b_alg = key_bytes + 8 * (n_global + 1) + 16 * n_global + mph_len
     result = {
         "metric": "MPHF build keys/s + key-bytes GB/s (device-resident), 1/2/4/8 MI355X",
-        "value": n_global / dt,
+        # ranks sharing a GPU (host-transport rehearsal) measure nothing: null, and the
+        # rehearsal's own rate rides in `rehearsal`
+        "value": None if shared else n_global / dt,
         "unit": "keys/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -249,6 +275,16 @@ def main() -> None:
                               "peak": HBM_PEAK_GBPS * world, "unit": "GB/s",
                               "frac": b_alg / dt / 1e9 / (HBM_PEAK_GBPS * world)},
     }
+    if shared:
+        result["rehearsal"] = {"keys_per_s": n_global / dt, "ranks": world, "gpus": n_dev,
+                               "note": "ranks share GPUs through the host transport: checks the N > 1 path end "
+                                       "to end, not a measurement"}
+    if fallback is not None and not shared:
+        # RCCL's communicator could not be made: the GPUs are distinct, so this is a real
+        # build on `world` GPUs with collectives staged through host memory (slower than xGMI)
+        result["transport_fallback"] = fallback
+    if bitmap_error is not None:
+        result["bitmap_error"] = bitmap_error
     # Roofline of the dominant kernel (rank 0's stage times, HIP events on the build stream).
     dom = max((k for k in stages if stage_alg_bytes(k, n, key_bytes_local, info) is not None),
               key=lambda k: stages[k], default=None)
@@ -295,19 +331,119 @@ def main() -> None:
     if world == 1 and not use_dist and not args.headline_only:
         result["lookup"] = lookup_rate(ctx, d_blob, d_offs, n, d_fp, d_po)
         result["finalize"] = finalize_rate(ctx, d_blob, d_offs, n)
+    if world == 1 and not use_dist and not args.no_secondary:
+        # the north_star decomposition on the same keys at one rank (RCCL communicator of one)
+        ctx.close()
+        del d_fp, d_po
+        torch.cuda.empty_cache()
+        result["bitmap_n1"] = bitmap_n1_line(s3imph, torch, d_blob, d_offs, n, key_bytes_local, local_rank,
+                                             args.steps, args.warmup)
     if world == 1 and not args.headline_only:
         result["host_e2e"] = host_e2e(s3imph, blob, offs, local_rank)
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(s3imph, cfg, args.seed)
-    if world == 1 and not use_dist and args.config != "c2" and not args.no_secondary:
-        del d_blob, d_offs, d_fp, d_po
+    if world == 1 and not use_dist and not args.no_secondary:
+        del d_blob, d_offs
         ctx.close()
         torch.cuda.empty_cache()
-        result["secondary"] = {"c2": secondary_line(s3imph, local_rank, args.seed, args.steps, args.warmup)}
+        sec = {}
+        for name in ("c2", "c5"):
+            if name != args.config:
+                sec[name] = secondary_line(s3imph, local_rank, args.seed, args.steps, args.warmup, name,
+                                           extras=name == "c2" and not args.headline_only)
+        result["secondary"] = sec
     print(json.dumps(result), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """Run this bench as N ranks, one process per GPU, through torchrun on 127.0.0.1 (the
+    contract's multi-GPU launch); the ranks inherit stdout, so rank 0's JSON line is this
+    command's output.  Returns torchrun's exit status."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL across processes)
+    env.setdefault("OMP_NUM_THREADS", "16")
+    print(f"[bench] launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def make_rccl_ctx(s3imph, torch, dist, device: int, rank: int, world: int):
+    """This rank's RCCL context, or (None, reason) when the communicator cannot be made on
+    some rank — then every rank takes the host transport and the line says so.  A rank whose
+    peer failed before joining would wait in ncclCommInitRank forever, so a watchdog ends
+    the process if the communicator and the agreement on it take longer than 300 s."""
+    import threading
+    uid = [s3imph.dist_unique_id() if rank == 0 else None]
+    if dist is not None:
+        dist.broadcast_object_list(uid, src=0)
+    done = threading.Event()
+
+    def watchdog():
+        if not done.wait(300):
+            print(f"[bench] rank {rank}: RCCL communicator not made within 300 s (a peer failed?)",
+                  file=sys.stderr, flush=True)
+            os._exit(3)
+    threading.Thread(target=watchdog, daemon=True).start()
+    ctx, note, ok = None, None, 1
+    try:
+        ctx = s3imph.DistBuilder(device, uid[0], rank, world)
+    except Exception as e:  # noqa: BLE001 - reported, then the fallback
+        ok, note = 0, f"host (RCCL communicator failed on rank {rank}: {e})"
+        print(f"[bench] rank {rank}: {note}", file=sys.stderr, flush=True)
+    if dist is not None:
+        t = torch.tensor([ok], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = int(t.item())
+    done.set()
+    if ok:
+        return ctx, None
+    if ctx is not None:
+        ctx.close()
+    return None, note or "host (RCCL communicator failed on another rank)"
+
+
+def bitmap_n1_line(s3imph, torch, d_blob, d_offs, n: int, key_bytes: int, device: int, steps: int,
+                   warmup: int) -> dict:
+    """The headline's keys through the north_star decomposition — per-level collision
+    bitmap, (A, C) planes, settle — at one rank (an RCCL communicator of one), strict (a
+    size-bound miss is an error, not a routed build), timed like the headline: W warm-up
+    builds, then K builds between two synchronisations.  Beside `value`, never as it."""
+    ctx = s3imph.DistBuilder(device, s3imph.dist_unique_id(), 0, 1)
+    try:
+        ctx.set_mode(dist_mode(s3imph, "bitmap"))
+        ctx.reserve(n, n)
+        cap = ctx.out_cap(n)
+        d_fp = torch.empty(max(cap, 1), dtype=torch.int64, device=d_blob.device)
+        d_po = torch.empty(max(cap, 1), dtype=torch.int64, device=d_blob.device)
+        try:
+            for _ in range(max(warmup, 1)):
+                ctx.build_shard(d_blob, d_offs, n, 0, d_fp, d_po, cap)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                ctx.build_shard(d_blob, d_offs, n, 0, d_fp, d_po, cap)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / steps
+        except s3imph.MPHFError as e:
+            return {"error": str(e)}
+        ctx.set_profiling(1)
+        ctx.build_shard(d_blob, d_offs, n, 0, d_fp, d_po, cap)
+        st = {k: round(v, 4) for k, v in ctx.stage_times().items()}
+        ctx.set_profiling(0)
+        return {"decomposition": "bitmap (strict)", "keys": n, "ms_per_step": dt * 1e3, "keys_per_s": n / dt,
+                "key_bytes_GBps": key_bytes / dt / 1e9, "steps": steps, "stages_ms": st}
+    finally:
+        ctx.close()
+        torch.cuda.empty_cache()
 
 
 def dist_mode(s3imph, decomp: str) -> int:
@@ -413,12 +549,15 @@ def host_e2e(s3imph, blob, offs, device: int, reps: int = 3) -> dict:
                     "chunk staging (8 workers), mph.bin into a reused caller buffer; output arrays reused"}
 
 
-def secondary_line(s3imph, device: int, seed: int, steps: int, warmup: int) -> dict:
-    """C2 (BASELINE configs[1]: 10M keys, avg 32 B) on the same GPU: ms/step and keys/s,
-    device-resident, same step as the headline.  Reported beside `value`, never as it."""
+def secondary_line(s3imph, device: int, seed: int, steps: int, warmup: int, name: str = "c2",
+                   extras: bool = True) -> dict:
+    """C2 (BASELINE configs[1]: 10M keys, avg 32 B) or C5's one-GPU share (configs[4]: 25M
+    keys, 1-1024 B log-uniform) on the same GPU: ms/step and keys/s, device-resident, same
+    step as the headline; `extras` adds finalize and the host-memory lines.  Reported beside
+    `value`, never as it."""
     import numpy as np
     import torch
-    cfg = CONFIGS["c2"]
+    cfg = CONFIGS[name]
     n = cfg["keys_per_gpu"]
     blob, offs = s3imph.gen_keys(cfg["kind"], seed, cfg["avg"], 0, n)
     dev = f"cuda:{device}"
@@ -439,13 +578,19 @@ def secondary_line(s3imph, device: int, seed: int, steps: int, warmup: int) -> d
     ctx.set_profiling(1)
     ctx.build(d_blob, d_offs, n, d_fp, d_po)
     stages = {k: round(v, 4) for k, v in ctx.stage_times().items()}
-    fin = finalize_rate(ctx, d_blob, d_offs, n)
+    ctx.set_profiling(0)
+    res = {"workload": cfg["workload"], "keys": n, "ms_per_step": dt * 1e3, "keys_per_s": n / dt,
+           "key_bytes": int(offs[-1]), "key_bytes_GBps": int(offs[-1]) / dt / 1e9, "steps": steps,
+           "stages_ms": stages}
+    if extras:
+        res["finalize"] = finalize_rate(ctx, d_blob, d_offs, n)
     ctx.close()
     del d_blob, d_offs, d_fp, d_po
     torch.cuda.empty_cache()
-    return {"workload": cfg["workload"], "keys": n, "ms_per_step": dt * 1e3, "keys_per_s": n / dt,
-            "key_bytes_GBps": int(offs[-1]) / dt / 1e9, "stages_ms": stages, "finalize": fin,
-            "host_e2e": host_e2e(s3imph, blob, offs, device), "builder_e2e": builder_e2e(s3imph, blob, offs, device)}
+    if extras:
+        res["host_e2e"] = host_e2e(s3imph, blob, offs, device)
+        res["builder_e2e"] = builder_e2e(s3imph, blob, offs, device)
+    return res
 
 
 def builder_e2e(s3imph, blob, offs, device: int, batch: int = 1 << 20, reps: int = 3) -> dict:

@@ -1068,6 +1068,10 @@ void ensure_dist_workspace(s3imph_ctx* c, uint64_t n_local, uint64_t n_global) {
 
 
 constexpr int kDistRetry = -1;
+// the bitmap decomposition missed a capacity, not a size bound (a reservation slot overflow,
+// a fed level whose P0 buffers could not be had, a tail geometry miss): rerun it once in its
+// conservative form (no settle-fed levels, no list levels through P0) before routing
+constexpr int kDistRetryBm = -2;
 constexpr uint64_t kChunkedRoute0Keys = 8ull << 20;  // sharded level 0 of this many keys per rank (N / P): 4 chunks
 constexpr int kRoute0Chunks = 4;
 
@@ -1681,7 +1685,8 @@ uint64_t bm_target_tiles() {
 
 int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                         uint64_t n_local, uint64_t key_base, uint64_t N, uint64_t* fp_out, uint64_t* pos_out,
-                        uint64_t out_cap, hipStream_t s, s3imph_build_info* info, std::string* msg) {
+                        uint64_t out_cap, hipStream_t s, bool conservative, s3imph_build_info* info,
+                        std::string* msg) {
   DistState& d = c->d;
   Comm& cm = *d.comm;
   const int P = d.nranks, R = d.rank;
@@ -1783,7 +1788,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     // (C3 level 1 at one rank: 4.8k tiles of 2^14)
     P0Bufs pl{};
     const uint64_t Td = tiles_of(wmax, tbd, 0);
-    const bool lp = L > 0 && c->p0 && bs.list20(L) && Td > bm_target_tiles() && Td <= kBmMaxTiles &&
+    const bool lp = L > 0 && !conservative && c->p0 && bs.list20(L) && Td > bm_target_tiles() && Td <= kBmMaxTiles &&
                     p0_try_bufs(c, np, (uint64_t)std::ceil(nb), s, &pl, tbd, true);
     const bool l0p = L == 0 && p0;
     unsigned tb = l0p ? tb0 : tbd;
@@ -1866,7 +1871,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     bool feed = false;
     uint64_t rc1 = 0;
     unsigned nb1 = 0;
-    if (more && next20 && staged && in20 && c->p0 && bm_feed_next()) {
+    if (more && next20 && staged && in20 && c->p0 && !conservative && bm_feed_next()) {
       const uint64_t ng1 = (uint64_t)std::ceil(nbn), Td1 = tiles_of(level_words(ng1), tbd, 0);
       if (Td1 > bm_target_tiles() && Td1 <= kBmMaxTiles) {
         const uint64_t np1 = (uint64_t)(npred * q * 1.1) + 4096;
@@ -1884,6 +1889,8 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     launch_bm_tile_settle(L, bk, in20, key_base, tc, bcap, tb, tiles, st, d.bm_g, d.bm_a, d.bm_tbase, out,
                           out16 ? d.bm_cap_out * sizeof(Rec) / sizeof(BmT16) : d.bm_cap_out, c->list[L & 1], d.cap_list,
                           next20, own_slice, s, staged, xs, out16, feed ? &npart : nullptr);
+    if (!conservative && L == 0 && dev_env("S3IMPH_FAULT_BM_OVERFLOW"))
+      launch_bm_flag(st, kStResOverflow, s);  // test hook: a capacity miss (the conservative rerun)
     fed = feed;
     fed_rc = rc1;
     fed_nb = nb1;
@@ -1930,9 +1937,11 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   if (c->debug)
     std::fprintf(stderr, "[s3imph] rank %d bitmap: %d sharded levels, replicated %llu records, flags 0x%x\n", R, Ls,
                  (unsigned long long)total, flags);
-  // global facts (the flags are gathered): every rank returns here.  A reservation slot
-  // overflow (a skewed tile) or a level beyond its bound reruns on the routed build.
-  if (flags & (kStBitmapBound | kStResOverflow | kStGeometry)) return kDistRetry;
+  // global facts (the flags are gathered): every rank returns here.  A level beyond its
+  // bound reruns on the routed build; a reservation slot overflow (a skewed tile, or a fed
+  // level without its P0 buffers) reruns this decomposition conservatively first.
+  if (flags & kStBitmapBound) return kDistRetry;
+  if (flags & (kStResOverflow | kStGeometry)) return conservative ? kDistRetry : kDistRetryBm;
   if (flags & kStOverflow) {
     *msg = "build MPHF: bitmap decomposition: list capacity exceeded";
     return S3IMPH_ERR_INTERNAL;
@@ -2002,7 +2011,7 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
       std::fprintf(stderr, " %llu/%llu", (unsigned long long)hs.n[l], (unsigned long long)hs.lvl_base[l]);
     std::fprintf(stderr, "\n");
   }
-  if (flags & (kStGeometry | kStTailOverflow | kStResOverflow)) return kDistRetry;
+  if (flags & (kStGeometry | kStTailOverflow | kStResOverflow)) return conservative ? kDistRetry : kDistRetryBm;
   if (flags & kStTooManyLevels) return dist_classify_stop(c, blob, offsets, n_local, s, msg);
   if (flags & kStKeyZero) {
     *msg = "MPHF Key(...) returned 0, possible hash collision with sentinel";
@@ -2144,22 +2153,31 @@ int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
   }
   ensure_dist_workspace(c, n_local, N);
   set_lds_attrs(c);
-  int rc = S3IMPH_OK;
-  // bitmap decomposition first when selected; its bound miss, and the routed build's
-  // geometry misses, fall back to the routed build and then to its conservative form
-  const int first = d.mode == kDistBitmap ? 0 : 1;
-  for (int attempt = first; attempt < 3; ++attempt) {
-    ev_begin(c);
-    ev_mark(c, s, "start");
-    rc = attempt == 0 ? dist_attempt_bitmap(c, blob, offsets, pos, n_local, key_base, N, fp_out, pos_out, out_cap, s,
-                                            info, msg)
-                      : dist_attempt(c, blob, offsets, pos, n_local, key_base, N, fp_out, pos_out, out_cap, s,
-                                     attempt > 1, info, msg);
-    if (rc == kDistRetry && attempt == 0 && (d.strict || dev_env("S3IMPH_DIST_STRICT"))) {
+  int rc = kDistRetry;
+  // bitmap decomposition first when selected (a capacity miss reruns it once conservatively);
+  // its bound miss, and the routed build's geometry misses, fall back to the routed build and
+  // then to its conservative form.  Strict mode fails instead of routing.
+  if (d.mode == kDistBitmap) {
+    for (int bm = 0; bm < 2; ++bm) {
+      ev_begin(c);
+      ev_mark(c, s, "start");
+      rc = dist_attempt_bitmap(c, blob, offsets, pos, n_local, key_base, N, fp_out, pos_out, out_cap, s, bm == 1,
+                               info, msg);
+      if (rc != kDistRetryBm) break;
+      if (c->debug)
+        std::fprintf(stderr, "[s3imph] rank %d bitmap: a capacity miss, rerunning conservatively\n", d.rank);
+    }
+    if (rc == kDistRetryBm) rc = kDistRetry;
+    if (rc == kDistRetry && (d.strict || dev_env("S3IMPH_DIST_STRICT"))) {
       *msg = "build MPHF: the bitmap decomposition missed its size bounds (S3IMPH_DIST_STRICT: no fallback)";
       return S3IMPH_ERR_INTERNAL;  // tests use this to prove the bitmap path built the index
     }
-    if (rc != kDistRetry) break;
+  }
+  for (int attempt = 1; rc == kDistRetry && attempt < 3; ++attempt) {
+    ev_begin(c);
+    ev_mark(c, s, "start");
+    rc = dist_attempt(c, blob, offsets, pos, n_local, key_base, N, fp_out, pos_out, out_cap, s, attempt > 1, info,
+                      msg);
   }
   if (rc != S3IMPH_OK) return rc;
   if (d.out_n > out_cap) {
@@ -2177,6 +2195,34 @@ int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
 
 s3imph_ctx* g_default[64] = {nullptr};
 std::mutex g_default_mu;
+
+bool reclaim_cached(s3imph_ctx* keep, const void* keep_set) {
+  bool any = release_idle_multi_sets(keep_set) > 0;
+  {
+    std::lock_guard<std::mutex> glk(g_default_mu);
+    for (s3imph_ctx* c : g_default) {
+      if (!c || c == keep) continue;
+      std::unique_lock<std::mutex> lk(c->mu, std::try_to_lock);
+      if (!lk.owns_lock()) continue;  // building right now
+      if (!c->hist && !c->s_blob && !c->fin) continue;  // nothing cached
+      (void)hipSetDevice(c->device);
+      if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+      free_workspace(c);
+      fin_scratch_free(c);
+      c->have_build = false;
+      c->rank_valid = false;
+      any = true;
+    }
+  }
+  if (keep && keep->fin) {
+    fin_scratch_free(keep);
+    any = true;
+  }
+  if (keep) (void)hipSetDevice(keep->device);
+  if (any && (dev_env("S3IMPH_DEBUG") || (keep && keep->debug)))
+    std::fprintf(stderr, "[s3imph] out of device memory: released cached workspaces, retrying once\n");
+  return any;
+}
 
 }  // namespace s3imph
 
@@ -2416,8 +2462,8 @@ uint64_t mph_bin_bound(uint64_t n) { return 8 * kPartitions + 8 + 8ull * kMaxLev
 // one (HashFeed), so the hash of arrived keys runs beside the rest of the copy; the build;
 // mph.bin marshalled on a second thread while fp / positions stream back through the pinned
 // workers.  With S3IMPH_DEBUG every phase is timed from entry to return (they sum to it).
-int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
-                    uint64_t n, uint64_t* fp_out, uint64_t* pos_out, MphOut* mph, std::string* msg) {
+int build_from_host_once(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
+                         uint64_t n, uint64_t* fp_out, uint64_t* pos_out, MphOut* mph, std::string* msg) {
   using clk = std::chrono::steady_clock;
   const auto te = clk::now();
   s3imph_ctx* c = default_ctx(device, msg);
@@ -2632,6 +2678,24 @@ int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, co
   }
 }
 
+// ... and once more when it ran out of HBM, after the other builds' cached workspaces are freed
+int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
+                    uint64_t n, uint64_t* fp_out, uint64_t* pos_out, MphOut* mph, std::string* msg) {
+  const int rc = build_from_host_once(device, blob, offsets, pos, n, fp_out, pos_out, mph, msg);
+  if (rc != S3IMPH_ERR_NOMEM) return rc;
+  std::string m2;
+  s3imph_ctx* c = default_ctx(device, &m2);
+  if (!c) return rc;
+  bool freed;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    freed = reclaim_cached(c);
+  }
+  if (!freed) return rc;
+  msg->clear();
+  return build_from_host_once(device, blob, offsets, pos, n, fp_out, pos_out, mph, msg);
+}
+
 int build_from_host(int device, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos, uint64_t n,
                     uint64_t* fp_out, uint64_t* pos_out, std::vector<uint8_t>* mph, std::string* msg) {
   MphOut o;
@@ -2750,12 +2814,15 @@ int s3imph_ctx_reserve(s3imph_ctx* c, uint64_t max_keys, uint64_t max_global_key
   std::lock_guard<std::mutex> lk(c->mu);
   try {
     HIPCHECK(hipSetDevice(c->device));
-    if (c->dist)
-      ensure_dist_workspace(c, max_keys, std::max(max_keys, max_global_keys));
-    else
-      ensure_workspace(c, max_keys);
-    HIPCHECK(hipDeviceSynchronize());
-    return S3IMPH_OK;
+    std::string msg;
+    return retry_on_nomem(c, nullptr, &msg, [&] {
+      if (c->dist)
+        ensure_dist_workspace(c, max_keys, std::max(max_keys, max_global_keys));
+      else
+        ensure_workspace(c, max_keys);
+      HIPCHECK(hipDeviceSynchronize());
+      return (int)S3IMPH_OK;
+    });
   } catch (const Fail& f) {
     return f.code;
   }
@@ -2771,8 +2838,9 @@ int s3imph_build_device(s3imph_ctx* c, const uint8_t* d_blob, const uint64_t* d_
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
     c->last_msg.clear();
-    int rc = c->dist ? S3IMPH_ERR_STATE
-                     : build_single(c, d_blob, d_offsets, d_pos, n, d_fp_out, d_pos_out, s, info, &msg);
+    int rc = c->dist ? S3IMPH_ERR_STATE : retry_on_nomem(c, s, &msg, [&] {
+      return build_single(c, d_blob, d_offsets, d_pos, n, d_fp_out, d_pos_out, s, info, &msg);
+    });
     c->last_msg = msg;
     info->status = rc;
     return rc;

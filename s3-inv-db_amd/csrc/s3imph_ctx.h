@@ -298,6 +298,32 @@ void launch_key_hashes(const uint8_t* blob, const uint64_t* offsets, uint64_t n,
 int marshal_locked(s3imph_ctx* c, uint8_t* out, uint64_t cap, uint64_t* len, std::string* msg);
 void ensure_s_pos(s3imph_ctx* c, uint64_t n);
 void release_multi_sets();  // s3imph_multi.hip
+int release_idle_multi_sets(const void* keep);  // s3imph_multi.hip: idle sets other than `keep`
+// A build that ran out of HBM: free the workspaces this process caches for OTHER builds — the
+// host builds' per-device default contexts and the idle multi-GPU sets (`keep_set` excepted)
+// — plus `keep`'s finalize scratch; contexts or sets another thread is building on are left
+// alone.  Returns whether anything was freed (s3imph_build.hip).
+bool reclaim_cached(s3imph_ctx* keep, const void* keep_set = nullptr);
+// Run the build step f (returns a status, may throw Fail); when it runs out of HBM, drain the
+// stream, reclaim_cached(keep) and run it once more (cached workspaces of earlier
+// builds must not fail a later, larger one).
+template <class F>
+int retry_on_nomem(s3imph_ctx* keep, hipStream_t s, std::string* msg, F&& f) {
+  int rc;
+  try {
+    rc = f();
+  } catch (const Fail& e) {
+    if (e.code != S3IMPH_ERR_NOMEM) throw;
+    rc = e.code;
+    *msg = e.msg;
+  }
+  if (rc != S3IMPH_ERR_NOMEM) return rc;
+  if (s) (void)hipStreamSynchronize(s);
+  (void)hipGetLastError();
+  if (!reclaim_cached(keep)) return rc;
+  msg->clear();
+  return f();
+}
 // Index finalize arrays (s3imph_finalize.hip): device pass over keys in HBM, and the
 // host-memory form that writes the five files.
 int finalize_device(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint32_t* depths, uint64_t n,

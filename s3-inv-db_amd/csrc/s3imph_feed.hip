@@ -465,8 +465,10 @@ int feed_build(Feed* f, std::vector<uint8_t>* mph, const std::function<FeedSink*
     hipStream_t s = c->own_stream;
     HIPCHECK(hipStreamWaitEvent(s, fed, 0));
     s3imph_build_info info;
-    int rc = build_single(c, f->blob.d, reinterpret_cast<const uint64_t*>(f->ends.d),
+    int rc = retry_on_nomem(c, s, msg, [&] {
+      return build_single(c, f->blob.d, reinterpret_cast<const uint64_t*>(f->ends.d),
                           reinterpret_cast<const uint64_t*>(f->pos.d), n, f->d_out[0], f->d_out[1], s, &info, msg);
+    });
     if (rc != S3IMPH_OK) return rc;  // nothing was written
     HIPCHECK(hipEventRecord(built, s));
     // the outgrown device buffers: the feed stream is past them (the build waited for it)

@@ -75,6 +75,12 @@ struct ThreadHub {
     aborted = true;
     cv.notify_all();
   }
+  // the host staging of the collectives (sized by the largest exchange so far) back to the OS
+  void free_buffers() {
+    for (auto& v : slot) std::vector<uint8_t>().swap(v);
+    for (auto& v : soff) std::vector<uint64_t>().swap(v);
+    for (auto& v : sbytes) std::vector<uint64_t>().swap(v);
+  }
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
     if (aborted) throw Fail{S3IMPH_ERR_RCCL, "build MPHF: a peer rank failed"};
@@ -236,14 +242,16 @@ std::map<std::tuple<std::vector<int>, bool, uint64_t>, std::unique_ptr<MultiCtx>
 std::vector<std::unique_ptr<MultiCtx>> g_retired;  // aborted sets (see build_from_host_multi)
 
 // Free the contexts (workspaces, communicators) of sets already taken out of g_multi, once no
-// build holds them; the emptied sets stay allocated (g_retired) for callers that still hold a
-// pointer and will see `released`.
+// build holds them, and the host transport's staging; the emptied shells (a few words each)
+// stay allocated (g_retired) for callers that still hold a pointer and will see `released`.
 void release_sets(std::vector<std::unique_ptr<MultiCtx>> sets) {
   for (auto& mc : sets) {
     {
       std::lock_guard<std::mutex> lk(mc->mu);
       for (s3imph_ctx* c : mc->ctx) s3imph_ctx_destroy(c);
       mc->ctx.clear();
+      std::vector<s3imph_ctx*>().swap(mc->ctx);
+      if (mc->hub) mc->hub->free_buffers();
       mc->released = true;
     }
     std::lock_guard<std::mutex> glk(g_multi_mu);
@@ -481,6 +489,7 @@ int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const ui
       }
       for (s3imph_ctx* c : mc->ctx) s3imph_ctx_destroy(c);
       mc->ctx.clear();
+      if (mc->hub) mc->hub->free_buffers();
       std::lock_guard<std::mutex> glk(g_multi_mu);
       for (auto it = g_multi.begin(); it != g_multi.end(); ++it)
         if (it->second.get() == mc) {
@@ -501,6 +510,28 @@ int build_from_host_multi(const std::vector<int>& devs, unsigned flags, const ui
     *msg = f.msg;
     return f.code;
   }
+}
+
+// every cached multi-GPU set that no build holds, except `keep` (a build that ran out of HBM
+// drops them before its one retry); returns how many were freed
+int release_idle_multi_sets(const void* keep) {
+  std::vector<std::unique_ptr<MultiCtx>> idle;
+  {
+    std::lock_guard<std::mutex> lk(g_multi_mu);
+    for (auto it = g_multi.begin(); it != g_multi.end();) {
+      MultiCtx* mc = it->second.get();
+      if (mc != keep && mc->mu.try_lock()) {  // (out of g_multi now: no new caller can take it)
+        mc->mu.unlock();
+        idle.push_back(std::move(it->second));
+        it = g_multi.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  const int n = (int)idle.size();
+  release_sets(std::move(idle));
+  return n;
 }
 
 // every cached multi-GPU set (s3imph_release_workspaces)
@@ -534,6 +565,11 @@ extern "C" int s3imph_build_host_multi(int num_gpus, const int* devices, unsigne
   int rc;
   try {
     rc = build_from_host_multi(devs, flags, blob, offsets, pos, n, fp_out, pos_out, &mph, &msg);
+    // out of HBM (the failed set is retired already): free the other cached workspaces, once more
+    if (rc == S3IMPH_ERR_NOMEM && reclaim_cached(nullptr)) {
+      msg.clear();
+      rc = build_from_host_multi(devs, flags, blob, offsets, pos, n, fp_out, pos_out, &mph, &msg);
+    }
   } catch (const std::bad_alloc&) {
     set_err(err, errlen, "out of host memory");
     return S3IMPH_ERR_NOMEM;

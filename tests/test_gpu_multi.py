@@ -143,6 +143,29 @@ def test_bitmap_level0_through_p0_tiles(s3, oracle_lib, monkeypatch, capfd, rank
     assert err.count("level 0 through P0 super-tiles") == ranks, err[-2000:]
 
 
+@pytest.mark.parametrize("ranks", [1, 2])
+def test_bitmap_capacity_miss_reruns_conservatively(s3, oracle_lib, monkeypatch, capfd, ranks):
+    """under S3IMPH_DIST_STRICT only a size-bound miss fails the bitmap build.  A
+    capacity miss (a reservation-slot overflow, or a settle-fed level without its P0 buffers:
+    injected after level 0 by S3IMPH_FAULT_BM_OVERFLOW) reruns the bitmap decomposition once in
+    its conservative form (no settle-fed levels, no list levels through P0): bit-exact, and
+    every rank reports the rerun."""
+    monkeypatch.setenv("S3IMPH_DEBUG", "1")
+    monkeypatch.setenv("S3IMPH_DIST_STRICT", "1")
+    monkeypatch.setenv("S3IMPH_FAULT_BM_OVERFLOW", "1")
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", str(2_000_000 + 29 * ranks))  # fresh contexts read S3IMPH_DEBUG
+    n = 18_000_000
+    blob, offs = s3.gen_keys(0, 37, 20, 0, n)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    if ranks == 1:
+        g = s3.build_host(blob, offs, num_gpus=1, flags=s3.MULTI_FORCE_SHARDED | s3.MULTI_BITMAP)
+    else:
+        g = s3.build_host(blob, offs, devices=[0] * ranks, flags=s3.MULTI_BITMAP)
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+    err = capfd.readouterr().err
+    assert err.count("a capacity miss, rerunning conservatively") == ranks, err[-2000:]
+
+
 @pytest.mark.parametrize("ranks", [2, 3])
 def test_thread_per_rank_chunked_level0_exchange(s3, oracle_lib, monkeypatch, capfd, ranks):
     """Shards of >= 8M keys take the chunked level 0 (s3imph_build.hip route0_chunked):

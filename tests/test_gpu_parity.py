@@ -246,12 +246,12 @@ def test_build_host_key_longer_than_u16(s3, oracle_lib):
 
 
 def test_build_host_into_reused_buffers_piecewise_hash(s3, oracle_lib):
-    """s3imph_build_host_into: the blob crosses PCIe in pieces and the level-0 hash of each piece
-    is launched as it lands (HashFeed); outputs and mph.bin go to caller buffers reused across
-    calls.  Sets of every level-0 path — P0 (18M keys: the fused partition hash in pieces),
-    the plain pair hash (2M), a skewed set (k_hash_skew after the last piece), a blob at a
-    non-zero offsets[0] with custom positions, a tiny set — each bit-exact vs the oracle, and
-    equal to s3imph_build_host's malloc'd mph.bin."""
+    """s3imph_build_host_into: outputs and mph.bin go to caller buffers reused across calls.
+    Sets of every level-0 path — P0 (18M keys), the plain pair hash (2M), a skewed set
+    (k_hash_skew), a blob at a non-zero offsets[0] with custom positions, a tiny set — each
+    bit-exact vs the oracle, and equal to s3imph_build_host's malloc'd mph.bin.  (Every blob
+    here is under 512 MiB, so with the default piece size it crosses PCIe as ONE piece; the
+    piecewise hash is test_piecewise_hash_every_level0_path.)"""
     cap = 18_000_000
     out = (np.zeros(cap, np.uint64), np.zeros(cap, np.uint64))
     mph_buf = np.zeros(s3.mph_bin_bound(cap), np.uint8)
@@ -692,17 +692,19 @@ def test_repeated_builds_identical(s3, oracle_lib, ctx, kind, avg):
 
 
 def _parity_subprocess(env: dict, cases) -> None:
-    """Build `cases` (n, kind, avg) through s3imph.build_host in a fresh process with
+    """Build `cases` (n, kind, avg[, custom positions]) through s3imph.build_host in a fresh process with
     `env` set (the library reads its A/B knobs once per process): bit-exact vs the oracle."""
     import subprocess
     import sys
     code = (
         "import sys; sys.path[:0]=[%r, %r]\n"
         "import numpy as np, torch, s3imph, oracle as O\n"
-        "for n, kind, avg in %r:\n"
+        "for case in %r:\n"
+        "    n, kind, avg = case[:3]\n"
         "    blob, offs = s3imph.gen_keys(kind, 3, avg, 0, n)\n"
-        "    st, fp, po, mph = O.lib().build(blob[: offs[-1]], offs)\n"
-        "    g = s3imph.build_host(blob, offs)\n"
+        "    pos = np.random.default_rng(n).permutation(n).astype(np.uint64) * np.uint64(5) if case[3:] else None\n"
+        "    st, fp, po, mph = O.lib().build_mt(blob[: offs[-1]], offs, pos, threads=16)\n"
+        "    g = s3imph.build_host(blob, offs, pos)\n"
         "    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po), n\n"
         "print('ok')\n"
     ) % (os.path.join(os.path.dirname(GOLDEN), "..", "s3-inv-db_amd"), os.path.join(os.path.dirname(GOLDEN), "..", "oracle"),
@@ -738,3 +740,13 @@ def test_reservation_overflow_reruns(s3, oracle_lib):
     flags the overflow, the build reruns on the counted path, outputs stay bit-exact."""
     _parity_subprocess({"S3IMPH_RES0": "2", "S3IMPH_RES_FILL": "1"},
                        [(3000, 0, 40), (300_000, 0, 24), (2_500_000, 1, 0)])
+
+
+def test_piecewise_hash_every_level0_path(s3, oracle_lib):
+    """the host build's blob crossing PCIe in many pieces (S3IMPH_PIECE_BITS=20: 1 MiB
+    and up, at most 16 pieces), the level-0 hash of each piece launched as it lands (HashFeed),
+    on every level-0 path below P0: the pair hash with caller positions (3M keys), the pair hash
+    with identity positions (2M), the skewed hash (1.5M); plus P0's fused hash (18M).
+    Bit-exact vs the oracle."""
+    _parity_subprocess({"S3IMPH_PIECE_BITS": "20"},
+                       [(3_000_000, 0, 24, True), (2_000_000, 0, 32), (1_500_000, 1, 0), (18_000_000, 0, 20)])

@@ -7,6 +7,7 @@ sums one rank's kernel time — the device time that rank would spend on its own
 transfers excluded: they are host copies here).  Prints the wall time of each build (not a
 scaling number: the ranks share one GPU and serialise).
     python tools/p8_geometry.py [P] [keys_per_rank] [avg] [builds]
+avg 0 selects the skewed generator (C5: lengths log-uniform on 1-1024 B).
 """
 import os
 import sys
@@ -25,7 +26,7 @@ AVG = int(sys.argv[3]) if len(sys.argv) > 3 else 64
 B = int(sys.argv[4]) if len(sys.argv) > 4 else 2
 n = P * K
 t = time.perf_counter()
-blob, offs = s3imph.gen_keys(0, 42, AVG, 0, n)
+blob, offs = s3imph.gen_keys(1 if AVG == 0 else 0, 42, AVG, 0, n)
 print(f"[p8] {P} ranks x {K} keys, avg {AVG} B: {n} keys, {int(offs[-1]) / 1e9:.1f} GB of key bytes "
       f"(generated in {time.perf_counter() - t:.1f} s)", file=sys.stderr, flush=True)
 out = (np.zeros(n, np.uint64), np.zeros(n, np.uint64))
@@ -37,5 +38,6 @@ for b in range(B):
 # a cheap property: every output slot written once (positions are a permutation of [0, n))
 seen = np.zeros(n, np.uint8)
 seen[po] = 1
-print(f"[p8] mph_pos covers {int(seen.sum())} of {n} slots", file=sys.stderr, flush=True)
+print(f"[p8] mph_pos covers {int(seen.sum())} of {n} slots; mph.bin sha256 "
+      f"{__import__('hashlib').sha256(mph).hexdigest()[:16]}", file=sys.stderr, flush=True)
 assert int(seen.sum()) == n
