@@ -2173,6 +2173,19 @@ int build_dist(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, cons
       return S3IMPH_ERR_INTERNAL;  // tests use this to prove the bitmap path built the index
     }
   }
+  // one rank has nothing to route: its routed build is the single-GPU build (P0 level 0 up to
+  // 2^31 keys, where the routed level 0 stops at 2^30 positions), outputs at their global p
+  // (S3IMPH_DIST_ROUTE_SELF keeps the routed kernels for the tests that drive them)
+  if (rc == kDistRetry && d.nranks == 1 && !c->route_self && (pos || key_base == 0)) {
+    if (n_local > out_cap) {
+      *msg = "build MPHF: output capacity " + std::to_string(out_cap) + " < " + std::to_string(n_local);
+      return S3IMPH_ERR_INVALID;
+    }
+    rc = build_single(c, blob, offsets, pos, n_local, fp_out, pos_out, s, info, msg);
+    if (rc != S3IMPH_OK) return rc;
+    d.seg.assign({0, n_local, 0});
+    d.out_n = n_local;
+  }
   for (int attempt = 1; rc == kDistRetry && attempt < 3; ++attempt) {
     ev_begin(c);
     ev_mark(c, s, "start");

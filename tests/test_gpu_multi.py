@@ -29,6 +29,19 @@ def _expect(oracle_lib, blob, offs, pos=None):
     return fp, po, mph
 
 
+def test_one_rank_routed_build_is_the_single_gpu_build(s3, oracle_lib, monkeypatch, capfd):
+    """A one-rank sharded build in the routed mode has nothing to route: it runs the single-GPU
+    pipeline (P0 level 0 for sets past 2048 tiles), outputs at their global positions."""
+    monkeypatch.setenv("S3IMPH_DEBUG", "1")
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", str((2 << 20) + 53))
+    blob, offs = s3.gen_keys(0, 14, 24, 0, 18_000_000)
+    fp, po, mph = _expect(oracle_lib, blob, offs)
+    g = s3.build_host(blob, offs, num_gpus=1, flags=s3.MULTI_FORCE_SHARDED)
+    assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po)
+    err = capfd.readouterr().err
+    assert "attempt 0: status 0x0" in err, err[-2000:]  # build_single's debug line
+
+
 def test_one_gpu_default_is_the_single_gpu_build(s3, oracle_lib):
     blob, offs = s3.gen_keys(0, 5, 32, 0, 300_000)
     fp, po, mph = _expect(oracle_lib, blob, offs)
@@ -38,8 +51,10 @@ def test_one_gpu_default_is_the_single_gpu_build(s3, oracle_lib):
 
 def test_one_gpu_sharded_over_rccl(s3, oracle_lib, monkeypatch):
     """num_gpus = 1 forced onto the sharded path: an in-process RCCL communicator
-    (ncclCommInitAll) carries every collective of the routed levels."""
-    monkeypatch.setenv("S3IMPH_DIST_SWITCH", "20000")
+    (ncclCommInitAll) carries every collective of the routed levels (S3IMPH_DIST_ROUTE_SELF:
+    one rank routes like P > 1; without it a one-rank routed build is the single-GPU build)."""
+    monkeypatch.setenv("S3IMPH_DIST_SWITCH", "20001")  # a fresh set (reads S3IMPH_DIST_ROUTE_SELF)
+    monkeypatch.setenv("S3IMPH_DIST_ROUTE_SELF", "1")
     blob, offs = s3.gen_keys(0, 6, 40, 0, 400_000)
     fp, po, mph = _expect(oracle_lib, blob, offs)
     for _ in range(2):  # the second build reuses the cached contexts and communicator
