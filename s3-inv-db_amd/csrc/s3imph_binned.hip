@@ -2839,12 +2839,16 @@ __device__ __forceinline__ uint64_t lb_resolve(unsigned long long* flags, uint64
 // k20: R20 records (identity positions: p = pos_base + key index, 12-B stage entries);
 // otherwise Rec records of any level whose tiles are 2^14 positions (16-B stage entries).
 // o20: the collided records leave as R20 (the next level's list is R20, BinBuffers::l20).
-template <bool k20>
+// kPN (P0F, level 0 of a single-GPU build): the collided records go straight to level 1's
+// super-tile regions (NextPart: per (block, super-tile) regions of R20, the level-0 hash's
+// scheme) instead of level 1's list; level 1's size came from k_p0_count before this kernel.
+template <bool k20, bool kPN = false>
 __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restrict__ bucket_v, uint64_t bucket_cap,
                                                   const unsigned* __restrict__ tcnt, unsigned long long* flags,
                                                   uint64_t* __restrict__ bits, Rec* __restrict__ next,
                                                   uint64_t* __restrict__ fp_out, uint64_t* __restrict__ pos_out,
-                                                  LevelState* st, uint64_t pos_base, bool o20) {
+                                                  LevelState* st, uint64_t pos_base, bool o20, NextPart pn = NextPart{}) {
+  static_assert(!kPN || k20, "the next level's regions hold R20 records");
   using PT = std::conditional_t<k20, uint32_t, uint64_t>;  // key index, or p
   __shared__ uint64_t sf[kP0Stage];
   __shared__ PT si[kP0Stage];
@@ -2853,7 +2857,12 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
   __shared__ unsigned s_cnt[2][kResShards];
   __shared__ unsigned long long s_t[2], s_b0, s_excl;
   __shared__ unsigned s_late;
-  if (!level_active(level, st)) return;
+  __shared__ unsigned p_cur[kPN ? kMaxRanks : 1];  // kPN: this block's fill of each level-1 region
+  if (!level_active(level, st)) {
+    if constexpr (kPN)  // (the next level's scatter reads every block's fills)
+      for (unsigned q = threadIdx.x; q < pn.S; q += kP0T) pn.pcnt[(uint64_t)blockIdx.x * pn.S + q] = 0;
+    return;
+  }
   const uint64_t N = st->out_cap;
   const bool out_on = level_out_on(st, level);
   const uint64_t words = st->words[level], magic = st->magic[level];
@@ -2901,6 +2910,30 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
       f_ = q->f;
       p_ = q->p;
     }
+  };
+  // kPN: level 1's geometry (sized by k_p0_level1_setup) and this block's region appends
+  uint64_t w1 = 0, m1 = 0, seed1 = 0;
+  uint32_t pmul = 0;
+  unsigned rcap = 0;
+  bool rover = false;
+  if constexpr (kPN) {
+    if (threadIdx.x < (unsigned)kMaxRanks) p_cur[threadIdx.x] = 0;  // (ordered by the barrier below)
+    w1 = st->words[level + 1];
+    m1 = st->magic[level + 1];
+    seed1 = level_seed(level + 1);
+    pmul = 0xffffffffu / pn.tps_sub + 1;  // exact for (position >> 14) < 2^18 (the hash's partition)
+    rcap = (unsigned)pn.reg_cap;
+  }
+  // a collided record into its level-1 super-tile's region of this block
+  auto put_region = [&](uint64_t kk, uint64_t ff, uint32_t ii) {
+    const uint64_t x1 = w1 >= (1ull << 19) ? bb_index_big(seed1, kk, w1, m1) : bb_index(seed1, kk, w1, m1);
+    unsigned sp = __umulhi((uint32_t)(x1 >> kRegTileMaxBits), pmul);
+    if (sp >= pn.S) sp = pn.S - 1;  // a level past its bound: the scatter flags the geometry
+    const unsigned at = atomicAdd(&p_cur[sp], 1u);
+    if (at < rcap)
+      pn.sup[((uint64_t)blockIdx.x * pn.S + sp) * rcap + at] = r20_make(kk, ff, ii);
+    else
+      rover = true;
   };
   uint64_t k[kP0R], f[kP0R];
   PT p[kP0R];
@@ -3047,9 +3080,13 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
           const unsigned j = (unsigned)r * kP0T + me;
           const unsigned x = LOC(r);
           const bool redo = j < nk && !((sA[x >> 5] >> (x & 31)) & 1u);
-          const uint64_t m = __ballot(redo);
-          if (redo) next_put(next, o20, o + __popcll(m & lt), k[r], f[r], pos_of(p[r]), pos_base);
-          o += __popcll(m);
+          if constexpr (kPN) {
+            if (redo) put_region(k[r], f[r], (uint32_t)p[r]);
+          } else {
+            const uint64_t m = __ballot(redo);
+            if (redo) next_put(next, o20, o + __popcll(m & lt), k[r], f[r], pos_of(p[r]), pos_base);
+            o += __popcll(m);
+          }
         }
       } else {
         #pragma unroll 1
@@ -3063,9 +3100,13 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
             const unsigned x = (unsigned)(bb_index(seed, jk, words, magic) - tbase);
             redo = !((sA[x >> 5] >> (x & 31)) & 1u);
           }
-          const uint64_t m = __ballot(redo);
-          if (redo) next_put(next, o20, o + __popcll(m & lt), jk, jf, pos_of(jp), pos_base);
-          o += __popcll(m);
+          if constexpr (kPN) {
+            if (redo) put_region(jk, jf, (uint32_t)jp);
+          } else {
+            const uint64_t m = __ballot(redo);
+            if (redo) next_put(next, o20, o + __popcll(m & lt), jk, jf, pos_of(jp), pos_base);
+            o += __popcll(m);
+          }
         }
       }
     }
@@ -3157,6 +3198,109 @@ __global__ __launch_bounds__(kP0T) void k_tile_p0(int level, const void* __restr
     cb = nb;
   }
   if (bad) atomicOr(&st->status, kStRank);
+  if constexpr (kPN) {  // (the tile loop ended on a barrier: every append is in p_cur)
+    __syncthreads();
+    for (unsigned q = tid; q < pn.S; q += kP0T) pn.pcnt[(uint64_t)blockIdx.x * pn.S + q] = min(p_cur[q], rcap);
+    if (rover) atomicOr(&st->status, kStResOverflow);  // a region overflowed: the build reruns
+  }
+}
+
+// ---- P0F: level 1 fed by level 0's tile kernel -------------------------------------------
+// Level 1's geometry needs its exact size, which the single-GPU build otherwise learns only
+// once level 0's tile kernel has finished; k_p0_count gets it first.  Per 2^14-position tile
+// of level 0 it marks A / C in LDS from each slot's in-tile position (a u16 the super-tile
+// scatter wrote beside the record: 2 B per key read instead of 20) and counts the settled keys,
+// popcount(A & ~C), into st->settled0; k_p0_level1_setup then sizes level 1 from N minus
+// them, and k_tile_p0<true, true> writes level 1's records straight into its super-tile regions
+// (the level-0 hash's scheme).  Level 1 then reaches 2^14-position register tiles through the
+// super-tile scatter, instead of the reservation scatter and the split kernel's sub-tile
+// scratch (40 B per record written and read back).
+constexpr int kCntT = 512;
+constexpr int kCntU = 4;  // slot positions in flight per thread
+__global__ __launch_bounds__(kCntT) void k_p0_count(const uint16_t* __restrict__ xs, const unsigned* __restrict__ tcnt,
+                                                   uint64_t bucket_cap, LevelState* st) {
+  __shared__ uint32_t sA[kP0W32], sC[kP0W32];
+  __shared__ unsigned s_fo[kResShards + 1];
+  __shared__ unsigned long long s_w[kCntT / 64];
+  if (st->status & kStStop) return;
+  const uint64_t T = st->ntiles[0];
+  if (T == 0) return;
+  const uint64_t cap = bucket_cap / T, scap = cap / kResShards;
+  const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  unsigned long long settled = 0;
+  for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {
+    for (unsigned w = tid; w < kP0W32; w += kCntT) {
+      sA[w] = 0;
+      sC[w] = 0;
+    }
+    if (wave == 0) {  // the tile's slot fills: exclusive prefix over lanes 0-7
+      const unsigned c = lane < (unsigned)kResShards ? tcnt[t * kResShards + lane] : 0u;
+      unsigned x = c;
+#pragma unroll
+      for (int d = 1; d < kResShards; d <<= 1) {
+        const unsigned y = __shfl_up(x, d);
+        if (lane >= (unsigned)d) x += y;
+      }
+      if (lane < (unsigned)kResShards) s_fo[lane] = x - c;
+      if (lane == (unsigned)kResShards - 1) s_fo[kResShards] = x;
+    }
+    __syncthreads();
+    unsigned fo[kResShards + 1];
+#pragma unroll
+    for (int q = 0; q <= kResShards; ++q) fo[q] = s_fo[q];
+    const unsigned nrec = fo[kResShards];
+    for (unsigned i0 = 0; i0 < nrec; i0 += kCntT * kCntU) {
+      unsigned x[kCntU];
+#pragma unroll
+      for (int u = 0; u < kCntU; ++u) {  // straight-line, clamped: all loads in flight together
+        const unsigned i = min(i0 + u * kCntT + tid, nrec - 1);
+        unsigned sh = 0;
+#pragma unroll
+        for (int q = 1; q < kResShards; ++q) sh += i >= fo[q] ? 1u : 0u;
+        unsigned b = fo[0];
+#pragma unroll
+        for (int q = 1; q < kResShards; ++q)
+          if (sh == (unsigned)q) b = fo[q];
+        x[u] = xs[t * cap + (uint64_t)sh * scap + (i - b)];
+      }
+#pragma unroll
+      for (int u = 0; u < kCntU; ++u) {
+        if (i0 + u * kCntT + tid >= nrec) continue;
+        const uint32_t bit = 1u << (x[u] & 31);
+        const uint32_t old = atomicOr(&sA[x[u] >> 5], bit);
+        if (old & bit) atomicOr(&sC[x[u] >> 5], bit);
+      }
+    }
+    __syncthreads();
+    for (unsigned w = tid; w < kP0W32; w += kCntT) settled += (unsigned)__popc(sA[w] & ~sC[w]);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) settled += __shfl_xor(settled, d);
+  if (lane == 0) s_w[wave] = settled;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long sum = 0;
+#pragma unroll
+    for (int w = 0; w < kCntT / 64; ++w) sum += s_w[w];
+    if (sum) atomicAdd(&st->settled0, sum);
+  }
+}
+
+// Level 1's words, Barrett reciprocal and word offsets from its exact size (n[0] minus level 0's
+// settled keys), as k_scatter_res's level setup would write them; n[1] itself is still counted
+// by level 0's tile kernel (the same value).
+__global__ void k_p0_level1_setup(LevelState* st, uint64_t cap_words) {
+  if (threadIdx.x != 0 || blockIdx.x != 0 || (st->status & kStStop)) return;
+  const uint64_t n1 = st->n[0] - st->settled0;
+  const uint64_t w = level_words(n1);
+  st->words[1] = w;
+  st->magic[1] = level_magic(w);
+  st->woff[1] = st->woff[0] + st->words[0];
+  st->woff[2] = st->woff[1] + w;
+  st->nlevels = 1;
+  if (st->woff[2] > cap_words) atomicOr(&st->status, kStOverflow);
+  if (n1 <= kGate) (atomicOr(&st->status, kStGeometry), atomicCAS(&st->pad0_, 0u, 6u));  // (never at P0 sizes)
 }
 
 // ------------------------------------------------------------ mid-size levels --------
@@ -4212,11 +4356,14 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
     // 382), and one block's count / scan / stage phases run beside the other's loads and stores
     constexpr unsigned bps = kResShards;
     if (p.tps <= 256)
-      k_scatter_p0<3072, 256, 512><<<p.S * bps, 512, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+      k_scatter_p0<3072, 256, 512><<<p.S * bps, 512, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags,
+                                                             b.st, b.tile_prof, kRegTileMaxBits, nullptr, level);
     else if (p.tps <= 512)
-      k_scatter_p0<3072, 512, 512><<<p.S * bps, 512, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+      k_scatter_p0<3072, 512, 512><<<p.S * bps, 512, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags,
+                                                             b.st, b.tile_prof, kRegTileMaxBits, nullptr, level);
     else
-      k_scatter_p0<2560, 1024, 512><<<p.S * bps, 512, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+      k_scatter_p0<2560, 1024, 512><<<p.S * bps, 512, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags,
+                                                              b.st, b.tile_prof, kRegTileMaxBits, nullptr, level);
     return;
   }
   static const unsigned bps_knob = [] {  // A/B knob S3IMPH_P0_BPS: blocks per super-tile (a multiple of 8)
@@ -4242,16 +4389,34 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
     return;
   }
   if (p.tps <= 256)
-    k_scatter_p0<6144, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+    k_scatter_p0<6144, 256><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st,
+                                                       b.tile_prof, kRegTileMaxBits, nullptr, level);
   else if (p.tps <= 512)
-    k_scatter_p0<6144, 512><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+    k_scatter_p0<6144, 512><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st,
+                                                       b.tile_prof, kRegTileMaxBits, nullptr, level);
   else
-    k_scatter_p0<6144, 1024><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st, b.tile_prof);
+    k_scatter_p0<6144, 1024><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st,
+                                                        b.tile_prof, kRegTileMaxBits, nullptr, level);
 }
 
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
   k_tile_p0<true><<<256, kP0T, 0, s>>>(0, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.bits, b.list[0], b.fp_out,
                                        b.pos_out, b.st, b.pos_base, b.list20(1));
+}
+
+void launch_p0_count(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
+  k_p0_count<<<1024, kCntT, 0, s>>>(p.x, p.tcnt, p.bucket_cap, b.st);
+  k_p0_level1_setup<<<1, 64, 0, s>>>(b.st, b.cap_words);
+}
+
+void launch_p0_tile_fed(const BinBuffers& b, const P0Bufs& p, const NextPart& np, hipStream_t s) {
+  k_tile_p0<true, true><<<kP0FedGrid, kP0T, 0, s>>>(0, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.bits, nullptr,
+                                                    b.fp_out, b.pos_out, b.st, b.pos_base, true, np);
+}
+
+void launch_p0_tile_level(int level, const BinBuffers& b, const P0Bufs& p, hipStream_t s) {
+  k_tile_p0<true><<<256, kP0T, 0, s>>>(level, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.bits, b.list[level & 1],
+                                       b.fp_out, b.pos_out, b.st, b.pos_base, b.list20(level + 1));
 }
 
 }  // namespace s3imph

@@ -637,6 +637,23 @@ bool p0_try_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s, P0Bu
   }
 }
 
+// P0F (A/B knob S3IMPH_P0F=0: off): level 1 of a P0 build fed by level 0's tile kernel
+bool p0f_on() {
+  static const bool v = [] {
+    const char* e = dev_env("S3IMPH_P0F");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+
+// P0F region capacity: level 0's tile kernel takes its tiles by ticket, so one block's share of
+// level 1's records follows its share of the tiles, not a Poisson fill: regions hold twice the
+// mean (a block would have to run twice its share of the tiles to overflow; then the build reruns)
+uint64_t p0f_region_cap(uint64_t n1, unsigned S) {
+  const double mean = (double)n1 / ((double)kP0FedGrid * S);
+  return (uint64_t)(2.0 * mean + 10.0 * std::sqrt(mean) + 256.0);
+}
+
 void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
   BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
@@ -646,10 +663,56 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
   if (!conservative && c->p0 && !pos && n <= kP0MaxKeys && !hash_only_knob() && T14 > p0_min_tiles() &&
       T14 <= kP0MaxS * kP0MaxTps) {
     // level 0 in 2^14-position register tiles through super-tiles (s3imph_internal.h, P0); its
-    // buffers (~1.2 n x 20 B) may not fit next to the workspace: then the split-kernel path
+    // buffers (~1.2 n x 20 B) may not fit next to the workspace: then the split-kernel path.
+    // P0F: a level 1 past the reservation scatter's 4096 tiles (C3: 4.8k) is fed by level 0's
+    // tile kernel when its regions fit the super-tile buffer; level 0's scatter then also writes
+    // each slot's in-tile position for the count pass (k_p0_count).
+    const double n1m = (double)n * q;
+    const uint64_t ng1 = (uint64_t)(n1m * 1.02 + 6.0 * std::sqrt(n1m)) + 1024;  // level 1's size bound
+    const uint64_t T1 = tiles_of(level_words(ng1), kRegTileMaxBits, 0);
+    bool fed = p0f_on() && T1 > kScatterTiles && T1 <= kP0MaxS * kP0MaxTps;
     P0Bufs p;
-    if (p0_try_bufs(c, n, n, s, &p)) {
+    if (p0_try_bufs(c, n, n, s, &p, kRegTileMaxBits, fed)) {
+      P0Bufs p1{};
+      if (fed) {  // level 1's super-tiles, its regions in c->p0_sup (free once level 0's scatter ran)
+        uint64_t need1 = 0;
+        p1 = p0_geom(c, ng1, ng1, kRegTileMaxBits, &need1);
+        p1.reg_cap = p0f_region_cap(ng1, p1.S);
+        fed = p1.S <= (unsigned)kMaxRanks && (uint64_t)kP0FedGrid * p1.S * p1.reg_cap <= c->p0_sup_cap &&
+              T1 <= c->p0_tiles && p0_fused(blob, p);
+        p1.sup = c->p0_sup;
+        p1.sup_cap = c->p0_sup_cap;
+        p1.nb = kP0FedGrid;
+        p1.pcnt = c->p0_pcnt;
+        p1.scnt = c->p0_scnt;
+        p1.bucket = p.bucket;  // (level 0's slots: read by its tile kernel before level 1's scatter)
+        p1.bucket_cap = p.bucket_cap;
+        p1.tcnt = p.tcnt;
+        p1.flags = p.flags;
+      }
+      if (!fed) p.x = nullptr;
       const LevelGeom g0 = choose_geom(n, kTargetTiles0, chunks0(n), kRegTileMaxBits);
+      if (fed) {
+        const LevelsPlan P = plan_levels_from(c, b, 2, (uint64_t)(n1m * q), g0, false);
+        b.l20 = c->l20_mask = plan_l20(c, b, P, true, n);
+        launch_init_state(c->d_st, n, n, s, offsets);
+        ev_mark(c, s, "init");
+        launch_p0_hash(blob, offsets, n, b, g0, p, s);
+        ev_mark(c, s, "hash_part0");
+        launch_p0_scatter(b, p, true, s);
+        launch_p0_count(b, p, s);
+        ev_mark(c, s, "scatter0_p0");
+        const NextPart np{p1.sup, p1.reg_cap, p1.pcnt, p1.tps_sub(), p1.S, nullptr};
+        launch_p0_tile_fed(b, p, np, s);
+        ev_mark(c, s, "tile0_p0");
+        HIPCHECK(hipMemsetAsync(p1.tcnt, 0, c->p0_tiles * kResShards * sizeof(unsigned), s));
+        launch_p0_scatter(b, p1, true, s, 1);
+        launch_p0_tile_level(1, b, p1, s);
+        ev_mark(c, s, "level1_p0");
+        fault_dup_record(c, c->list[1], s, b.list20(2));
+        run_levels(c, b, P, 2, s);
+        return;
+      }
       // the list levels' plan first: level 0's tile kernel writes level 1's list as R20 or Rec
       const LevelsPlan P = plan_levels_from(c, b, 1, (uint64_t)((double)n * q), g0, false);
       b.l20 = c->l20_mask = plan_l20(c, b, P, true, n);

@@ -55,6 +55,8 @@ struct LevelState {
   unsigned long long dS[kMaxLevels + 2];       // words per rank range (owner = word / dS)
   unsigned long long dmagic[kMaxLevels + 2];   // Barrett reciprocal of dS
   unsigned long long gn[kMaxLevels + 2];       // global key count of level L
+  // P0F (single GPU): level 0's settled keys, counted before its tile kernel (k_p0_count)
+  unsigned long long settled0;
 };
 
 #if defined(__HIPCC__)
@@ -307,7 +309,16 @@ bool p0_fused(const uint8_t* blob, const P0Bufs& p);  // the hash partitions (al
 uint64_t p0_region_cap(uint64_t n, unsigned S, unsigned blocks);  // records per (hash block, super-tile) region
 unsigned p0_skew_blocks(int skew_cfg);               // k_hash_skew's grid (its fused partition's blocks)
 constexpr int kH0GridHost = 4096;                    // = k_hash0_pair's grid (kH0Grid)
+constexpr int kP0FedGrid = 256;                      // P0F: level 0's tile kernel blocks (level 1's region producers)
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
+// P0F: level 1 fed by level 0's tile kernel (s3imph_binned.hip).  launch_p0_count: level 0's
+// settled keys from the slots' in-tile positions (p.x), then level 1 sized on the device;
+// launch_p0_tile_fed: level 0's tiles with the collided records into level 1's super-tile
+// regions (np); launch_p0_tile_level: a list level's 2^14 tiles from the super-tile slots
+void launch_p0_count(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
+struct NextPart;
+void launch_p0_tile_fed(const BinBuffers& b, const P0Bufs& p, const NextPart& np, hipStream_t s);
+void launch_p0_tile_level(int level, const BinBuffers& b, const P0Bufs& p, hipStream_t s);
 void binned_set_lds_limits();
 void launch_binned_count(int level, const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b,
                          LevelGeom g, int grid_chunks, hipStream_t s, bool histogram = true);
