@@ -2162,6 +2162,10 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   HIPCHECK(hipMemcpyAsync(M, &st->status, 4, hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   ev_collect(c);
+  if (c->debug) {  // the level-0 hash's waves: duration and shader clock of this rank's hash
+    std::fprintf(stderr, "[s3imph] rank %d bitmap: level-0 hash profile\n", R);
+    print_tile_profile(c);
+  }
   {  // this rank's placement flag: agreed, so every rank returns the same way
     int lrc = S3IMPH_OK;
     if ((unsigned)M[0] & kStRank) {
