@@ -119,7 +119,10 @@ void s3imph_free(void *p);
 /* Free the device workspaces the host-memory builds keep between calls (the default context
  * of every device, the cached per-rank contexts of s3imph_build_host_multi); the next build
  * allocates again.  Call when no build is running (a pipeline between index builds, or
- * before handing HBM to something else). */
+ * before handing HBM to something else).  A build that runs out of HBM does the same for the
+ * caches it is not using (those no other thread is building on) and retries once before
+ * returning S3IMPH_ERR_NOMEM (s3imph_build_host[_into|_multi], s3imph_builder_build,
+ * s3imph_build_device, s3imph_ctx_reserve). */
 int s3imph_release_workspaces(void);
 
 /* Multi-GPU host-memory build for ONE calling process (the reference's caller is one
@@ -233,8 +236,11 @@ int s3imph_ctx_create_dist_host(int device, const s3imph_host_comm *comm, int ra
  *                        than its host-side bound reruns the build on ROUTE.
  * Both give byte-identical outputs.  No reference counterpart (bbhash.New runs on one
  * thread, mphf_streaming.go:141).  S3IMPH_DIST_STRICT or-ed into BITMAP: no fallback — a
- * level past its bound fails the build (S3IMPH_ERR_INTERNAL) instead of rerunning on ROUTE
- * (a benchmark of the bitmap decomposition uses it so it never times the other one). */
+ * level past its size bound fails the build (S3IMPH_ERR_INTERNAL) instead of rerunning on
+ * ROUTE (a benchmark of the bitmap decomposition uses it so it never times the other one); a
+ * capacity miss (a reservation-slot overflow, a settle-fed level without its buffers) reruns
+ * the bitmap decomposition once in its conservative form in either mode.  With one rank,
+ * ROUTE is the single-GPU build (nothing to route). */
 #define S3IMPH_DIST_ROUTE 0
 #define S3IMPH_DIST_BITMAP 1
 #define S3IMPH_DIST_STRICT 0x100
