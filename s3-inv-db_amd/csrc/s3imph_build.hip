@@ -904,6 +904,10 @@ int build_single(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, co
     *msg = "build MPHF: more than 2^32-1 keys on one GPU";
     return S3IMPH_ERR_INVALID;
   }
+  if (64 * level_words(n) > ((uint64_t)kMaxTiles << kTileMaxBits)) {  // level 0 past 4096 tiles of 2^19
+    *msg = "build MPHF: more than 2^30 keys on one GPU (level 0 past 2^31 positions): shard them over several GPUs";
+    return S3IMPH_ERR_INVALID;
+  }
   ensure_workspace(c, n);
   set_lds_attrs(c);
   for (int attempt = 0; attempt < 2; ++attempt) {

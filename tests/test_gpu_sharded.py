@@ -14,7 +14,9 @@ fallback (S3IMPH_DIST_STRICT) — the same rank code RCCL drives on an 8-GPU nod
   the oracle at 125M);
 - the P0 tile bound: one rank at exactly kBmMaxTiles = 32 768 level-0 tiles of 2^16 positions
   (N = 2^30 keys: 2^31 positions) equals the single-GPU build; one key more misses the bound:
-  an error under strict mode, the routed decomposition (same bytes) otherwise.
+  an error under strict mode; otherwise the routed fallback, which at one rank is the single-GPU
+  build, refuses the set cleanly (no single GPU takes level 0 past 2^31 positions; two or more
+  ranks split them).
 """
 import numpy as np
 import pytest
@@ -108,9 +110,9 @@ def test_bitmap_level0_at_and_past_the_p0_tile_bound(monkeypatch, capfd):
     with pytest.raises(s3imph.MPHFError) as e:
         s3imph.build_host(blob, offs, num_gpus=1, flags=s3imph.MULTI_FORCE_SHARDED | s3imph.MULTI_BITMAP, out=out)
     assert "size bounds" in str(e.value)
+    # without strict mode the build falls back to routing, which at one rank is the single-GPU
+    # build — and no single GPU takes level 0 past 2^31 positions: a clear error, not a fault
     monkeypatch.delenv("S3IMPH_DIST_STRICT")
-    g = s3imph.build_host(blob, offs, num_gpus=1, flags=s3imph.MULTI_FORCE_SHARDED | s3imph.MULTI_BITMAP, out=out)
-    s3imph.release_workspaces()
-    mph1, fp1, po1 = _single_gpu(blob, offs)
-    assert g[2] == mph1
-    assert np.array_equal(g[0], fp1) and np.array_equal(g[1], po1)
+    with pytest.raises(s3imph.MPHFError) as e:
+        s3imph.build_host(blob, offs, num_gpus=1, flags=s3imph.MULTI_FORCE_SHARDED | s3imph.MULTI_BITMAP, out=out)
+    assert e.value.status == s3imph.ERR_INVALID and "more than 2^30 keys on one GPU" in str(e.value)
