@@ -657,6 +657,7 @@ uint64_t p0f_region_cap(uint64_t n1, unsigned S) {
 void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
                     uint64_t n, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s, bool conservative) {
   BinBuffers b = make_bufs(c, pos, fp_out, pos_out, s);
+  b.dist = false;  // the whole set on this GPU (also a one-rank sharded build, build_dist's routed fallback)
   c->l20_mask = 0;
   const double q = 1.0 - std::exp(-0.5);
   const uint64_t T14 = tiles_of(level_words(n), kRegTileMaxBits, 0);
