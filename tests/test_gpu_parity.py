@@ -750,3 +750,12 @@ def test_piecewise_hash_every_level0_path(s3, oracle_lib):
     Bit-exact vs the oracle."""
     _parity_subprocess({"S3IMPH_PIECE_BITS": "20"},
                        [(3_000_000, 0, 24, True), (2_000_000, 0, 32), (1_500_000, 1, 0), (18_000_000, 0, 20)])
+
+
+def test_p0f_fed_level1_bit_exact(s3, oracle_lib):
+    """P0F (developer knob S3IMPH_P0F=1): level 1 of a 90M-key P0 build (4.4k 2^14
+    tiles, past the reservation scatter's 4096) fed by level 0's tile kernel — a count pass
+    over the slots' in-tile positions sizes level 1 first, level 0's tiles write level 1's
+    records straight into its super-tile regions, level 1 runs the super-tile scatter and the
+    register tiles; a skewed 90M set the same way: bit-exact vs the oracle."""
+    _parity_subprocess({"S3IMPH_P0F": "1"}, [(90_000_000, 0, 24), (90_000_000, 1, 0)])
