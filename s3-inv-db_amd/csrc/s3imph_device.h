@@ -43,6 +43,10 @@ __host__ __device__ __forceinline__ typename std::common_type<A, B>::type max(A 
 #ifndef S3IMPH_NT_LOADS
 #define S3IMPH_NT_LOADS 1
 #endif
+// fnv_window two stream words per iteration (A/B: -DS3IMPH_FNV_UNROLL2=0, one word)
+#ifndef S3IMPH_FNV_UNROLL2
+#define S3IMPH_FNV_UNROLL2 1
+#endif
 #ifndef S3IMPH_NT_SKEW
 #define S3IMPH_NT_SKEW 0
 #endif
@@ -227,7 +231,22 @@ static __device__ __forceinline__ void fnv_window(const uint32_t* win, unsigned 
   // the next stream word's dwords are read one iteration ahead, so the LDS latency hides
   // behind the current word's 64 steps (reads stay within w[0 .. 2 nfull + 2], as the tail's)
   uint32_t cur = w[0], n1 = w[1], n2 = w[2];
-  for (unsigned q = 0; q < nfull; ++q) {
+  unsigned q = 0;
+#if S3IMPH_FNV_UNROLL2
+  // two stream words per iteration: half the loop control and no register rotation moves
+  // (the 16 bytes' dwords w[2q+3 .. 2q+6] requested ahead, within w[0 .. 2 nfull + 2])
+  for (; q + 2 <= nfull; q += 2) {
+    const uint32_t m1 = w[2 * q + 3], m2 = w[2 * q + 4], m3 = w[2 * q + 5], m4 = w[2 * q + 6];
+    fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n1, cur, sb));
+    fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n2, n1, sb));
+    fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(m1, n2, sb));
+    fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(m2, m1, sb));
+    cur = m2;
+    n1 = m3;
+    n2 = m4;
+  }
+#endif
+  for (; q < nfull; ++q) {
     const uint32_t m1 = w[2 * q + 3], m2 = w[2 * q + 4];
     fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n1, cur, sb));
     fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n2, n1, sb));
