@@ -43,9 +43,11 @@ __host__ __device__ __forceinline__ typename std::common_type<A, B>::type max(A 
 #ifndef S3IMPH_NT_LOADS
 #define S3IMPH_NT_LOADS 1
 #endif
-// fnv_window two stream words per iteration (A/B: -DS3IMPH_FNV_UNROLL2=0, one word)
+// fnv_window two stream words per loop iteration: measured neutral to slightly slower (C3 hash
+// 2.53-2.61 vs 2.56-2.64 ms, 4 alternating builds each, profiles/r6_hash/fnv_unroll2_ab_r6h.txt:
+// the loop control it saves issues beside the multiply chain anyway); off
 #ifndef S3IMPH_FNV_UNROLL2
-#define S3IMPH_FNV_UNROLL2 1
+#define S3IMPH_FNV_UNROLL2 0
 #endif
 #ifndef S3IMPH_NT_SKEW
 #define S3IMPH_NT_SKEW 0
