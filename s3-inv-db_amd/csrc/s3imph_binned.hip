@@ -310,6 +310,9 @@ struct P0Part {
   uint64_t reg_cap;  // records per (hash block, super-tile) region
   unsigned* pcnt;    // region fills, written at each block's end
   unsigned tps, S;
+  // overlapped scatter (k_scatter_p0d<kOv>, beside this kernel): each block's XCD, published
+  // with its fills once its region runs are in that XCD's L2; null: no publication
+  unsigned* hxcc = nullptr;
 };
 template <int NT, int BB, bool PF, bool RT = false, bool PT = false>
 __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(const uint8_t* __restrict__ blob,
@@ -385,10 +388,21 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
       for (uint64_t q = g0; q < kTcntWords; q += gs) tcnt[q] = 0;
     }
   }
+  // overlap: this block's XCD at once (the overlapped scatter learns which hash blocks share
+  // its XCD from the first ones: the dispatcher deals blocks to the XCDs round-robin)
+  if (PT && pt.hxcc && tid == 0) __hip_atomic_store(&pt.hxcc[bid], xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t per = (n + NBK - 1) / NBK;
   uint64_t g = (uint64_t)bid * per;
   const uint64_t gend = min(n, g + per);
   if (g >= gend) {
+    if (PT && pt.hxcc) {  // (no region runs: published at once)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __syncthreads();
+      if (tid < pt.S) __hip_atomic_store(&pt.pcnt[(uint64_t)bid * pt.S + tid], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(&st->h0_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
     if (PT && tid < pt.S) pt.pcnt[(uint64_t)bid * pt.S + tid] = 0;
     return;
   }
@@ -677,6 +691,18 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   if (zero) atomicOr(&st->status, kStKeyZero);
   if (RT && tid == 0 && r_over) atomicOr(&st->status, kStRouteOverflow);
   if (PT && tid == 0 && r_over) atomicOr(&st->status, kStOverflow | kStResOverflow);
+  if (PT && pt.hxcc) {
+    // publication for the overlapped scatter, which reads this block's regions through the
+    // same XCD's L2 while the hash runs on: every thread's region stores complete (in L2)
+    // before the barrier, the fills after it, then the block counts as done
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (tid < pt.S)
+      __hip_atomic_store(&pt.pcnt[(uint64_t)bid * pt.S + tid], p_cur[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&st->h0_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   if (PT && tid < pt.S) pt.pcnt[(uint64_t)bid * pt.S + tid] = p_cur[tid];  // wave 0 updated p_cur
 }
 
@@ -1699,6 +1725,214 @@ __global__ __launch_bounds__(NT) void k_scatter_p0(P0In in, unsigned bps, unsign
   }
 #undef P0PROF
   if (geo) (atomicOr(&st->status, kStGeometry), atomicCAS(&st->pad0_, 0u, 5u));
+  if (s_over && tid == 0) atomicOr(&st->status, kStOverflow | kStResOverflow);
+}
+
+// ---- the super-tile scatter, direct form; overlapped with the level-0 hash --------------
+// A round's records stay in registers and go straight to their tiles' slots: LDS holds only
+// the per-tile counts and run bases (~5 KB), so a block fits beside three hash blocks on a CU.
+// A super-tile's records are cut into parts by hash block: part x C + c (XCD x, chunk c)
+// holds the regions of hash blocks x + 8 (c R + i), i < R = NB / 8C, and its records take
+// reservation shard x.
+// kOv: persistent blocks launched beside the level-0 hash (k_hash0_pair with P0Part::hxcc).
+// A block takes the parts of the residue class of hash blocks that runs on its own XCD (the
+// dispatcher deals a launch's blocks to the XCDs round-robin, from a varying first XCD: the
+// class is learned from the first eight hash blocks' published XCDs, each part's checked) by
+// ticket, chunk-major, and waits for the part's hash blocks: they wrote their region runs through its L2, so their fills — published with agent-scope
+// stores after a workgroup release — make the runs readable here without an L2 write-back.  A
+// part whose hash blocks ran elsewhere or are not done within the spin bound, and every part
+// still open when the hash has finished, is left to the follow-up launch (!kOv: one block per
+// (super-tile, part), after the hash, so across a kernel boundary), which skips the parts the
+// overlapped launch marked done.
+struct P0Ov {
+  const unsigned* hxcc = nullptr;  // each hash block's XCD (kOv)
+  unsigned* done = nullptr;        // [part][super-tile] scattered by the overlapped launch
+  unsigned C = 8;                  // chunks per XCD
+};
+constexpr int kDT = 256;
+constexpr int kDU = 16;                       // records per thread and round (4096 per round)
+constexpr unsigned kPcntOpen = 0xffffffffu;   // a region fill not yet published
+constexpr unsigned kOvSpin = 1u << 20;        // wait rounds for a part's hash blocks (~s_sleep 8 each)
+
+template <int kT, bool kOv>
+__global__ __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_scatter_p0d(P0In in, unsigned tps, R20* __restrict__ bucket, uint64_t bcap,
+                                                     unsigned* __restrict__ tcnt, unsigned long long* __restrict__ flags,
+                                                     LevelState* st, P0Ov ov) {
+  __shared__ unsigned cnt[kT];
+  __shared__ unsigned cur[kT];
+  __shared__ unsigned rp[65];
+  __shared__ unsigned s_item, s_ok, s_over;
+  if (st->status & kStStop) return;
+  const unsigned tid = threadIdx.x, lane = lane_id();
+  const uint64_t words = st->words[0], magic = st->magic[0];
+  const uint64_t T = tiles_of(words, kRegTileMaxBits, 0);
+  const bool skw = st->skew != 0;
+  if (kOv && skw) return;  // the skewed hash's regions come after this launch: the follow-up's
+  if (!kOv) {
+    if (blockIdx.x == 0 && tid == 0) {
+      st->ntiles[0] = T;
+      st->nchunks[0] = 0;
+    }
+    for (uint64_t t = (uint64_t)blockIdx.x * kDT + tid; t < T; t += (uint64_t)gridDim.x * kDT) flags[t] = 0;
+  }
+  const unsigned NB = skw ? in.NB_skew : in.NB;
+  const uint64_t reg_cap = skw ? in.reg_cap_skew : in.reg_cap;
+  const unsigned C = ov.C, R = NB / (8 * C), parts = 8 * C;
+  const uint64_t cap = bcap / T, scap = cap / kResShards;
+  const uint64_t seed = level_seed(0);
+  // kOv: the residue class r (hash blocks r, r + 8, ...) that runs on this block's XCD, from
+  // the XCDs the first eight hash blocks publish at their start
+  unsigned x_me = 0;
+  if (kOv) {
+    if (tid < 64) {
+      const unsigned me = xcc_id();
+      unsigned hx = kPcntOpen;
+      uint64_t m = 0;
+      for (unsigned spin = 0; spin < kOvSpin; ++spin) {
+        if (lane < 8) hx = __hip_atomic_load(const_cast<unsigned*>(ov.hxcc) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        m = __ballot(lane < 8 && hx == me);
+        if (m) break;
+        __builtin_amdgcn_s_sleep(8);
+      }
+      if (lane == 0) s_item = m ? (unsigned)__builtin_ctzll(m) : ~0u;
+    }
+    __syncthreads();
+    x_me = s_item;
+    if (x_me >= 8) return;  // no class found: the follow-up takes every part
+    __syncthreads();
+  }
+  if (tid == 0) s_over = 0;
+  for (unsigned t = tid; t < (unsigned)kT; t += kDT) cnt[t] = 0;
+  __syncthreads();
+  bool geo = false;
+  for (;;) {
+    unsigned sidx, part;
+    if (kOv) {
+      if (tid == 0) {
+        unsigned it = ~0u;
+        if (__hip_atomic_load(&st->h0_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < NB)
+          it = (unsigned)atomicAdd(&st->ov_ticket[x_me], 1ull);
+        s_item = it;
+      }
+      __syncthreads();
+      const unsigned it = s_item;
+      if (it >= C * in.S) break;
+      sidx = it % in.S;
+      part = x_me * C + it / in.S;
+    } else {
+      sidx = blockIdx.x / parts;
+      part = blockIdx.x % parts;
+      if (ov.done && ov.done[(uint64_t)part * in.S + sidx]) break;
+    }
+    const unsigned x = part / C, c = part % C;
+    const uint64_t t0 = (uint64_t)sidx * tps;
+    if (t0 >= T) {
+      if (kOv) continue;
+      break;
+    }
+    const unsigned tn = (unsigned)min<uint64_t>(tps, T - t0);
+    if (tn > (unsigned)kT) {
+      geo = true;
+      break;
+    }
+    // the part's runs: lane i of wave 0 reads hash block x + 8 (c R + i)'s fill
+    if (tid < 64) {
+      const unsigned hb = x + 8 * (c * R + lane);
+      unsigned* const pp = const_cast<unsigned*>(in.pcnt) + (uint64_t)hb * in.S + sidx;
+      unsigned v = 0;
+      bool ok = true;
+      if (kOv) {
+        if (lane < R) v = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (unsigned spin = 0;; ++spin) {
+          const bool open = lane < R && v == kPcntOpen;
+          if (!__ballot(open)) break;
+          if (spin >= kOvSpin) {
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(8);
+          if (open) v = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (ok) {  // every hash block of the part ran on this XCD
+          const unsigned me = xcc_id();
+          const unsigned hx =
+              lane < R ? __hip_atomic_load(const_cast<unsigned*>(ov.hxcc) + hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : me;
+          if (__ballot(hx != me)) ok = false;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      } else if (lane < R) {
+        v = *pp;
+      }
+      if (!ok || lane >= R) v = 0;
+      unsigned incl = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned y = __shfl_up(incl, d);
+        if (lane >= (unsigned)d) incl += y;
+      }
+      rp[lane] = incl - v;
+      if (lane == 63) rp[64] = incl;
+      if (lane == 0) s_ok = ok ? 1u : 0u;
+    }
+    __syncthreads();
+    if (kOv && !s_ok) break;  // left to the follow-up launch
+    const unsigned tot = rp[64];
+    const R20* const rbase = in.sup;
+    for (unsigned r0 = 0; r0 < tot; r0 += kDT * kDU) {
+      uint4 rq[kDU];
+      uint32_t rz[kDU];
+      unsigned trk[kDU];
+      // the round's loads straight-line, all in flight together (indices clamped, not guarded)
+#pragma unroll
+      for (int u = 0; u < kDU; ++u) {
+        const unsigned j = min(r0 + (unsigned)u * kDT + tid, tot - 1);
+        unsigned a = 0, z = R;  // the run holding j: rp[a] <= j < rp[a + 1]
+        while (z - a > 1) {
+          const unsigned mid = (a + z) >> 1;
+          if (rp[mid] <= j) a = mid;
+          else z = mid;
+        }
+        const unsigned hb = x + 8 * (c * R + a);
+        const uint32_t* w = (rbase + ((uint64_t)hb * in.S + sidx) * reg_cap + (j - rp[a]))->w;
+        rq[u] = *reinterpret_cast<const uint4*>(w);  // dword-aligned 16-B load
+        rz[u] = w[4];
+      }
+#pragma unroll
+      for (int u = 0; u < kDU; ++u) {
+        trk[u] = ~0u;
+        if (r0 + (unsigned)u * kDT + tid < tot) {
+          const uint64_t k = (uint64_t)rq[u].x | ((uint64_t)rq[u].y << 32);
+          const uint64_t t = (bb_index(seed, k, words, magic) >> kRegTileMaxBits) - t0;
+          if (t < tn) trk[u] = ((unsigned)t << 13) | atomicAdd(&cnt[t], 1u);
+          else geo = true;
+        }
+      }
+      __syncthreads();
+      for (unsigned t = tid; t < tn; t += kDT) {
+        const unsigned n = cnt[t];
+        if (n) {
+          const unsigned at = atomicAdd(&tcnt[(t0 + t) * kResShards + x], n);
+          if (at + n > scap) s_over = 1;
+          cur[t] = (unsigned)((t0 + t) * cap + x * scap + at);
+          cnt[t] = 0;
+        }
+      }
+      __syncthreads();
+      if (s_over) break;
+#pragma unroll
+      for (int u = 0; u < kDU; ++u) {
+        if (trk[u] != ~0u) {
+          uint32_t* d = bucket[cur[trk[u] >> 13] + (trk[u] & 8191u)].w;
+          *reinterpret_cast<uint4*>(d) = rq[u];
+          d[4] = rz[u];
+        }
+      }
+    }
+    if (s_over) break;
+    if (kOv && tid == 0) ov.done[(uint64_t)part * in.S + sidx] = 1u;
+    if (!kOv) break;
+  }
+  if (geo) (atomicOr(&st->status, kStGeometry), atomicCAS(&st->pad0_, 0u, 6u));
   if (s_over && tid == 0) atomicOr(&st->status, kStOverflow | kStResOverflow);
 }
 
@@ -4081,8 +4315,20 @@ void binned_set_lds_limits() {
 template <bool PT>
 void launch_hash_pieces(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                         unsigned long long* prof, const P0Part& pt, hipStream_t s) {
+  // A/B knob S3IMPH_H0_PAD: dynamic LDS bytes added to each block (3072: three blocks per CU
+  // instead of four, leaving the LDS of one co-resident 256-thread super-tile scatter block)
+  // The overlapped scatter (pt.hxcc) takes the fourth slot: 3072 B by default (S3IMPH_OV_PAD)
+  static const unsigned pad = [] {
+    const char* e = dev_env("S3IMPH_H0_PAD");
+    return e ? (unsigned)std::atoi(e) : 0u;
+  }();
+  static const unsigned ov_pad = [] {
+    const char* e = dev_env("S3IMPH_OV_PAD");
+    return e ? (unsigned)std::atoi(e) : 3072u;
+  }();
+  const unsigned pd = PT && pt.hxcc ? ov_pad : pad;
   auto go = [&](unsigned b0, unsigned nb) {
-    k_hash0_pair<kH0T, kH0B, true, false, PT><<<nb, kH0T, 0, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
+    k_hash0_pair<kH0T, kH0B, true, false, PT><<<nb, kH0T, pd, s>>>(blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st,
                                                                  g.tb, g.chunk, b.tcnt, prof, Route0{}, pt, b0,
                                                                  (unsigned)kH0Grid);
   };
@@ -4318,7 +4564,7 @@ void launch_p0_hash(const uint8_t* blob, const uint64_t* offsets, uint64_t n, co
                     const P0Bufs& p, hipStream_t s) {
   if (p0_fused(blob, p)) {
     unsigned long long* prof = b.tile_prof ? b.tile_prof + (uint64_t)(kMaxLevels - 3) * kMaxTiles * 8 : nullptr;
-    const P0Part pt{p.sup, p.reg_cap, p.pcnt, p.tps_sub(), p.S};
+    const P0Part pt{p.sup, p.reg_cap, p.pcnt, p.tps_sub(), p.S, p.hxcc};
     launch_hash_pieces<true>(blob, offsets, n, b, g, prof, pt, s);
     if (b.feed) b.feed->ensure(n);
     // a skewed set: k_hash_skew's groups partition the same way, into regions of its own
@@ -4372,6 +4618,24 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
     return v / kResShards * kResShards;
   }();
   const unsigned bps = bps_knob ? bps_knob : std::max(1u, kP0ScatterBlocks / p.S / kResShards) * kResShards;
+  // A/B knob S3IMPH_P0_SMALL: 256-thread blocks with 1280-record rounds (~33 KB of LDS, less than
+  // three padded hash blocks leave on a CU), as many blocks per super-tile as keep a block's runs
+  // <= 256
+  static const bool small = [] {
+    const char* e = dev_env("S3IMPH_P0_SMALL");
+    return e && std::atoi(e) != 0;
+  }();
+  if (small && !p.x && p.tps <= 512) {
+    const unsigned nb = fused ? in.NB : 0u;
+    const unsigned bsm = std::max(bps, ((nb + 255) / 256 + kResShards - 1) / kResShards * kResShards);
+    if (p.tps <= 256)
+      k_scatter_p0<1280, 256, 256><<<p.S * bsm, 256, 0, s>>>(in, bsm, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags,
+                                                             b.st, b.tile_prof, kRegTileMaxBits, nullptr, level);
+    else
+      k_scatter_p0<1280, 512, 256><<<p.S * bsm, 256, 0, s>>>(in, bsm, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags,
+                                                             b.st, b.tile_prof, kRegTileMaxBits, nullptr, level);
+    return;
+  }
   if (p.x) {
     // the bitmap decomposition: tiles of 2^p.tb positions, each record's in-tile position to
     // p.x as well; its levels have at most kBmMaxTiles tiles in <= 64 super-tiles of <= 1024
@@ -4397,6 +4661,23 @@ void launch_p0_scatter(const BinBuffers& b, const P0Bufs& p, bool fused, hipStre
   else
     k_scatter_p0<6144, 1024><<<p.S * bps, kSB, 0, s>>>(in, bps, p.tps, p.bucket, p.bucket_cap, p.tcnt, p.flags, b.st,
                                                         b.tile_prof, kRegTileMaxBits, nullptr, level);
+}
+
+// The super-tile scatter's direct form (k_scatter_p0d): ov, the persistent launch beside the
+// level-0 hash (one block per CU); otherwise one block per (super-tile, part), skipping the
+// parts an overlapped launch finished (p.ov_done, or none).
+void launch_p0_scatter_direct(const BinBuffers& b, const P0Bufs& p, bool ov, hipStream_t s) {
+  const P0In in{p.sup, p.reg_cap, p.pcnt, (unsigned)kH0Grid, p.S, p0_skew_blocks(b.skew_cfg),
+                p.reg_cap_skew, p.sup_cap, p.scnt, true};
+  const P0Ov o{p.hxcc, p.ov_done, kP0OvChunks};
+  const unsigned grid = ov ? 256u : p.S * 8u * kP0OvChunks;
+#define S3_P0D(KT)                                                                                                  \
+  (ov ? k_scatter_p0d<KT, true> : k_scatter_p0d<KT, false>)<<<grid, kDT, 0, s>>>(in, p.tps, p.bucket, p.bucket_cap,  \
+                                                                                   p.tcnt, p.flags, b.st, o)
+  if (p.tps <= 256) S3_P0D(256);
+  else if (p.tps <= 512) S3_P0D(512);
+  else S3_P0D(1024);
+#undef S3_P0D
 }
 
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s) {

@@ -111,6 +111,7 @@ void free_workspace(s3imph_ctx* c) {
   dfree(c->bucket); dfree(c->list[0]); dfree(c->list[1]);
   dfree(c->tcnt);
   dfree(c->p0_tcnt); dfree(c->p0_flags); dfree(c->p0_scnt); dfree(c->p0_pcnt); dfree(c->p0_sup); dfree(c->p0_x);
+  dfree(c->p0_ov);
   c->p0_x_cap = 0;
   c->p0_tiles = 0;
   c->p0_sup_cap = 0;
@@ -640,6 +641,43 @@ bool p0_try_bufs(s3imph_ctx* c, uint64_t n, uint64_t n_geom, hipStream_t s, P0Bu
 // P0F (developer knob S3IMPH_P0F=1; off by default): level 1 of a P0 build fed by level 0's
 // tile kernel.  Bit-exact, but measured slower on C3 (level 1 -0.32 ms, the
 // count pass +0.15, the in-tile positions' partial-line writes +0.17, the fed tile +0.08)
+// The super-tile scatter overlapped on the level-0 hash (bit-exact, measured slower:
+// the hash loses more beside it than the scatter's time): S3IMPH_P0_OV=1 turns it on (developer
+// switch); S3IMPH_P0_DIRECT=1 runs the direct form alone after the hash (A/B knob)
+bool p0_ov_on() {
+  static const bool v = [] {
+    const char* e = dev_env("S3IMPH_P0_OV");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+bool p0_direct_on() {
+  static const bool v = [] {
+    const char* e = dev_env("S3IMPH_P0_DIRECT");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+
+// Overlap set-up, on s after the build's state init: every region fill open, no part done;
+// the overlapped scatter then starts on c->ov_stream (it spins on the fills the hash publishes)
+void p0_ov_launch(s3imph_ctx* c, const BinBuffers& b, P0Bufs& p, hipStream_t s) {
+  if (!c->ov_stream) {
+    HIPCHECK(hipStreamCreateWithFlags(&c->ov_stream, hipStreamNonBlocking));
+    for (auto& e : c->ov_ev) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  if (!c->p0_ov) dalloc(c->p0_ov, (uint64_t)kH0GridHost + 8ull * kP0OvChunks * kMaxRanks);
+  p.hxcc = c->p0_ov;
+  p.ov_done = c->p0_ov + kH0GridHost;
+  HIPCHECK(hipMemsetAsync(p.pcnt, 0xff, (uint64_t)kH0GridHost * p.S * sizeof(unsigned), s));
+  HIPCHECK(hipMemsetAsync(p.hxcc, 0xff, (uint64_t)kH0GridHost * sizeof(unsigned), s));
+  HIPCHECK(hipMemsetAsync(p.ov_done, 0, 8ull * kP0OvChunks * p.S * sizeof(unsigned), s));
+  HIPCHECK(hipEventRecord(c->ov_ev[0], s));
+  HIPCHECK(hipStreamWaitEvent(c->ov_stream, c->ov_ev[0], 0));
+  launch_p0_scatter_direct(b, p, true, c->ov_stream);
+  HIPCHECK(hipEventRecord(c->ov_ev[1], c->ov_stream));
+}
+
 bool p0f_on() {
   static const bool v = [] {
     const char* e = dev_env("S3IMPH_P0F");
@@ -721,9 +759,19 @@ void enqueue_binned(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets,
       b.l20 = c->l20_mask = plan_l20(c, b, P, true, n);
       launch_init_state(c->d_st, n, n, s, offsets);
       ev_mark(c, s, "init");
+      // the super-tile scatter overlapped on the hash (fused regions of a device-resident set)
+      const bool ov = p0_ov_on() && p0_fused(blob, p) && !b.feed && p.tps <= 1024;
+      if (ov) p0_ov_launch(c, b, p, s);
       launch_p0_hash(blob, offsets, n, b, g0, p, s);
       ev_mark(c, s, "hash_part0");
-      launch_p0_scatter(b, p, p0_fused(blob, p), s);
+      if (ov) {
+        HIPCHECK(hipStreamWaitEvent(s, c->ov_ev[1], 0));
+        launch_p0_scatter_direct(b, p, false, s);
+      } else if (p0_direct_on() && p0_fused(blob, p) && p.tps <= 1024) {
+        launch_p0_scatter_direct(b, p, false, s);
+      } else {
+        launch_p0_scatter(b, p, p0_fused(blob, p), s);
+      }
       ev_mark(c, s, "scatter0_p0");
       launch_p0_tile(b, p, s);
       ev_mark(c, s, "tile0_p0");
@@ -2891,6 +2939,9 @@ int s3imph_ctx_destroy(s3imph_ctx* c) {
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   for (hipEvent_t e : c->copy_evs)
+    if (e) (void)hipEventDestroy(e);
+  if (c->ov_stream) (void)hipStreamDestroy(c->ov_stream);
+  for (hipEvent_t e : c->ov_ev)
     if (e) (void)hipEventDestroy(e);
   delete c;
   return S3IMPH_OK;

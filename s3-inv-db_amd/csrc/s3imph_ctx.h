@@ -234,6 +234,12 @@ struct s3imph_ctx {
   uint64_t p0_sup_cap = 0;
   uint16_t* p0_x = nullptr;       // bitmap decomposition: in-tile position of each level-0 R20 slot
   uint64_t p0_x_cap = 0;
+  // level 0's super-tile scatter overlapped on the hash: its stream, the events that order it
+  // (after the build's state init / before the follow-up scatter), and the hash blocks' XCDs +
+  // the finished parts (kH0GridHost + 8 kP0OvChunks kMaxRanks u32)
+  hipStream_t ov_stream = nullptr;
+  hipEvent_t ov_ev[2] = {};
+  unsigned* p0_ov = nullptr;
   // R20 list levels (BinBuffers::l20): on unless S3IMPH_L20=0 (A/B knob); l20_mask is the
   // last build's mask (classify_stop reads its stop level's list in that format)
   bool l20 = true;

@@ -79,6 +79,14 @@ static __device__ __forceinline__ uint4 ld_stream16(const void* p) {
 
 static __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
+// The XCD (accelerator complex die) this wave runs on: each has its own L2, so a producer and
+// a consumer on the same XCD exchange data through that L2 without an L2 write-back.
+static __device__ __forceinline__ unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 7u;
+}
+
 // A wave-uniform 64-bit value moved to scalar registers.
 static __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);

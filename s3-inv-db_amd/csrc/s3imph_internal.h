@@ -57,6 +57,10 @@ struct LevelState {
   unsigned long long gn[kMaxLevels + 2];       // global key count of level L
   // P0F (single GPU): level 0's settled keys, counted before its tile kernel (k_p0_count)
   unsigned long long settled0;
+  // P0 overlap (single GPU): level-0 hash blocks done, the overlapped scatter's per-XCD tickets
+  unsigned int h0_done;
+  unsigned int ov_pad_;
+  unsigned long long ov_ticket[8];
 };
 
 #if defined(__HIPCC__)
@@ -294,6 +298,11 @@ struct P0Bufs {
   uint16_t* x = nullptr;       // bitmap decomposition: each slot's position in its tile (the mark's input)
   unsigned nb = 0;             // the regions' producer blocks (0: the level-0 hash's grid; a bitmap
                                // list level fed by the previous settle: its grid, NextPart)
+  // level 0 with the super-tile scatter overlapped on the hash (single GPU, fused regions):
+  // each hash block's XCD (kH0GridHost) and the parts the overlapped launch finished
+  // (8 kP0OvChunks x S); null otherwise
+  unsigned* hxcc = nullptr;
+  unsigned* ov_done = nullptr;
   // super-tiles in 2^14-position units (tps tiles of 2^tb): the partition passes cut
   // (position >> 14) by this, so they need not know tb
   unsigned tps_sub() const { return tps << (tb - kRegTileMaxBits); }
@@ -311,6 +320,10 @@ unsigned p0_skew_blocks(int skew_cfg);               // k_hash_skew's grid (its 
 constexpr int kH0GridHost = 4096;                    // = k_hash0_pair's grid (kH0Grid)
 constexpr int kP0FedGrid = 256;                      // P0F: level 0's tile kernel blocks (level 1's region producers)
 void launch_p0_tile(const BinBuffers& b, const P0Bufs& p, hipStream_t s);
+// level 0's super-tile scatter in its direct form: ov, the persistent launch beside the hash;
+// otherwise the follow-up over the parts it left (or all of them)
+constexpr unsigned kP0OvChunks = 8;  // hash-block chunks per XCD (kH0GridHost / 64 blocks each)
+void launch_p0_scatter_direct(const BinBuffers& b, const P0Bufs& p, bool ov, hipStream_t s);
 // P0F: level 1 fed by level 0's tile kernel (s3imph_binned.hip).  launch_p0_count: level 0's
 // settled keys from the slots' in-tile positions (p.x), then level 1 sized on the device;
 // launch_p0_tile_fed: level 0's tiles with the collided records into level 1's super-tile

@@ -714,6 +714,49 @@ def _parity_subprocess(env: dict, cases) -> None:
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
+def _parity_device_subprocess(env: dict, cases, builds: int = 2) -> None:
+    """Build `cases` (n, kind, avg) device-resident (s3imph.DeviceBuilder: keys and outputs in
+    HBM) `builds` times each in a fresh process with `env` set: bit-exact vs the oracle."""
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path[:0]=[%r, %r]\n"
+        "import numpy as np, torch, s3imph, oracle as O\n"
+        "ctx = s3imph.DeviceBuilder(0)\n"
+        "for n, kind, avg in %r:\n"
+        "    blob, offs = s3imph.gen_keys(kind, 3, avg, 0, n)\n"
+        "    st, fp, po, mph = O.lib().build_mt(blob[: offs[-1]], offs, None, threads=16)\n"
+        "    d_blob = torch.from_numpy(blob).to('cuda')\n"
+        "    d_offs = torch.from_numpy(offs.view(np.int64)).to('cuda')\n"
+        "    for b in range(%d):\n"
+        "        d_fp = torch.zeros(n, dtype=torch.int64, device='cuda')\n"
+        "        d_po = torch.zeros(n, dtype=torch.int64, device='cuda')\n"
+        "        ctx.build(d_blob, d_offs, n, d_fp, d_po)\n"
+        "        assert ctx.mph_bin() == mph, (n, b)\n"
+        "        assert np.array_equal(d_fp.cpu().numpy().view(np.uint64), fp), (n, b)\n"
+        "        assert np.array_equal(d_po.cpu().numpy().view(np.uint64), po), (n, b)\n"
+        "ctx.close()\n"
+        "print('ok')\n"
+    ) % (os.path.join(os.path.dirname(GOLDEN), "..", "s3-inv-db_amd"), os.path.join(os.path.dirname(GOLDEN), "..", "oracle"),
+         list(cases), builds)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=280,
+                       env={**os.environ, **env})
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_p0_scatter_overlapped_on_hash_bit_exact(s3, oracle_lib):
+    """Level 0's super-tile scatter overlapped on the hash (S3IMPH_P0_OV=1): the
+    direct-form scatter runs beside k_hash0_pair on a second stream, taking each XCD's parts as
+    their hash blocks publish them, the follow-up launch the rest; then the direct form alone
+    (S3IMPH_P0_DIRECT=1).  Uniform sets at 509 / 191 / 1024-tile super-tiles (C3 100M and
+    smaller) and a skewed set (the follow-up takes every part): bit-exact, two builds each."""
+    cases = [(100_000_000, 0, 64), (30_000_000, 0, 16), (40_000_000, 1, 0)]
+    _parity_device_subprocess({"S3IMPH_DEV": "1", "S3IMPH_P0_OV": "1"}, cases)
+    _parity_device_subprocess({"S3IMPH_DEV": "1", "S3IMPH_P0_OV": "1", "S3IMPH_P0_TPS": "191"}, cases[:1], builds=1)
+    _parity_device_subprocess({"S3IMPH_DEV": "1", "S3IMPH_P0_OV": "1", "S3IMPH_P0_MAXS": "4"}, cases[1:2], builds=1)
+    _parity_device_subprocess({"S3IMPH_DEV": "1", "S3IMPH_P0_DIRECT": "1"}, cases[:2], builds=1)
+
+
 def test_p0_many_super_tiles_bit_exact(s3, oracle_lib):
     """More than 32 super-tiles on the two-block-per-CU super-tile scatter (S3IMPH_P0_BIG=0,
     S3IMPH_P0_TPS=48: 45 / 51 super-tiles on 17.5M uniform / 20M skewed keys, 8 blocks of 512
