@@ -792,11 +792,11 @@ __device__ __forceinline__ uint64_t run_off(const void* base, uint64_t i, uint64
 }
 template <bool k16>
 __global__ __launch_bounds__(kBT) void k_bm_place_bounds(const PlaceRun* __restrict__ runs, int P, uint64_t lo,
-                                                         uint64_t nwin, uint32_t* __restrict__ bnd) {
+                                                         uint64_t first, uint64_t nwin, uint32_t* __restrict__ bnd) {
   const uint64_t gid = (uint64_t)blockIdx.x * kBT + threadIdx.x;
   if (gid >= (uint64_t)P * (nwin + 1)) return;
   const int q = (int)(gid / (nwin + 1));
-  const uint64_t w = gid % (nwin + 1), key = w * kPlaceWin;
+  const uint64_t w = gid % (nwin + 1), key = first + w * kPlaceWin;
   const PlaceRun r = runs[q];
   uint64_t a = 0, b = r.n;  // first entry with offset >= key
   while (a < b) {
@@ -808,7 +808,7 @@ __global__ __launch_bounds__(kBT) void k_bm_place_bounds(const PlaceRun* __restr
 }
 template <bool k16>
 __global__ __launch_bounds__(kBT) void k_bm_place_merge(const PlaceRun* __restrict__ runs, int P, uint64_t lo,
-                                                        uint64_t limit, uint64_t nwin,
+                                                        uint64_t first, uint64_t limit, uint64_t nwin,
                                                         const uint32_t* __restrict__ bnd,
                                                         uint64_t* __restrict__ fp_out, uint64_t* __restrict__ pos_out,
                                                         LevelState* st) {
@@ -816,7 +816,7 @@ __global__ __launch_bounds__(kBT) void k_bm_place_merge(const PlaceRun* __restri
   __shared__ uint32_t s_i0[kMaxRanks], s_pre[kMaxRanks + 1];
   __shared__ const void* s_rb[kMaxRanks];  // the runs' bases and key bases, in LDS: an entry's
   __shared__ uint64_t s_kb[kMaxRanks];     // address waits on no global load but its own
-  const uint64_t w = blockIdx.x, w0 = w * kPlaceWin;
+  const uint64_t w = blockIdx.x, w0 = first + w * kPlaceWin;
   if (w >= nwin) return;
   const unsigned wn = (unsigned)min<uint64_t>(kPlaceWin, limit - w0), tid = threadIdx.x;
   // the window's entries over the runs, flattened: run q's part is [s_pre[q], s_pre[q + 1])
@@ -1049,20 +1049,21 @@ void launch_bm_tile_settle(int level, const void* bucket, bool r20, uint64_t pos
 }
 
 
-// runs: P device PlaceRun entries (this rank's own run included); limit: slice offsets the
-// merge fills (below the replicated tail); bnd: P x (nwin + 1) u32 scratch
-void launch_bm_place_merge(const void* runs, bool k16, int P, uint64_t lo, uint64_t limit, uint32_t* bnd,
-                           uint64_t* fp_out, uint64_t* pos_out, LevelState* st, hipStream_t s) {
-  if (!limit) return;
-  const uint64_t nwin = (limit + kPlaceWin - 1) / kPlaceWin;
+// runs: P device PlaceRun entries (this rank's own run included), each sorted by slice offset;
+// [first, limit): the slice offsets the merge fills, exactly one entry each over the runs (a
+// group of levels' settled keys below the replicated tail); bnd: P x (nwin + 1) u32 scratch
+void launch_bm_place_merge(const void* runs, bool k16, int P, uint64_t lo, uint64_t first, uint64_t limit,
+                           uint32_t* bnd, uint64_t* fp_out, uint64_t* pos_out, LevelState* st, hipStream_t s) {
+  if (limit <= first) return;
+  const uint64_t nwin = (limit - first + kPlaceWin - 1) / kPlaceWin;
   const PlaceRun* r = static_cast<const PlaceRun*>(runs);
   const int gb = grid_for((uint64_t)P * (nwin + 1), kBT, 1 << 20);
   if (k16) {
-    k_bm_place_bounds<true><<<gb, kBT, 0, s>>>(r, P, lo, nwin, bnd);
-    k_bm_place_merge<true><<<(int)nwin, kBT, 0, s>>>(r, P, lo, limit, nwin, bnd, fp_out, pos_out, st);
+    k_bm_place_bounds<true><<<gb, kBT, 0, s>>>(r, P, lo, first, nwin, bnd);
+    k_bm_place_merge<true><<<(int)nwin, kBT, 0, s>>>(r, P, lo, first, limit, nwin, bnd, fp_out, pos_out, st);
   } else {
-    k_bm_place_bounds<false><<<gb, kBT, 0, s>>>(r, P, lo, nwin, bnd);
-    k_bm_place_merge<false><<<(int)nwin, kBT, 0, s>>>(r, P, lo, limit, nwin, bnd, fp_out, pos_out, st);
+    k_bm_place_bounds<false><<<gb, kBT, 0, s>>>(r, P, lo, first, nwin, bnd);
+    k_bm_place_merge<false><<<(int)nwin, kBT, 0, s>>>(r, P, lo, first, limit, nwin, bnd, fp_out, pos_out, st);
   }
 }
 uint64_t bm_place_bound_words(int P, uint64_t limit) { return (uint64_t)P * ((limit + kPlaceWin - 1) / kPlaceWin + 1); }

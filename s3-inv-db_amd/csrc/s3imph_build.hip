@@ -1758,6 +1758,9 @@ void ensure_bm_workspace(s3imph_ctx* c, uint64_t N) {
 }
 
 void free_bm_workspace(DistState& d) {
+  if (d.xo) (void)hipStreamSynchronize(d.xo);  // (a level group's exchange reads these buffers)
+  dfree(d.xrecv);
+  d.cap_xrecv = 0;
   dfree(d.bm_a); dfree(d.bm_g); dfree(d.bm_dec);
   dfree(d.bm_lanes); dfree(d.bm_slice); dfree(d.bm_recv); dfree(d.bm_tsum); dfree(d.bm_tbase);
   dfree(d.bm_out);
@@ -1799,6 +1802,58 @@ uint64_t bm_target_tiles() {
     return e ? std::max<uint64_t>(64, std::strtoull(e, nullptr, 10)) : kScatterTiles;
   }();
   return v;
+}
+
+// The bitmap decomposition's output exchange by level group: levels 0 and 1 each
+// leave once settled, beside the next levels (S3IMPH_XCH_LEVELS=0: one exchange at the end, as
+// before round 6; A/B knob).  S3IMPH_XCH_STREAM=1 (test knob) puts the host-side transports'
+// exchanges on the exchange stream too (RCCL with a split communicator always does).
+bool xch_levels_on() {
+  static const bool v = [] {
+    const char* e = dev_env("S3IMPH_XCH_LEVELS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+bool xch_stream_knob() {
+  static const bool v = [] {
+    const char* e = dev_env("S3IMPH_XCH_STREAM");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+constexpr int kXchGroups = 3;  // level 0, level 1, the rest
+constexpr uint64_t kXchStride = (uint64_t)(kMaxRanks + 3) * (kMaxRanks + 1);  // a group's snapshot + gathered words
+
+// the exchange's buffers: per group the snapshot, gathered (device) and its pinned mirror, then
+// the merge's run descriptors; the received entries (this rank's slice at most); the merge's
+// window bounds over the slice; the exchange stream and its events
+void ensure_xch(s3imph_ctx* c, uint64_t mine, uint64_t es, int P) {
+  DistState& d = c->d;
+  const uint64_t words = kXchGroups * kXchStride + (uint64_t)kXchGroups * 3 * kMaxRanks;
+  if (!d.xch) dalloc(d.xch, words);
+  if (!d.h_xch) {
+    void* h = nullptr;
+    HIPCHECK(hipHostMalloc(&h, 8 * words, hipHostMallocDefault));
+    d.h_xch = static_cast<unsigned long long*>(h);
+  }
+  const uint64_t need = mine * es + 16;
+  if (need > d.cap_xrecv) {
+    d.cap_xrecv = 0;
+    dalloc(d.xrecv, need);
+    d.cap_xrecv = need;
+  }
+  const uint64_t bw = bm_place_bound_words(P, mine);
+  if (bw > d.bm_bnd_cap) {
+    d.bm_bnd_cap = 0;
+    dalloc(d.bm_bnd, bw);
+    d.bm_bnd_cap = bw;
+  }
+  if (!d.xo) {
+    HIPCHECK(hipStreamCreateWithFlags(&d.xo, hipStreamNonBlocking));
+    for (auto& e : d.ev_xg) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&d.ev_xdone, hipEventDisableTiming));
+  }
 }
 
 int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* pos,
@@ -1872,6 +1927,100 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   const bool out16 = !pos;
   const uint64_t es = out16 ? sizeof(BmT16) : sizeof(Rec);
   HIPCHECK(hipMemsetAsync(d.scnt, 0, 8ull * (P + 1), s));
+  // ---- the output exchange by level group ---------------------------------
+  // Settled keys bound for other slices leave in groups — level 0, level 1, then the rest —
+  // each once its levels are settled: a snapshot of the settle's cumulative per-slice counts
+  // (with this rank's list length, its key base and the group's end rank) is gathered on the
+  // build's stream; a level later the host reads it (an event) and puts the group's all-to-all
+  // and its slice merge on the exchange stream (RCCL: its own communicator), beside the next
+  // levels' work.  The checks read the gathered counts only: every rank takes the same branch.
+  const uint64_t XW = (uint64_t)P + 4;  // snapshot words per rank
+  const uint64_t out_cap_e = out16 ? d.bm_cap_out * sizeof(Rec) / sizeof(BmT16) : d.bm_cap_out;  // list entries
+  const bool xin = P > 1 && xch_levels_on();
+  const bool xasync = P > 1 && (d.xcomm != nullptr || xch_stream_knob());
+  Comm& xcm = d.xcomm && xasync ? *d.xcomm : cm;
+  hipStream_t xst = s;
+  int xsnaps = 0, xsent = 0;
+  uint64_t xracc = 0, xp_end = 0;
+  bool xbad = false;
+  if (P > 1) {
+    ensure_xch(c, mine, es, P);
+    if (xasync) xst = d.xo;
+  }
+  struct XJoin {  // every exit waits for the exchanges in flight (they read this build's buffers)
+    hipStream_t x;
+    ~XJoin() {
+      if (x) (void)hipStreamSynchronize(x);
+    }
+  } xjoin{xasync ? d.xo : nullptr};
+  // group xsnaps's snapshot, after the settle of level Lnext - 1
+  auto xsnap = [&](int Lnext) {
+    unsigned long long* dv = d.xch + (uint64_t)xsnaps * kXchStride;
+    HIPCHECK(hipMemcpyAsync(dv, d.scnt, 8ull * P, hipMemcpyDeviceToDevice, s));
+    HIPCHECK(hipMemcpyAsync(dv + P, out_cnt, 8, hipMemcpyDeviceToDevice, s));
+    launch_set_u64(dv + P + 1, key_base, s);
+    HIPCHECK(hipMemcpyAsync(dv + P + 2, &st->lvl_base[Lnext], 8, hipMemcpyDeviceToDevice, s));
+    launch_set_u64(dv + P + 3, out_cap_e, s);
+    cm.allgather(dv, dv + XW, 8 * XW, s);
+    HIPCHECK(hipMemcpyAsync(d.h_xch + (uint64_t)xsnaps * kXchStride + XW, dv + XW, 8 * XW * P, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipEventRecord(d.ev_xg[xsnaps], s));
+    ++xsnaps;
+  };
+  // group xsent's all-to-all and merge (its snapshot taken)
+  auto xsend = [&]() {
+    const int gi = xsent++;
+    HIPCHECK(hipEventSynchronize(d.ev_xg[gi]));
+    const unsigned long long* G = d.h_xch + (uint64_t)gi * kXchStride + XW;
+    const unsigned long long* Gp = gi ? d.h_xch + (uint64_t)(gi - 1) * kXchStride + XW : nullptr;
+    auto at = [&](const unsigned long long* M, int r, uint64_t j) -> uint64_t { return M ? M[(uint64_t)r * XW + j] : 0; };
+    auto cnt = [&](int r, int t) -> uint64_t { return at(G, r, t) - at(Gp, r, t); };
+    const uint64_t p_lo = at(Gp, 0, P + 2), p_hi = at(G, 0, P + 2);
+    // every rank's receipts against its slice's share of the group's ranks, its sends against
+    // its list's growth, one end rank everywhere
+    bool ok = p_lo <= p_hi && p_lo == xp_end;
+    for (int r = 0; r < P && ok; ++r) {
+      const uint64_t rlo = std::min<uint64_t>((uint64_t)r * slice, N), rhi = std::min<uint64_t>(N, rlo + slice);
+      uint64_t in = 0, lst = 0;
+      for (int q = 0; q < P; ++q) {
+        in += cnt(q, r);
+        lst += cnt(r, q);
+      }
+      const uint64_t a = std::min(std::max(p_lo, rlo), rhi), b = std::min(std::max(p_hi, rlo), rhi);
+      if (in != b - a || lst != at(G, r, P) - at(Gp, r, P) || at(G, r, P + 2) != p_hi || at(G, r, P) > at(G, r, P + 3))
+        ok = false;
+    }
+    xp_end = p_hi;
+    if (!ok) {
+      xbad = true;
+      return;
+    }
+    std::vector<uint64_t> soff(P), sbytes(P), roff(P), rbytes(P);
+    const uint64_t olo = at(Gp, R, P);  // this rank's list entries before the group
+    uint64_t sent = 0, got = 0;
+    for (int t = 0; t < P; ++t) {
+      soff[t] = (olo + sent) * es;
+      sbytes[t] = t == R ? 0 : cnt(R, t) * es;
+      sent += cnt(R, t);
+      roff[t] = (xracc + got) * es;
+      rbytes[t] = t == R ? 0 : cnt(t, R) * es;
+      if (t != R) got += cnt(t, R);
+    }
+    if (xasync) HIPCHECK(hipStreamWaitEvent(xst, d.ev_xg[gi], 0));
+    xcm.alltoallv(out, soff.data(), sbytes.data(), d.xrecv, roff.data(), rbytes.data(), xst);
+    // the merge's runs: sender q's entries of this slice and group (this rank's own in place)
+    unsigned long long* run_h = d.h_xch + kXchGroups * kXchStride + (uint64_t)gi * 3 * kMaxRanks;
+    unsigned long long* run_d = d.xch + kXchGroups * kXchStride + (uint64_t)gi * 3 * kMaxRanks;
+    for (int q = 0; q < P; ++q) {
+      const uint8_t* rb = q == R ? reinterpret_cast<const uint8_t*>(out) + soff[R] : d.xrecv + roff[q];
+      run_h[3 * q] = (unsigned long long)(uintptr_t)rb;
+      run_h[3 * q + 1] = cnt(q, R);
+      run_h[3 * q + 2] = at(G, q, P + 1);
+    }
+    HIPCHECK(hipMemcpyAsync(run_d, run_h, 24ull * P, hipMemcpyHostToDevice, xst));
+    const uint64_t a = std::min(std::max(p_lo, lo), lo + mine) - lo, b = std::min(std::max(p_hi, lo), lo + mine) - lo;
+    launch_bm_place_merge(run_d, out16, P, lo, a, b, d.bm_bnd, fp_out, pos_out, st, xst);
+    xracc += got;
+  };
   HIPCHECK(hipMemsetAsync(c->tcnt, 0, (size_t)kMaxDistLevels * kTcntStride * sizeof(unsigned), s));
   // The level's records go through the reservation scatter into tiles over the level's
   // whole position range (this rank's records only); the tile kernels then mark and
@@ -2009,6 +2158,11 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
                           next20, own_slice, s, staged, xs, out16, feed ? &npart : nullptr);
     if (!conservative && L == 0 && dev_env("S3IMPH_FAULT_BM_OVERFLOW"))
       launch_bm_flag(st, kStResOverflow, s);  // test hook: a capacity miss (the conservative rerun)
+    {  // levels 0 and 1: their group's snapshot now, the previous group's exchange out
+      const bool snap = xin && more && L <= 1;
+      if (snap) xsnap(L + 1);
+      while (xsent < xsnaps - (snap ? 1 : 0)) xsend();
+    }
     fed = feed;
     fed_rc = rc1;
     fed_nb = nb1;
@@ -2028,6 +2182,10 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
     ++L;
   }
   const int Ls = L + 1;  // first replicated level
+  if (P > 1) {  // the level groups still pending, then the last group's snapshot (sent beside the tail)
+    while (xsent < xsnaps) xsend();
+    xsnap(Ls);
+  }
   // ---- gather every rank's remaining records; all ranks finish the build identically,
   // the tail's outputs (global p in [N - total, N)) into scratch (kh / fp are free now)
   unsigned long long* M = d.h_pinned;
@@ -2097,6 +2255,8 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
   const LevelGeom gcons = choose_geom(std::max<uint64_t>(total, 1), kTargetTiles, kTargetChunks, kRegTileMaxBits);
   enqueue_levels_from(c, bt, Ls, total, gcons, false, s);
   HIPCHECK(hipGetLastError());
+  if (P > 1)
+    while (xsent < xsnaps) xsend();  // the last level group's exchange, beside the tail's levels
   HIPCHECK(hipMemcpyAsync(c->h_st, st, sizeof(LevelState), hipMemcpyDeviceToHost, s));
   HIPCHECK(hipMemcpyAsync(M, out_cnt, 8, hipMemcpyDeviceToHost, s));
   if (P == 1) HIPCHECK(hipMemcpyAsync(M + 8, d.scnt, 8, hipMemcpyDeviceToHost, s));  // the exchange's counts
@@ -2144,73 +2304,26 @@ int dist_attempt_bitmap(s3imph_ctx* c, const uint8_t* blob, const uint64_t* offs
            " of " + std::to_string(N) + " keys";
     return S3IMPH_ERR_INTERNAL;
   }
-  // ---- settled triples to the owners of their output slices: this rank's settled list is
-  // sorted by p, so its run for slice t (d.scnt[t] records, counted by the settle) goes to
-  // rank t as it lies; the own run is a hole (those keys were placed by the settle)
-  if (P > 1) {
-    launch_set_u64(d.scnt + P, key_base, s);  // (scnt[P] is free here) every rank's key base, for the 16-B entries
-    cm.allgather(d.scnt, d.mat, 8ull * (P + 1), s);
-    HIPCHECK(hipMemcpyAsync(M, d.mat, 8ull * (P + 1) * P, hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
-  } else {  // (read with the tail's state above)
-    M[0] = own1;
-    M[1] = key_base;
-  }
-  std::vector<uint64_t> sbytes(P), soff(P), rbytes(P), roff(P);
-  uint64_t acc = 0, got = 0, sent = 0;
-  std::vector<unsigned long long> tab(2 * (size_t)P);  // per sender: first received entry, key base
-  for (int t = 0; t < P; ++t) {
-    const uint64_t cnt_t = M[(uint64_t)R * (P + 1) + t];
-    soff[t] = sent * es;
-    sbytes[t] = t == R ? 0 : cnt_t * es;
-    sent += cnt_t;
-    const uint64_t in_t = M[(uint64_t)t * (P + 1) + R];
-    roff[t] = acc;
-    rbytes[t] = t == R ? 0 : in_t * es;
-    tab[t] = acc / es;
-    tab[P + t] = M[(uint64_t)t * (P + 1) + P];
-    acc += rbytes[t];
-    if (t != R) got += in_t;
-  }
-  const uint64_t own = M[(uint64_t)R * (P + 1) + R];
+  // ---- the settled keys reached their slices' owners by level group (the last group beside
+  // the tail, above); every rank checked every group against the gathered counts
   const uint64_t g0 = N - total;
-  const uint64_t tail_mine = std::min<uint64_t>(N, lo + mine) > std::max(g0, lo)
-                                 ? std::min<uint64_t>(N, lo + mine) - std::max(g0, lo) : 0;
-  {  // rank-local consistency of the output exchange: agreed before the all-to-all
-    int lrc = S3IMPH_OK;
-    if (sent != n_out || got + own + tail_mine != mine || got > d.cap_list) {
-      *msg = "build MPHF: internal error: output slice of rank " + std::to_string(R) + " receives " +
-             std::to_string(got) + " + " + std::to_string(own) + " + " + std::to_string(tail_mine) + " of " +
-             std::to_string(mine) + " entries";
-      lrc = S3IMPH_ERR_INTERNAL;
-    }
-    const int rc = dist_agree(c, lrc, s, msg);
-    if (rc != S3IMPH_OK) return rc;
-  }
-  Rec* recv = c->list[Ls & 1];
-  if (P > 1) cm.alltoallv(out, soff.data(), sbytes.data(), recv, roff.data(), rbytes.data(), s);
   if (P > 1) {
-    // the slice below the replicated tail from the P p-sorted runs: the received ones and this
-    // rank's own run, in place in its settled list
-    const uint64_t limit = g0 > lo ? std::min<uint64_t>(mine, g0 - lo) : 0;
-    const uint64_t bw = bm_place_bound_words(P, limit);
-    if (bw > d.bm_bnd_cap) {
-      d.bm_bnd_cap = 0;
-      dalloc(d.bm_bnd, bw);
-      d.bm_bnd_cap = bw;
+    if (xbad || xp_end != g0) {
+      *msg = "build MPHF: internal error: the output exchange's counts do not cover the slices";
+      return S3IMPH_ERR_INTERNAL;
     }
-    unsigned long long* run_h = d.h_pinned + kSmallWords + 2 * 16;  // (after dist_agree's words; 3 P <= 192)
-    unsigned long long* run_d = d.small + 6144;                     // (d.small: gathers below 4096, out_cnt at 4096)
-    HIPCHECK(hipStreamSynchronize(s));  // run_h is reused by the next build
-    for (int sq = 0; sq < P; ++sq) {  // run sq: sender sq's entries for this slice
-      const uint8_t* rb = sq == R ? reinterpret_cast<const uint8_t*>(out) + soff[R]
-                                  : reinterpret_cast<const uint8_t*>(recv) + roff[sq];
-      run_h[3 * sq] = (unsigned long long)(uintptr_t)rb;
-      run_h[3 * sq + 1] = sq == R ? own : M[(uint64_t)sq * (P + 1) + R];
-      run_h[3 * sq + 2] = tab[P + sq];
+    if (xasync) {  // the build's stream resumes once every group is placed
+      HIPCHECK(hipEventRecord(d.ev_xdone, xst));
+      HIPCHECK(hipStreamWaitEvent(s, d.ev_xdone, 0));
     }
-    HIPCHECK(hipMemcpyAsync(run_d, run_h, 24ull * P, hipMemcpyHostToDevice, s));
-    launch_bm_place_merge(run_d, out16, P, lo, limit, d.bm_bnd, fp_out, pos_out, st, s);
+  } else {  // one rank placed its settled keys during the settles: they and the tail's cover the slice
+    const uint64_t tail_mine = std::min<uint64_t>(N, lo + mine) > std::max(g0, lo)
+                                   ? std::min<uint64_t>(N, lo + mine) - std::max(g0, lo) : 0;
+    if (own1 != n_out || own1 + tail_mine != mine) {
+      *msg = "build MPHF: internal error: output slice of rank " + std::to_string(R) + " holds " +
+             std::to_string(own1) + " + " + std::to_string(tail_mine) + " of " + std::to_string(mine) + " entries";
+      return S3IMPH_ERR_INTERNAL;
+    }
   }
   launch_bm_tail_copy(c->kh, c->fp, g0, total, lo, mine, fp_out, pos_out, s);
   ev_mark(c, s, "exchange_out");
@@ -2931,9 +3044,17 @@ int s3imph_ctx_destroy(s3imph_ctx* c) {
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   free_workspace(c);
   fin_scratch_free(c);
+  if (c->d.xo) (void)hipStreamSynchronize(c->d.xo);
+  delete c->d.xcomm;
+  c->d.xcomm = nullptr;
   delete c->d.comm;
   c->d.comm = nullptr;
   if (c->d.xs) (void)hipStreamDestroy(c->d.xs);
+  if (c->d.xo) (void)hipStreamDestroy(c->d.xo);
+  for (hipEvent_t e : c->d.ev_xg)
+    if (e) (void)hipEventDestroy(e);
+  if (c->d.ev_xdone) (void)hipEventDestroy(c->d.ev_xdone);
+  if (c->d.h_xch) (void)hipHostFree(c->d.h_xch);
   for (hipEvent_t e : {c->d.ev_route, c->d.ev_counts, c->d.ev_x})
     if (e) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -3055,6 +3176,29 @@ int s3imph_ctx_create_dist(int device, const uint8_t id[128], int rank, int nran
   rc_comm->nranks = nranks;
   c->dist = true;
   c->d.comm = rc_comm;
+  if (nranks > 1) {
+    // the output exchange's own communicator (split from this one: the same ranks), so that a
+    // level group's exchange on its stream never waits behind, or holds up, the next levels'
+    // collectives; every rank keeps it only if every rank got it
+    ncclComm_t xc = nullptr;
+    const bool got = ncclCommSplit(rc_comm->comm, 0, rank, &xc, nullptr) == ncclSuccess && xc;
+    int ok = got ? 1 : 0;
+    int* d_ok = nullptr;
+    bool agreed = hipMalloc(&d_ok, sizeof(int)) == hipSuccess &&
+                  hipMemcpy(d_ok, &ok, sizeof(int), hipMemcpyHostToDevice) == hipSuccess &&
+                  ncclAllReduce(d_ok, d_ok, 1, ncclInt32, ncclMin, rc_comm->comm, nullptr) == ncclSuccess &&
+                  hipMemcpy(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess;
+    if (d_ok) (void)hipFree(d_ok);
+    if (agreed && ok == 1) {
+      RcclComm* x = new RcclComm();
+      x->comm = xc;
+      x->rank = rank;
+      x->nranks = nranks;
+      c->d.xcomm = x;
+    } else if (got) {
+      (void)ncclCommDestroy(xc);
+    }
+  }
   c->d.rank = rank;
   c->d.nranks = nranks;
   return S3IMPH_OK;

@@ -105,6 +105,18 @@ struct DistState {
   // level 0's exchange runs on its own stream, chunk by chunk, beside the next chunk's hash
   hipStream_t xs = nullptr;
   hipEvent_t ev_route = nullptr, ev_counts = nullptr, ev_x = nullptr;
+  // the bitmap decomposition's output exchange by level group (levels 0 and 1 as soon as they
+  // are settled, then the rest): per group the settle's per-slice counts, gathered
+  // (device + pinned mirror), the merge's run descriptors; the received entries; the exchange's
+  // stream, its group events and its completion; its communicator (RCCL: split from `comm`, so
+  // the exchange runs beside the next levels' collectives; null: `comm` on the build's stream)
+  unsigned long long* xch = nullptr;
+  unsigned long long* h_xch = nullptr;
+  uint8_t* xrecv = nullptr;
+  uint64_t cap_xrecv = 0;  // bytes
+  hipStream_t xo = nullptr;
+  hipEvent_t ev_xg[4] = {}, ev_xdone = nullptr;
+  Comm* xcomm = nullptr;
   std::string agree_msg;  // message of a failure agreed inside route0_chunked
 };
 

@@ -466,10 +466,10 @@ struct BmT16 {
 };
 
 // P > 1: the slice's settled keys from the P p-sorted runs (runs: device array of P
-// {base, n, key_base}) merged through LDS windows below slice offset `limit`; bnd: scratch of
-// bm_place_bound_words(P, limit) u32
-void launch_bm_place_merge(const void* runs, bool k16, int P, uint64_t lo, uint64_t limit, uint32_t* bnd,
-                           uint64_t* fp_out, uint64_t* pos_out, LevelState* st, hipStream_t s);
+// {base, n, key_base}) merged through LDS windows over slice offsets [first, limit) (a group of
+// levels' keys, below the replicated tail); bnd: scratch of bm_place_bound_words(P, limit) u32
+void launch_bm_place_merge(const void* runs, bool k16, int P, uint64_t lo, uint64_t first, uint64_t limit,
+                           uint32_t* bnd, uint64_t* fp_out, uint64_t* pos_out, LevelState* st, hipStream_t s);
 uint64_t bm_place_bound_words(int P, uint64_t limit);
 void launch_bm_tail_copy(const uint64_t* sfp, const uint64_t* spos, uint64_t g0, uint64_t total, uint64_t lo,
                          uint64_t cnt, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s);

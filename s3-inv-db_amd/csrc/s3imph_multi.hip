@@ -232,8 +232,10 @@ struct MultiCtx {
     if (aborted) return;
     aborted = true;
     if (hub) hub->abort();
-    for (s3imph_ctx* c : ctx)
+    for (s3imph_ctx* c : ctx) {
       if (c->d.comm) c->d.comm->abort();
+      if (c->d.xcomm) c->d.xcomm->abort();
+    }
   }
 };
 

@@ -249,3 +249,43 @@ def test_builder_on_several_gpus_writes_identical_files(s3, oracle_lib, tmp_path
             "prefix_blob.bin": kb.tobytes(), "prefix_offsets.u64": O.s3id_u64_array(ko)}
     for name, data in want.items():
         assert (out / name).read_bytes() == data, name
+
+
+def _bitmap_subprocess(env: dict, cases) -> None:
+    """Bitmap-decomposition builds of `cases` (ranks, kind, avg, n) on the thread-per-rank
+    transport, in a fresh process with `env` set (the library reads its knobs once per
+    process): bit-exact vs the oracle, twice each (the second build reuses the contexts)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = (
+        "import sys; sys.path[:0]=[%r, %r]\n"
+        "import numpy as np, torch, s3imph, oracle as O\n"
+        "for ranks, kind, avg, n in %r:\n"
+        "    blob, offs = s3imph.gen_keys(kind, 8, avg, 0, n)\n"
+        "    st, fp, po, mph = O.lib().build_mt(blob[: offs[-1]], offs, None, threads=16)\n"
+        "    for _ in range(2):\n"
+        "        g = s3imph.build_host(blob, offs, devices=[0] * ranks, flags=s3imph.MULTI_BITMAP)\n"
+        "        assert g[2] == mph and np.array_equal(g[0], fp) and np.array_equal(g[1], po), (ranks, n)\n"
+        "print('ok')\n"
+    ) % (os.path.join(here, "..", "s3-inv-db_amd"), os.path.join(here, "..", "oracle"), list(cases))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=280,
+                       env={**os.environ, "S3IMPH_DEV": "1", "S3IMPH_DIST_STRICT": "1", **env})
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_bitmap_output_exchange_by_level_group(s3, oracle_lib):
+    """The bitmap build's output exchange by level group: levels 0 and 1 leave as
+    soon as they are settled and land in their slices through per-group merges, the rest at
+    the end.  On the build's stream (the host transports' default), on the exchange stream
+    (S3IMPH_XCH_STREAM=1: the order RCCL runs them in, events included), and as one exchange at
+    the end (S3IMPH_XCH_LEVELS=0); 2, 3 and 8 ranks, skewed lengths on one case, sets with one,
+    two and several sharded levels (S3IMPH_DIST_SWITCH): bit-exact."""
+    cases = [(2, 0, 32, 3_000_000), (3, 1, 0, 2_000_000), (8, 0, 24, 6_000_000)]
+    _bitmap_subprocess({"S3IMPH_DIST_SWITCH": "20000"}, cases)
+    _bitmap_subprocess({"S3IMPH_DIST_SWITCH": "20000", "S3IMPH_XCH_STREAM": "1"}, cases)
+    _bitmap_subprocess({"S3IMPH_DIST_SWITCH": "20000", "S3IMPH_XCH_LEVELS": "0"}, cases[:2])
+    # one and two sharded levels: the last group alone, level 0 then the rest
+    _bitmap_subprocess({"S3IMPH_DIST_SWITCH": "2500000", "S3IMPH_XCH_STREAM": "1"}, [(2, 0, 32, 3_000_000)])
+    _bitmap_subprocess({"S3IMPH_DIST_SWITCH": "800000", "S3IMPH_XCH_STREAM": "1"}, [(2, 0, 32, 3_000_000)])
