@@ -204,7 +204,11 @@ int s3imph_ctx_stage_times(s3imph_ctx *ctx, float *ms, int cap, int *count, char
  *    caller writes at their global offsets (e.g. pwrite into the column files).
  * ------------------------------------------------------------------------ */
 
-/* Rank 0 creates the 128-byte RCCL unique id; the host broadcasts it. */
+/* Rank 0 creates the 128-byte RCCL unique id; the host broadcasts it.
+ * s3imph_ctx_create_dist is collective: every rank calls it with the same id.  At
+ * nranks > 1 it also splits a second communicator off the first (ncclCommSplit, kept only
+ * if every rank got one): the bitmap decomposition's output exchange runs on it, on its own
+ * stream, beside the next levels' collectives. */
 int s3imph_dist_unique_id(uint8_t id_out[128]);
 
 int s3imph_ctx_create_dist(int device, const uint8_t id[128], int rank, int nranks,
