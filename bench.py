@@ -87,8 +87,10 @@ def main() -> None:
     ap.add_argument("--decomp", default="bitmap", choices=["route", "bitmap"],
                     help="sharded levels (N > 1 or --dist): the north_star's per-level collision bitmap, "
                          "(A, C) planes exchanged over RCCL (bitmap, default; timed with no fallback), or "
-                         "records routed to position owners (route); the other is timed beside it "
-                         "(alt_decomposition)")
+                         "records routed to position owners (route)")
+    ap.add_argument("--alt", action="store_true",
+                    help="N > 1: also time the other decomposition on the same shards (alt_decomposition); "
+                         "off by default, so the scaling line depends on the timed decomposition alone")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 line beside the C3 headline")
     ap.add_argument("--headline-only", action="store_true",
                     help="skip the lookup / finalize / host_e2e lines (profiling runs)")
@@ -235,10 +237,10 @@ def main() -> None:
     n_global = plan.n_global
     stages = {k: v / prof_steps for k, v in stage_sum.items()}
     # The other decomposition of the sharded levels, timed the same way on the same keys
-    # (N > 1 only; beside `value`, never as it): the driver's multi-GPU runs then measure
-    # both the routed build and the per-level collision-bitmap reduction over RCCL.
+    # (N > 1 with --alt; beside `value`, never as it).  Off by default: the routed build has
+    # never run over RCCL at N > 1, and a line must not depend on it.
     alt = None
-    if world > 1 and not args.headline_only:
+    if world > 1 and args.alt and not args.headline_only:
         alt = alt_decomposition(s3imph, ctx, step, args, barrier, dist)
 
     if rank != 0:
