@@ -1760,6 +1760,7 @@ void ensure_bm_workspace(s3imph_ctx* c, uint64_t N) {
 void free_bm_workspace(DistState& d) {
   if (d.xo) (void)hipStreamSynchronize(d.xo);  // (a level group's exchange reads these buffers)
   dfree(d.xrecv);
+  dfree(d.xch);
   d.cap_xrecv = 0;
   dfree(d.bm_a); dfree(d.bm_g); dfree(d.bm_dec);
   dfree(d.bm_lanes); dfree(d.bm_slice); dfree(d.bm_recv); dfree(d.bm_tsum); dfree(d.bm_tbase);
