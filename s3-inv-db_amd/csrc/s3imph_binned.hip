@@ -3592,6 +3592,7 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, LevelS
   return *s_ok != 0;
 }
 
+template <int kG>
 __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0, Rec* list1, uint64_t* bits,
                                                       uint64_t cap_words, uint64_t* __restrict__ fp_out,
                                                       uint64_t* __restrict__ pos_out, LevelState* st,
@@ -3606,20 +3607,26 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
   do {                                                                            \
     if (tp && threadIdx.x == 0 && (li) < 64) tp[(li) * 8 + (i)] = wall_clock64(); \
   } while (0)
-  constexpr unsigned kSlW = (unsigned)((kMidW32 + kMidG - 1) / kMidG);  // owner slice, u32 words
+  using Cfg = MidCfg<kG>;
+  constexpr unsigned kSeg = Cfg::kSeg;
+  constexpr int kE = kG / 64;  // owners (senders) per lane in wave 0's scans
+  static_assert(kG % 64 == 0 && kG <= 256, "mid workgroups");
+  constexpr unsigned kSlW = (unsigned)((Cfg::kW32 + kG - 1) / kG);  // owner slice, u32 words
+  static_assert(kSlW <= (unsigned)kMidT, "one owner word per thread");
   __shared__ uint32_t sA[kSlW], sC[kSlW], sP[kSlW];
   __shared__ uint64_t sf[kMidStage], sp[kMidStage];
-  __shared__ unsigned s_cnt[kMidG], s_spre[kMidG + 1];
-  __shared__ unsigned long long s_pre[kMidG + 1];
-  __shared__ unsigned s_cpre[kMidG + 1];  // collided records of the owners before
+  __shared__ unsigned s_cnt[kG], s_spre[kG + 1];
+  __shared__ unsigned long long s_pre[kG + 1];
+  __shared__ unsigned s_cpre[kG + 1];  // collided records of the owners before
   __shared__ unsigned s_wc[kMidT / 64];
   __shared__ unsigned long long s_wbase[kMidT / 64];
   __shared__ int s_go, s_ok;
 
   const unsigned g = blockIdx.x, G = gridDim.x;
-  unsigned* bar = &st->mid_bar;  // zeroed by k_init_state: one mid launch per build attempt
-  unsigned* xc = mid + kMidXc;  // [owner][sender] segment counts
-  unsigned long long* tot = reinterpret_cast<unsigned long long*>(mid + kMidTot);
+  // zeroed by k_init_state: one launch of each form per build attempt
+  unsigned* bar = kG == kMidG ? &st->mid_bar : &st->mid_bar2;
+  unsigned* xc = mid + Cfg::kXc;  // [owner][sender] segment counts
+  unsigned long long* tot = reinterpret_cast<unsigned long long*>(mid + Cfg::kTot);
   const uint64_t N = st->out_cap;
   unsigned target = 0;
   bool bad = false;
@@ -3655,7 +3662,7 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
         }
         if (n <= kGate || woff + words > cap_words) {
           go = 0;  // the tail takes this level (or the workspace is too small: rerun)
-        } else if (n > kMidMaxKeys) {
+        } else if (n > Cfg::kMax) {
           if (g == 0) atomicOr(&st->status, kStTailOverflow);  // bigger than predicted: rerun
           go = 0;
         } else if (!st->preset[L] && !st->preset[p] && n == (L > L0 ? n_prev : st->n[p])) {
@@ -3695,7 +3702,7 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
       }
     }
     // ---- route: records -> (owner, sender) segments
-    if (tid < kMidG) s_cnt[tid] = 0;
+    if (tid < (unsigned)kG) s_cnt[tid] = 0;
     __syncthreads();
     {
       bool over = false;
@@ -3705,8 +3712,8 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
           const unsigned x = (unsigned)bb_index(seed, k[r], words, magic);
           const unsigned o = (x >> 5) / sl;
           const unsigned slot = atomicAdd(&s_cnt[o], 1u);
-          if (slot < kMidSeg)
-            xb[((uint64_t)o * kMidG + g) * kMidSeg + slot] = Rec{k[r], f[r], pp[r]};
+          if (slot < kSeg)
+            xb[((uint64_t)o * kG + g) * kSeg + slot] = Rec{k[r], f[r], pp[r]};
           else
             over = true;
         }
@@ -3714,22 +3721,34 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
       if (over) atomicOr(&st->status, kStTailOverflow);
     }
     __syncthreads();
-    if (tid < G) xc[tid * kMidG + g] = min(s_cnt[tid], (unsigned)kMidSeg);
+    if (tid < G) xc[tid * kG + g] = min(s_cnt[tid], kSeg);
     MPROF(li, 1);
     target += G;
     if (!grid_sync(bar, target, st, &s_ok)) break;
     MPROF(li, 2);
     // ---- own: gather this slice's records, mark A / C, bits, word rank prefix, total
-    if (wave == 0) {  // segment prefix over the senders
-      const unsigned v = lane < G ? xc[g * kMidG + lane] : 0u;
-      unsigned xs = v;
+    if (wave == 0) {  // segment prefix over the senders (kE consecutive senders per lane)
+      unsigned v[kE], sum = 0;
+#pragma unroll
+      for (int e = 0; e < kE; ++e) {
+        const unsigned q = lane * kE + e;
+        v[e] = q < G ? xc[g * kG + q] : 0u;
+        sum += v[e];
+      }
+      unsigned xs = sum;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const unsigned y = __shfl_up(xs, d);
         if (lane >= (unsigned)d) xs += y;
       }
-      if (lane < G) s_spre[lane] = xs - v;
-      if (lane == G - 1) s_spre[G] = xs;
+      unsigned ex = xs - sum;
+#pragma unroll
+      for (int e = 0; e < kE; ++e) {
+        const unsigned q = lane * kE + e;
+        if (q <= G) s_spre[q] = ex;  // (q == G: the total, when G ends inside this lane's run)
+        ex += v[e];
+      }
+      if (lane == 63) s_spre[G] = xs;
     }
     for (unsigned w = tid; w < sl; w += kMidT) {
       sA[w] = 0;
@@ -3751,7 +3770,7 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
           if (s_spre[mid2] <= j) lo = mid2;
           else hi = mid2;
         }
-        const Rec* q = xb + ((uint64_t)g * kMidG + lo) * kMidSeg + (j - s_spre[lo]);
+        const Rec* q = xb + ((uint64_t)g * kG + lo) * kSeg + (j - s_spre[lo]);
         k[r] = q->k;
         f[r] = q->f;
         pp[r] = q->p;
@@ -3795,15 +3814,21 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
     // workgroups in the settle except these counts (ranks, outputs and the next list's runs
     // are placed from them), and a sender overwrites an owner's exchange segments only after
     // the next level's first barrier, which follows every owner's reads here.
-    if (wave == 0) {
+    if (wave == 0) {  // (kE consecutive owners per lane)
       const unsigned tagv = (seq << 6) | (unsigned)li;
-      unsigned long long v = 0;
+      unsigned long long v[kE];
       unsigned spins = 0;
       int okv = 1;
       for (;;) {
-        v = lane < G ? __hip_atomic_load(&tot[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                     : ((unsigned long long)tagv << 32);
-        if (__all((unsigned)(v >> 32) == tagv)) break;
+        bool mine = true;
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+          const unsigned q = lane * kE + e;
+          v[e] = q < G ? __hip_atomic_load(&tot[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : ((unsigned long long)tagv << 32);
+          mine = mine && (unsigned)(v[e] >> 32) == tagv;
+        }
+        if (__all(mine)) break;
         if (++spins > (1u << 22)) {  // bounded, as grid_sync
           if (lane == 0) atomicOr(&st->status, kStTailOverflow);
           okv = 0;
@@ -3811,10 +3836,18 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      const unsigned long long sv = lane < G ? (v & 0xffffu) : 0ull;
-      const unsigned cv = lane < G ? (unsigned)((v >> 16) & 0xffffu) : 0u;
-      unsigned long long xs = sv;
-      unsigned xc2 = cv;
+      unsigned long long sv[kE], ssum = 0;
+      unsigned cv[kE], csum = 0;
+#pragma unroll
+      for (int e = 0; e < kE; ++e) {
+        const bool in = lane * kE + e < G;
+        sv[e] = in ? (v[e] & 0xffffu) : 0ull;
+        cv[e] = in ? (unsigned)((v[e] >> 16) & 0xffffu) : 0u;
+        ssum += sv[e];
+        csum += cv[e];
+      }
+      unsigned long long xs = ssum;
+      unsigned xc2 = csum;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const unsigned long long y = __shfl_up(xs, d);
@@ -3824,11 +3857,19 @@ __global__ __launch_bounds__(kMidT) void k_mid_levels(int L0, int L1, Rec* list0
           xc2 += y2;
         }
       }
-      if (lane < G) {
-        s_pre[lane] = xs - sv;
-        s_cpre[lane] = xc2 - cv;
+      unsigned long long exs = xs - ssum;
+      unsigned exc = xc2 - csum;
+#pragma unroll
+      for (int e = 0; e < kE; ++e) {
+        const unsigned q = lane * kE + e;
+        if (q <= G) {
+          s_pre[q] = exs;
+          s_cpre[q] = exc;
+        }
+        exs += sv[e];
+        exc += cv[e];
       }
-      if (lane == G - 1) {
+      if (lane == 63) {
         s_pre[G] = xs;
         s_cpre[G] = xc2;
       }
@@ -4518,9 +4559,16 @@ static unsigned mid_seq() {
   return (q.fetch_add(1, std::memory_order_relaxed) + 1) & ((1u << 26) - 1);
 }
 
-void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s) {
-  k_mid_levels<<<kMidG, kMidT, 0, s>>>(L0, L1, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out, b.pos_out, b.st,
-                                       b.mid, reinterpret_cast<Rec*>(b.mid + kMidXb), b.tile_prof, mid_seq());
+void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s, bool big) {
+  if (big)
+    k_mid_levels<kMidGBig><<<kMidGBig, kMidT, 0, s>>>(L0, L1, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out,
+                                                     b.pos_out, b.st, b.mid,
+                                                     reinterpret_cast<Rec*>(b.mid + MidCfg<kMidGBig>::kXb),
+                                                     b.tile_prof, mid_seq());
+  else
+    k_mid_levels<kMidG><<<kMidG, kMidT, 0, s>>>(L0, L1, b.list[0], b.list[1], b.bits, b.cap_words, b.fp_out,
+                                                b.pos_out, b.st, b.mid, reinterpret_cast<Rec*>(b.mid + MidCfg<kMidG>::kXb),
+                                                b.tile_prof, mid_seq());
 }
 
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s) {

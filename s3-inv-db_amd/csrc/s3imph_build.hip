@@ -103,6 +103,7 @@ void free_bm_workspace(DistState& d);
 
 void free_workspace(s3imph_ctx* c) {
   dfree(c->mid);
+  c->mid_cap = 0;
   dfree(c->split);
   dfree(c->kh); dfree(c->fp); dfree(c->bits); dfree(c->rank_base);
   c->rank_base_cap = 0;
@@ -277,6 +278,7 @@ void fault_dup_record(s3imph_ctx* c, Rec* list, hipStream_t s, bool r20 = false)
     HIPCHECK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(list) + sz, list, sz, hipMemcpyDeviceToDevice, s));
 }
 
+int mid_big_mode();
 BinBuffers make_bufs(s3imph_ctx* c, const uint64_t* pos, uint64_t* fp_out, uint64_t* pos_out, hipStream_t s) {
   BinBuffers b{};
   b.feed = c->feed;
@@ -302,7 +304,17 @@ BinBuffers make_bufs(s3imph_ctx* c, const uint64_t* pos, uint64_t* fp_out, uint6
     HIPCHECK(hipMemsetAsync(c->tile_prof, 0, nprof * sizeof(unsigned long long), s));
     b.tile_prof = c->tile_prof;
   }
-  if (!c->mid) dalloc(c->mid, kMidScratchU32);
+  {  // the 256-workgroup mid levels' scratch (201 MB) for sets that may have a level of 440k-1.75M keys
+    const uint64_t need = c->cap_keys >= kMidBigMinKeys && mid_big_mode() != 0
+                              ? std::max<uint64_t>(kMidScratchU32, MidCfg<kMidGBig>::kScratchU32)
+                              : kMidScratchU32;
+    if (!c->mid || c->mid_cap < need) {
+      c->mid_cap = 0;
+      dfree(c->mid);
+      dalloc(c->mid, need);
+      c->mid_cap = need;
+    }
+  }
   b.mid = c->mid;
   // 2^15 / 2^16-position tiles appear once a level has more than 2^14 x 4096 positions
   if (!c->split && c->cap_keys > (kMaxTiles << kRegTileMaxBits) / 2) dalloc(c->split, split_scratch_records());
@@ -342,6 +354,19 @@ Grids level_grids(uint64_t nk, uint64_t size, LevelGeom g) {
 // Shards follow the XCDs (blockIdx % 8): 16 shards measured far slower (C3 level-0
 // scatter 1.60 -> 2.87 ms), the runs of an XCD's blocks no longer meet in its L2.  An overflow is caught on the device and
 // the build reruns on the counted path.
+// Mid levels over every CU (k_mid_levels<kMidGBig>) for levels of 440k-1.75M keys (A/B knob
+// S3IMPH_MID_BIG: 0 off (default), 1 those levels only, 2 every level down to the tail).
+// Bit-exact, and slower than the binned kernels it replaces (C2 levels 0.280 -> 0.320 / 0.354
+// ms, C5 0.54 -> 0.58 / 0.61): a level's barrier and all-gather over 256
+// workgroups cost more than a level's two launches.
+int mid_big_mode() {
+  static const int v = [] {
+    const char* e = dev_env("S3IMPH_MID_BIG");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 bool res_fits(const s3imph_ctx* c, uint64_t nb, uint64_t size, uint64_t T = 0) {
   if (nb * (nb > kResSmallKeys ? c->res_fill : 4) <= c->bucket_cap) return true;
   if (T == 0) {
@@ -430,6 +455,7 @@ struct LevelsPlan {
     ListPlan pl;
   };
   std::vector<Lv> lv;
+  int midB0 = -1, midB1 = -1;  // levels over kMidGBig workgroups (k_mid_levels<kMidGBig>), before mid0..mid1
   int mid0 = -1, mid1 = -1;
   int launched;  // the last big level launched (L0 - 1 if none)
 };
@@ -445,6 +471,27 @@ LevelsPlan plan_levels_from(s3imph_ctx* c, const BinBuffers& b, int L0, uint64_t
     // kStTailOverflow and rerun conservatively).
     const double pred = (double)n0 * std::pow(q, L - L0);
     if (!conservative && pred * kTailMargin < (double)kTailKeys) break;
+    // a level of 440k-1.75M keys (bound: 2 % + 6 sigma, as the binned geometry's): the
+    // 256-workgroup mid kernel, with the levels after it that the small one would not take
+    // (mode 2: every level down to the tail)
+    // (its grid barrier needs all 256 CUs at once: not while other ranks share the GPU)
+    const int mb = !c->dist || (c->d.comm && c->d.comm->owns_gpu()) ? mid_big_mode() : 0;
+    if (!conservative && mb != 0 && P.midB0 < 0 && pred * kMidMargin > (double)kMidMaxKeys &&
+        c->mid_cap >= MidCfg<kMidGBig>::kScratchU32 &&
+        pred * 1.02 + 6.0 * std::sqrt(pred) + 1024.0 <= (double)kMidMaxKeysBig) {
+      int L1 = L;
+      while (L1 + 1 <= big && L1 + 1 < kMaxLevels - 1) {
+        const double pn = pred * std::pow(q, L1 + 1 - L);
+        if (pn * kTailMargin < (double)kTailKeys) break;
+        if (mb == 1 && pn * kMidMargin <= (double)kMidMaxKeys) break;
+        ++L1;
+      }
+      P.midB0 = L;
+      P.midB1 = L1;
+      P.launched = L1;
+      L = L1;
+      continue;
+    }
     if (!conservative && pred * kMidMargin <= (double)kMidMaxKeys) {
       // this level and the rest above the tail: one persistent launch
       int L1 = L;
@@ -491,6 +538,7 @@ int run_levels(s3imph_ctx* c, const BinBuffers& b, const LevelsPlan& P, int L0, 
     const LevelGeom g = v.pl.g;
     enqueue_list_level(c, b, v.L, v.nb, v.size, false, &g, s, v.tight);
   }
+  if (P.midB0 >= 0) launch_binned_mid(P.midB0, P.midB1, b, s, true);
   if (P.mid0 >= 0) launch_binned_mid(P.mid0, P.mid1, b, s);
   ev_mark(c, s, "levels");
   launch_binned_tail(L0, P.launched, b, s);

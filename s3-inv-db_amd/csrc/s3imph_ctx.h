@@ -68,6 +68,9 @@ struct Comm {
   // a peer failed: make every pending and future collective of this rank return (RCCL:
   // ncclCommAbort, whose kernels then exit); the communicator is unusable afterwards
   virtual void abort() {}
+  // this rank has its GPU to itself (RCCL: one rank per device); the host transports let
+  // ranks share one, so no kernel of a rank may wait for all of the GPU's CUs at once
+  virtual bool owns_gpu() const { return false; }
 };
 
 constexpr uint64_t kDistSwitchKeysDefault = 2ull << 20;  // levels below this run replicated
@@ -138,6 +141,7 @@ struct RcclComm final : Comm {
     bool expected = false;
     if (comm && aborted.compare_exchange_strong(expected, true)) (void)ncclCommAbort(comm);
   }
+  bool owns_gpu() const override { return true; }
   void live() const {
     if (aborted.load(std::memory_order_acquire))
       throw Fail{S3IMPH_ERR_RCCL, "RCCL communicator aborted: a peer rank failed"};
@@ -201,7 +205,8 @@ struct FinScratch;  // s3imph_finalize.hip
 struct s3imph_ctx {
   int device = 0;
   s3imph::FinScratch* fin = nullptr;  // finalize-pass scratch (s3imph_finalize.hip), lazily made
-  uint32_t* mid = nullptr;            // k_mid_levels scratch (kMidScratchU32), lazily made
+  uint32_t* mid = nullptr;            // k_mid_levels scratch (kMidScratchU32, or the 256-workgroup form's), lazily made
+  uint64_t mid_cap = 0;               // ... its u32 words
   Rec* split = nullptr;               // k_tile_split scratch, made for sets big enough for 2^15+ tiles
   hipStream_t own_stream = nullptr;
   std::mutex mu;

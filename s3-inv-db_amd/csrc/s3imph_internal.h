@@ -59,7 +59,7 @@ struct LevelState {
   unsigned long long settled0;
   // P0 overlap (single GPU): level-0 hash blocks done, the overlapped scatter's per-XCD tickets
   unsigned int h0_done;
-  unsigned int ov_pad_;
+  unsigned int mid_bar2;  // k_mid_levels<kMidGBig>'s grid-barrier counter (zeroed by k_init_state)
   unsigned long long ov_ticket[8];
 };
 
@@ -182,6 +182,27 @@ constexpr uint64_t kMidTot = kMidXc + (uint64_t)kMidG * kMidG;  // even: u64-ali
 constexpr uint64_t kMidXb = kMidTot + 2 * kMidG + 16;          // 16-byte aligned
 constexpr uint64_t kMidScratchU32 = kMidXb + (uint64_t)kMidG * kMidG * kMidSeg * 6;
 constexpr double kMidMargin = 1.15;  // a level predicted above kMidMaxKeys / kMidMargin stays binned
+// The same kernel over every CU (k_mid_levels<kMidGBig>) for the levels above kMidMaxKeys up to
+// kMidMaxKeysBig (owners again average <= 6.9k of 8k slots; a level's size is predicted within
+// 2 % + 6 sigma, the bound the binned geometry uses): per-(owner, sender) segments of kMidSegBig
+// records (a sender's <= 8192 records over 256 owners: 32 on average), its own barrier counter.
+constexpr int kMidGBig = 256;
+constexpr unsigned kMidSegBig = 128;
+constexpr unsigned long long kMidMaxKeysBig = 1750ull << 10;
+constexpr uint64_t kMidBigMinKeys = 1ull << 20;  // sets this big get the 256-workgroup scratch
+template <int G>
+struct MidCfg {
+  static constexpr unsigned kSeg = G == kMidG ? kMidSeg : kMidSegBig;
+  static constexpr unsigned long long kMax = G == kMidG ? kMidMaxKeys : kMidMaxKeysBig;
+  static constexpr uint64_t kW32 = 2 * ((2 * kMax + 63) / 64);  // u32 words of the largest level
+  // scratch (u32 units): 64 unused, segment counts [G][G], per-owner totals [G] u64, exchange [G][G][kSeg] Rec
+  static constexpr uint64_t kXc = 64;
+  static constexpr uint64_t kTot = kXc + (uint64_t)G * G;
+  static constexpr uint64_t kXb = kTot + 2 * G + 16;
+  static constexpr uint64_t kScratchU32 = kXb + (uint64_t)G * G * kSeg * 6;
+};
+static_assert(MidCfg<kMidG>::kXb == kMidXb && MidCfg<kMidG>::kScratchU32 == kMidScratchU32, "mid scratch layout");
+static_assert(MidCfg<kMidGBig>::kTot % 2 == 0 && MidCfg<kMidGBig>::kXb % 4 == 0, "mid scratch alignment");
 constexpr int kTailThreads = 1024;
 constexpr int kTailLdsWords32 = 2 * 2 * ((kGammaNum * kTailKeys + 63) / 64);  // A and C, u32 words
 
@@ -343,8 +364,9 @@ void launch_binned_tile(int level, const BinBuffers& b, LevelGeom g, int grid_ti
 void launch_binned_scatter_res(int level, const BinBuffers& b, LevelGeom g, int grid, hipStream_t s,
                                uint64_t i_lo = 0, uint64_t i_hi = 0, uint64_t tmax = 0);
 void launch_binned_tail(int first_level, int big_launched, const BinBuffers& b, hipStream_t s);
-// levels L0..L1 (each predicted above the tail and at most kMidMaxKeys keys) in one launch
-void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s);
+// levels L0..L1 (each predicted above the tail and at most kMidMaxKeys keys; big: at most
+// kMidMaxKeysBig, over kMidGBig workgroups) in one launch
+void launch_binned_mid(int L0, int L1, const BinBuffers& b, hipStream_t s, bool big = false);
 
 // ---- multi-GPU launchers (s3imph_dist.hip) ------------------------------------------
 constexpr int kMaxRanks = 64;

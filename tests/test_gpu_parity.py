@@ -757,6 +757,14 @@ def test_p0_scatter_overlapped_on_hash_bit_exact(s3, oracle_lib):
     _parity_device_subprocess({"S3IMPH_DEV": "1", "S3IMPH_P0_DIRECT": "1"}, cases[:2], builds=1)
 
 
+def test_mid_levels_over_every_cu_bit_exact(s3, oracle_lib):
+    """The mid-size levels on 256 workgroups (S3IMPH_MID_BIG=1: the levels of 440k-1.75M keys;
+    =2: every level down to the tail; off by default): C2's 10M keys and a skewed
+    4M set, bit-exact, two builds each (the second reuses the 256-workgroup scratch)."""
+    _parity_device_subprocess({"S3IMPH_DEV": "1", "S3IMPH_MID_BIG": "1"}, [(10_000_000, 0, 32), (4_000_000, 1, 0)])
+    _parity_device_subprocess({"S3IMPH_DEV": "1", "S3IMPH_MID_BIG": "2"}, [(10_000_000, 0, 32)], builds=1)
+
+
 def test_p0_many_super_tiles_bit_exact(s3, oracle_lib):
     """More than 32 super-tiles on the two-block-per-CU super-tile scatter (S3IMPH_P0_BIG=0,
     S3IMPH_P0_TPS=48: 45 / 51 super-tiles on 17.5M uniform / 20M skewed keys, 8 blocks of 512
