@@ -620,8 +620,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
         }
       }
     }
-    if (PT) {  // ---- the round's R20 records to their super-tiles' slots (this block's XCD shard)
-      static_assert(G * sizeof(R20) + G <= sizeof(sw), "the partition stage aliases the byte window");
+    if (PT) {  // ---- the round's R20 records straight to their slots of this block's super-tile regions
       unsigned od[2] = {0, 0}, ork[2] = {0, 0};
 #pragma unroll
       for (int h = 0; h < 2; ++h)
