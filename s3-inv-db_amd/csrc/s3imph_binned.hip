@@ -733,19 +733,23 @@ constexpr unsigned kSkLB = 256;        // length classes (4 B each)
 // ~12.5 steps on average, so the group barrier waited ~17 % of a wave's life; 5120 keys
 // over 12 waves give ~21 (C5 hash 1.65-1.66 -> 1.60-1.62 ms, `profiles/r3_skew*/`; 11, 10 and
 // 13 waves, and 8 waves with 4096 keys, measured slower).
+// kRes false: the partition form only (P0's level 0, pt.sup set), whose records leave for
+// their super-tile regions as each batch ends: no per-key result arrays in LDS, so two
+// blocks fit a CU with 5120-key groups (S3IMPH_SKEW_CFG 3; 16 waves per CU instead of 12).
 template <int kSkT, int kSkG>
 constexpr size_t sk_stage_bytes() { return (size_t)(kSkT / 64) * 64 * kSkS; }
-template <int kSkT, int kSkG>
+template <int kSkT, int kSkG, bool kRes = true>
 constexpr size_t sk_lds_bytes() {
-  return sk_stage_bytes<kSkT, kSkG>() + 2 * kSkG * sizeof(uint64_t) + kSkG * sizeof(unsigned short) +
+  return sk_stage_bytes<kSkT, kSkG>() + (kRes ? 2 * kSkG * sizeof(uint64_t) : 0) + kSkG * sizeof(unsigned short) +
          kSkLB * sizeof(unsigned) + 16;
 }
 static_assert(sk_lds_bytes<1024, 4096>() <= 160 * 1024, "k_hash_skew's LDS");
 static_assert(2 * sk_lds_bytes<512, 2048>() <= 160 * 1024, "k_hash_skew's LDS, two blocks per CU");
 static_assert(sk_lds_bytes<768, 5120>() <= 160 * 1024, "k_hash_skew's LDS, 12 waves");
+static_assert(2 * sk_lds_bytes<512, 5120, false>() <= 160 * 1024, "k_hash_skew's LDS, partition form, two blocks per CU");
 static_assert(kSkU * 16 == 64, "a load instruction covers 16 keys x 64 B");
 
-template <int kSkT, int kSkG>
+template <int kSkT, int kSkG, bool kRes = true>
 __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict__ blob,
                                                        const uint64_t* __restrict__ offsets, uint64_t n,
                                                        uint64_t* __restrict__ kh, uint64_t* __restrict__ fp,
@@ -759,7 +763,11 @@ __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict
   // super-tile through an LDS cursor per super-tile, instead of kh / fp in key order
   __shared__ unsigned sk_pcur[kMaxRanks];
   if (!st->skew) return;  // k_hash0_pair hashed this near-uniform set
-  const bool part = pt.sup != nullptr;
+  const bool part = kRes ? pt.sup != nullptr : true;
+  if (!kRes && pt.sup == nullptr) {  // (the host launches the partition form only with regions)
+    if (threadIdx.x == 0) atomicOr(&st->status, kStGeometry);
+    return;
+  }
   const uint32_t p_mul = part ? 0xffffffffu / pt.tps + 1 : 0u;
   const uint64_t p_words = st->words[0], p_magic = st->magic[0];
   bool p_over = false;
@@ -772,8 +780,8 @@ __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict
   uint4* stage = reinterpret_cast<uint4*>(sk_lds);
   constexpr size_t kSkStage = sk_stage_bytes<kSkT, kSkG>();
   uint64_t* res_a = reinterpret_cast<uint64_t*>(sk_lds + kSkStage);
-  uint64_t* res_b = res_a + kSkG;
-  unsigned short* sidx = reinterpret_cast<unsigned short*>(res_b + kSkG);
+  uint64_t* res_b = res_a + (kRes ? kSkG : 0);
+  unsigned short* sidx = reinterpret_cast<unsigned short*>(res_b + (kRes ? kSkG : 0));
   unsigned* cnt = reinterpret_cast<unsigned*>(sidx + kSkG);
   unsigned* next = cnt + kSkLB;
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -975,7 +983,7 @@ __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict
             pt.sup[((uint64_t)blockIdx.x * pt.S + od) * pt.reg_cap + at] = r20_make(a, f, (uint32_t)(grp + cur.k));
           else
             p_over = true;
-        } else {
+        } else if (kRes) {
           // results by key in LDS, written back in key order with coalesced stores (each
           // lane's own 8-byte stores cost more: they count against vmcnt, which every step
           // waits on, 1.64 -> 2.11 ms on C5 even with 8192-key groups in the freed LDS)
@@ -987,7 +995,7 @@ __global__ __launch_bounds__(kSkT, 4) void k_hash_skew(const uint8_t* __restrict
     }
     const unsigned long long e0t = prof ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();
-    if (!part) {
+    if (kRes && !part) {
       for (unsigned k = tid; k < m; k += kSkT) {
         const uint64_t a = res_a[k];
         kh[grp + k] = a;
@@ -4314,7 +4322,8 @@ uint64_t split_scratch_records() { return split_scratch_recs(); }
 // b.skew_cfg (S3IMPH_SKEW_CFG at context creation) selects the block / group shape: 2
 // (default) one 768-thread block per CU with 5120-key groups, 1 one 1024-thread block with
 // 4096-key groups (C5 1.65 vs 1.61 ms), 0 two 512-thread blocks per CU with 2048-key groups
-// (1.75 ms); S3IMPH_SKEW_ORDER=0 alternates the longest and the shortest batch instead of
+// (1.75 ms), 3 (partition form only, else 2) two 512-thread blocks per CU with 5120-key groups
+// and no result arrays; S3IMPH_SKEW_ORDER=0 alternates the longest and the shortest batch instead of
 // longest first.
 void launch_hash_skew(const uint8_t* blob, const uint64_t* offsets, uint64_t n, const BinBuffers& b, LevelGeom g,
                       unsigned long long* prof, hipStream_t s, const P0Part& pt = P0Part{}) {
@@ -4323,10 +4332,13 @@ void launch_hash_skew(const uint8_t* blob, const uint64_t* offsets, uint64_t n, 
     const char* e = dev_env("S3IMPH_SKEW_ORDER");
     return e ? std::atoi(e) : 1;
   }();
-  if (cfg == 1)
+  if (cfg == 3 && pt.sup)  // the partition form, two blocks per CU (p0_skew_blocks sized its regions)
+    k_hash_skew<512, 5120, false><<<512, 512, sk_lds_bytes<512, 5120, false>(), s>>>(
+        blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order, pt);
+  else if (cfg == 1)
     k_hash_skew<1024, 4096><<<256, 1024, sk_lds_bytes<1024, 4096>(), s>>>(
         blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order, pt);
-  else if (cfg == 2)
+  else if (cfg == 2 || cfg == 3)
     k_hash_skew<768, 5120><<<256, 768, sk_lds_bytes<768, 5120>(), s>>>(
         blob, offsets, n, b.kh, b.fp, b.flags, b.sflags, b.st, g.tb, g.chunk, b.tcnt, prof, order, pt);
   else
@@ -4341,6 +4353,8 @@ void binned_set_lds_limits() {
                             (int)sk_lds_bytes<512, 2048>());
   (void)hipFuncSetAttribute((const void*)k_hash_skew<768, 5120>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sk_lds_bytes<768, 5120>());
+  (void)hipFuncSetAttribute((const void*)k_hash_skew<512, 5120, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sk_lds_bytes<512, 5120, false>());
   (void)hipFuncSetAttribute((const void*)k_tile<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)std::max(tile_lds_bytes(kTileMaxBits), tile_lds_bytes(kCacheBits)));
   (void)hipFuncSetAttribute((const void*)k_tile_reg<512, 20, 2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -4602,7 +4616,7 @@ uint64_t p0_region_cap(uint64_t n, unsigned S, unsigned blocks) {
   const double per = (double)((n + blocks - 1) / blocks), mean = per / S;
   return (uint64_t)(mean + 10.0 * std::sqrt(mean) + 32.0);
 }
-unsigned p0_skew_blocks(int skew_cfg) { return skew_cfg == 0 ? 512u : 256u; }  // launch_hash_skew's grid
+unsigned p0_skew_blocks(int skew_cfg) { return skew_cfg == 0 || skew_cfg == 3 ? 512u : 256u; }  // launch_hash_skew's grid
 
 // P0 level 0's hash and first partition: fused (k_hash0_pair<..., PT>) for an aligned blob
 // of up to kMaxRanks super-tiles, with k_hash_skew + the partition pass standing by for a

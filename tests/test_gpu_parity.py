@@ -772,6 +772,13 @@ def test_p0_many_super_tiles_bit_exact(s3, oracle_lib):
     _parity_subprocess({"S3IMPH_P0_TPS": "48", "S3IMPH_P0_BIG": "0"}, [(17_500_000, 0, 20), (20_000_000, 1, 0)])
 
 
+def test_skew_partition_two_blocks_bit_exact(s3, oracle_lib):
+    """k_hash_skew's partition form without result arrays, two 512-thread blocks per CU
+    (S3IMPH_SKEW_CFG=3; off by default, profiles/r6_skew/): a 20M-key skewed set through
+    P0's 512 region sets, bit-exact."""
+    _parity_subprocess({"S3IMPH_SKEW_CFG": "3"}, [(20_000_000, 1, 0)])
+
+
 def test_p0_super_tile_cap_bit_exact(s3, oracle_lib):
     """S3IMPH_P0_MAXS=8 (A/B knob; 64 by default): 60M short keys in 8 super-tiles of 916 tiles
     (the super-tile scatter's 1024-tile-counter form) instead of 15 of ~489: bit-exact."""
