@@ -335,7 +335,10 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   constexpr int KW = (BB / 16 + NT - 1) / NT;  // 16-byte window chunks per thread
   constexpr unsigned kLB = 256;                // length classes of the sort
   constexpr int NW = NT / 64;
-  __shared__ uint64_t sw[BB / 8 + 2];          // the round's window (+ 16 B: a lane may read one word past)
+  // S3IMPH_FNV_PAIR: the window starts kWP words in, so >= 8 bytes precede every key (the
+  // zero-prefixed first word of fnv_window_pair reads them, masked)
+  constexpr unsigned kWP = S3IMPH_FNV_PAIR ? 2u : 0u;
+  __shared__ uint64_t sw[BB / 8 + 2 + kWP];    // the round's window (+ 16 B: a lane may read one word past)
   // sorted slot -> key's window offset (< BB) | length (<= BB) << 16: one LDS word per key
   static_assert(BB <= 32768, "offset and length in 16 bits each");
   __shared__ unsigned sol[G];
@@ -348,8 +351,15 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
   __shared__ uint64_t r_base[RT || PT ? kMaxRanks : 1];
   __shared__ unsigned r_over;
   __shared__ unsigned p_cur[PT ? kMaxRanks : 1];  // PT: this block's fill of each super-tile region
+  __shared__ uint64_t s_fnv_init[S3IMPH_FNV_PAIR ? 8 : 1];  // fnv_prefixed_basis(pad), pad 0..7
   if (st->skew) return;  // k_hash_count0 hashes skewed sets (and clears the tile state)
   const unsigned tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  if (S3IMPH_FNV_PAIR && tid < 8) {  // (ordered before the first hash by the round's barriers)
+    constexpr uint64_t kInit[8] = {fnv_prefixed_basis(0), fnv_prefixed_basis(1), fnv_prefixed_basis(2),
+                                   fnv_prefixed_basis(3), fnv_prefixed_basis(4), fnv_prefixed_basis(5),
+                                   fnv_prefixed_basis(6), fnv_prefixed_basis(7)};
+    s_fnv_init[tid] = kInit[tid];
+  }
   static_assert(!RT || G * sizeof(Rec) + G <= sizeof(sw), "the route stage aliases the byte window");
   // RT: level 0's geometry and owner ranges; this rank's own-record shift (records received
   // for earlier key chunks sit before its own ones)
@@ -449,13 +459,13 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
     for (int k = 0; k < KW; ++k) {
       const unsigned c = tid + (unsigned)k * NT;
       if (c < nfull) {
-        sw[2 * c] = (uint64_t)wr[k].x | ((uint64_t)wr[k].y << 32);
-        sw[2 * c + 1] = (uint64_t)wr[k].z | ((uint64_t)wr[k].w << 32);
+        sw[kWP + 2 * c] = (uint64_t)wr[k].x | ((uint64_t)wr[k].y << 32);
+        sw[kWP + 2 * c + 1] = (uint64_t)wr[k].z | ((uint64_t)wr[k].w << 32);
       }
     }
     if (tail8 && tid == 0) {  // once per blob: the last 8 readable bytes (a blocking load)
-      sw[2 * nfull] = *reinterpret_cast<const uint64_t*>(blob + (end8 - 8));
-      sw[2 * nfull + 1] = 0;
+      sw[kWP + 2 * nfull] = *reinterpret_cast<const uint64_t*>(blob + (end8 - 8));
+      sw[kWP + 2 * nfull + 1] = 0;
     }
     for (unsigned b = tid; b < kLB; b += NT) lcnt[b] = 0;
     if ((RT || PT) && tid < kMaxRanks) r_cnt[tid] = 0;
@@ -512,7 +522,7 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
       if (fits[h]) {
         const unsigned slot = lcnt[cls[h]] + rk[h];
         sidx[slot] = (unsigned short)(tid + (unsigned)h * NT);
-        sol[slot] = (unsigned)(t_b0[h] - rw) | ((unsigned)(t_b1[h] - t_b0[h]) << 16);
+        sol[slot] = ((unsigned)(t_b0[h] - rw) + 8u * kWP) | ((unsigned)(t_b1[h] - t_b0[h]) << 16);
       }
     __syncthreads();
     const uint64_t r0 = g;
@@ -538,6 +548,19 @@ __global__ __launch_bounds__(NT, 2048 / NT * NT / 256 / 2) void k_hash0_pair(con
           fp[r0] = b;
         }
         zero |= (a == 0);
+      }
+    } else if (S3IMPH_FNV_PAIR) {
+      // the lane's two keys as one word loop (fnv_window_pair)
+      const bool vA = tid < (m + 1) / 2, vB = tid < m / 2;
+      if (vA) {
+        const unsigned olA = sol[tid], olB = vB ? sol[m - 1 - tid] : 0u;
+        rj[0] = sidx[tid];
+        rj[1] = vB ? sidx[m - 1 - tid] : 0u;
+        fnv_window_pair(reinterpret_cast<const uint32_t*>(sw), olA & 0xffffu, olA >> 16, olB & 0xffffu, olB >> 16, vB,
+                        s_fnv_init, ra[0], rb[0], ra[1], rb[1]);
+        rv[0] = true;
+        rv[1] = vB;
+        zero |= ra[0] == 0 || (vB && ra[1] == 0);
       }
     } else {
 #pragma unroll

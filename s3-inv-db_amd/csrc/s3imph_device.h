@@ -52,6 +52,11 @@ __host__ __device__ __forceinline__ typename std::common_type<A, B>::type max(A 
 #ifndef S3IMPH_NT_SKEW
 #define S3IMPH_NT_SKEW 0
 #endif
+// k_hash0_pair's two keys per lane as ONE word loop (fnv_window_pair): each key zero-prefixed
+// to whole 8-byte words, no tail loops; A/B switch (S3IMPH_FNV_PAIR=1 at compile time)
+#ifndef S3IMPH_FNV_PAIR
+#define S3IMPH_FNV_PAIR 0
+#endif
 // Stores of whole runs that this build does not read back soon: the tile kernels' staged
 // fp_out / pos_out runs and the unfused hash's key-order kh / fp, with the non-temporal hint
 // (S3IMPH_NT_OUT, default on: C2 0.777 -> 0.765 ms, C3 6.45 -> 6.43 ms,
@@ -270,6 +275,79 @@ static __device__ __forceinline__ void fnv_window(const uint32_t* win, unsigned 
                rem);
   ha = (uint64_t)alo | ((uint64_t)ahi << 32);
   hb = (uint64_t)blo | ((uint64_t)bhi << 32);
+}
+
+// ---- two keys as one word loop (S3IMPH_FNV_PAIR) ------------------------------------
+// A key of len bytes hashed as pad = (-len) mod 8 zero bytes and then its bytes: both FNV
+// forms map a zero byte to h * P, so starting from offset_basis * P^-pad the pad steps
+// arrive at offset_basis exactly, and the key is whole 8-byte words.  The window must hold
+// >= 8 readable bytes before every key (the bytes before a key's start are masked to zero).
+__host__ __device__ constexpr uint64_t fnv_prime_inverse() {
+  uint64_t x = kFnvPrime;  // P odd: x = P is right to 3 bits; each Newton step doubles them
+  for (int i = 0; i < 5; ++i) x *= 2 - kFnvPrime * x;
+  return x;
+}
+static_assert(kFnvPrime * fnv_prime_inverse() == 1, "P^-1 mod 2^64");
+__host__ __device__ constexpr uint64_t fnv_prefixed_basis(unsigned pad) {
+  uint64_t h = kFnvOffset;
+  for (unsigned i = 0; i < pad; ++i) h *= fnv_prime_inverse();
+  return h;
+}
+// Keys A (len lA at byte oA of win) and B (if hasB) of one lane: the lane runs ceil(lA/8) +
+// ceil(lB/8) words in one loop, switching state after A's last word, so a wave whose lanes
+// pair a short key with a long one runs to the largest SUM of word counts instead of the
+// largest A plus the largest B plus two byte-step tails.  init[pad] = fnv_prefixed_basis(pad).
+static __device__ __forceinline__ void fnv_mask_first(unsigned pad, uint32_t& mlo, uint32_t& mhi) {
+  mlo = pad >= 4 ? 0u : ~0u << (8 * pad);
+  mhi = pad <= 4 ? ~0u : ~0u << (8 * (pad - 4));
+}
+static __device__ __forceinline__ void fnv_window_pair(const uint32_t* win, unsigned oA, unsigned lA, unsigned oB,
+                                                       unsigned lB, bool hasB, const uint64_t* init, uint64_t& haA,
+                                                       uint64_t& hbA, uint64_t& haB, uint64_t& hbB) {
+  const unsigned padA = (8u - (lA & 7u)) & 7u, padB = (8u - (lB & 7u)) & 7u;
+  const unsigned WA = (lA + padA) >> 3, W = WA + (hasB ? (lB + padB) >> 3 : 0u);
+  uint64_t h0 = init[padA];
+  uint32_t alo = (uint32_t)h0, ahi = (uint32_t)(h0 >> 32), blo = alo, bhi = ahi;
+  uint32_t mlo, mhi;
+  fnv_mask_first(padA, mlo, mhi);
+  unsigned s0 = oA - padA;
+  if (WA == 0) {  // an empty A: its hashes are offset_basis; B from the start
+    haA = hbA = kFnvOffset;
+    h0 = init[padB];
+    alo = blo = (uint32_t)h0;
+    ahi = bhi = (uint32_t)(h0 >> 32);
+    fnv_mask_first(padB, mlo, mhi);
+    s0 = oB - padB;
+  }
+  const uint32_t* w = win + (s0 >> 2);
+  unsigned sb = s0 & 3u;
+  uint32_t cur = w[0], n1 = w[1], n2 = w[2];
+  for (unsigned q = 0; q < W; ++q) {
+    const uint32_t m1 = w[3], m2 = w[4];
+    fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n1, cur, sb) & mlo);
+    fnv_4b(alo, ahi, blo, bhi, __builtin_amdgcn_alignbyte(n2, n1, sb) & mhi);
+    mlo = mhi = ~0u;
+    cur = n2;
+    n1 = m1;
+    n2 = m2;
+    w += 2;
+    if (q + 1 == WA) {  // A done: B's state, first-word mask and words
+      haA = (uint64_t)alo | ((uint64_t)ahi << 32);
+      hbA = (uint64_t)blo | ((uint64_t)bhi << 32);
+      h0 = init[padB];
+      alo = blo = (uint32_t)h0;
+      ahi = bhi = (uint32_t)(h0 >> 32);
+      fnv_mask_first(padB, mlo, mhi);
+      const unsigned s1 = oB - padB;
+      w = win + (s1 >> 2);
+      sb = s1 & 3u;
+      cur = w[0];
+      n1 = w[1];
+      n2 = w[2];
+    }
+  }
+  haB = (uint64_t)alo | ((uint64_t)ahi << 32);
+  hbB = (uint64_t)blo | ((uint64_t)bhi << 32);
 }
 
 // fnv_window continuing a running state (alo:ahi FNV-1a, blo:bhi FNV-1): the bytes of a
